@@ -1,0 +1,196 @@
+"""Fusion frames/sec (warp + integrate + solve), 640x480 (->640x448) synthetic depth -> 512³ TSDF @4 mm,
+~2k-node ED graph, 10k matches, on MI355X.
+
+One step = one frame of the reference's fusion loop (lepard_nicp_test.py:test4): GN solve
+(DeformNet.optimize formulation, 10 iterations) -> update node transforms -> fused skin-cache warp +
+TSDF/weight/colour integrate of the new frame. All inputs are device-resident before timing.
+
+  python bench.py [--gpus N --steps K --warmup W] [--mode replicas|shard] [--dims 512] [--nodes 2000]
+
+--mode replicas (default, BASELINE config 5): one independent 512³ scene per GPU, no collective,
+    value = frames of all ranks / max-rank time (weak scaling).
+--mode shard (BASELINE config 4 style): ONE volume x-sharded across ranks (bricks), matches sharded,
+    one RCCL all-reduce of the GN JᵀJ/Jᵀr accumulators per GN iteration; value = frames / time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
+    p.add_argument("--dims", type=int, default=512)
+    p.add_argument("--voxel", type=float, default=0.004)
+    p.add_argument("--nodes", type=int, default=2000)
+    p.add_argument("--matches", type=int, default=10000)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=1 << 24)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from occlusionfusion_amd import synthetic as S
+    from occlusionfusion_amd.pipeline import FusionPipeline
+
+    D = a.dims
+    origin = (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
+    seq = S.SyntheticSequence.build(a.nodes, seed=3)
+    shard = (rank, world) if (a.mode == "shard" and world > 1) else None
+    pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)
+    total = a.warmup + a.steps + 1
+    frames = [pipe.prepare(t) for t in range(total)]
+    torch.cuda.synchronize()
+    pipe.integrate_source(frames[0])
+    cache = pipe.wf.skin_tsdf_cache()
+    K = cache.k
+    n_skin_valid = int((cache.anchors.view(-1, 4)[:, K - 1] != -1).sum().item()) if cache.n_list else 0
+    torch.cuda.synchronize()
+
+    def solve(fi):
+        if a.mode == "shard" and world > 1:
+            g = pipe
+            out = pipe.solver.optimize_distributed(g.nodes_t, g.edges_t, g.ew_t, fi.tpos, fi.conf, fi.src, fi.anchors,
+                                                   fi.weights, fi.tgt, pipe.intr, prev_rot=pipe.prev_rot,
+                                                   prev_trans=pipe.prev_trans, sync=False)
+            pipe.prev_rot, pipe.prev_trans = out["node_rotations"], out["node_translations"]
+            return out
+        return pipe.solve(fi)
+
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    for t in range(1, 1 + a.warmup):
+        solve(frames[t])
+        pipe.integrate(frames[t], t)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    marks = []
+    pipe.vol.n_updated.zero_()
+    t0 = time.perf_counter()
+    for t in range(1 + a.warmup, total):
+        e0, e1, e2 = ev(), ev(), ev()
+        e0.record()
+        out = solve(frames[t])
+        e1.record()
+        pipe.integrate(frames[t], t, count_updates=True)
+        e2.record()
+        marks.append((e0, e1, e2, out))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
+    t_int = np.array([m[1].elapsed_time(m[2]) for m in marks]) * 1e-3
+    pcg = [int(m[3]["_status"][2].item()) for m in marks]
+    gn_it = [int(m[3]["_status"][1].item()) for m in marks]
+    valid = [int(m[3]["_status"][0].item()) for m in marks]
+    U = int(pipe.vol.n_updated.item()) / a.steps
+
+    frames_done = a.steps * (world if a.mode == "replicas" else 1)
+    value = frames_done / elapsed
+    # algorithmic bytes of one integrate launch: anchors 8 B per voxel of every
+    # listed brick; weights 16 B + tsdf/weight 8 B read per skin-valid voxel; per updated voxel
+    # tsdf/weight write 8 B + colour read+write 8 B.
+    B = cache.n_list * 512 * 8 + n_skin_valid * 24 + U * 16
+    t_int_avg = float(np.mean(t_int))
+    achieved = B / t_int_avg
+    res = {
+        "metric": "fusion frames/sec (warp+integrate+solve), 640x480 depth -> 512^3 TSDF",
+        "value": value, "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
+        "scaling": "weak" if a.mode == "replicas" else "strong", "vs_baseline": None, "dtype": "f32/f64",
+        "data": "synthetic (seeded sphere+plane non-rigid sequence, 1 mm noise; SURVEY §8(d))",
+        "config": {"workload": f"{D}^3 TSDF @{a.voxel * 1e3:g} mm, {seq.nodes.shape[0]} nodes, "
+                               f"{a.matches} matches, 640x448 depth, GN 10 it",
+                   "mode": a.mode, "dims": D, "voxel_size_m": a.voxel, "nodes": int(seq.nodes.shape[0]),
+                   "matches": a.matches, "parallelism": f"{a.mode}{world}"},
+        "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * t_int_avg,
+                         "pcg_iters_per_frame": float(np.mean(pcg)), "gn_iters": float(np.mean(gn_it)),
+                         "valid_solves": int(np.sum(valid))},
+        "roofline": {"kernel": "k_integrate<true> (fused warp+integrate)", "bound": "hbm", "achieved": achieved / 1e9,
+                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": achieved / PEAK_HBM, "traffic": None,
+                     "bytes_per_launch": B, "listed_bricks": cache.n_list, "skin_valid_voxels": n_skin_valid,
+                     "updated_voxels": U},
+    }
+    if rank == 0 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(pipe, frames[total - 1], total - 1, a)
+    if rank == 0:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pipe, fi, t, a):
+    """C/OpenMP port of the reference CPU warp+integrate (oracle/cpu_ref.c) on a uniform random sample of
+    the volume's voxels (skin precomputed, as the reference caches it), scaled to the whole volume."""
+    from oracle import cpu_ref
+    vol = pipe.vol
+    Dx, Dy, Dz = (int(d) for d in vol._vol_dim)
+    V = Dx * Dy * Dz
+    n = min(a.cpu_sample, V)
+    rng = np.random.default_rng(0)
+    vox = np.sort(rng.choice(V, n, replace=False))
+    i, r = vox // (Dy * Dz), vox % (Dy * Dz)
+    j, k = r // Dz, r % Dz
+    o = vol._vol_origin.astype(np.float64)
+    vs = np.float64(vol._voxel_size)
+    pts = np.stack([(o[0] + vs * i.astype(np.float32).astype(np.float64)),
+                    (o[1] + vs * j.astype(np.float32).astype(np.float64)),
+                    (o[2] + vs * k.astype(np.float32).astype(np.float64))], 1).astype(np.float32)
+    an, w, v = pipe.wf.skin_device(pts)
+    an, w, v = an.cpu().numpy(), w.cpu().numpy(), v.cpu().numpy().astype(np.uint8)
+    tsdf, color, weight = (x.reshape(-1).copy() for x in vol.get_volume())
+    R = pipe.prev_rot.cpu().numpy().reshape(-1, 9)
+    T = pipe.prev_trans.cpu().numpy()
+    im = fi.im.cpu().numpy()
+    from oracle import fusion_oracle as fo
+    depth, cim = fo.depth_of(im), fo.pack_color(im)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    cpu_ref.integrate((Dx, Dy, Dz), vol._vol_origin, vol._voxel_size, vox, depth, cim, pipe.intr, tsdf, weight, color,
+                      warp=True, anchors=an, weights=w, valid=v, R=R, T=T, nodes=pipe.graph.nodes)
+    dt = time.perf_counter() - t0
+    per_frame = dt * V / n
+    return {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"warp+integrate of {n} uniformly sampled voxels of the {Dx}^3 frame (x{V / n:.0f} scaled), "
+                      f"skin precomputed; GN solve NOT included; {dt:.3f}s measured",
+            "ms_per_frame_warp_integrate": 1e3 * per_frame}
+
+
+if __name__ == "__main__":
+    main()

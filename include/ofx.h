@@ -1,0 +1,192 @@
+/*
+ * ofx.h — C ABI of the MI355X-native non-rigid TSDF fusion hot path (libofx.so).
+ *
+ * Drop-in boundary for remmel/OcclusionFusion's fusion core. Every entry point
+ * takes plain device pointers + sizes and a HIP stream; no torch / numpy types
+ * cross this ABI. All work is stream-ordered and asynchronous unless an entry
+ * point says otherwise. Caller owns every buffer; the library owns only scratch
+ * tied to an opaque handle (GN solver). Errors: int status (0 ok, <0 error) and
+ * ofx_last_error() (thread-local string). Nothing throws across the ABI.
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   ofx_volume_reset        TSDFVolume.__init__ dense init tsdf=1, w=0, c=0   fusion_with_occlusion/tsdf.py:133-141
+ *   ofx_volume_to_dense     TSDFVolume.get_volume (D2H on request)          tsdf.py:673-680
+ *   ofx_volume_from_dense   TSDFVolume.load_volume                          tsdf.py:689-702
+ *   ofx_pack_color          TSDFVolume.update colour folding                tsdf.py:545-566
+ *   ofx_skin_volume_bricks  WarpField.skin_tsdf (cache build, brick cull)   warpfield.py:131-141
+ *   ofx_skin_volume         WarpField.skin over TSDFVolume.world_pts       warpfield.py:83-129, tsdf.py:294-307
+ *   ofx_skin_points         WarpField.skin(points, nodes)                  warpfield.py:83-129
+ *                           (k-NN twin of csrc compute_pixel_anchors_euclidean, csrc/cpu/graph_proc.cpp:610-709)
+ *   ofx_pack_nodes          Registration.deform_ED gathers of R, t, g       NonRigidICP/model/registration_fusion.py:168-170
+ *   ofx_integrate           WarpField.deform_tsdf + TSDFVolume.integrate    warpfield.py:369-380, tsdf.py:378-494
+ *                           (fused: skin cache -> ED warp -> project -> SDF/weight/colour update)
+ *   ofx_deform_points       ED_warp / deform_ED / deform_mesh / normals     NonRigidICP/model/geometry.py:9-25,
+ *                                                                          registration_fusion.py:157-184, warpfield.py:312-367
+ *   ofx_visibility          TSDFVolume.check_visibility                     tsdf.py:576-612
+ *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
+ */
+#ifndef OFX_H
+#define OFX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFX_ABI_VERSION 1
+
+typedef void* ofx_stream_t; /* hipStream_t; NULL = legacy default stream */
+
+enum {
+  OFX_OK = 0,
+  OFX_ERR_ARG = -1,      /* bad argument / shape */
+  OFX_ERR_HIP = -2,      /* HIP runtime error */
+  OFX_ERR_RANGE = -3,    /* size limit exceeded (e.g. > 65534 nodes) */
+  OFX_ERR_STATE = -4,    /* call order violated */
+  OFX_ERR_ALLOC = -5
+};
+
+const char* ofx_last_error(void);
+int ofx_abi_version(void);
+
+/* Voxel volume: dense grid (reference C-order semantics), stored on device as
+ * 8x8x8 bricks, brick-major. A shard owns bricks [brick_x0, brick_x1) along x. */
+typedef struct ofx_volume_desc {
+  int32_t dim[3];       /* Dx, Dy, Dz (TSDFVolume._vol_dim) */
+  int32_t brick_x0;     /* first brick column along x owned by this shard */
+  int32_t brick_x1;     /* one past the last (full volume: ceil(Dx/8)) */
+  int32_t _pad0;
+  float origin[3];      /* TSDFVolume._vol_origin (f32) */
+  float _pad1;
+  double voxel_size;    /* TSDFVolume._voxel_size (f64) */
+  double trunc_margin;  /* TSDFVolume._trunc_margin (0.04) */
+} ofx_volume_desc;
+
+typedef struct ofx_camera {
+  float fx, fy, cx, cy; /* cam_intr (cast to f32 as tsdf.py:357) */
+  int32_t width, height;
+} ofx_camera;
+
+/* number of voxel slots (bricks*512) a shard stores */
+int ofx_volume_num_slots(const ofx_volume_desc* desc, int64_t* n_slots);
+
+int ofx_volume_reset(const ofx_volume_desc* desc, float* tsdf, float* weight, float* color, ofx_stream_t s);
+/* bricked shard -> C-order dense (Dx_shard, Dy, Dz) where Dx_shard = min(8*x1,Dx) - 8*x0 */
+int ofx_volume_to_dense(const ofx_volume_desc* desc, const float* bricked, float* dense, ofx_stream_t s);
+int ofx_volume_from_dense(const ofx_volume_desc* desc, const float* dense, float* bricked, ofx_stream_t s);
+
+/* rgb (3,H,W) f32 in [0,1] -> packed colour (H,W) f32 (tsdf.py:561-562) */
+int ofx_pack_color(const float* rgb, int32_t height, int32_t width, float* packed, ofx_stream_t s);
+
+/* Skinning of the voxel grid.
+ * Step 1: list the shard's bricks that can hold a skin-valid voxel (>= K nodes within
+ *         4*node_coverage of the brick). brick_list: int32[num_bricks], count: device int32[1].
+ * Step 2: per-voxel k-NN for the listed bricks -> anchors uint16[n_list*512*4] (0xFFFF = -1),
+ *         weights f32[n_list*512*4]; slot = list position.                                */
+int ofx_skin_volume_bricks(const ofx_volume_desc* desc, const float* nodes, int32_t n_nodes,
+                           double node_coverage, int32_t k, int32_t* brick_list, int32_t* count,
+                           ofx_stream_t s);
+int ofx_skin_volume(const ofx_volume_desc* desc, const float* nodes, int32_t n_nodes, double node_coverage,
+                    int32_t k, const int32_t* brick_list, int32_t n_list, uint16_t* anchors, float* weights,
+                    ofx_stream_t s);
+/* Skinning of arbitrary points: anchors int32[P*K] (-1 beyond 4σ), weights f32[P*K], valid u8[P] */
+int ofx_skin_points(const float* points, int64_t n_points, const float* nodes, int32_t n_nodes,
+                    double node_coverage, int32_t k, int32_t* anchors, float* weights, uint8_t* valid,
+                    ofx_stream_t s);
+/* Expand the bricked skin cache to C-order (V,4) int32 / f32 / valid u8 (testing & API parity). */
+int ofx_skin_volume_to_dense(const ofx_volume_desc* desc, const int32_t* brick_list, int32_t n_list,
+                             const uint16_t* anchors, const float* weights, int32_t k, int32_t* anchors_out,
+                             float* weights_out, uint8_t* valid_out, ofx_stream_t s);
+
+/* Node transforms (node-relative, as Registration.deform_ED uses them):
+ * R f32[N*9] row-major, T f32[N*3], g f32[N*3] -> packed f32[N*16] */
+int ofx_pack_nodes(const float* R, const float* T, const float* g, int32_t n_nodes, float* packed,
+                   ofx_stream_t s);
+
+/* Fused warp + integrate of one frame into the shard.
+ *   warp = 0 : source frame — every voxel, world position, no skin (tsdf.py:395-398)
+ *   warp = 1 : bricks in brick_list, ED-warped positions, skin-valid voxels only (tsdf.py:401,464)
+ * color_im / color may be NULL (no colour integration). n_updated (device u64) may be NULL. */
+int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
+                  int32_t warp, const float* packed_nodes, int32_t n_nodes, int32_t k,
+                  const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
+                  double obs_weight, float* tsdf, float* weight, float* color,
+                  unsigned long long* n_updated, ofx_stream_t s);
+
+/* ED warp of points: out = Σ w (R(x-g)+g+t) for valid points, x otherwise.
+ * normals = 1: WarpField.deform_normals semantics (R only, renormalised). valid may be NULL (all valid). */
+int ofx_deform_points(const float* points, int64_t n_points, const int32_t* anchors, const float* weights,
+                      const uint8_t* valid, int32_t k, const float* packed_nodes, int32_t n_nodes,
+                      int32_t normals, float* out, ofx_stream_t s);
+
+/* check_visibility: valid u8[P], depth_diff f64[P] */
+int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
+                   double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s);
+
+/* ---------------- Gauss-Newton (DeformNet.optimize) ---------------- */
+typedef struct ofx_gn_params {
+  int32_t num_iter;          /* 10 (model.py:91) */
+  int32_t use_edge_weighting;/* 0 (custom_settings.py:41) */
+  int32_t pcg_max_iter;      /* inner PCG cap */
+  int32_t _pad;
+  double lambda_flow;        /* 0   (model.py:96) — squared weights, sqrt taken inside (model.py:374-377) */
+  double lambda_depth;       /* 1   (model.py:101) */
+  double lambda_arap;        /* 0.5 (model.py:105) */
+  double lambda_motion;      /* 1   (model.py:108) */
+  double lm_factor;          /* 1e-7 (model.py:111) */
+  double stop_loss_diff;     /* 1   (model.py:114) */
+  double pcg_tol;            /* relative residual target of the inner solve */
+} ofx_gn_params;
+
+typedef struct ofx_gn_problem {
+  int32_t n_nodes, n_matches, n_neighbors, _pad;
+  const float* nodes;           /* (N,3) */
+  const int32_t* edges;         /* (N,n_neighbors), -1 padded */
+  const float* edge_weights;    /* (N,n_neighbors) or NULL */
+  const float* target_node_pos; /* (N,3) motion-complete targets */
+  const float* node_conf;       /* (N) */
+  const float* src;             /* (M,3) */
+  const int32_t* anchors;       /* (M,4) all >= 0 */
+  const float* weights;         /* (M,4) */
+  const float* tgt;             /* (M,3) */
+  const float* target_px;       /* (M) or NULL (only used if lambda_flow != 0) */
+  const float* target_py;
+  const float* prev_rot;        /* (N,9) or NULL -> identity */
+  const float* prev_trans;      /* (N,3) or NULL -> zero */
+  float fx, fy, cx, cy;
+} ofx_gn_problem;
+
+/* status (device int32[4]): [valid_solve, gn_iterations_accepted, pcg_iterations_total, ill_posed]
+ * loss_log (device f64[num_iter*4]): per accepted iteration [total, data, arap, motion] */
+typedef struct ofx_gn_result {
+  float* rot;        /* (N,9) */
+  float* trans;      /* (N,3) */
+  int32_t* status;
+  double* loss_log;
+} ofx_gn_result;
+
+int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle);
+int ofx_gn_destroy(void* handle);
+/* Upload + build the block-sparse JᵀJ pattern (co-anchored node pairs, edges, diagonal).
+ * Synchronises the stream once to size the pattern; *nnz_blocks receives the block count. */
+int ofx_gn_setup(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params, int64_t* nnz_blocks,
+                 ofx_stream_t s);
+/* Assemble A (f64[nnz_blocks*36]) and rhs (f64[6N+4]: b = -Jᵀr then [loss² total,data,arap,motion])
+ * from matches [m0,m1); regularizers (ARAP, motion) added iff add_reg. Zeroes both first.
+ * In a multi-GPU solve every rank calls this on its match shard, the caller all-reduces
+ * (sum) A and rhs, then every rank calls ofx_gn_step with identical buffers. */
+int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int32_t add_reg, double* A,
+                     double* rhs, ofx_stream_t s);
+/* LM damping, block-Jacobi PCG solve, early-stop bookkeeping, R <- exp(x_rot) R, t += x_t. */
+int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_stream_t s);
+int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s);
+/* setup + num_iter x (linearize + step) + finish, single device */
+int ofx_gn_solve(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params,
+                 const ofx_gn_result* res, ofx_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFX_H */

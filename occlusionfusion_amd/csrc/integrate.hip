@@ -1,0 +1,260 @@
+// Fused ED warp + TSDF integrate, plus point warp / visibility helpers.
+//
+// Per voxel (reference CPU path, fusion_with_occlusion/tsdf.py:378-494):
+//   x  = vox2world(i,j,k)                                   (tsdf.py:338-349, f32)
+//   x' = Σ_k w_k (R_k (x - g_k) + g_k + t_k)  if warp       (NonRigidICP/model/geometry.py:9-25, f32,
+//                                                            registration_fusion.py:157-184; invalid skin -> skipped,
+//                                                            tsdf.py:464)
+//   u  = int(round_half_even((x'*fx)/z + cx)), v likewise   (tsdf.py:351-364, f64 with f32 intrinsics)
+//   valid iff 0<=u<W, 0<=v<H, z>0, d=depth[v,u]>0, d-z >= -trunc        (tsdf.py:576-612)
+//   dist = min(1,(d-z)/trunc); w' = f32(w+obs); tsdf' = f32((f32(w*tsdf) + obs*dist)/w')  (tsdf.py:366-376)
+//   colour: per-channel running average in f32, rint, min 255  (tsdf.py:479-494)
+//
+// MI355X layout: tsdf/weight/colour are 8³ bricks (2 KiB contiguous per array per brick); one
+// 256-thread workgroup owns one brick (2 voxels per thread, coalesced 4/8/16-B loads). For warped
+// frames the grid is the compacted list of skinned bricks, and the skin cache of a brick is stored
+// contiguously by list slot: anchors ushort4 (8 B) + weights float4 (16 B) per voxel. Node records
+// (64 B) and the depth/colour images are gathered through L1/L2. Voxels with invalid skin read 8 B
+// and stop. All arithmetic is un-contracted (-ffp-contract=off) so results are bit-identical to the
+// oracle restatement.
+#include "ofx_common.h"
+
+namespace ofx {
+
+struct CamD {
+  double fx, fy, cx, cy;
+  int W, H;
+};
+
+// Warp one voxel position with its K anchors (f32, reference op order).
+__device__ __forceinline__ void ed_warp(const float4* __restrict__ nodes, const int ids[4], const float w[4], int K,
+                                        float& x, float& y, float& z) {
+  float ax = 0.f, ay = 0.f, az = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float4* n = nodes + 4 * (int64_t)ids[k];
+    float4 r0 = n[0], r1 = n[1], r2 = n[2], tt = n[3];
+    float dx = x - r0.w, dy = y - r1.w, dz = z - r2.w;
+    float rx = r0.x * dx; rx = rx + r0.y * dy; rx = rx + r0.z * dz;
+    float ry = r1.x * dx; ry = ry + r1.y * dy; ry = ry + r1.z * dz;
+    float rz = r2.x * dx; rz = rz + r2.y * dy; rz = rz + r2.z * dz;
+    float yx = ((rx + r0.w) + tt.x) * w[k];
+    float yy = ((ry + r1.w) + tt.y) * w[k];
+    float yz = ((rz + r2.w) + tt.z) * w[k];
+    if (k == 0) { ax = yx; ay = yy; az = yz; }
+    else { ax = ax + yx; ay = ay + yy; az = az + yz; }
+  }
+  x = ax; y = ay; z = az;
+}
+
+// Projection + visibility (tsdf.py:351-364, 576-612). Returns pixel index or -1.
+__device__ __forceinline__ int64_t project(const CamD& c, float x, float y, float z, double& Z) {
+  double X = x, Y = y;
+  Z = z;
+  double u = rint((X * c.fx) / Z + c.cx);
+  double v = rint((Y * c.fy) / Z + c.cy);
+  if (!(u >= 0.0 && u < (double)c.W && v >= 0.0 && v < (double)c.H && Z > 0.0)) return -1;
+  return (int64_t)v * c.W + (int64_t)u;
+}
+
+__device__ __forceinline__ float cdiv(float a, float b) { return (float)((double)a / (double)b); }
+
+// One voxel update; returns 1 if the voxel was integrated.
+__device__ __forceinline__ int update_voxel(const CamD& c, const float* __restrict__ depth,
+                                            const float* __restrict__ color_im, double trunc, double obs, float x,
+                                            float y, float z, int64_t vi, float* __restrict__ tsdf,
+                                            float* __restrict__ weight, float* __restrict__ color) {
+  double Z;
+  int64_t pix = project(c, x, y, z, Z);
+  if (pix < 0) return 0;
+  float d = depth[pix];
+  double dd = (double)d - Z;
+  if (!(d > 0.f && dd >= -trunc)) return 0;
+  double dist = fmin(1.0, dd / trunc);
+  float w_old = weight[vi];
+  float t_old = tsdf[vi];
+  float w_new = (float)((double)w_old + obs);
+  float prod = w_old * t_old;
+  float t_new = (float)(((double)prod + obs * dist) / (double)w_new);
+  weight[vi] = w_new;
+  tsdf[vi] = t_new;
+  if (color) {
+    const float C = 65536.0f;
+    float oc = color[vi];
+    float ob = floorf(oc / C);
+    float og = floorf((oc - ob * C) / 256.0f);
+    float orr = (oc - ob * C) - og * 256.0f;
+    float nc = color_im[pix];
+    float nb = floorf(nc / C);
+    float ng = floorf((nc - nb * C) / 256.0f);
+    float nr = (nc - nb * C) - ng * 256.0f;
+    float ow = (float)obs;
+    float b2 = fminf(255.0f, rintf(cdiv(w_old * ob + ow * nb, w_new)));
+    float g2 = fminf(255.0f, rintf(cdiv(w_old * og + ow * ng, w_new)));
+    float r2 = fminf(255.0f, rintf(cdiv(w_old * orr + ow * nr, w_new)));
+    color[vi] = (b2 * C + g2 * 256.0f) + r2;
+  }
+  return 1;
+}
+
+__device__ __forceinline__ void count_updates(int n, unsigned long long* counter) {
+  if (!counter) return;
+  // wave64 reduction then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(counter, (unsigned long long)n);
+}
+
+template <bool WARP>
+__global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const float* __restrict__ depth,
+                                                    const float* __restrict__ color_im,
+                                                    const float4* __restrict__ nodes, int K,
+                                                    const int32_t* __restrict__ list,
+                                                    const ushort4* __restrict__ anchors,
+                                                    const float4* __restrict__ weights, double trunc, double obs,
+                                                    float* __restrict__ tsdf, float* __restrict__ weight,
+                                                    float* __restrict__ color, unsigned long long* counter) {
+  const int64_t slot = blockIdx.x;
+  const int64_t b = WARP ? (int64_t)list[slot] : slot;
+  int64_t bz = b % g.nbz;
+  int64_t r = b / g.nbz;
+  int64_t by = r % g.nby;
+  int64_t bx = r / g.nby + g.bx0;
+  const int i0 = (int)bx * kBrick, j0 = (int)by * kBrick, k0 = (int)bz * kBrick;
+  int n_upd = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int l = threadIdx.x + h * 256;
+    const int i = i0 + (l >> 6), j = j0 + ((l >> 3) & 7), k = k0 + (l & 7);
+    if (i >= g.Dx || j >= g.Dy || k >= g.Dz) continue;
+    float x = vox2world(g.ox, g.vs, i);
+    float y = vox2world(g.oy, g.vs, j);
+    float z = vox2world(g.oz, g.vs, k);
+    if (WARP) {
+      const int64_t si = slot * kBrickVox + l;
+      ushort4 a = anchors[si];
+      int ids[4] = {a.x, a.y, a.z, a.w};
+      if (ids[K - 1] == kNoAnchor) continue;  // skin-invalid voxel: never integrated after the source frame
+      float4 ww = weights[si];
+      float w[4] = {ww.x, ww.y, ww.z, ww.w};
+      ed_warp(nodes, ids, w, K, x, y, z);
+    }
+    n_upd += update_voxel(c, depth, color_im, trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
+  }
+  count_updates(n_upd, counter);
+}
+
+__global__ __launch_bounds__(256) void k_deform_points(const float* __restrict__ pts, int64_t n,
+                                                        const int32_t* __restrict__ anchors,
+                                                        const float* __restrict__ weights,
+                                                        const uint8_t* __restrict__ valid, int K,
+                                                        const float4* __restrict__ nodes, int normals,
+                                                        float* __restrict__ out) {
+  int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  float x = pts[3 * p], y = pts[3 * p + 1], z = pts[3 * p + 2];
+  bool v = valid ? valid[p] != 0 : true;
+  if (v) {
+    int ids[4];
+    float w[4];
+    for (int k = 0; k < K; ++k) { ids[k] = anchors[p * K + k]; w[k] = weights[p * K + k]; }
+    if (!normals) {
+      ed_warp(nodes, ids, w, K, x, y, z);
+    } else {
+      // WarpField.deform_normals: deform_lbs with zero translation, weights==0 skipped (warpfield.py:208-231,312-345)
+      float ax = 0.f, ay = 0.f, az = 0.f;
+      for (int k = 0; k < K; ++k) {
+        if (w[k] == 0.f) continue;
+        const float4* nd = nodes + 4 * (int64_t)ids[k];
+        float4 r0 = nd[0], r1 = nd[1], r2 = nd[2];
+        float rx = r0.x * x; rx = rx + r0.y * y; rx = rx + r0.z * z;
+        float ry = r1.x * x; ry = ry + r1.y * y; ry = ry + r1.z * z;
+        float rz = r2.x * x; rz = rz + r2.y * y; rz = rz + r2.z * z;
+        ax = ax + w[k] * rx; ay = ay + w[k] * ry; az = az + w[k] * rz;
+      }
+      x = ax; y = ay; z = az;
+    }
+  }
+  if (normals) {
+    float nrm = (float)sqrt((double)((x * x + y * y) + z * z));
+    x = cdiv(x, nrm); y = cdiv(y, nrm); z = cdiv(z, nrm);
+  }
+  out[3 * p] = x; out[3 * p + 1] = y; out[3 * p + 2] = z;
+}
+
+__global__ void k_visibility(const float* __restrict__ pts, int64_t n, CamD c, const float* __restrict__ depth,
+                             double trunc, uint8_t* __restrict__ valid, double* __restrict__ ddiff) {
+  int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  double Z;
+  int64_t pix = project(c, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], Z);
+  double dv = pix >= 0 ? (double)depth[pix] : 0.0;
+  double dd = dv - Z;
+  valid[p] = (dv > 0.0 && dd >= -trunc) ? 1 : 0;
+  if (ddiff) ddiff[p] = dd;
+}
+
+static CamD make_cam(const ofx_camera* cam) {
+  CamD c;
+  c.fx = cam->fx; c.fy = cam->fy; c.cx = cam->cx; c.cy = cam->cy;
+  c.W = cam->width; c.H = cam->height;
+  return c;
+}
+
+}  // namespace ofx
+
+using namespace ofx;
+
+extern "C" {
+
+int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
+                  int32_t warp, const float* packed_nodes, int32_t n_nodes, int32_t k, const int32_t* brick_list,
+                  int32_t n_list, const uint16_t* anchors, const float* weights, double obs_weight, float* tsdf,
+                  float* weight, float* color, unsigned long long* n_updated, ofx_stream_t s) {
+  BrickGeom g;
+  int st = make_geom(desc, &g);
+  if (st) return st;
+  OFX_CHECK_ARG(cam && depth && tsdf && weight, "null buffer");
+  OFX_CHECK_ARG(cam->width > 0 && cam->height > 0, "bad camera size");
+  OFX_CHECK_ARG((color == nullptr) == (color_im == nullptr), "color and color_im must both be set or both NULL");
+  CamD c = make_cam(cam);
+  hipStream_t hs = as_stream(s);
+  if (!warp) {
+    hipLaunchKernelGGL(k_integrate<false>, dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth, color_im,
+                       (const float4*)nullptr, 1, (const int32_t*)nullptr, (const ushort4*)nullptr,
+                       (const float4*)nullptr, desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+  } else {
+    OFX_CHECK_ARG(k >= 1 && k <= 4 && n_nodes >= k, "bad k/n_nodes");
+    OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
+    if (n_list == 0) return OFX_OK;
+    OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights, "null warp buffer");
+    hipLaunchKernelGGL(k_integrate<true>, dim3((unsigned)n_list), dim3(256), 0, hs, g, c, depth, color_im,
+                       (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors, (const float4*)weights,
+                       desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+  }
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_deform_points(const float* points, int64_t n_points, const int32_t* anchors, const float* weights,
+                      const uint8_t* valid, int32_t k, const float* packed_nodes, int32_t n_nodes, int32_t normals,
+                      float* out, ofx_stream_t s) {
+  OFX_CHECK_ARG(n_points >= 0 && k >= 1 && k <= 4 && n_nodes >= k, "bad sizes");
+  if (n_points == 0) return OFX_OK;
+  OFX_CHECK_ARG(points && anchors && weights && packed_nodes && out, "null buffer");
+  hipLaunchKernelGGL(k_deform_points, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
+                     n_points, anchors, weights, valid, k, (const float4*)packed_nodes, normals, out);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
+                   double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s) {
+  OFX_CHECK_ARG(cam && n_points >= 0, "bad args");
+  if (n_points == 0) return OFX_OK;
+  OFX_CHECK_ARG(points && depth && valid, "null buffer");
+  hipLaunchKernelGGL(k_visibility, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
+                     n_points, make_cam(cam), depth, trunc_margin, valid, depth_diff);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,213 @@
+"""Gauss-Newton non-rigid registration behind the reference's solver APIs, backed by libofx.
+
+* GaussNewtonSolver.optimize — DeformNet.optimize (model/model.py:222-859) for one batch item:
+  same inputs (graph nodes/edges, motion-complete node targets + confidence, source points with
+  anchors/weights, target points, intrinsics, prev rot/trans), same outputs (node_rotations,
+  node_translations, valid_solve, convergence_info).
+* Registration.optimize — NonRigidICP/model/registration_fusion.py:98-145 API (returns
+  node_rotations, node_translations, deformed_nodes_to_target, warped_verts, convergence_info,
+  source/target frame ids) with the GN solver in place of the Adam/lietorch loop.
+* optimize_distributed — match-sharded multi-GPU solve: every rank assembles JᵀJ/Jᵀr over its own
+  matches, one all-reduce (sum) of the block-sparse accumulators per GN iteration, identical solve
+  on every rank.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr, byref
+
+GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
+                   lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=1000, pcg_tol=1e-8)
+MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
+
+
+def _t(x, device, dtype):
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x), device=device).to(dtype).contiguous()
+
+
+class GaussNewtonSolver:
+    def __init__(self, max_nodes, max_matches=MAX_MATCHES_EVAL, device=None, **params):
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.params = dict(GN_DEFAULTS)
+        self.params.update(params)
+        self.max_nodes, self.max_matches = int(max_nodes), int(max_matches)
+        h = _lib.c_void_p()
+        with torch.cuda.device(self.device):
+            call("ofx_gn_create", self.max_nodes, self.max_matches, byref(h))
+        self._h = h
+        self._keep = []
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.ofx_gn_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def _params(self):
+        p = _lib.GnParams()
+        q = self.params
+        p.num_iter = int(q["num_iter"])
+        p.use_edge_weighting = int(bool(q["use_edge_weighting"]))
+        p.pcg_max_iter = int(q["pcg_max_iter"])
+        p.lambda_flow, p.lambda_depth = float(q["lambda_flow"]), float(q["lambda_depth"])
+        p.lambda_arap, p.lambda_motion = float(q["lambda_arap"]), float(q["lambda_motion"])
+        p.lm_factor, p.stop_loss_diff, p.pcg_tol = float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"])
+        return p
+
+    def _problem(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
+                 source_points, anchors, weights, target_points, intrinsics, target_px, target_py, prev_rot,
+                 prev_trans):
+        d = self.device
+        ts = dict(nodes=_t(graph_nodes, d, torch.float32).reshape(-1, 3))
+        N = ts["nodes"].shape[0]
+        ts["edges"] = _t(graph_edges, d, torch.int32).reshape(N, -1)
+        ts["ew"] = _t(graph_edges_weights, d, torch.float32)
+        ts["tpos"] = (_t(target_node_position, d, torch.float32).reshape(N, 3) if target_node_position is not None
+                      else ts["nodes"].clone())
+        ts["conf"] = (_t(node_confidence, d, torch.float32).reshape(N) if node_confidence is not None
+                      else torch.zeros(N, device=d))
+        ts["src"] = _t(source_points, d, torch.float32).reshape(-1, 3)
+        M = ts["src"].shape[0]
+        ts["anc"] = _t(anchors, d, torch.int32).reshape(M, 4)
+        ts["wts"] = _t(weights, d, torch.float32).reshape(M, 4)
+        ts["tgt"] = _t(target_points, d, torch.float32).reshape(M, 3)
+        ts["tpx"] = _t(target_px, d, torch.float32)
+        ts["tpy"] = _t(target_py, d, torch.float32)
+        ts["prev_rot"] = _t(prev_rot, d, torch.float32)
+        ts["prev_trans"] = _t(prev_trans, d, torch.float32)
+        if N > self.max_nodes or M > self.max_matches:
+            raise ValueError(f"problem ({N} nodes, {M} matches) exceeds solver capacity "
+                             f"({self.max_nodes}, {self.max_matches})")
+        pb = _lib.GnProblem()
+        pb.n_nodes, pb.n_matches, pb.n_neighbors = N, M, ts["edges"].shape[1]
+        pb.nodes, pb.edges, pb.edge_weights = ptr(ts["nodes"]), ptr(ts["edges"]), ptr(ts["ew"])
+        pb.target_node_pos, pb.node_conf = ptr(ts["tpos"]), ptr(ts["conf"])
+        pb.src, pb.anchors, pb.weights, pb.tgt = ptr(ts["src"]), ptr(ts["anc"]), ptr(ts["wts"]), ptr(ts["tgt"])
+        pb.target_px, pb.target_py = ptr(ts["tpx"]), ptr(ts["tpy"])
+        pb.prev_rot, pb.prev_trans = ptr(ts["prev_rot"]), ptr(ts["prev_trans"])
+        fx, fy, cx, cy = (float(v) for v in np.asarray(intrinsics, np.float64).reshape(-1)[:4])
+        pb.fx, pb.fy, pb.cx, pb.cy = fx, fy, cx, cy
+        self._keep = ts  # keep inputs alive while the stream uses them
+        return pb, N, M
+
+    def _result(self, N):
+        d = self.device
+        out = dict(rot=torch.empty((N, 3, 3), device=d), trans=torch.empty((N, 3), device=d),
+                   status=torch.zeros(4, dtype=torch.int32, device=d),
+                   loss=torch.zeros((int(self.params["num_iter"]), 4), dtype=torch.float64, device=d))
+        r = _lib.GnResult()
+        r.rot, r.trans, r.status, r.loss_log = ptr(out["rot"]), ptr(out["trans"]), ptr(out["status"]), ptr(out["loss"])
+        return r, out
+
+    @staticmethod
+    def _pack(out, sync):
+        res = {"node_rotations": out["rot"], "node_translations": out["trans"], "_status": out["status"],
+               "_loss": out["loss"]}
+        if sync:
+            st = out["status"].cpu().numpy()
+            loss = out["loss"].cpu().numpy()[:st[1]]
+            res["valid_solve"] = int(st[0])
+            res["convergence_info"] = {"total": loss[:, 0].tolist(), "data": loss[:, 1].tolist(),
+                                       "arap": loss[:, 2].tolist(), "motion": loss[:, 3].tolist(),
+                                       "valid": int(st[0]), "gn_iterations": int(st[1]),
+                                       "pcg_iterations": int(st[2]), "errors": (["Solver failed: Ill-posed system!"]
+                                                                                 if st[3] else [])}
+        return res
+
+    def optimize(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
+                 source_points, anchors, weights, target_points, intrinsics, target_px=None, target_py=None,
+                 prev_rot=None, prev_trans=None, sync=True):
+        """model.py:222-859 (batch item). Returns torch device tensors (+ host convergence info if sync)."""
+        pb, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
+                                 node_confidence, source_points, anchors, weights, target_points, intrinsics,
+                                 target_px, target_py, prev_rot, prev_trans)
+        r, out = self._result(N)
+        prm = self._params()
+        call("ofx_gn_solve", self._h, byref(pb), byref(prm), byref(r), stream_ptr())
+        return self._pack(out, sync)
+
+    def optimize_distributed(self, *args, group=None, sync=True, **kw):
+        """Match-sharded solve over torch.distributed: rank r assembles matches [r*M/W, (r+1)*M/W);
+        A and rhs are all-reduced (sum) once per GN iteration; rank 0 adds ARAP + motion rows."""
+        import torch.distributed as dist
+        pb, N, M = self._problem(*args, **kw)
+        prm = self._params()
+        nnz = _lib.c_int64()
+        call("ofx_gn_setup", self._h, byref(pb), byref(prm), byref(nnz), stream_ptr())
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        m0, m1 = (M * rank) // world, (M * (rank + 1)) // world
+        A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=self.device)
+        rhs = torch.empty(6 * N + 4, dtype=torch.float64, device=self.device)
+        for it in range(int(self.params["num_iter"])):
+            call("ofx_gn_linearize", self._h, it, m0, m1, 1 if rank == 0 else 0, ptr(A), ptr(rhs), stream_ptr())
+            dist.all_reduce(A, group=group)
+            dist.all_reduce(rhs, group=group)
+            call("ofx_gn_step", self._h, it, ptr(A), ptr(rhs), stream_ptr())
+        r, out = self._result(N)
+        call("ofx_gn_finish", self._h, byref(r), stream_ptr())
+        return self._pack(out, sync)
+
+
+class Registration:
+    """registration_fusion.py:37-397 API with the Gauss-Newton solver (DeformNet.optimize formulation)."""
+
+    def __init__(self, canonical_vertices, graph, warpfield, K, vis=None, max_matches=MAX_MATCHES_EVAL, seed=0,
+                 **gn_params):
+        self.graph = graph
+        self.warpfield = warpfield
+        self.intrinsics = np.asarray(K, np.float64)
+        self.vis = vis
+        self.device = warpfield.device
+        self.max_matches = max_matches
+        self.rng = np.random.default_rng(seed)
+        self.solver = GaussNewtonSolver(graph.nodes.shape[0], max_matches, self.device, **gn_params)
+        self.prev_rot = None
+        self.prev_trans = None
+        self.update(canonical_vertices)
+
+    def update(self, canonical_vertices):
+        """registration_fusion.py:66-85: skin the canonical vertices, keep the valid ones."""
+        a, w, v = self.warpfield.skin_device(canonical_vertices)
+        self.valid_source_verts = v.cpu().numpy()
+        vt = torch.as_tensor(np.ascontiguousarray(canonical_vertices, np.float32), device=self.device)
+        self.source_pcd = vt[v]
+        self.point_anchors = a[v]
+        self.anchor_weight = w[v]
+
+    def _intr4(self):
+        K = self.intrinsics
+        return (K[0, 0], K[1, 1], K[0, 2], K[1, 2]) if K.shape == (3, 3) else tuple(K.reshape(-1)[:4])
+
+    def optimize(self, optical_flow_data, scene_flow_data, complete_node_motion_data, target_frame_data,
+                 landmarks=None):
+        tm = np.asarray(scene_flow_data["target_matches"], np.float32)[self.valid_source_verts]
+        vv = np.asarray(scene_flow_data["valid_verts"], bool)
+        sel = np.nonzero(vv[: self.source_pcd.shape[0]])[0]
+        if sel.size > self.max_matches:           # model.py:319-334 (reference: unseeded randperm)
+            sel = np.sort(self.rng.choice(sel, self.max_matches, replace=False))
+        idx = torch.as_tensor(sel, device=self.device, dtype=torch.int64)
+        tloc, tconf = complete_node_motion_data if complete_node_motion_data is not None else (None, None)
+        out = self.solver.optimize(self.graph.nodes, self.graph.edges, self.graph.edges_weights, tloc, tconf,
+                                   self.source_pcd[idx], self.point_anchors[idx], self.anchor_weight[idx],
+                                   tm[sel], self._intr4(), prev_rot=self.prev_rot, prev_trans=self.prev_trans)
+        R, T = out["node_rotations"], out["node_translations"]
+        self.prev_rot, self.prev_trans = R.clone(), T.clone()
+        nodes_t = torch.as_tensor(self.graph.nodes, device=self.device)
+        self.warpfield.set_node_transforms(R, T)
+        warped = self.warpfield.deform_device(self.source_pcd, self.point_anchors, self.anchor_weight)
+        res = {"warped_verts": warped, "node_rotations": R.cpu().numpy(), "node_translations": T.cpu(),
+               "deformed_nodes_to_target": nodes_t + T, "convergence_info": out["convergence_info"],
+               "valid_solve": out["valid_solve"],
+               "source_frame_id": optical_flow_data["source_id"], "target_frame_id": optical_flow_data["target_id"]}
+        return res

@@ -1,0 +1,213 @@
+"""Synthetic depth sequences and deformation graphs for benches and tests.
+
+Pinhole 640x480, fx=fy=525, cx=319.5, cy=239.5, centre-cropped to 640x448 as the reference frame
+loader does (cy -= 16; options.py:13-14, utils/image_proc.py:303-311). Depth in metres (f32),
+1 mm Gaussian noise, quantised to 1 mm. Scene: sphere R=0.35 m at (0,0,1.4) in front of a
+1.6x1.2 m backing plane at z=1.75 (the survey's 0.6x0.6 m plane is fully hidden by the sphere
+silhouette, so it is enlarged). Non-rigid motion: the sphere breathes (radius) and drifts (centre);
+the plane is static.
+
+Graphs: greedy coverage sampling of surface points (the rule of csrc sample_nodes,
+csrc/cpu/graph_proc.cpp:79-136, with a spatial hash instead of the O(N²) scan) and 8 Euclidean
+nearest-node edges (csrc compute_edges_euclidean semantics, graph_proc.cpp:302-356).
+"""
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Intrinsics:
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+    width: int
+    height: int
+
+    def as_vec(self):
+        return np.array([self.fx, self.fy, self.cx, self.cy], np.float64)
+
+
+def bench_camera(scale=1):
+    """640x480 -> 640x448 crop; scale=2 gives the 320x240 (-> 320x224) camera of config 1."""
+    return Intrinsics(525.0 / scale, 525.0 / scale, 319.5 / scale, (239.5 - 16) / scale, 640 // scale, 448 // scale)
+
+
+@dataclass
+class SphereScene:
+    center: tuple = (0.0, 0.0, 1.4)
+    radius: float = 0.35
+    plane_z: float = 1.75
+    plane_half: tuple = (0.8, 0.6)
+
+    def frame_params(self, t):
+        """Sphere centre/radius at frame t (smooth non-rigid drift + breathing)."""
+        c = np.array(self.center, np.float64)
+        c = c + np.array([0.01 * math.sin(0.3 * t), 0.008 * math.sin(0.2 * t + 1.0), 0.012 * math.sin(0.25 * t)])
+        r = self.radius * (1.0 + 0.03 * math.sin(0.35 * t))
+        return c, r
+
+    def deform_points(self, pts, t):
+        """Ground-truth motion of canonical (frame-0) surface points to frame t."""
+        pts = np.asarray(pts, np.float64)
+        c0, r0 = self.frame_params(0)
+        c, r = self.frame_params(t)
+        out = pts.copy()
+        on_sphere = pts[:, 2] < self.plane_z - 0.02
+        out[on_sphere] = c + (r / r0) * (pts[on_sphere] - c0)
+        return out
+
+    def render(self, cam, t=0, rng=None, noise=0.001):
+        H, W = cam.height, cam.width
+        u, v = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
+        dx = (u - cam.cx) / cam.fx
+        dy = (v - cam.cy) / cam.fy
+        c, r = self.frame_params(t)
+        # sphere: |z*(dx,dy,1) - c|^2 = r^2
+        a = dx * dx + dy * dy + 1.0
+        b = -2.0 * (dx * c[0] + dy * c[1] + c[2])
+        cc = c @ c - r * r
+        disc = b * b - 4 * a * cc
+        zs = np.where(disc >= 0, (-b - np.sqrt(np.maximum(disc, 0))) / (2 * a), np.inf)
+        zp = np.full_like(dx, self.plane_z)
+        inplane = (np.abs(dx * self.plane_z) <= self.plane_half[0]) & (np.abs(dy * self.plane_z) <= self.plane_half[1])
+        zp = np.where(inplane, zp, np.inf)
+        z = np.minimum(zs, zp)
+        if rng is not None and noise > 0:
+            z = z + rng.normal(0.0, noise, z.shape)
+        z = np.where(np.isfinite(z), np.round(z * 1000.0) / 1000.0, 0.0)
+        return z.astype(np.float32)
+
+
+def backproject(depth, cam):
+    """depth_2_pc (NonRigidICP/model/geometry.py:44-59) for valid pixels -> (P,3) f32."""
+    H, W = depth.shape
+    u, v = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
+    m = depth > 0
+    z = depth[m].astype(np.float64)
+    X = (u[m] - cam.cx) * z / cam.fx
+    Y = (v[m] - cam.cy) * z / cam.fy
+    return np.stack([X, Y, z], 1).astype(np.float32)
+
+
+def make_image(depth, rgb=None):
+    """(6,H,W) f32 image as the reference frame loader builds it: rgb in [0,1], then points (X,Y,Z)."""
+    H, W = depth.shape
+    if rgb is None:
+        yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing='ij')
+        rgb = np.stack([xx, yy, 0.5 * (xx + yy)]).astype(np.float32)
+    im = np.zeros((6, H, W), np.float32)
+    im[:3] = rgb
+    im[5] = depth
+    return im
+
+
+def sample_nodes(points, coverage, seed=0):
+    """Greedy coverage sampling (csrc sample_nodes rule: a point becomes a node iff no node lies
+    within `coverage`), visiting points in a seeded shuffled order, spatial-hash accelerated."""
+    pts = np.asarray(points, np.float32)
+    order = np.random.default_rng(seed).permutation(pts.shape[0])
+    cell = float(coverage)
+    c2 = float(coverage) ** 2
+    grid = {}
+    nodes = []
+    keys = np.floor(pts / cell).astype(np.int64)
+    for idx in order:
+        p = pts[idx]
+        k = keys[idx]
+        ok = True
+        for dx in (-1, 0, 1):
+            for dy in (-1, 0, 1):
+                for dz in (-1, 0, 1):
+                    for q in grid.get((k[0] + dx, k[1] + dy, k[2] + dz), ()):
+                        d = p - nodes[q]
+                        if float(d @ d) <= c2:
+                            ok = False
+                            break
+                    if not ok:
+                        break
+                if not ok:
+                    break
+            if not ok:
+                break
+        if ok:
+            grid.setdefault((k[0], k[1], k[2]), []).append(len(nodes))
+            nodes.append(p)
+    return np.array(nodes, np.float32).reshape(-1, 3)
+
+
+def euclidean_edges(nodes, k=8):
+    """k nearest other nodes (ascending distance), -1 padded; uniform edge weights 1/k."""
+    nodes = np.asarray(nodes, np.float32)
+    N = nodes.shape[0]
+    kk = min(k, N - 1)
+    edges = -np.ones((N, k), np.int32)
+    for s in range(0, N, 2048):
+        d = ((nodes[s:s + 2048, None, :] - nodes[None]) ** 2).sum(-1)
+        d[np.arange(d.shape[0]), np.arange(s, s + d.shape[0])] = np.inf
+        if kk > 0:
+            idx = np.argsort(d, axis=1, kind='stable')[:, :kk]
+            edges[s:s + d.shape[0], :kk] = idx
+    w = np.where(edges >= 0, 1.0 / k, 0.0).astype(np.float32)
+    return edges, w
+
+
+def coverage_for_nodes(points, target_nodes, seed=0, iters=8):
+    """Bisection on node coverage to hit ~target_nodes."""
+    lo, hi = 0.002, 0.5
+    sub = points[np.random.default_rng(seed).permutation(points.shape[0])[:60000]]
+    best = None
+    for _ in range(iters):
+        mid = math.sqrt(lo * hi)
+        n = sample_nodes(sub, mid, seed).shape[0]
+        best = mid
+        if n > target_nodes:
+            lo = mid
+        else:
+            hi = mid
+    return best
+
+
+@dataclass
+class SyntheticSequence:
+    """A seeded sequence: frames, canonical surface, graph and per-frame solver inputs."""
+    cam: Intrinsics
+    scene: SphereScene
+    nodes: np.ndarray
+    edges: np.ndarray
+    edge_weights: np.ndarray
+    node_coverage: float
+    canonical_points: np.ndarray
+    seed: int = 0
+
+    @staticmethod
+    def build(n_nodes=2000, cam=None, seed=3, coverage=None):
+        cam = cam or bench_camera()
+        scene = SphereScene()
+        d0 = scene.render(cam, 0, np.random.default_rng(seed))
+        pts = backproject(d0, cam)
+        cov = coverage if coverage is not None else coverage_for_nodes(pts, n_nodes, seed)
+        sub = pts[np.random.default_rng(seed).permutation(pts.shape[0])[:60000]]
+        nodes = sample_nodes(sub, cov, seed)
+        edges, ew = euclidean_edges(nodes, 8)
+        return SyntheticSequence(cam, scene, nodes, edges, ew, float(cov), pts, seed)
+
+    def frame(self, t):
+        rng = np.random.default_rng(self.seed * 1000 + t)
+        return make_image(self.scene.render(self.cam, t, rng))
+
+    def solver_inputs(self, t, n_matches=10000, occluded_conf=0.3):
+        """Matches (canonical surface point -> its position at frame t + 1 mm noise) and node motion
+        targets (ground-truth node motion, confidence 1 visible / occluded_conf otherwise)."""
+        rng = np.random.default_rng(self.seed * 7919 + t)
+        sel = rng.choice(self.canonical_points.shape[0], size=min(n_matches, self.canonical_points.shape[0]),
+                         replace=False)
+        src = self.canonical_points[np.sort(sel)]
+        tgt = self.scene.deform_points(src, t) + rng.normal(0, 0.001, src.shape)
+        tpos = self.scene.deform_points(self.nodes, t)
+        c, r = self.scene.frame_params(t)
+        facing = (self.nodes[:, 2] < c[2]) | (self.nodes[:, 2] > self.scene.plane_z - 0.02)
+        conf = np.where(facing, 1.0, occluded_conf).astype(np.float32)
+        return src.astype(np.float32), tgt.astype(np.float32), tpos.astype(np.float32), conf

@@ -1,0 +1,241 @@
+"""TSDFVolume — drop-in for fusion_with_occlusion/tsdf.py:TSDFVolume, backed by libofx (HIP, gfx950).
+
+Same constructor (bbox, max_depth, cam_intr, fopt, visualizer), same `integrate(image_data,
+obs_weight=1.)`, `update(im, frame_id)`, `get_volume() -> (tsdf, color, weight)`,
+`check_visibility(points) -> (valid, depth_diff)`, `get_visible_nodes()`, `save_volume/load_volume`,
+`clear()`. Volume state stays device-resident (8³ bricks); get_volume() copies D2H only on request.
+Only the CPU-mode semantics of the reference are implemented (round-half-even pixels, no ray factor:
+tsdf.py:442-494); its pycuda kernel (tsdf.py:192-288) computes different numbers and is not mirrored.
+"""
+import logging
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr, byref
+
+log = logging.getLogger(__name__)
+TRUNC_MARGIN = 0.04  # tsdf.py:127
+
+
+def _opt(fopt, name, default=None):
+    if fopt is None:
+        return default
+    if isinstance(fopt, dict):
+        return fopt.get(name, default)
+    return getattr(fopt, name, default)
+
+
+def volume_geometry(bbox, max_depth, cam_intr, voxel_dim=None, voxel_size=None):
+    """tsdf.py:55-129: frustum bounds of the bbox at max_depth -> (vol_bnds, vol_dim, voxel_size, origin f32)."""
+    fx, fy, cx, cy = (float(v) for v in cam_intr[:4])
+    w_min, h_min, w_max, h_max = bbox
+    md = np.array([0, max_depth, max_depth, max_depth, max_depth])
+    pts = np.array([(np.array([0, w_min, w_min, w_max, w_max]) - cx) * md / fx,
+                    (np.array([0, h_min, h_max, h_min, h_max]) - cy) * md / fy, md])
+    vol_bnds = np.asarray([np.min(pts, axis=1), np.max(pts, axis=1)]).T
+    if voxel_dim is not None:
+        vol_dim = np.array([voxel_dim] * 3) if isinstance(voxel_dim, (int, np.integer)) else np.asarray(voxel_dim)
+        assert vol_dim.shape[0] == 3, f"Voxel dimension should have length = 3 found {voxel_dim}"
+        vs = float(((vol_bnds[:, 1] - vol_bnds[:, 0]) / vol_dim).max())
+    elif voxel_size is not None:
+        vs = float(voxel_size)
+        vol_dim = np.ceil((vol_bnds[:, 1] - vol_bnds[:, 0]) / vs).astype(int)
+    else:
+        raise ValueError("fopt needs voxel_dim or voxel_size")
+    vol_bnds[:, 1] = vol_bnds[:, 0] + vol_dim * vs
+    return vol_bnds, vol_dim.astype(np.int64), vs, vol_bnds[:, 0].astype(np.float32)
+
+
+def shard_bricks(n_bricks_x, rank, world):
+    """Contiguous x-slab of bricks for `rank` of `world` (spatial volume sharding)."""
+    base, rem = divmod(n_bricks_x, world)
+    x0 = rank * base + min(rank, rem)
+    return x0, x0 + base + (1 if rank < rem else 0)
+
+
+class TSDFVolume:
+    """Volumetric TSDF fusion of RGB-D images (tsdf.py:37-876), MI355X-resident."""
+
+    def __init__(self, bbox, max_depth, cam_intr, fopt, visualizer=None, device=None, shard=None):
+        vd = _opt(fopt, "voxel_dim")
+        vs = _opt(fopt, "voxel_size")
+        vol_bnds, vol_dim, voxel_size, origin = volume_geometry(bbox, max_depth, cam_intr, vd, vs)
+        self._init(vol_bnds, vol_dim, voxel_size, origin, cam_intr, fopt, visualizer, device, shard)
+
+    @classmethod
+    def from_grid(cls, origin, voxel_size, vol_dim, cam_intr, fopt=None, visualizer=None, device=None, shard=None):
+        """Direct grid construction (benchmark configs): origin (3,), voxel size (m), dims (3,)."""
+        self = cls.__new__(cls)
+        origin = np.asarray(origin, np.float32)
+        vol_dim = np.asarray(vol_dim, np.int64).reshape(3)
+        vol_bnds = np.stack([origin.astype(np.float64), origin.astype(np.float64) + vol_dim * float(voxel_size)], 1)
+        self._init(vol_bnds, vol_dim, float(voxel_size), origin, cam_intr, fopt, visualizer, device, shard)
+        return self
+
+    def _init(self, vol_bnds, vol_dim, voxel_size, origin, cam_intr, fopt, visualizer, device, shard):
+        self.fopt = fopt if fopt is not None else SimpleNamespace(source_frame=0, skip_rate=1)
+        self.vis = visualizer
+        self.cam_intr = np.eye(3)
+        self.cam_intr[0, 0], self.cam_intr[1, 1], self.cam_intr[0, 2], self.cam_intr[1, 2] = (float(v) for v in cam_intr[:4])
+        self._vol_bnds = vol_bnds
+        self._vol_dim = np.asarray(vol_dim, np.int64)
+        self._voxel_size = voxel_size
+        self._vol_origin = np.asarray(origin, np.float32)
+        self._trunc_margin = TRUNC_MARGIN
+        self._color_const = 256 * 256
+        self.gpu_mode = True
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        nbx = int((self._vol_dim[0] + 7) // 8)
+        rank, world = shard if shard is not None else (0, 1)
+        self.shard = (rank, world)
+        self.brick_x0, self.brick_x1 = shard_bricks(nbx, rank, world)
+        self.desc = _lib.VolumeDesc()
+        self.desc.dim[:] = [int(d) for d in self._vol_dim]
+        self.desc.brick_x0, self.desc.brick_x1 = self.brick_x0, self.brick_x1
+        self.desc.origin[:] = [float(o) for o in self._vol_origin]
+        self.desc.voxel_size = float(self._voxel_size)
+        self.desc.trunc_margin = float(self._trunc_margin)
+        n = _lib.c_int64()
+        call("ofx_volume_num_slots", byref(self.desc), byref(n))
+        self.n_slots = int(n.value)
+        self.n_bricks = self.n_slots // 512
+        self.x_lo = self.brick_x0 * 8
+        self.x_hi = min(self.brick_x1 * 8, int(self._vol_dim[0]))
+        kw = dict(dtype=torch.float32, device=self.device)
+        self.tsdf_b = torch.empty(self.n_slots, **kw)
+        self.weight_b = torch.empty(self.n_slots, **kw)
+        self.color_b = torch.empty(self.n_slots, **kw)
+        self.n_updated = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.with_color = True
+        call("ofx_volume_reset", byref(self.desc), ptr(self.tsdf_b), ptr(self.weight_b), ptr(self.color_b), stream_ptr())
+        self.warpfield = None
+        self._world_pts = None
+        self.log = log
+
+    # ------------------------------------------------------------------ frame input
+    def camera(self):
+        c = _lib.Camera()
+        c.fx, c.fy = float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1])
+        c.cx, c.cy = float(self.cam_intr[0, 2]), float(self.cam_intr[1, 2])
+        c.height, c.width = int(self.depth_t.shape[0]), int(self.depth_t.shape[1])
+        return c
+
+    def update(self, im, frame_id):
+        """tsdf.py:545-572: unpack the (6,H,W) frame; depth = im[-1]; colour folded on device."""
+        im_t = im if isinstance(im, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(im, dtype=np.float32))
+        im_t = im_t.to(self.device, torch.float32, non_blocking=True)
+        assert im_t.dim() == 3 and im_t.shape[0] >= 4, f"Input not correct: expected (6,H,W), got {tuple(im_t.shape)}"
+        self.im = im
+        self.depth_t = im_t[-1].contiguous()
+        H, W = self.depth_t.shape
+        self.color_t = torch.empty((H, W), dtype=torch.float32, device=self.device)
+        rgb = im_t[:3].contiguous()
+        call("ofx_pack_color", ptr(rgb), H, W, ptr(self.color_t), stream_ptr())
+        if hasattr(self, "frame_id"):
+            skip = _opt(self.fopt, "skip_rate", 1)
+            assert self.frame_id + skip == frame_id, \
+                f"Updating image data failed. Previous frame:{self.frame_id}, current frame:{frame_id} not integrated."
+        self.frame_id = frame_id
+
+    @property
+    def depth_im(self):
+        return self.depth_t.cpu().numpy()
+
+    @property
+    def color_im(self):
+        return self.color_t.cpu().numpy()
+
+    # ------------------------------------------------------------------ integrate
+    def integrate(self, image_data, obs_weight=1.):
+        """tsdf.py:378-494: warp (non-source frames) + integrate, fused on device."""
+        self.update(image_data["im"], image_data["id"])
+        self.integrate_device(obs_weight)
+
+    def integrate_device(self, obs_weight=1., count_updates=False):
+        """Integrate the current (already updated) frame; no host synchronisation."""
+        src = _opt(self.fopt, "source_frame", 0)
+        cam = self.camera()
+        cptr = ptr(self.color_b) if self.with_color else None
+        ciptr = ptr(self.color_t) if self.with_color else None
+        nu = ptr(self.n_updated) if count_updates else None
+        if self.frame_id == src:
+            call("ofx_integrate", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, 0, None, 0, 1, None, 0,
+                 None, None, float(obs_weight), ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu, stream_ptr())
+        else:
+            if self.warpfield is None:
+                raise RuntimeError("non-source frame integrate needs tsdf.warpfield (WarpField) to be set")
+            cache = self.warpfield.skin_tsdf_cache()
+            nodes = self.warpfield.packed_nodes()
+            call("ofx_integrate", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, 1, ptr(nodes),
+                 self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
+                 ptr(cache.weights), float(obs_weight), ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu, stream_ptr())
+
+    # ------------------------------------------------------------------ readback
+    def _dense(self, t):
+        Dy, Dz = int(self._vol_dim[1]), int(self._vol_dim[2])
+        out = torch.empty((self.x_hi - self.x_lo, Dy, Dz), dtype=torch.float32, device=self.device)
+        call("ofx_volume_to_dense", byref(self.desc), ptr(t), ptr(out), stream_ptr())
+        return out
+
+    def get_volume_device(self):
+        """(tsdf, color, weight) C-order device tensors of this shard (x-slab [x_lo, x_hi))."""
+        return self._dense(self.tsdf_b), self._dense(self.color_b), self._dense(self.weight_b)
+
+    def get_volume(self):
+        """tsdf.py:673-680: (tsdf, color, weight) numpy f32 (Dx_shard, Dy, Dz)."""
+        return tuple(t.cpu().numpy() for t in self.get_volume_device())
+
+    def save_volume(self, datapath):
+        """Stacked (3,Dx,Dy,Dz) [tsdf, color, weight] as tsdf.py:682-687 — written with np.save (no pickle)."""
+        data = np.stack(self.get_volume(), 0)
+        with open(datapath, "wb") as f:
+            np.save(f, data)
+
+    def load_volume(self, datapath):
+        data = np.load(datapath, allow_pickle=False)
+        for arr, dst in zip(data, (self.tsdf_b, self.color_b, self.weight_b)):
+            src = torch.from_numpy(np.ascontiguousarray(arr, np.float32)).to(self.device)
+            call("ofx_volume_from_dense", byref(self.desc), ptr(src), ptr(dst), stream_ptr())
+        torch.cuda.current_stream().synchronize()
+
+    # ------------------------------------------------------------------ geometry helpers
+    @property
+    def world_pts(self):
+        """vox2world over the C-order grid (tsdf.py:294-307,338-349), numpy (V_shard,3) f32."""
+        if self._world_pts is None:
+            o = self._vol_origin.astype(np.float64)
+            vs = np.float64(self._voxel_size)
+            axes = []
+            rng = [(self.x_lo, self.x_hi), (0, int(self._vol_dim[1])), (0, int(self._vol_dim[2]))]
+            for j, (a, b) in enumerate(rng):
+                axes.append((o[j] + vs * np.arange(a, b, dtype=np.float32).astype(np.float64)).astype(np.float32))
+            g = np.stack(np.meshgrid(*axes, indexing="ij"), -1)
+            self._world_pts = g.reshape(-1, 3)
+        return self._world_pts
+
+    def check_visibility(self, points):
+        """tsdf.py:599-612 -> (valid bool (P,), depth_diff f64 (P,))."""
+        pts = torch.as_tensor(np.ascontiguousarray(points, np.float32), device=self.device)
+        P = pts.shape[0]
+        valid = torch.empty(P, dtype=torch.uint8, device=self.device)
+        dd = torch.empty(P, dtype=torch.float64, device=self.device)
+        cam = self.camera()
+        call("ofx_visibility", ptr(pts), P, byref(cam), ptr(self.depth_t), float(self._trunc_margin), ptr(valid),
+             ptr(dd), stream_ptr())
+        return valid.cpu().numpy().astype(bool), dd.cpu().numpy()
+
+    def get_visible_nodes(self):
+        """tsdf.py:614-638 (without the .npy side file)."""
+        assert self.warpfield.frame_id == self.frame_id
+        visible, _ = self.check_visibility(self.warpfield.get_deformed_nodes())
+        return visible
+
+    def clear(self):
+        """tsdf.py:857-876."""
+        for a in ("reduced_graph_dict", "deformed_model", "canonical_model"):
+            if hasattr(self, a):
+                delattr(self, a)

@@ -1,0 +1,209 @@
+"""WarpField + EDGraph — drop-ins for fusion_with_occlusion/warpfield.py and the state part of
+embedded_deformation_graph.py, backed by libofx.
+
+Transforms are kept node-relative on device (R_k, T_k with x' = R_k(x-g_k)+g_k+T_k, as
+Registration.deform_ED applies them, registration_fusion.py:157-184). The reference's origin-form
+`translations` (t = -R g + g + T, warpfield.py:407-408) are exposed as a derived property.
+"""
+import logging
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr, byref
+
+log = logging.getLogger(__name__)
+
+
+class EDGraph:
+    """Embedded-deformation graph state (embedded_deformation_graph.py:26-52,241-256): nodes (N,3) f32,
+    edges (N,8) i32 (-1 padded), edges_weights (N,8) f32, clusters (N,1) i32, generation parameters.
+    Construction from a mesh (csrc erode/sample/geodesic edges) is outside this hot path."""
+
+    def __init__(self, nodes, edges, edges_weights=None, clusters=None, node_coverage=0.05, graph_neighbours=8):
+        self.nodes = np.ascontiguousarray(nodes, np.float32)
+        self.edges = np.ascontiguousarray(edges, np.int32)
+        N = self.nodes.shape[0]
+        self.edges_weights = (np.ascontiguousarray(edges_weights, np.float32) if edges_weights is not None
+                              else np.where(self.edges >= 0, 1.0 / max(1, self.edges.shape[1]), 0).astype(np.float32))
+        self.clusters = (np.asarray(clusters, np.int32).reshape(N, 1) if clusters is not None
+                         else np.zeros((N, 1), np.int32))
+        self.num_nodes = N
+        self.graph_generation_parameters = {"node_coverage": float(node_coverage),
+                                            "graph_neighbours": int(graph_neighbours),
+                                            "max_triangle_distance": 0.05, "erosion_num_iterations": 10,
+                                            "erosion_min_neighbours": 4}
+
+
+@dataclass
+class SkinCache:
+    brick_list: torch.Tensor   # int32 [n_list] shard-local brick ids
+    n_list: int
+    anchors: torch.Tensor      # uint16 as int16 storage [n_list*512*4]
+    weights: torch.Tensor      # f32 [n_list*512*4]
+    k: int
+
+
+def _t(x, device, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x), device=device).to(dtype).contiguous()
+
+
+class WarpField:
+    """Warp field over an EDGraph and a TSDFVolume (warpfield.py:21-604)."""
+
+    def __init__(self, graph, tsdf, visualizer=None, kdtree_leaf_size=16):
+        self.graph = graph
+        self.tsdf = tsdf
+        self.vis = visualizer
+        self.device = tsdf.device
+        src = getattr(tsdf.fopt, "source_frame", 0) if not isinstance(tsdf.fopt, dict) else tsdf.fopt.get("source_frame", 0)
+        self.frame_id = src
+        self.log = log
+        self.updating_warpfield = False
+        self._set_graph(graph)
+        tsdf.warpfield = self
+
+    def _set_graph(self, graph):
+        N = graph.nodes.shape[0]
+        self.num_nodes = N
+        self.graph_neighbours = min(N, 4)                                   # warpfield.py:60
+        self.node_coverage = float(graph.graph_generation_parameters["node_coverage"])
+        self.nodes_t = _t(graph.nodes, self.device, torch.float32)
+        self.R_t = torch.eye(3, device=self.device).repeat(N, 1, 1).contiguous()
+        self.T_t = torch.zeros((N, 3), device=self.device)
+        self.deformed_nodes = graph.nodes.copy()
+        self._packed = None
+        self._cache = None
+
+    # ------------------------------------------------------------------ transforms
+    @property
+    def rotations(self):
+        return self.R_t.cpu().numpy()
+
+    @property
+    def translations(self):
+        """Origin form t = -R g + g + T (warpfield.py:407-408)."""
+        R, T, g = self.R_t.double(), self.T_t.double(), self.nodes_t.double()
+        return (-(R @ g.unsqueeze(-1)).squeeze(-1) + g + T).float().cpu().numpy()
+
+    def set_node_transforms(self, R, T):
+        """Node-relative rotations (N,3,3) and translations (N,3), device or host."""
+        self.R_t = _t(R, self.device, torch.float32).reshape(self.num_nodes, 3, 3)
+        self.T_t = _t(T, self.device, torch.float32).reshape(self.num_nodes, 3)
+        self._packed = None
+
+    def packed_nodes(self):
+        if self._packed is None:
+            self._packed = torch.empty((self.num_nodes, 16), dtype=torch.float32, device=self.device)
+            call("ofx_pack_nodes", ptr(self.R_t), ptr(self.T_t), ptr(self.nodes_t), self.num_nodes, ptr(self._packed),
+                 stream_ptr())
+        return self._packed
+
+    def update_transformations(self, nnrt_data):
+        """warpfield.py:389-420: adopt the solver's node-relative (R, T); deformed nodes; frame id."""
+        assert self.frame_id == self.tsdf.frame_id, \
+            f"Warpfield maps to:{self.frame_id}th frame but TSDF maps to:{self.tsdf.frame_id}th frame"
+        self.set_node_transforms(nnrt_data["node_rotations"], nnrt_data["node_translations"])
+        dn = nnrt_data["deformed_nodes_to_target"]
+        self.deformed_nodes = dn.detach().cpu().numpy() if isinstance(dn, torch.Tensor) else np.asarray(dn)
+        self.frame_id = nnrt_data["target_frame_id"]
+
+    def get_transformation_wrt_graph_node(self):
+        """warpfield.py:422-436 -> (rotations, node-relative translations)."""
+        return self.rotations, self.T_t.cpu().numpy()
+
+    def get_transformation_wrt_origin(self, rotations, translations):
+        """warpfield.py:438-449: translations + g - R g."""
+        N = rotations.shape[0]
+        g = self.graph.nodes[:N].astype(np.float64)
+        return rotations, translations + g - np.einsum("nij,nj->ni", rotations, g)
+
+    def get_deformed_nodes(self):
+        assert self.frame_id == self.tsdf.frame_id
+        return self.deformed_nodes
+
+    # ------------------------------------------------------------------ skinning
+    def skin_device(self, points, nodes=None):
+        """Device skinning -> (anchors int32 (P,K), weights f32 (P,K), valid bool (P,)) tensors."""
+        pts = _t(points, self.device, torch.float32).reshape(-1, 3)
+        nd = self.nodes_t if nodes is None else _t(nodes, self.device, torch.float32).reshape(-1, 3)
+        K = min(nd.shape[0], 4)
+        P = pts.shape[0]
+        anchors = torch.empty((P, K), dtype=torch.int32, device=self.device)
+        weights = torch.empty((P, K), dtype=torch.float32, device=self.device)
+        valid = torch.empty(P, dtype=torch.uint8, device=self.device)
+        call("ofx_skin_points", ptr(pts), P, ptr(nd), nd.shape[0], self.node_coverage, K, ptr(anchors), ptr(weights),
+             ptr(valid), stream_ptr())
+        return anchors, weights, valid.bool()
+
+    def skin(self, points, nodes=None, ensure_num_neigbours=False):
+        """warpfield.py:83-129 (numpy in, numpy out)."""
+        a, w, v = self.skin_device(points, nodes)
+        return a.cpu().numpy(), w.cpu().numpy(), v.cpu().numpy()
+
+    def skin_tsdf_cache(self):
+        """Bricked skin cache of the TSDF voxel grid (warpfield.py:131-141 cache semantics)."""
+        if self._cache is None or self.updating_warpfield:
+            t = self.tsdf
+            K = self.graph_neighbours
+            blist = torch.empty(max(1, t.n_bricks), dtype=torch.int32, device=self.device)
+            cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+            call("ofx_skin_volume_bricks", byref(t.desc), ptr(self.nodes_t), self.num_nodes, self.node_coverage, K,
+                 ptr(blist), ptr(cnt), stream_ptr())
+            n_list = int(cnt.item())
+            anchors = torch.empty(max(1, n_list) * 512 * 4, dtype=torch.int16, device=self.device)
+            weights = torch.empty(max(1, n_list) * 512 * 4, dtype=torch.float32, device=self.device)
+            call("ofx_skin_volume", byref(t.desc), ptr(self.nodes_t), self.num_nodes, self.node_coverage, K, ptr(blist),
+                 n_list, ptr(anchors), ptr(weights), stream_ptr())
+            self._cache = SkinCache(blist[:max(1, n_list)], n_list, anchors, weights, K)
+        return self._cache
+
+    def skin_tsdf(self):
+        """API parity: dense (V,K) anchors, weights and valid mask of the voxel grid (numpy)."""
+        c = self.skin_tsdf_cache()
+        t = self.tsdf
+        V = (t.x_hi - t.x_lo) * int(t._vol_dim[1]) * int(t._vol_dim[2])
+        a = torch.empty((V, c.k), dtype=torch.int32, device=self.device)
+        w = torch.empty((V, c.k), dtype=torch.float32, device=self.device)
+        v = torch.empty(V, dtype=torch.uint8, device=self.device)
+        call("ofx_skin_volume_to_dense", byref(t.desc), ptr(c.brick_list), c.n_list, ptr(c.anchors), ptr(c.weights),
+             c.k, ptr(a), ptr(w), ptr(v), stream_ptr())
+        return a.cpu().numpy(), w.cpu().numpy(), v.cpu().numpy().astype(bool)
+
+    # ------------------------------------------------------------------ deformation
+    def deform_device(self, points, anchors, weights, valid=None, normals=False):
+        pts = _t(points, self.device, torch.float32).reshape(-1, 3)
+        a = _t(anchors, self.device, torch.int32)
+        w = _t(weights, self.device, torch.float32)
+        v = None if valid is None else _t(valid, self.device, torch.uint8)
+        out = torch.empty_like(pts)
+        call("ofx_deform_points", ptr(pts), pts.shape[0], ptr(a), ptr(w), ptr(v), a.shape[1], ptr(self.packed_nodes()),
+             self.num_nodes, 1 if normals else 0, ptr(out), stream_ptr())
+        return out
+
+    def deform(self, points, anchors, weights, reshape_gpu_vol=None, valid_pts=None):
+        """warpfield.py:270-305 (use_pytorch=True branch -> deform_ED semantics)."""
+        return self.deform_device(points, anchors, weights, valid_pts).cpu().numpy()
+
+    def deform_normals(self, normals, anchors, weights, reshape_gpu_vol=None, valid_pts=None):
+        """warpfield.py:312-345."""
+        return self.deform_device(normals, anchors, weights, valid_pts, normals=True).cpu().numpy()
+
+    def deform_mesh(self, vertices, normals):
+        """warpfield.py:347-367."""
+        a, w, v = self.skin(vertices)
+        dv = self.deform(vertices, a, w, None, v)
+        dn = self.deform_normals(normals, a, w, None, v) if normals is not None else None
+        return dv, dn, a, w, v
+
+    def deform_tsdf(self):
+        """warpfield.py:369-380 -> (deformed world points (V,3), valid (V,)) — materialises the whole grid
+        on the host; the integrate path never calls this (it warps on the fly inside ofx_integrate)."""
+        assert self.frame_id == self.tsdf.frame_id
+        a, w, v = self.skin_tsdf()
+        pts = self.tsdf.world_pts
+        return self.deform(pts, a, w, None, v), v

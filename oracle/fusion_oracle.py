@@ -1,0 +1,528 @@
+"""numpy restatement of the reference fusion hot path — TEST INFRASTRUCTURE ONLY.
+
+Every function cites the reference lines it follows. dtype flow is reproduced
+deliberately (numba/numpy promotion rules of the reference):
+float32 where the reference stores float32, float64 where numba/numpy promote.
+
+Parity unpinned against reference *outputs* for integrate/warp (the reference
+Python cannot be imported in this container); pinned by closed-form KATs in
+tests/test_oracle_kat.py. Skinning k-NN is pinned against the compiled
+reference csrc (oracle/build_ref.py).
+"""
+import math
+
+import numpy as np
+
+F32 = np.float32
+F64 = np.float64
+TRUNC_MARGIN = 0.04          # tsdf.py:127 (fixed, independent of voxel size)
+COLOR_CONST = 256 * 256      # tsdf.py:90
+
+
+# ----------------------------------------------------------------------------
+# a1: volume geometry  (tsdf.py:55-59, 75-129)
+# ----------------------------------------------------------------------------
+def volume_geometry(bbox, max_depth, cam_intr, voxel_dim=None, voxel_size=None):
+    """Returns (vol_bnds (3,2) f64, vol_dim (3,) int, voxel_size float, origin (3,) f32, trunc).
+
+    bbox = (w_min, h_min, w_max, h_max); cam_intr = (fx, fy, cx, cy).
+    voxel_dim wins over voxel_size, as `hasattr(fopt,"voxel_dim")` is tested first (tsdf.py:95).
+    """
+    K = np.eye(3)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = cam_intr[0], cam_intr[1], cam_intr[2], cam_intr[3]
+    w_min, h_min, w_max, h_max = bbox
+    md = np.array([0, max_depth, max_depth, max_depth, max_depth])
+    view_frust_pts = np.array([
+        (np.array([0, w_min, w_min, w_max, w_max]) - K[0, 2]) * md / K[0, 0],
+        (np.array([0, h_min, h_max, h_min, h_max]) - K[1, 2]) * md / K[1, 1],
+        md,
+    ])
+    vol_bnds = np.asarray([np.min(view_frust_pts, axis=1), np.max(view_frust_pts, axis=1)]).T
+    if voxel_dim is not None:
+        if isinstance(voxel_dim, int):
+            vol_dim = np.array([voxel_dim] * 3)
+        else:
+            vol_dim = np.asarray(voxel_dim)
+        vs = ((vol_bnds[:, 1] - vol_bnds[:, 0]) / vol_dim).max()
+    elif voxel_size is not None:
+        vs = float(voxel_size)
+        vol_dim = np.ceil((vol_bnds[:, 1] - vol_bnds[:, 0]) / vs).copy(order='C').astype(int)
+    else:
+        raise ValueError("need voxel_dim or voxel_size")
+    vol_bnds[:, 1] = vol_bnds[:, 0] + vol_dim * vs
+    origin = vol_bnds[:, 0].copy(order='C').astype(F32)
+    return vol_bnds, vol_dim.astype(np.int64), float(vs), origin, TRUNC_MARGIN
+
+
+def world_points(origin, vol_dim, voxel_size):
+    """vox2world over the C-order meshgrid (tsdf.py:294-307, 338-349).
+
+    numba: f32 origin + (f64 voxel_size * f32 coord) computed in f64, stored f32.
+    """
+    Dx, Dy, Dz = (int(d) for d in vol_dim)
+    o = np.asarray(origin, F32).astype(F64)
+    vs = F64(voxel_size)
+    ax = [(o[j] + vs * np.arange(n, dtype=F32).astype(F64)).astype(F32) for j, n in enumerate((Dx, Dy, Dz))]
+    pts = np.empty((Dx, Dy, Dz, 3), F32)
+    pts[..., 0] = ax[0][:, None, None]
+    pts[..., 1] = ax[1][None, :, None]
+    pts[..., 2] = ax[2][None, None, :]
+    return pts.reshape(-1, 3)
+
+
+# ----------------------------------------------------------------------------
+# a2: frame unpack (tsdf.py:545-566)
+# ----------------------------------------------------------------------------
+def pack_color(im):
+    """im (6,H,W) f32 -> packed color (H,W) f32 = floor(b*65536 + g*256 + r) of 255*rgb."""
+    c = 255 * np.moveaxis(np.asarray(im)[:3], 0, -1).astype(F32)
+    return np.floor(c[..., 2] * COLOR_CONST + c[..., 1] * 256 + c[..., 0])
+
+
+def depth_of(im):
+    return np.asarray(im)[-1]
+
+
+# ----------------------------------------------------------------------------
+# a3: skinning (warpfield.py:83-129)
+# ----------------------------------------------------------------------------
+def exp_f32(x):
+    """Canonical f32 exp of the oracle: f64 exp rounded to f32.
+
+    The reference uses numpy's float32 SIMD exp (warpfield.py:114) whose last bit
+    is platform dependent; the oracle and the HIP kernel both use this
+    correctly-rounded form (documented deviation).
+    """
+    return np.exp(np.asarray(x, F32).astype(F64)).astype(F32)
+
+
+def knn_sqdist(points, nodes, k, chunk=1 << 14):
+    """Exact k nearest nodes by f32 squared distance ((dx²+dy²)+dz², pykdtree calc_dist order),
+    ties broken by lower node index. Returns (sqdist (P,k) f32, idx (P,k) int64)."""
+    points = np.asarray(points, F32)
+    nodes = np.asarray(nodes, F32)
+    P = points.shape[0]
+    out_d = np.empty((P, k), F32)
+    out_i = np.empty((P, k), np.int64)
+    for s in range(0, P, chunk):
+        p = points[s:s + chunk]
+        dx = p[:, None, 0] - nodes[None, :, 0]
+        dy = p[:, None, 1] - nodes[None, :, 1]
+        dz = p[:, None, 2] - nodes[None, :, 2]
+        d2 = (dx * dx + dy * dy) + dz * dz                      # f32, no FMA
+        if k < nodes.shape[0]:
+            part = np.argpartition(d2, k - 1, axis=1)[:, :k]
+            cand_d = np.take_along_axis(d2, part, axis=1)
+            o = np.lexsort((part, cand_d), axis=-1)              # order by (d2, idx)
+            sel = np.take_along_axis(part, o, axis=1)
+            kth = np.take_along_axis(d2, sel[:, -1:], axis=1)
+            tie = (d2 <= kth).sum(axis=1) > k                    # tie straddles the k-th slot
+            for r in np.nonzero(tie)[0]:
+                sel[r] = np.argsort(d2[r], kind='stable')[:k]
+        else:
+            sel = np.argsort(d2, axis=1, kind='stable')
+        out_i[s:s + chunk] = sel
+        out_d[s:s + chunk] = np.take_along_axis(d2, sel, axis=1)
+    return out_d, out_i
+
+
+def skin(points, nodes, node_coverage, k=None):
+    """WarpField.skin (warpfield.py:83-129). Returns (anchors i32 (P,K), weights f32 (P,K), valid bool (P,)).
+
+    K = min(N, 4) (warpfield.py:60). dist = sqrt(sqdist) in f32 (pykdtree), cut-off
+    `dist > 4*node_coverage` strict (:109), w = exp(-dist**2/(2σ²)) in f32 (:114),
+    valid = all K anchors >= 0 (:120), w /= (Σw + 1e-6) (:121).
+    """
+    nodes = np.asarray(nodes, F32)
+    K = min(nodes.shape[0], 4) if k is None else k
+    sq, idx = knn_sqdist(points, nodes, K)
+    dist = np.sqrt(sq)                                           # f32
+    dist[dist > F32(4 * node_coverage)] = np.inf
+    anchors = idx.astype(np.int32)
+    anchors[dist == np.inf] = -1
+    denom = F32(2.0 * (node_coverage ** 2))
+    weights = exp_f32(-(dist ** 2) / denom)
+    valid = np.sum(anchors >= 0, axis=-1) == K
+    wsum = weights[:, 0].copy()
+    for j in range(1, K):
+        wsum = wsum + weights[:, j]                              # ((w0+w1)+w2)+w3, f32
+    weights = weights / (wsum[:, None] + F32(1e-6))
+    return anchors, weights.astype(F32), valid
+
+
+# ----------------------------------------------------------------------------
+# a4: ED warp (geometry.py:9-25 via registration_fusion.py:157-184)
+# ----------------------------------------------------------------------------
+def ed_warp(points, anchors, weights, valid, node_R, node_T, nodes):
+    """y = Σ_k w_k (R_k (x - g_k) + g_k + t_k) in f32, per-op rounding, summed k=0..3 in order.
+
+    Invalid points keep x (deform_ED returns a copy of `points` with only valid rows replaced).
+    R is applied as a 3x3 matrix, row i = ((R_i0 d0 + R_i1 d1) + R_i2 d2).
+    """
+    x = np.asarray(points, F32)
+    out = x.copy()
+    v = np.asarray(valid, bool)
+    if not v.any():
+        return out
+    xv = x[v]
+    a = np.asarray(anchors)[v]
+    w = np.asarray(weights, F32)[v]
+    R = np.asarray(node_R, F32)
+    T = np.asarray(node_T, F32)
+    g = np.asarray(nodes, F32)
+    acc = None
+    for k in range(a.shape[1]):
+        ak = a[:, k]
+        gk, Rk, tk = g[ak], R[ak], T[ak]
+        d = xv - gk
+        r = np.stack([(Rk[:, i, 0] * d[:, 0] + Rk[:, i, 1] * d[:, 1]) + Rk[:, i, 2] * d[:, 2] for i in range(3)], 1)
+        y = ((r + gk) + tk) * w[:, k:k + 1]
+        acc = y if acc is None else acc + y
+    out[v] = acc
+    return out
+
+
+# ----------------------------------------------------------------------------
+# a7: CPU integrate (tsdf.py:378-494 with 329-376, 576-612)
+# ----------------------------------------------------------------------------
+def cam2pix(cam_pts_f64, intr):
+    """tsdf.py:351-364: (x*fx)/z + cx in f64 with f32 intrinsics, np.round (half-even), int().
+    Returns float64 rounded pixel coordinates (int() of them is taken by the caller's range test)."""
+    fx, fy, cx, cy = (F64(F32(v)) for v in intr)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        px = np.rint((cam_pts_f64[:, 0] * fx) / cam_pts_f64[:, 2] + cx)
+        py = np.rint((cam_pts_f64[:, 1] * fy) / cam_pts_f64[:, 2] + cy)
+    return px, py
+
+
+def check_visibility(cam_pts_f64, depth_im, intr, trunc=TRUNC_MARGIN):
+    """tsdf.py:576-612. Returns (valid_pts, depth_diff f64, px int64, py int64)."""
+    H, W = depth_im.shape
+    px, py = cam2pix(cam_pts_f64, intr)
+    z = cam_pts_f64[:, 2]
+    valid_pix = (px >= 0) & (px < W) & (py >= 0) & (py < H) & (z > 0)
+    pxi = np.where(valid_pix, px, 0).astype(np.int64)
+    pyi = np.where(valid_pix, py, 0).astype(np.int64)
+    depth_val = np.zeros(px.shape, F64)
+    depth_val[valid_pix] = depth_im[pyi[valid_pix], pxi[valid_pix]]
+    depth_diff = depth_val - z
+    valid_pts = (depth_val > 0) & (depth_diff >= -trunc)
+    return valid_pts, depth_diff, pxi, pyi
+
+
+def integrate(tsdf, weight, color, pts, valid_points, depth_im, color_im, intr,
+              obs_weight=1.0, trunc=TRUNC_MARGIN, with_color=True):
+    """In-place CPU integrate over flat f32 volumes (V,). Returns number of updated voxels.
+
+    pts (V,3) f32 (world or warped), valid_points (V,) bool.
+    """
+    cam = np.asarray(pts, F32).astype(F64)                    # rigid_transform(inv(I)) -> exact f64
+    valid_pts, depth_diff, pxi, pyi = check_visibility(cam, np.asarray(depth_im, F32), intr, trunc)
+    valid_pts &= np.asarray(valid_points, bool)
+    dist = np.minimum(1, depth_diff / trunc)
+    idx = np.nonzero(valid_pts)[0]
+    w_old = weight[idx]
+    tsdf_vals = tsdf[idx]
+    vd = dist[idx]
+    ow = F64(obs_weight)
+    w_new = (w_old.astype(F64) + ow).astype(F32)
+    prod = (w_old * tsdf_vals).astype(F32)                    # numba f32*f32 -> f32
+    tsdf_new = ((prod.astype(F64) + ow * vd) / w_new.astype(F64)).astype(F32)
+    weight[idx] = w_new
+    tsdf[idx] = tsdf_new
+    if with_color:
+        old_color = color[idx]
+        old_b = np.floor(old_color / F32(COLOR_CONST))
+        old_g = np.floor((old_color - old_b * F32(COLOR_CONST)) / F32(256))
+        old_r = old_color - old_b * F32(COLOR_CONST) - old_g * F32(256)
+        new_color = np.asarray(color_im, F32)[pyi[idx], pxi[idx]]
+        new_b = np.floor(new_color / F32(COLOR_CONST))
+        new_g = np.floor((new_color - new_b * F32(COLOR_CONST)) / F32(256))
+        new_r = new_color - new_b * F32(COLOR_CONST) - new_g * F32(256)
+        owf = F32(obs_weight)
+        nb = np.minimum(F32(255.), np.rint((w_old * old_b + owf * new_b) / w_new))
+        ng = np.minimum(F32(255.), np.rint((w_old * old_g + owf * new_g) / w_new))
+        nr = np.minimum(F32(255.), np.rint((w_old * old_r + owf * new_r) / w_new))
+        color[idx] = nb * F32(COLOR_CONST) + ng * F32(256) + nr
+    return int(idx.size)
+
+
+# ----------------------------------------------------------------------------
+# a9: transform conventions (warpfield.py:389-449)
+# ----------------------------------------------------------------------------
+def to_origin_form(R, T, nodes):
+    """t_origin = -R g + g + T (warpfield.py:407-408)."""
+    return -np.einsum('nij,nj->ni', R, nodes) + nodes + T
+
+
+# ----------------------------------------------------------------------------
+# a10: Gauss-Newton (model/model.py:222-859), dense float64 restatement
+# ----------------------------------------------------------------------------
+def angle_axis_to_rotation_matrix(aa):
+    """kornia 0.7.0 angle_axis_to_rotation_matrix (called at model.py:744).
+
+    θ² > 1e-6: Rodrigues with axis = ω/(θ+1e-6); else first-order I + [ω]×.
+    """
+    aa = np.asarray(aa, F64)
+    theta2 = np.sum(aa * aa, axis=1)
+    theta = np.sqrt(theta2)
+    w = aa / (theta + 1e-6)[:, None]
+    wx, wy, wz = w[:, 0], w[:, 1], w[:, 2]
+    c, s = np.cos(theta), np.sin(theta)
+    oc = 1.0 - c
+    Rn = np.stack([
+        c + wx * wx * oc, wx * wy * oc - wz * s, wy * s + wx * wz * oc,
+        wz * s + wx * wy * oc, c + wy * wy * oc, -wx * s + wy * wz * oc,
+        -wy * s + wx * wz * oc, wx * s + wy * wz * oc, c + wz * wz * oc], 1).reshape(-1, 3, 3)
+    rx, ry, rz = aa[:, 0], aa[:, 1], aa[:, 2]
+    one = np.ones_like(rx)
+    Rt = np.stack([one, -rz, ry, rz, one, -rx, -ry, rx, one], 1).reshape(-1, 3, 3)
+    mask = (theta2 > 1e-6)[:, None, None]
+    return np.where(mask, Rn, Rt)
+
+
+def skew(v):
+    """vec_to_skew_mat @ v (model.py:133-144): [[0,-z,y],[z,0,-x],[-y,x,0]]."""
+    z = np.zeros(v.shape[0])
+    return np.stack([z, -v[:, 2], v[:, 1], v[:, 2], z, -v[:, 0], -v[:, 1], v[:, 0], z], 1).reshape(-1, 3, 3)
+
+
+GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5,
+                   lambda_motion=1.0, lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False)
+
+
+def gn_edges(graph_edges):
+    """Valid directed edges in (node, slot) order (model.py:356-364)."""
+    ge = np.asarray(graph_edges)
+    ii, kk = np.nonzero(ge >= 0)
+    return np.stack([ii, ge[ii, kk]], 1).astype(np.int64), (ii, kk)
+
+
+def gn_optimize(graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
+                source_points, anchors, weights, target_points, intrinsics,
+                target_px=None, target_py=None, prev_rot=None, prev_trans=None, **params):
+    """One DeformNet.optimize solve (model.py:222-859) for a single batch item, dense float64.
+
+    Reproduces: LM schedule (:418-419), data rows with the flow-rotation operator-precedence
+    quirk (:505-510), ARAP rows (:554-601), motion rows (:604-612), A = JᵀJ + λI, b = -Jᵀr
+    (:641-662), LU solve (:694-709), loss-based early stop (:726-732), R ← exp(x_rot)·R,
+    t += x_trans (:744-748). Returns dict(node_rotations, node_translations, valid_solve,
+    convergence_info).
+    """
+    p = dict(GN_DEFAULTS)
+    p.update(params)
+    from scipy.linalg import lu_factor, lu_solve
+    g = np.asarray(graph_nodes, F64)
+    N = g.shape[0]
+    src = np.asarray(source_points, F64)
+    M = src.shape[0]
+    anc = np.asarray(anchors, np.int64)
+    wts = np.asarray(weights, F64)
+    tgt = np.asarray(target_points, F64)
+    tpos = np.asarray(target_node_position, F64)
+    conf = np.asarray(node_confidence, F64).reshape(-1)
+    fx, fy, cx, cy = (float(v) for v in intrinsics)
+    tpx = np.zeros(M) if target_px is None else np.asarray(target_px, F64).reshape(-1)
+    tpy = np.zeros(M) if target_py is None else np.asarray(target_py, F64).reshape(-1)
+    edges, (ei, ek) = gn_edges(graph_edges)
+    E = edges.shape[0]
+    n_nb = np.asarray(graph_edges).shape[1]
+    ew = np.ones(E)
+    if p['use_edge_weighting']:
+        ew = float(n_nb) * np.asarray(graph_edges_weights, F64)[ei, ek]
+
+    lf, ld = math.sqrt(p['lambda_flow']), math.sqrt(p['lambda_depth'])
+    lm_, la = math.sqrt(p['lambda_motion']), math.sqrt(p['lambda_arap'])
+    lm_factor = p['lm_factor']
+    R = np.tile(np.eye(3), (N, 1, 1)) if prev_rot is None else np.asarray(prev_rot, F64).reshape(N, 3, 3).copy()
+    t = np.zeros((N, 3)) if prev_trans is None else np.asarray(prev_trans, F64).reshape(N, 3).copy()
+    conv = dict(total=[], data=[], arap=[], motion=[], errors=[])
+    ill_posed = False
+    rowsM = np.arange(M) * 3
+    res = None
+    for gn_i in range(p['num_iter']):
+        if gn_i % 3 == 2:
+            lm_factor /= 2
+        J = np.zeros((M * 3, N * 6))
+        defp = np.zeros((M, 3))
+        for k in range(4):
+            nk = anc[:, k]
+            rot = np.einsum('mij,mj->mi', R[nk], src - g[nk])
+            defp += wts[:, k:k + 1] * (rot + g[nk] + t[nk])
+        zinv = 1.0 / (defp[:, 2] + 1e-7)
+        fx_mul_x, fy_mul_y = fx * defp[:, 0], fy * defp[:, 1]
+        fx_div_z, fy_div_z = fx * zinv, fy * zinv
+        fx_mul_x_div_z, fy_mul_y_div_z = fx_mul_x * zinv, fy_mul_y * zinv
+        mfx = -fx_mul_x_div_z * zinv
+        mfy = -fy_mul_y_div_z * zinv
+        for k in range(4):
+            nk = anc[:, k]
+            wk = wts[:, k]
+            rot = np.einsum('mij,mj->mi', R[nk], src - g[nk])
+            S = -skew(wk[:, None] * rot)
+            ct = 3 * N + 3 * nk
+            J[rowsM, ct + 0] += lf * wk * fx_div_z
+            J[rowsM, ct + 2] += lf * wk * mfx
+            J[rowsM + 1, ct + 1] += lf * wk * fy_div_z
+            J[rowsM + 1, ct + 2] += lf * wk * mfy
+            J[rowsM, ct + 0] += ld * wk
+            J[rowsM + 1, ct + 1] += ld * wk
+            J[rowsM + 2, ct + 2] += ld * wk
+            cr = 3 * nk
+            for j in range(3):      # flow part with the reference's precedence quirk (model.py:505-510)
+                J[rowsM, cr + j] += lf * fx_div_z * S[:, 0, j] + mfx * S[:, 2, j]
+                J[rowsM + 1, cr + j] += lf * fy_div_z * S[:, 1, j] + mfy * S[:, 2, j]
+            for i in range(3):
+                for j in range(3):
+                    J[rowsM + i, cr + j] += ld * S[:, i, j]
+        rd = np.zeros(M * 3)
+        rd[rowsM] = lf * (fx_mul_x_div_z + cx - tpx)
+        rd[rowsM + 1] = lf * (fy_mul_y_div_z + cy - tpy)
+        rd[rowsM] += ld * (defp[:, 0] - tgt[:, 0])
+        rd[rowsM + 1] += ld * (defp[:, 1] - tgt[:, 1])
+        rd[rowsM + 2] += ld * (defp[:, 2] - tgt[:, 2])
+        blocks_J, blocks_r = [J], [rd]
+        ra = None
+        if E > 0:
+            Ja = np.zeros((E * 3, N * 6))
+            i0, i1 = edges[:, 0], edges[:, 1]
+            rowsE = np.arange(E) * 3
+            delta = np.einsum('eij,ej->ei', R[i0], g[i1] - g[i0])
+            ra = (la * ew[:, None] * (delta + g[i0] + t[i0] - (g[i1] + t[i1]))).reshape(-1)
+            for c in range(3):
+                Ja[rowsE + c, 3 * N + 3 * i0 + c] += la * ew
+                Ja[rowsE + c, 3 * N + 3 * i1 + c] += -la * ew
+            Sa = -la * ew[:, None, None] * skew(delta)
+            for i in range(3):
+                for j in range(3):
+                    Ja[rowsE + i, 3 * i0 + j] += Sa[:, i, j]
+            blocks_J.append(Ja)
+            blocks_r.append(ra)
+        Jm = np.zeros((N * 3, N * 6))
+        ids = np.arange(N)
+        for c in range(3):
+            Jm[ids * 3 + c, 3 * N + 3 * ids + c] += lm_ * conf
+        rm = (lm_ * conf[:, None] * (t + g - tpos)).reshape(-1)
+        blocks_J.append(Jm)
+        blocks_r.append(rm)
+        Jall = np.concatenate(blocks_J, 0)
+        res = np.concatenate(blocks_r, 0)
+        A = Jall.T @ Jall + np.eye(6 * N) * lm_factor
+        b = -(Jall.T @ res)
+        try:
+            x = lu_solve(lu_factor(A), b)
+        except Exception:
+            ill_posed = True
+            conv['errors'].append("Solver failed: Ill-posed system!")
+            break
+        if not np.all(np.isfinite(x)):
+            ill_posed = True
+            conv['errors'].append("Solver failed: Non-finite solution x!")
+            break
+        loss_total = float(np.linalg.norm(res))
+        if len(conv['total']):
+            if loss_total - conv['total'][-1] > p['stop_loss_diff']:
+                break
+            if loss_total == conv['total'][-1]:
+                break
+        conv['data'].append(float(np.linalg.norm(rd)))
+        conv['total'].append(loss_total)
+        R_inc = angle_axis_to_rotation_matrix(x[:3 * N].reshape(N, 3))
+        R = R_inc @ R
+        t = t + x[3 * N:].reshape(N, 3)
+        if ra is not None:
+            conv['arap'].append(float(np.linalg.norm(ra)))
+        conv['motion'].append(float(np.linalg.norm(rm)))
+    valid = (not ill_posed) and res is not None and bool(np.all(np.isfinite(res)))
+    if not valid:
+        R = np.tile(np.eye(3), (N, 1, 1))
+        t = np.zeros((N, 3))
+    conv['valid'] = int(valid)
+    return dict(node_rotations=R, node_translations=t, valid_solve=int(valid), convergence_info=conv)
+
+
+def gn_system(graph_nodes, graph_edges, target_node_position, node_confidence, source_points, anchors,
+              weights, target_points, intrinsics, R, t, lm_factor=1e-7, include_data=True, include_reg=True,
+              **params):
+    """A, b, ||res|| of one GN linearisation at (R, t) — dense, for block-level and sharding tests.
+    include_data / include_reg select the data rows / the ARAP+motion rows (a match shard's share)."""
+    out = {}
+    p = dict(GN_DEFAULTS)
+    p.update(params)
+    p['num_iter'] = 1
+    p['lm_factor'] = lm_factor
+    # reuse gn_optimize's assembly by a single-iteration call would update R,t; rebuild here instead
+    g = np.asarray(graph_nodes, F64)
+    N = g.shape[0]
+    src = np.asarray(source_points, F64)
+    M = src.shape[0]
+    anc = np.asarray(anchors, np.int64)
+    wts = np.asarray(weights, F64)
+    tgt = np.asarray(target_points, F64)
+    conf = np.asarray(node_confidence, F64).reshape(-1)
+    tpos = np.asarray(target_node_position, F64)
+    fx, fy, cx, cy = (float(v) for v in intrinsics)
+    R = np.asarray(R, F64)
+    t = np.asarray(t, F64)
+    ld, la, lmo = math.sqrt(p['lambda_depth']), math.sqrt(p['lambda_arap']), math.sqrt(p['lambda_motion'])
+    defp = np.zeros((M, 3))
+    for k in range(4):
+        nk = anc[:, k]
+        defp += wts[:, k:k + 1] * (np.einsum('mij,mj->mi', R[nk], src - g[nk]) + g[nk] + t[nk])
+    zinv = 1.0 / (defp[:, 2] + 1e-7)
+    mfx = -(fx * defp[:, 0] * zinv) * zinv
+    mfy = -(fy * defp[:, 1] * zinv) * zinv
+    rowsM = np.arange(M) * 3
+    J = np.zeros((M * 3, N * 6))
+    for k in range(4):
+        nk = anc[:, k]
+        wk = wts[:, k]
+        S = -skew(wk[:, None] * np.einsum('mij,mj->mi', R[nk], src - g[nk]))
+        for c in range(3):
+            J[rowsM + c, 3 * N + 3 * nk + c] += ld * wk
+        for j in range(3):
+            J[rowsM, 3 * nk + j] += mfx * S[:, 2, j]
+            J[rowsM + 1, 3 * nk + j] += mfy * S[:, 2, j]
+        for i in range(3):
+            for j in range(3):
+                J[rowsM + i, 3 * nk + j] += ld * S[:, i, j]
+    rd = (ld * (defp - tgt)).reshape(-1)
+    edges, _ = gn_edges(graph_edges)
+    E = edges.shape[0] if include_reg else 0
+    Js, rs = ([J], [rd]) if include_data else ([], [])
+    if E:
+        i0, i1 = edges[:, 0], edges[:, 1]
+        delta = np.einsum('eij,ej->ei', R[i0], g[i1] - g[i0])
+        rs.append((la * (delta + g[i0] + t[i0] - (g[i1] + t[i1]))).reshape(-1))
+        Ja = np.zeros((E * 3, N * 6))
+        rowsE = np.arange(E) * 3
+        for c in range(3):
+            Ja[rowsE + c, 3 * N + 3 * i0 + c] += la
+            Ja[rowsE + c, 3 * N + 3 * i1 + c] += -la
+        Sa = -la * skew(delta)
+        for i in range(3):
+            for j in range(3):
+                Ja[rowsE + i, 3 * i0 + j] += Sa[:, i, j]
+        Js.append(Ja)
+    if include_reg:
+        Jm = np.zeros((N * 3, N * 6))
+        ids = np.arange(N)
+        for c in range(3):
+            Jm[ids * 3 + c, 3 * N + 3 * ids + c] += lmo * conf
+        Js.append(Jm)
+        rs.append((lmo * conf[:, None] * (t + g - tpos)).reshape(-1))
+    if not Js:
+        Js, rs = [np.zeros((0, 6 * N))], [np.zeros(0)]
+    Jall = np.concatenate(Js, 0)
+    res = np.concatenate(rs, 0)
+    out['A'] = Jall.T @ Jall + np.eye(6 * N) * lm_factor
+    out['b'] = -(Jall.T @ res)
+    out['loss'] = float(np.linalg.norm(res))
+    out['loss2'] = float(res @ res)
+    return out
+
+
+def node_major_perm(N):
+    """Permutation from the reference's [rot(3N) | trans(3N)] unknown order to [node: rot3, trans3]."""
+    return np.concatenate([[3 * i, 3 * i + 1, 3 * i + 2, 3 * N + 3 * i, 3 * N + 3 * i + 1, 3 * N + 3 * i + 2]
+                           for i in range(N)])

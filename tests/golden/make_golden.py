@@ -1,0 +1,125 @@
+"""Generate the committed golden fixtures in tests/golden/ (run in the CPU build container).
+
+  skin_csrc.npz       — skinning k-NN vectors produced by the REFERENCE's own compiled C++
+                        (csrc compute_pixel_anchors_euclidean / sample_nodes / compute_edges_euclidean,
+                        built from /root/reference by oracle/build_ref.py) + the oracle's skin of the
+                        same points. Pins the oracle's k-NN to the reference.
+  integrate_small.npz — a 66x52x70 volume fused over a source frame and one ED-warped frame by the
+                        oracle restatement of tsdf.py/warpfield.py/geometry.py (inputs + expected
+                        tsdf/weight/colour + skin valid mask).
+  gn_small.npz        — one DeformNet.optimize solve (N≈100, M=600) by the dense f64 oracle.
+
+Usage: python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import fusion_oracle as fo  # noqa: E402
+from occlusionfusion_amd import synthetic as S  # noqa: E402
+
+
+def small_setup(seed=11):
+    cam = S.Intrinsics(525.0 / 4, 525.0 / 4, 319.5 / 4, (239.5 - 16) / 4, 160, 112)
+    scene = S.SphereScene()
+    rng = np.random.default_rng(seed)
+    d0 = scene.render(cam, 0, rng)
+    d1 = scene.render(cam, 1, rng)
+    pts = S.backproject(d0, cam)
+    nodes = S.sample_nodes(pts, 0.07, seed)
+    edges, ew = S.euclidean_edges(nodes, 8)
+    return cam, scene, d0, d1, pts, nodes, edges, ew
+
+
+def small_transforms(scene, nodes, t, seed):
+    rng = np.random.default_rng(seed)
+    N = nodes.shape[0]
+    aa = rng.normal(0, 0.02, (N, 3))
+    R = fo.angle_axis_to_rotation_matrix(aa).astype(np.float32)
+    T = (scene.deform_points(nodes, t) - nodes + rng.normal(0, 0.002, (N, 3))).astype(np.float32)
+    return R, T
+
+
+def make_skin_csrc():
+    from oracle.build_ref import build
+    m = build()
+    rng = np.random.default_rng(5)
+    surf = rng.normal(size=(4000, 3))
+    surf = 0.3 * surf / np.linalg.norm(surf, axis=1, keepdims=True) + np.array([0, 0, 1.4])
+    surf = surf.astype(np.float32)
+    npos = np.zeros((0, 3), np.float32)
+    nidx = np.zeros((0, 1), np.int32)
+    n = m.sample_nodes(surf, np.ones((surf.shape[0], 1), bool), npos, nidx, 0.05, False, False)
+    nodes = np.ascontiguousarray(npos[:n])
+    edges = m.compute_edges_euclidean(nodes, 8)
+    q = (surf[rng.choice(surf.shape[0], 3000)] + rng.normal(0, 0.05, (3000, 3))).astype(np.float32)
+    img = np.ascontiguousarray(q.T.reshape(3, 1, -1))
+    pa = np.zeros((0,), np.int32)
+    pw = np.zeros((0,), np.float32)
+    m.compute_pixel_anchors_euclidean(nodes, img, 0.05, pa, pw)
+    oa, ow, ov = fo.skin(q, nodes, 0.05)
+    np.savez_compressed(os.path.join(HERE, "skin_csrc.npz"), points=q, nodes=nodes, node_coverage=0.05,
+                        csrc_edges=edges, csrc_anchors=pa.reshape(-1, 4), csrc_weights=pw.reshape(-1, 4),
+                        oracle_anchors=oa, oracle_weights=ow, oracle_valid=ov)
+    print("skin_csrc:", nodes.shape[0], "nodes,", q.shape[0], "points")
+
+
+def make_integrate_small():
+    cam, scene, d0, d1, pts, nodes, edges, ew = small_setup()
+    origin = np.array([-0.40, -0.33, 0.95], np.float32)
+    vs = 0.012
+    dims = np.array([66, 52, 70])
+    intr = (cam.fx, cam.fy, cam.cx, cam.cy)
+    im0, im1 = S.make_image(d0), S.make_image(d1)
+    world = fo.world_points(origin, dims, vs)
+    V = world.shape[0]
+    tsdf = np.ones(V, np.float32)
+    weight = np.zeros(V, np.float32)
+    color = np.zeros(V, np.float32)
+    fo.integrate(tsdf, weight, color, world, np.ones(V, bool), fo.depth_of(im0), fo.pack_color(im0), intr)
+    t0, w0, c0 = tsdf.copy(), weight.copy(), color.copy()
+    cov = 0.07
+    anchors, weights, valid = fo.skin(world, nodes, cov)
+    R, T = small_transforms(scene, nodes, 1, 7)
+    warped = fo.ed_warp(world, anchors, weights, valid, R, T, nodes)
+    n1 = fo.integrate(tsdf, weight, color, warped, valid, fo.depth_of(im1), fo.pack_color(im1), intr)
+    np.savez_compressed(os.path.join(HERE, "integrate_small.npz"), origin=origin, voxel_size=vs, dims=dims,
+                        intr=np.array(intr), width=cam.width, height=cam.height, im0=im0, im1=im1, nodes=nodes,
+                        node_coverage=cov, R=R, T=T, tsdf0=t0, weight0=w0, color0=c0, tsdf1=tsdf, weight1=weight,
+                        color1=color, skin_valid=valid, n_updated1=n1)
+    print("integrate_small:", V, "voxels,", nodes.shape[0], "nodes,", int(valid.sum()), "skinned,", n1, "updated")
+
+
+def make_gn_small():
+    cam, scene, d0, d1, pts, nodes, edges, ew = small_setup(seed=13)
+    rng = np.random.default_rng(17)
+    sel = rng.choice(pts.shape[0], 900, replace=False)
+    src = pts[np.sort(sel)]
+    a, w, v = fo.skin(src, nodes, 0.07)
+    src, a, w = src[v][:600], a[v][:600], w[v][:600]
+    tgt = (scene.deform_points(src, 2) + rng.normal(0, 0.001, src.shape)).astype(np.float32)
+    tpos = scene.deform_points(nodes, 2).astype(np.float32)
+    conf = np.where(rng.uniform(size=nodes.shape[0]) < 0.7, 1.0, 0.3).astype(np.float32)
+    intr = np.array([cam.fx, cam.fy, cam.cx, cam.cy])
+    out = fo.gn_optimize(nodes, edges, ew, tpos, conf, src, a, w, tgt, intr)
+    ci = out["convergence_info"]
+    np.savez_compressed(os.path.join(HERE, "gn_small.npz"), nodes=nodes, edges=edges, edge_weights=ew, tpos=tpos,
+                        conf=conf, src=src, anchors=a, weights=w, tgt=tgt, intr=intr,
+                        R=out["node_rotations"], t=out["node_translations"], valid=out["valid_solve"],
+                        loss_total=np.array(ci["total"]))
+    print("gn_small:", nodes.shape[0], "nodes,", src.shape[0], "matches, loss", ci["total"][:3], "...")
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["skin", "integrate", "gn"]
+    if "skin" in which:
+        make_skin_csrc()
+    if "integrate" in which:
+        make_integrate_small()
+    if "gn" in which:
+        make_gn_small()

@@ -1,0 +1,229 @@
+"""GPU parity: libofx (HIP, gfx950) through the C ABI vs the oracle / golden fixtures.
+
+Bar: bit-exact for skin anchors/weights, warped positions, tsdf/weight/colour (the kernels replay
+the reference's f32/f64 rounding with -ffp-contract=off); GN node transforms within 1e-5 of the
+dense f64 LU oracle (north_star tolerance).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fusion_oracle as fo
+
+pytestmark = pytest.mark.gpu
+
+
+def _g(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+class _Opt:
+    source_frame = 0
+    skip_rate = 1
+
+
+def _small_volume(g, shard=None):
+    from occlusionfusion_amd import TSDFVolume
+    return TSDFVolume.from_grid(g["origin"], float(g["voxel_size"]), g["dims"], tuple(g["intr"]), _Opt(), shard=shard)
+
+
+def _graph(g):
+    from occlusionfusion_amd import EDGraph
+    from occlusionfusion_amd.synthetic import euclidean_edges
+    e, w = euclidean_edges(g["nodes"], 8)
+    return EDGraph(g["nodes"], e, w, node_coverage=float(g["node_coverage"]))
+
+
+def test_library_is_native(cuda):
+    from occlusionfusion_amd import _lib
+    assert _lib.lib.ofx_abi_version() == 1
+    assert os.path.exists(_lib.LIB_PATH)
+
+
+def test_skin_points_bitexact(cuda, golden_dir):
+    from occlusionfusion_amd import WarpField
+    g = _g(golden_dir, "skin_csrc.npz")
+    gi = _g(golden_dir, "integrate_small.npz")
+    vol = _small_volume(gi)
+    from occlusionfusion_amd import EDGraph
+    graph = EDGraph(g["nodes"], -np.ones((len(g["nodes"]), 8), np.int32), node_coverage=float(g["node_coverage"]))
+    wf = WarpField(graph, vol)
+    a, w, v = wf.skin(g["points"])
+    np.testing.assert_array_equal(a, g["oracle_anchors"])
+    np.testing.assert_array_equal(w, g["oracle_weights"])
+    np.testing.assert_array_equal(v, g["oracle_valid"])
+
+
+def test_skin_volume_matches_oracle(cuda, golden_dir):
+    from occlusionfusion_amd import WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    vol = _small_volume(g)
+    wf = WarpField(_graph(g), vol)
+    a, w, v = wf.skin_tsdf()
+    np.testing.assert_array_equal(v, g["skin_valid"])
+    world = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))
+    oa, ow, ov = fo.skin(world[v], g["nodes"], float(g["node_coverage"]))
+    np.testing.assert_array_equal(a[v], oa)
+    np.testing.assert_array_equal(w[v], ow)
+
+
+def test_integrate_source_and_warped_frames_bitexact(cuda, golden_dir):
+    from occlusionfusion_amd import WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    vol = _small_volume(g)
+    vol.integrate({"im": g["im0"], "id": 0})
+    t, c, w = vol.get_volume()
+    D = tuple(g["dims"])
+    np.testing.assert_array_equal(t, g["tsdf0"].reshape(D))
+    np.testing.assert_array_equal(w, g["weight0"].reshape(D))
+    np.testing.assert_array_equal(c, g["color0"].reshape(D))
+    wf = WarpField(_graph(g), vol)
+    wf.frame_id = 1
+    wf.set_node_transforms(g["R"], g["T"])
+    vol.integrate({"im": g["im1"], "id": 1})
+    t, c, w = vol.get_volume()
+    np.testing.assert_array_equal(t, g["tsdf1"].reshape(D))
+    np.testing.assert_array_equal(w, g["weight1"].reshape(D))
+    np.testing.assert_array_equal(c, g["color1"].reshape(D))
+
+
+def test_sharded_volume_equals_full(cuda, golden_dir):
+    """Spatial x-slab sharding (3 shards in one process) reproduces the full volume exactly."""
+    from occlusionfusion_amd import WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    parts = []
+    for r in range(3):
+        vol = _small_volume(g, shard=(r, 3))
+        vol.integrate({"im": g["im0"], "id": 0})
+        wf = WarpField(_graph(g), vol)
+        wf.frame_id = 1
+        wf.set_node_transforms(g["R"], g["T"])
+        vol.integrate({"im": g["im1"], "id": 1})
+        parts.append(vol.get_volume())
+    D = tuple(g["dims"])
+    for i, key in enumerate(("tsdf1", "color1", "weight1")):
+        full = np.concatenate([p[i] for p in parts], 0)
+        np.testing.assert_array_equal(full, g[key].reshape(D))
+
+
+def test_deform_points_and_visibility(cuda, golden_dir):
+    from occlusionfusion_amd import WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    vol = _small_volume(g)
+    wf = WarpField(_graph(g), vol)
+    wf.set_node_transforms(g["R"], g["T"])
+    rng = np.random.default_rng(0)
+    pts = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))[rng.choice(240240, 5000)]
+    a, w, v = wf.skin(pts)
+    out = wf.deform(pts, a, w, None, v)
+    np.testing.assert_array_equal(out, fo.ed_warp(pts, a, w, v, g["R"], g["T"], g["nodes"]))
+    vol.update(g["im0"], 0)
+    valid, dd = vol.check_visibility(out)
+    ov, odd, _, _ = fo.check_visibility(out.astype(np.float64), fo.depth_of(g["im0"]), tuple(g["intr"]))
+    np.testing.assert_array_equal(valid, ov)
+    np.testing.assert_array_equal(dd, odd)
+
+
+def test_volume_save_load_roundtrip(cuda, golden_dir, tmp_path):
+    g = _g(golden_dir, "integrate_small.npz")
+    vol = _small_volume(g)
+    vol.integrate({"im": g["im0"], "id": 0})
+    p = str(tmp_path / "vol.npy")
+    vol.save_volume(p)
+    vol2 = _small_volume(g)
+    vol2.load_volume(p)
+    for x, y in zip(vol.get_volume(), vol2.get_volume()):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_edge_cases_few_nodes_and_empty_skin(cuda, golden_dir):
+    """K = min(N,4) < 4 (3-node graph) and a warped frame whose graph skins no brick at all."""
+    from occlusionfusion_amd import EDGraph, WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    nodes3 = g["nodes"][:3]
+    vol = _small_volume(g)
+    vol.integrate({"im": g["im0"], "id": 0})
+    wf = WarpField(EDGraph(nodes3, -np.ones((3, 8), np.int32), node_coverage=0.07), vol)
+    a, w, v = wf.skin_tsdf()
+    world = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))
+    oa, ow, ov = fo.skin(world, nodes3, 0.07)
+    assert a.shape[1] == 3
+    np.testing.assert_array_equal(v, ov)
+    wf.frame_id = 1
+    vol.integrate({"im": g["im1"], "id": 1})
+    t, c, wt = vol.get_volume()
+    T = g["tsdf0"].copy()
+    W = g["weight0"].copy()
+    C = g["color0"].copy()
+    x = fo.ed_warp(world, oa, ow, ov, np.tile(np.eye(3, dtype=np.float32), (3, 1, 1)), np.zeros((3, 3), np.float32), nodes3)
+    fo.integrate(T, W, C, x, ov, fo.depth_of(g["im1"]), fo.pack_color(g["im1"]), tuple(g["intr"]))
+    np.testing.assert_array_equal(t.reshape(-1), T)
+    np.testing.assert_array_equal(wt.reshape(-1), W)
+    # far-away graph: nothing skinned, warped integrate is a no-op
+    vol2 = _small_volume(g)
+    vol2.integrate({"im": g["im0"], "id": 0})
+    wf2 = WarpField(EDGraph(g["nodes"] + 100.0, -np.ones((len(g["nodes"]), 8), np.int32), node_coverage=0.07), vol2)
+    assert wf2.skin_tsdf_cache().n_list == 0
+    wf2.frame_id = 1
+    vol2.integrate({"im": g["im1"], "id": 1})
+    np.testing.assert_array_equal(vol2.get_volume()[0].reshape(-1), g["tsdf0"])
+
+
+def _gn_inputs(g):
+    return (g["nodes"], g["edges"], g["edge_weights"], g["tpos"], g["conf"], g["src"], g["anchors"], g["weights"],
+            g["tgt"], g["intr"])
+
+
+def test_gn_matches_dense_oracle(cuda, golden_dir):
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    s = GaussNewtonSolver(len(g["nodes"]), 1000)
+    out = s.optimize(*_gn_inputs(g))
+    assert out["valid_solve"] == int(g["valid"])
+    np.testing.assert_allclose(out["node_rotations"].cpu().numpy(), g["R"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(out["node_translations"].cpu().numpy(), g["t"], atol=1e-5, rtol=0)
+    lt = np.array(out["convergence_info"]["total"])
+    assert len(lt) == len(g["loss_total"])
+    np.testing.assert_allclose(lt, g["loss_total"], rtol=1e-6)
+
+
+def test_gn_assembly_matches_dense_system(cuda, golden_dir):
+    """ofx_gn_linearize's block-sparse A, b equal the dense oracle JᵀJ, -Jᵀr (node-major order)."""
+    from occlusionfusion_amd import GaussNewtonSolver, _lib
+    from occlusionfusion_amd._lib import call, ptr, stream_ptr, byref
+    g = _g(golden_dir, "gn_small.npz")
+    N = len(g["nodes"])
+    s = GaussNewtonSolver(N, 1000)
+    pb, N, M = s._problem(*_gn_inputs(g), None, None, None, None)
+    prm = s._params()
+    nnz = _lib.c_int64()
+    call("ofx_gn_setup", s._h, byref(pb), byref(prm), byref(nnz), stream_ptr())
+    A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=cuda)
+    rhs = torch.empty(6 * N + 4, dtype=torch.float64, device=cuda)
+    call("ofx_gn_linearize", s._h, 0, 0, M, 1, ptr(A), ptr(rhs), stream_ptr())
+    torch.cuda.synchronize()
+    sysd = fo.gn_system(g["nodes"], g["edges"], g["tpos"], g["conf"], g["src"], g["anchors"], g["weights"], g["tgt"],
+                        g["intr"], np.tile(np.eye(3), (N, 1, 1)), np.zeros((N, 3)), lm_factor=0.0)
+    p = fo.node_major_perm(N)
+    Ad = sysd["A"][np.ix_(p, p)]
+    bd = sysd["b"][p]
+    # the BSR pattern is internal: compare the multiset of block values (+ zero padding blocks)
+    Ab = A.cpu().numpy().reshape(-1, 6, 6)
+    blocks_dense = Ad.reshape(N, 6, N, 6).transpose(0, 2, 1, 3)
+    nzmask = np.abs(blocks_dense).sum((2, 3)) > 0
+    assert Ab.shape[0] >= nzmask.sum()
+    np.testing.assert_allclose(np.sort(Ab.reshape(-1)), np.sort(np.concatenate(
+        [blocks_dense[nzmask].reshape(-1), np.zeros((Ab.shape[0] - nzmask.sum()) * 36)])), rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rhs.cpu().numpy()[:6 * N], bd, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rhs.cpu().numpy()[6 * N:6 * N + 3].sum(), sysd["loss2"], rtol=1e-9)
+
+
+def test_gn_repeatable(cuda, golden_dir):
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    s = GaussNewtonSolver(len(g["nodes"]), 1000)
+    a = s.optimize(*_gn_inputs(g))
+    b = s.optimize(*_gn_inputs(g))
+    np.testing.assert_allclose(a["node_translations"].cpu().numpy(), b["node_translations"].cpu().numpy(), atol=1e-9)

@@ -1,0 +1,221 @@
+"""CPU: the oracle restatement against the reference's golden vectors and closed-form known answers.
+
+Pins: skinning k-NN against the reference's compiled C++ (tests/golden/skin_csrc.npz, produced by
+csrc compute_pixel_anchors_euclidean built from /root/reference). Integrate / warp / GN: no
+reference outputs exist (reference Python not importable, no asserting reference tests) ->
+closed-form KATs here + regression of the committed fixtures.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import fusion_oracle as fo
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+# --------------------------------------------------------------------- skin vs reference csrc
+def test_skin_knn_matches_reference_csrc(golden_dir):
+    g = _load(golden_dir, "skin_csrc.npz")
+    d2, idx = fo.knn_sqdist(g["points"], g["nodes"], 4)
+    ca = g["csrc_anchors"]
+    valid = (ca >= 0).all(1)
+    assert valid.mean() > 0.99
+    same = (idx[valid] == ca[valid])
+    # csrc breaks exact distance ties the other way; any disagreement must be a tie
+    if not same.all():
+        nodes, pts = g["nodes"], g["points"][valid]
+        r, c = np.nonzero(~same)
+        dd = lambda j: ((pts[r] - nodes[j]) ** 2).sum(1)
+        assert np.allclose(dd(idx[valid][r, c]), dd(ca[valid][r, c]), rtol=0, atol=0)
+    assert same.mean() > 0.999
+
+
+def test_skin_weights_match_reference_csrc(golden_dir):
+    """csrc normalises by Σw (no 4σ cut-off, no +1e-6); rescale the oracle's weights the same way."""
+    g = _load(golden_dir, "skin_csrc.npz")
+    ov, ow = g["oracle_valid"], g["oracle_weights"].astype(np.float64)
+    cw = g["csrc_weights"].astype(np.float64)
+    rescaled = ow / ow.sum(1, keepdims=True)          # w/(S+1e-6) renormalised = w/S
+    np.testing.assert_allclose(rescaled[ov], cw[ov], rtol=2e-5, atol=1e-7)
+    assert (g["oracle_anchors"][ov] == g["csrc_anchors"][ov]).mean() > 0.999
+
+
+def test_skin_cutoff_and_normalisation():
+    nodes = np.array([[0, 0, 0], [0.1, 0, 0], [0, 0.1, 0], [0, 0, 0.1], [5, 5, 5]], np.float32)
+    pts = np.array([[0.01, 0.02, 0.03], [0.3, 0.3, 0.3], [4.9, 5, 5]], np.float32)
+    a, w, v = fo.skin(pts, nodes, 0.05)
+    assert v.tolist() == [True, False, False]
+    assert a[0].tolist()[0] == 0
+    assert (a[2][1:] == -1).all() and a[2][0] == 4        # only one node within 4σ=0.2
+    assert abs(w[0].sum() - 1.0) < 1e-5 and w[0].sum() < 1.0
+    assert w[2, 1:].sum() == 0
+
+
+def test_skin_k_less_than_4():
+    nodes = np.array([[0, 0, 0], [0.05, 0, 0]], np.float32)
+    a, w, v = fo.skin(np.zeros((1, 3), np.float32), nodes, 0.05)
+    assert a.shape == (1, 2) and v[0]
+
+
+# --------------------------------------------------------------------- integrate KATs
+def _plane_setup(D=1.0, W=64, H=48, f=60.0):
+    depth = np.full((H, W), D, np.float32)
+    intr = (f, f, (W - 1) / 2, (H - 1) / 2)
+    return depth, intr
+
+
+def test_integrate_fronto_parallel_plane_kat():
+    """Voxels on the optical axis in front of a plane at depth D: tsdf = min(1,(D-z)/0.04);
+    voxels deeper than D+trunc are untouched; weight counts observations."""
+    depth, intr = _plane_setup()
+    z = np.linspace(0.5, 1.2, 141).astype(np.float32)
+    pts = np.stack([np.zeros_like(z), np.zeros_like(z), z], 1)
+    V = len(z)
+    tsdf, weight, color = np.ones(V, np.float32), np.zeros(V, np.float32), np.zeros(V, np.float32)
+    cim = np.zeros_like(depth)
+    fo.integrate(tsdf, weight, color, pts, np.ones(V, bool), depth, cim, intr)
+    dd = 1.0 - z.astype(np.float64)
+    upd = dd >= -0.04
+    np.testing.assert_array_equal(weight, upd.astype(np.float32))
+    np.testing.assert_allclose(tsdf[upd], np.minimum(1.0, dd[upd] / 0.04), rtol=0, atol=1e-6)
+    assert (tsdf[~upd] == 1).all()
+    fo.integrate(tsdf, weight, color, pts, np.ones(V, bool), depth, cim, intr, obs_weight=3.0)
+    np.testing.assert_array_equal(weight[upd], 4.0)
+
+
+def test_cam2pix_round_half_even_and_negative_zero():
+    intr = (1.0, 1.0, 0.0, 0.0)
+    pts = np.array([[2.5, 0.5, 1.0], [3.5, -0.4, 1.0], [-0.5, 1.5, 1.0], [-0.6, 0, 1.0]], np.float64)
+    px, py = fo.cam2pix(pts, intr)
+    assert px.tolist() == [2.0, 4.0, -0.0, -1.0]
+    assert py.tolist()[:3] == [0.0, -0.0, 2.0]
+    depth = np.ones((4, 8), np.float32)
+    valid, _, pxi, pyi = fo.check_visibility(pts, depth, intr)
+    assert valid.tolist() == [True, True, True, False]   # -0.4 -> -0 -> int 0 is in bounds
+
+
+def test_color_running_average_kat():
+    depth, intr = _plane_setup()
+    pts = np.array([[0, 0, 0.99]], np.float32)
+    rgb = np.zeros((3,) + depth.shape, np.float32)
+    rgb[0], rgb[1], rgb[2] = 10 / 255, 20 / 255, 30 / 255
+    im = np.concatenate([rgb, np.zeros((2,) + depth.shape, np.float32), depth[None]], 0)
+    cim = fo.pack_color(im)
+    t, w, c = np.ones(1, np.float32), np.zeros(1, np.float32), np.zeros(1, np.float32)
+    fo.integrate(t, w, c, pts, np.ones(1, bool), depth, cim, intr)
+    b, g_, r = c[0] // 65536, (c[0] % 65536) // 256, c[0] % 256
+    assert (r, g_, b) == (10, 20, 30)
+    rgb2 = rgb * 0 + np.array([20, 40, 61], np.float32)[:, None, None] / 255
+    im2 = np.concatenate([rgb2, np.zeros((2,) + depth.shape, np.float32), depth[None]], 0)
+    fo.integrate(t, w, c, pts, np.ones(1, bool), depth, fo.pack_color(im2), intr)
+    b, g_, r = c[0] // 65536, (c[0] % 65536) // 256, c[0] % 256
+    assert (r, g_, b) == (15, 30, 46)    # (30+61)/2 = 45.5 -> half-even 46
+
+
+def test_ed_warp_identity_shrinks_by_weight_sum():
+    nodes = np.array([[0, 0, 0], [0.02, 0, 0], [0, 0.02, 0], [0, 0, 0.02]], np.float32)
+    x = np.array([[0.01, 0.01, 0.01]], np.float32)
+    a, w, v = fo.skin(x, nodes, 0.05)
+    R = np.tile(np.eye(3, dtype=np.float32), (4, 1, 1))
+    y = fo.ed_warp(x, a, w, v, R, np.zeros((4, 3), np.float32), nodes)
+    np.testing.assert_allclose(y, x * w.sum(), rtol=1e-6)
+    T = np.tile(np.array([[0.1, 0, 0]], np.float32), (4, 1))
+    y2 = fo.ed_warp(x, a, w, v, R, T, nodes)
+    np.testing.assert_allclose(y2 - y, [[0.1 * w.sum(), 0, 0]], rtol=1e-5)
+
+
+def test_world_points_and_geometry():
+    vb, dim, vs, origin, trunc = fo.volume_geometry((10, 20, 50, 60), 2.0, (100.0, 100.0, 32.0, 24.0), voxel_size=0.01)
+    assert trunc == 0.04
+    np.testing.assert_allclose(vb[:, 0], [min(0, (10 - 32) * 2 / 100), min(0, (20 - 24) * 2 / 100), 0])
+    assert (dim == np.ceil((np.array([(50 - 32) * 0.02, (60 - 24) * 0.02, 2.0]) - vb[:, 0]) / 0.01)).all()
+    vb2, dim2, vs2, _, _ = fo.volume_geometry((10, 20, 50, 60), 2.0, (100.0, 100.0, 32.0, 24.0), voxel_dim=64)
+    assert (dim2 == 64).all() and np.isclose(vs2, ((vb2[:, 1] - vb2[:, 0]) / 64).max())
+    wp = fo.world_points(origin, (3, 4, 5), vs)
+    assert wp.shape == (60, 3)
+    assert wp[1, 2] == np.float32(np.float64(origin[2]) + vs * 1.0)
+
+
+# --------------------------------------------------------------------- GN KATs
+def _grid_graph(n=4, s=0.05):
+    g = np.stack(np.meshgrid(np.arange(n), np.arange(n), indexing="ij"), -1).reshape(-1, 2) * s
+    nodes = np.concatenate([g, np.full((len(g), 1), 1.0)], 1).astype(np.float32)
+    from occlusionfusion_amd.synthetic import euclidean_edges
+    e, w = euclidean_edges(nodes, 8)
+    return nodes, e, w
+
+
+def test_gn_pure_translation_recovered():
+    nodes, edges, ew = _grid_graph()
+    rng = np.random.default_rng(0)
+    src = (nodes[rng.integers(0, len(nodes), 300)] + rng.normal(0, 0.01, (300, 3))).astype(np.float32)
+    a, w, v = fo.skin(src, nodes, 0.05)
+    d = np.array([0.01, -0.02, 0.005])
+    out = fo.gn_optimize(nodes, edges, ew, nodes + d, np.ones(len(nodes)), src[v], a[v], w[v], src[v] + d,
+                         (500, 500, 320, 240))
+    assert out["valid_solve"] == 1
+    # ED warp of src with recovered transforms reproduces the targets (weights sum slightly < 1)
+    R, t = out["node_rotations"], out["node_translations"]
+    assert np.abs(t - d).max() < 2e-3
+    assert np.allclose(R, np.eye(3), atol=5e-3)
+
+
+def test_kornia_angle_axis_matches_rodrigues():
+    from scipy.spatial.transform import Rotation
+    aa = np.random.default_rng(1).normal(0, 0.3, (50, 3))
+    R = fo.angle_axis_to_rotation_matrix(aa)
+    np.testing.assert_allclose(R, Rotation.from_rotvec(aa).as_matrix(), atol=5e-6)
+    small = np.array([[1e-4, -2e-4, 3e-4]])
+    Rs = fo.angle_axis_to_rotation_matrix(small)
+    np.testing.assert_array_equal(Rs[0], [[1, -3e-4, -2e-4], [3e-4, 1, -1e-4], [2e-4, 1e-4, 1]])
+
+
+def test_gn_system_block_structure():
+    """A is symmetric; the data block of node pair (i,j) is non-zero only if i,j co-anchor a match."""
+    nodes, edges, ew = _grid_graph()
+    rng = np.random.default_rng(2)
+    src = (nodes[rng.integers(0, len(nodes), 50)] + rng.normal(0, 0.01, (50, 3))).astype(np.float32)
+    a, w, v = fo.skin(src, nodes, 0.05)
+    N = len(nodes)
+    s = fo.gn_system(nodes, edges, nodes, np.zeros(N), src[v], a[v], w[v], src[v], (500, 500, 320, 240),
+                     np.tile(np.eye(3), (N, 1, 1)), np.zeros((N, 3)), lm_factor=0.0, include_reg=False)
+    A = s["A"]
+    assert np.allclose(A, A.T)
+    p = fo.node_major_perm(N)
+    B = A[np.ix_(p, p)].reshape(N, 6, N, 6).transpose(0, 2, 1, 3)
+    co = np.zeros((N, N), bool)
+    for row in a[v]:
+        co[np.ix_(row, row)] = True
+    nz = np.abs(B).sum((2, 3)) > 0
+    assert not (nz & ~co).any()
+
+
+# --------------------------------------------------------------------- oracle regression
+def test_oracle_reproduces_integrate_fixture(golden_dir):
+    g = _load(golden_dir, "integrate_small.npz")
+    world = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))
+    V = world.shape[0]
+    intr = tuple(g["intr"])
+    t, w, c = np.ones(V, np.float32), np.zeros(V, np.float32), np.zeros(V, np.float32)
+    fo.integrate(t, w, c, world, np.ones(V, bool), fo.depth_of(g["im0"]), fo.pack_color(g["im0"]), intr)
+    np.testing.assert_array_equal(t, g["tsdf0"])
+    a, ww, v = fo.skin(world, g["nodes"], float(g["node_coverage"]))
+    np.testing.assert_array_equal(v, g["skin_valid"])
+    x = fo.ed_warp(world, a, ww, v, g["R"], g["T"], g["nodes"])
+    fo.integrate(t, w, c, x, v, fo.depth_of(g["im1"]), fo.pack_color(g["im1"]), intr)
+    np.testing.assert_array_equal(t, g["tsdf1"])
+    np.testing.assert_array_equal(w, g["weight1"])
+    np.testing.assert_array_equal(c, g["color1"])
+
+
+@pytest.mark.slow
+def test_oracle_reproduces_gn_fixture(golden_dir):
+    g = _load(golden_dir, "gn_small.npz")
+    out = fo.gn_optimize(g["nodes"], g["edges"], g["edge_weights"], g["tpos"], g["conf"], g["src"], g["anchors"],
+                         g["weights"], g["tgt"], g["intr"])
+    np.testing.assert_allclose(out["node_rotations"], g["R"], atol=1e-9)
+    np.testing.assert_allclose(out["node_translations"], g["t"], atol=1e-9)

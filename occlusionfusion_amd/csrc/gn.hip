@@ -15,12 +15,17 @@
 //   early stop on loss increase > stop_diff or unchanged loss (model.py:726-732), then
 //   R ← exp([x_ω]) R (kornia 0.7 angle_axis_to_rotation_matrix), t += x_t (model.py:744-748).
 //
-// MI355X design: JᵀJ is stored as 6x6 f64 blocks in BSR over the node adjacency (diagonal, graph
-// edges, co-anchored node pairs) with a dense NxN slot map for O(1) scatter; one thread per
-// (match, anchor) builds its 3x6 Jacobian and scatters J_kᵀJ_l blocks with native f64 atomics.
-// PCG = 2 kernels per iteration (fused p-update+SpMV+dot, fused axpy+precondition+dots), each ending
-// in a last-workgroup reduction of per-workgroup partials in fixed order (deterministic scalars),
-// agent-scope release/acquire hand-off per CDNA4 G16.
+// MI355X design.
+//  * Every residual row-triple is a "term" (data: 4 anchored nodes, ARAP edge: 2, motion: 1) whose
+//    3x6 Jacobian blocks are written to a scratch array once per GN iteration (k_terms).
+//  * JᵀJ lives as 6x6 f64 blocks in BSR over the node adjacency (diagonal, edges, co-anchored
+//    pairs). Per solve, each block gets a sorted list of the (term, p, q) products that land on it,
+//    so assembly is a deterministic gather: one wave per block, lane = block entry (k_blocks); the
+//    rhs is the same per node entry (k_rhs). No atomics -> bitwise reproducible A and b.
+//  * PCG: 2 kernels per iteration (p-update fused into SpMV; axpy + block-Cholesky preconditioner
+//    + dots). Scalars never leave the device: each kernel writes per-workgroup partial sums and every
+//    workgroup of the NEXT kernel re-derives the same scalars from them in a fixed order (kernel
+//    boundaries give visibility; no fences, no tickets). The host only polls convergence in chunks.
 #include <math.h>
 #include <vector>
 
@@ -32,36 +37,73 @@ namespace ofx {
 struct Gn {
   int max_nodes = 0, max_matches = 0;
   int N = 0, M = 0, NB = 0;
+  int64_t T = 0;        // terms = M + N*NB + N
   ofx_gn_params prm{};
   float fx = 0, fy = 0, cx = 0, cy = 0;
   // problem (f64 device copies)
   double *nodes = nullptr, *tpos = nullptr, *conf = nullptr, *src = nullptr, *wts = nullptr, *tgt = nullptr,
          *tpx = nullptr, *tpy = nullptr, *ew = nullptr;
   int32_t *anc = nullptr, *edges = nullptr;
-  // pattern
+  // terms
+  int32_t* term_node = nullptr;  // T*4, -1 = unused entry
+  double* J = nullptr;           // T*4*18
+  double* res = nullptr;         // T*3
+  int64_t T_cap = 0;
+  // pattern + contribution lists
   int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;
+  int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr;
+  int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr;
   int64_t nnzb = 0, nnzb_cap = 0;
   // state
   double *R = nullptr, *t = nullptr;
   double *A_own = nullptr, *rhs_own = nullptr;
-  double *Dinv = nullptr, *x = nullptr, *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr, *q = nullptr;
-  double* part = nullptr;   // per-WG partials, 4 per WG
-  double* scal = nullptr;   // [alpha, beta, rz, bb, rr, pq, loss_prev, ...]
-  int32_t* flags = nullptr; // see F_* below
-  uint32_t* tickets = nullptr;
+  double *L = nullptr, *x = nullptr, *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr, *q = nullptr;
+  double *part_s = nullptr, *part_u = nullptr, *part_b = nullptr, *part_loss = nullptr;
+  int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;
+  double* scal = nullptr;
+  int32_t* flags = nullptr;
   double* loss_log = nullptr;
-  int32_t* host_flag = nullptr;  // pinned
+  int32_t* host_flags = nullptr;  // pinned
+  int last_pcg = 0;
   bool setup_done = false;
 };
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_COUNT = 8 };
-enum { S_ALPHA = 0, S_BETA = 1, S_RZ = 2, S_BB = 3, S_RR = 4, S_PQ = 5, S_LOSS_PREV = 6, S_COUNT = 8 };
-constexpr int kPcgBlock = 256;  // threads per WG in node-parallel PCG kernels (4 rows per WG in SpMV)
+enum { S_LOSS_PREV = 0, S_COUNT = 4 };
+constexpr int kBlk = 256;       // threads per WG
+constexpr int kRowsPerWG = 4;   // SpMV: one wave per block row
 
-// --------------------------------------------------------------------------------------------
-__device__ __forceinline__ void atomic_add_f64(double* p, double v) { unsafeAtomicAdd(p, v); }
+// ---------------------------------------------------------------------------- reductions
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double s[kBlk];
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < (unsigned)o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  double r = s[0];
+  __syncthreads();
+  return r;
+}
 
+// Sum of p[i*stride + off], i < n, in a fixed order; every thread of the WG gets the same bits.
+__device__ __forceinline__ double wg_sum_fixed(const double* __restrict__ p, int n, int stride, int off) {
+  __shared__ double s_res;
+  if (threadIdx.x < 64) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += 64) acc += p[(int64_t)i * stride + off];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (threadIdx.x == 0) s_res = acc;
+  }
+  __syncthreads();
+  double r = s_res;
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------------------- setup kernels
 __global__ void k_to_f64(const float* __restrict__ s, double* __restrict__ d, int64_t n) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) d[i] = s ? (double)s[i] : 0.0;
@@ -80,30 +122,34 @@ __global__ void k_init_state(const float* __restrict__ prev_R, const float* __re
   for (int c = 0; c < 3; ++c) t[3 * i + c] = prev_t ? (double)prev_t[3 * i + c] : 0.0;
 }
 
-// ---- pattern build ----
-__global__ void k_mark(int N, int M, int NB, const int32_t* __restrict__ anc, const int32_t* __restrict__ edges,
-                       int32_t* __restrict__ map) {
+// term t -> its (up to 4) nodes
+__global__ void k_term_nodes(Gn g) {
   int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int64_t n_match_pairs = (int64_t)M * 16;
-  int64_t n_edge = (int64_t)N * NB;
-  if (t < N) map[t * N + t] = 1;
-  if (t < n_match_pairs) {
-    int64_t m = t / 16;
-    int k = (t / 4) % 4, l = t % 4;
-    int a = anc[m * 4 + k], b = anc[m * 4 + l];
-    map[(int64_t)a * N + b] = 1;
+  if (t >= g.T) return;
+  int n[4] = {-1, -1, -1, -1};
+  if (t < g.M) {
+    for (int k = 0; k < 4; ++k) n[k] = g.anc[t * 4 + k];
+  } else if (t < g.M + (int64_t)g.N * g.NB) {
+    int64_t e = t - g.M;
+    int j = g.edges[e];
+    if (j >= 0) { n[0] = (int)(e / g.NB); n[1] = j; }
+  } else {
+    n[0] = (int)(t - g.M - (int64_t)g.N * g.NB);
   }
-  if (t < n_edge) {
-    int i = (int)(t / NB);
-    int j = edges[t];
-    if (j >= 0) {
-      map[(int64_t)i * N + j] = 1;
-      map[(int64_t)j * N + i] = 1;
-    }
+  for (int k = 0; k < 4; ++k) g.term_node[t * 4 + k] = n[k];
+}
+
+__global__ void k_mark(Gn g) {
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= g.T) return;
+  const int32_t* n = g.term_node + t * 4;
+  for (int p = 0; p < 4; ++p) {
+    if (n[p] < 0) continue;
+    for (int q = 0; q < 4; ++q)
+      if (n[q] >= 0) g.map[(int64_t)n[p] * g.N + n[q]] = 1;
   }
 }
 
-// per row: count marks (one WG per row)
 __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restrict__ map, int32_t* __restrict__ cnt) {
   __shared__ int s[256];
   int i = blockIdx.x;
@@ -118,25 +164,26 @@ __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restr
   if (threadIdx.x == 0) cnt[i] = s[0];
 }
 
-__global__ __launch_bounds__(1024) void k_scan_rows(int N, const int32_t* __restrict__ cnt, int32_t* __restrict__ row_ptr) {
+// exclusive scan of cnt[0..n) into off[0..n], single workgroup
+__global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restrict__ cnt, int32_t* __restrict__ off) {
   __shared__ int64_t part[1024];
-  int per = (N + blockDim.x - 1) / blockDim.x;
-  int s = threadIdx.x * per, e = min(N, s + per);
+  int64_t per = (n + blockDim.x - 1) / blockDim.x;
+  int64_t s = threadIdx.x * per, e = min(n, s + per);
   int64_t c = 0;
-  for (int i = s; i < e; ++i) c += cnt[i];
+  for (int64_t i = s; i < e; ++i) c += cnt[i];
   part[threadIdx.x] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t acc = 0;
     for (int i = 0; i < (int)blockDim.x; ++i) { int64_t v = part[i]; part[i] = acc; acc += v; }
-    row_ptr[N] = (int32_t)acc;
+    off[n] = (int32_t)acc;
   }
   __syncthreads();
   int64_t o = part[threadIdx.x];
-  for (int i = s; i < e; ++i) { row_ptr[i] = (int32_t)o; o += cnt[i]; }
+  for (int64_t i = s; i < e; ++i) { off[i] = (int32_t)o; o += cnt[i]; }
 }
 
-// per row: ordered assignment of slots (one WG per row, chunked block prefix)
+// ordered slot assignment per block row (one WG per row)
 __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__ map, const int32_t* __restrict__ row_ptr,
                                                     int32_t* __restrict__ col) {
   __shared__ int s[256];
@@ -149,7 +196,6 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
     int f = (j < N) ? (map[(int64_t)i * N + j] != 0) : 0;
     s[threadIdx.x] = f;
     __syncthreads();
-    // inclusive scan (Hillis-Steele)
     for (int o = 1; o < (int)blockDim.x; o <<= 1) {
       int v = (threadIdx.x >= (unsigned)o) ? s[threadIdx.x - o] : 0;
       __syncthreads();
@@ -171,32 +217,55 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
   }
 }
 
-// ---- assembly ----
-// add J_aᵀ J_b (J: 3x6 row-major) into block
-__device__ __forceinline__ void add_block(double* __restrict__ blk, const double* Ja, const double* Jb) {
-#pragma unroll
-  for (int c = 0; c < 6; ++c)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      double v = Ja[c] * Jb[j] + Ja[6 + c] * Jb[6 + j] + Ja[12 + c] * Jb[12 + j];
-      if (v != 0.0) atomic_add_f64(blk + c * 6 + j, v);
-    }
-}
-
-__device__ __forceinline__ void add_rhs(double* __restrict__ rhs6, const double* Ja, const double r[3]) {
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-    double v = Ja[c] * r[0] + Ja[6 + c] * r[1] + Ja[12 + c] * r[2];
-    if (v != 0.0) atomic_add_f64(rhs6 + c, -v);
+__global__ void k_pair_count(Gn g) {
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= g.T) return;
+  const int32_t* n = g.term_node + t * 4;
+  for (int p = 0; p < 4; ++p) {
+    if (n[p] < 0) continue;
+    atomicAdd(&g.node_cnt[n[p]], 1);
+    for (int q = 0; q < 4; ++q)
+      if (n[q] >= 0) atomicAdd(&g.blk_cnt[g.map[(int64_t)n[p] * g.N + n[q]]], 1);
   }
 }
 
+// scatter (order fixed later by k_seg_sort); blk_cnt/node_cnt are reused as cursors (zeroed first)
+__global__ void k_pair_scatter(Gn g) {
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= g.T) return;
+  const int32_t* n = g.term_node + t * 4;
+  for (int p = 0; p < 4; ++p) {
+    if (n[p] < 0) continue;
+    int pos = g.node_off[n[p]] + atomicAdd(&g.node_cnt[n[p]], 1);
+    g.node_list[pos] = (int32_t)(t * 4 + p);
+    for (int q = 0; q < 4; ++q) {
+      if (n[q] < 0) continue;
+      int s = g.map[(int64_t)n[p] * g.N + n[q]];
+      int pb = g.blk_off[s] + atomicAdd(&g.blk_cnt[s], 1);
+      g.blk_list[pb] = (int32_t)(t * 16 + p * 4 + q);
+    }
+  }
+}
+
+__global__ void k_seg_sort(const int32_t* __restrict__ off, int64_t nseg, int32_t* __restrict__ list) {
+  int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  int b = off[s], e = off[s + 1];
+  for (int i = b + 1; i < e; ++i) {
+    int v = list[i];
+    int j = i - 1;
+    while (j >= b && list[j] > v) { list[j + 1] = list[j]; --j; }
+    list[j + 1] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------- linearisation
 struct DataCoef {
-  double lf, ld, fx, fy, cx, cy;
+  double lf, ld, la, lm, fx, fy, cx, cy;
 };
 
 __device__ void data_jacobian(const Gn& g, const DataCoef& dc, int64_t m, int k, const double p[3], double zinv,
-                              double J[18]) {
+                              double* __restrict__ J) {
   int a = g.anc[m * 4 + k];
   double w = g.wts[m * 4 + k];
   const double* R = g.R + 9 * (int64_t)a;
@@ -206,10 +275,11 @@ __device__ void data_jacobian(const Gn& g, const DataCoef& dc, int64_t m, int k,
   double v1 = w * (R[3] * d0 + R[4] * d1 + R[5] * d2);
   double v2 = w * (R[6] * d0 + R[7] * d1 + R[8] * d2);
   // S = -[v]x
-  double S[9] = {0.0, v2, -v1, -v2, 0.0, v0, v1, -v0, 0.0};
+  const double S[9] = {0.0, v2, -v1, -v2, 0.0, v0, v1, -v0, 0.0};
   double fxdz = dc.fx * zinv, fydz = dc.fy * zinv;
   double mfx = -(dc.fx * p[0] * zinv) * zinv;
   double mfy = -(dc.fy * p[1] * zinv) * zinv;
+#pragma unroll
   for (int j = 0; j < 3; ++j) {
     J[0 + j] = dc.lf * fxdz * S[0 + j] + mfx * S[6 + j] + dc.ld * S[0 + j];
     J[6 + j] = dc.lf * fydz * S[3 + j] + mfy * S[6 + j] + dc.ld * S[3 + j];
@@ -235,192 +305,189 @@ __device__ void deformed_point(const Gn& g, int64_t m, double p[3]) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_data(Gn g, DataCoef dc, int m0, int m1, double* __restrict__ A,
-                                              double* __restrict__ rhs) {
-  int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int64_t m = m0 + tid / 4;
-  int k = (int)(tid % 4);
-  if (m >= m1) return;
-  double p[3];
-  deformed_point(g, m, p);
-  double zinv = 1.0 / (p[2] + 1e-7);
-  double r[3];
-  double tpx = g.tpx ? g.tpx[m] : 0.0, tpy = g.tpy ? g.tpy[m] : 0.0;
-  r[0] = dc.lf * (dc.fx * p[0] * zinv + dc.cx - tpx) + dc.ld * (p[0] - g.tgt[3 * m]);
-  r[1] = dc.lf * (dc.fy * p[1] * zinv + dc.cy - tpy) + dc.ld * (p[1] - g.tgt[3 * m + 1]);
-  r[2] = dc.ld * (p[2] - g.tgt[3 * m + 2]);
-  double Jk[18], Jl[18];
-  data_jacobian(g, dc, m, k, p, zinv, Jk);
-  int a = g.anc[m * 4 + k];
-  for (int l = 0; l < 4; ++l) {
-    int b = g.anc[m * 4 + l];
-    if (l == k) {
-      add_block(A + 36 * (int64_t)g.map[(int64_t)a * g.N + a], Jk, Jk);
+// One thread per term: residual triple + 3x6 Jacobian block of each of its nodes; loss partials.
+// Terms outside this rank's share (data matches outside [m0,m1), regularisers when !add_reg) are
+// written as exact zeros so the fixed contribution lists stay valid.
+__global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m1, int add_reg) {
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  double r[3] = {0.0, 0.0, 0.0};
+  double l2[3] = {0.0, 0.0, 0.0};
+  double bad = 0.0;
+  if (t < g.T) {
+    double* J = g.J + t * 72;
+    if (t < g.M) {
+      if (t >= m0 && t < m1) {
+        double p[3];
+        deformed_point(g, t, p);
+        double zinv = 1.0 / (p[2] + 1e-7);
+        double tpx = g.tpx[t], tpy = g.tpy[t];
+        r[0] = dc.lf * (dc.fx * p[0] * zinv + dc.cx - tpx) + dc.ld * (p[0] - g.tgt[3 * t]);
+        r[1] = dc.lf * (dc.fy * p[1] * zinv + dc.cy - tpy) + dc.ld * (p[1] - g.tgt[3 * t + 1]);
+        r[2] = dc.ld * (p[2] - g.tgt[3 * t + 2]);
+        for (int k = 0; k < 4; ++k) data_jacobian(g, dc, t, k, p, zinv, J + 18 * k);
+        l2[0] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+      } else {
+        for (int c = 0; c < 72; ++c) J[c] = 0.0;
+      }
+    } else if (t < g.M + (int64_t)g.N * g.NB) {
+      int64_t e = t - g.M;
+      int j = g.edges[e];
+      if (j >= 0) {
+        if (add_reg) {
+          int i = (int)(e / g.NB);
+          double s = dc.la * g.ew[e];
+          const double* Ri = g.R + 9 * (int64_t)i;
+          const double* gi = g.nodes + 3 * (int64_t)i;
+          const double* gj = g.nodes + 3 * (int64_t)j;
+          const double* ti = g.t + 3 * (int64_t)i;
+          const double* tj = g.t + 3 * (int64_t)j;
+          double e0 = gj[0] - gi[0], e1 = gj[1] - gi[1], e2 = gj[2] - gi[2];
+          double d0 = Ri[0] * e0 + Ri[1] * e1 + Ri[2] * e2;
+          double d1 = Ri[3] * e0 + Ri[4] * e1 + Ri[5] * e2;
+          double d2 = Ri[6] * e0 + Ri[7] * e1 + Ri[8] * e2;
+          r[0] = s * (d0 + gi[0] + ti[0] - (gj[0] + tj[0]));
+          r[1] = s * (d1 + gi[1] + ti[1] - (gj[1] + tj[1]));
+          r[2] = s * (d2 + gi[2] + ti[2] - (gj[2] + tj[2]));
+          // node i: [-s[d]x | s I] ; node j: [0 | -s I]
+          const double Ji[18] = {0.0, s * d2, -s * d1, s, 0, 0, -s * d2, 0.0, s * d0, 0, s, 0, s * d1, -s * d0, 0.0, 0, 0, s};
+          for (int c = 0; c < 18; ++c) J[c] = Ji[c];
+          for (int c = 0; c < 18; ++c) J[18 + c] = 0.0;
+          J[18 + 3] = -s; J[18 + 10] = -s; J[18 + 17] = -s;
+          l2[1] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        } else {
+          for (int c = 0; c < 36; ++c) J[c] = 0.0;
+        }
+      }
     } else {
-      data_jacobian(g, dc, m, l, p, zinv, Jl);
-      add_block(A + 36 * (int64_t)g.map[(int64_t)a * g.N + b], Jk, Jl);
+      int i = (int)(t - g.M - (int64_t)g.N * g.NB);
+      for (int c = 0; c < 18; ++c) J[c] = 0.0;
+      if (add_reg) {
+        double c = dc.lm * g.conf[i];
+        for (int q = 0; q < 3; ++q) r[q] = c * (g.t[3 * i + q] + g.nodes[3 * i + q] - g.tpos[3 * i + q]);
+        J[3] = c; J[10] = c; J[17] = c;
+        l2[2] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+      }
     }
+    g.res[3 * t] = r[0]; g.res[3 * t + 1] = r[1]; g.res[3 * t + 2] = r[2];
+    bad = (isfinite(l2[0]) && isfinite(l2[1]) && isfinite(l2[2])) ? 0.0 : 1.0;
   }
-  add_rhs(rhs + 6 * (int64_t)a, Jk, r);
-  if (k == 0) {
-    double l2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
-    double* tail = rhs + 6 * (int64_t)g.N;
-    atomic_add_f64(tail + 0, l2);
-    if (!isfinite(l2)) atomic_add_f64(tail + 3, 1.0);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_arap(Gn g, double la, double* __restrict__ A, double* __restrict__ rhs) {
-  int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e >= (int64_t)g.N * g.NB) return;
-  int j = g.edges[e];
-  if (j < 0) return;
-  int i = (int)(e / g.NB);
-  double w = g.ew[e];
-  const double* R = g.R + 9 * (int64_t)i;
-  const double* gi = g.nodes + 3 * (int64_t)i;
-  const double* gj = g.nodes + 3 * (int64_t)j;
-  const double* ti = g.t + 3 * (int64_t)i;
-  const double* tj = g.t + 3 * (int64_t)j;
-  double e0 = gj[0] - gi[0], e1 = gj[1] - gi[1], e2 = gj[2] - gi[2];
-  double d0 = R[0] * e0 + R[1] * e1 + R[2] * e2;
-  double d1 = R[3] * e0 + R[4] * e1 + R[5] * e2;
-  double d2 = R[6] * e0 + R[7] * e1 + R[8] * e2;
-  double s = la * w;
-  double r[3] = {s * (d0 + gi[0] + ti[0] - (gj[0] + tj[0])), s * (d1 + gi[1] + ti[1] - (gj[1] + tj[1])),
-                 s * (d2 + gi[2] + ti[2] - (gj[2] + tj[2]))};
-  // Srot = -s [d]x
-  double Ji[18] = {0.0, s * d2, -s * d1, s, 0, 0,
-                   -s * d2, 0.0, s * d0, 0, s, 0,
-                   s * d1, -s * d0, 0.0, 0, 0, s};
-  double Jj[18] = {0, 0, 0, -s, 0, 0,
-                   0, 0, 0, 0, -s, 0,
-                   0, 0, 0, 0, 0, -s};
-  int64_t N = g.N;
-  add_block(A + 36 * (int64_t)g.map[i * N + i], Ji, Ji);
-  add_block(A + 36 * (int64_t)g.map[i * N + j], Ji, Jj);
-  add_block(A + 36 * (int64_t)g.map[j * N + i], Jj, Ji);
-  add_block(A + 36 * (int64_t)g.map[j * N + j], Jj, Jj);
-  add_rhs(rhs + 6 * (int64_t)i, Ji, r);
-  add_rhs(rhs + 6 * (int64_t)j, Jj, r);
-  double l2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
-  double* tail = rhs + 6 * N;
-  atomic_add_f64(tail + 1, l2);
-  if (!isfinite(l2)) atomic_add_f64(tail + 3, 1.0);
-}
-
-__global__ __launch_bounds__(256) void k_motion(Gn g, double lm, double* __restrict__ A, double* __restrict__ rhs) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.N) return;
-  double c = lm * g.conf[i];
-  double r[3];
-  for (int q = 0; q < 3; ++q) r[q] = c * (g.t[3 * i + q] + g.nodes[3 * i + q] - g.tpos[3 * i + q]);
-  double* blk = A + 36 * (int64_t)g.map[(int64_t)i * g.N + i];
-  double cc = c * c;
-  if (cc != 0.0)
-    for (int q = 0; q < 3; ++q) atomic_add_f64(blk + (3 + q) * 6 + (3 + q), cc);
-  for (int q = 0; q < 3; ++q)
-    if (c * r[q] != 0.0) atomic_add_f64(rhs + 6 * (int64_t)i + 3 + q, -c * r[q]);
-  double l2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
-  double* tail = rhs + 6 * (int64_t)g.N;
-  atomic_add_f64(tail + 2, l2);
-  if (!isfinite(l2)) atomic_add_f64(tail + 3, 1.0);
-}
-
-// ---- last-workgroup deterministic reduction (agent-scope release/acquire, CDNA4 G16) ----
-// Each WG writes `nv` partials to part[wg*4 + v]; returns true in exactly one WG (the last arriver),
-// whose threads may then read every partial.
-__device__ __forceinline__ bool last_wg_arrive(uint32_t* ticket, int nwg) {
-  __shared__ int s_last;
-  __syncthreads();
+  double s0 = block_sum(l2[0]), s1 = block_sum(l2[1]), s2 = block_sum(l2[2]), s3 = block_sum(bad);
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int last = (t == (uint32_t)(nwg - 1));
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *ticket = 0;  // reset for the next launch (kernel boundary orders it)
+    double* P = g.part_loss + 4 * (int64_t)blockIdx.x;
+    P[0] = s0; P[1] = s1; P[2] = s2; P[3] = s3;
+  }
+}
+
+// One wave per JᵀJ block: lane (c,j) sums its entry over the block's sorted (term,p,q) list.
+__global__ __launch_bounds__(kBlk) void k_blocks(Gn g, double* __restrict__ A) {
+  const int64_t s = blockIdx.x * (int64_t)(kBlk / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= g.nnzb || lane >= 36) return;
+  const int c = lane / 6, j = lane % 6;
+  double v = 0.0;
+  const int b = g.blk_off[s], e = g.blk_off[s + 1];
+  for (int k = b; k < e; ++k) {
+    int code = g.blk_list[k];
+    int64_t t = code >> 4;
+    const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
+    const double* Jq = g.J + t * 72 + 18 * (code & 3);
+    v += Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
+  }
+  A[s * 36 + lane] = v;
+}
+
+// b = -Jᵀr, thread per (node, component); WG 0 also reduces the loss partials into the rhs tail.
+__global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
+  int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0) {
+    double d0 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 0);
+    double d1 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 1);
+    double d2 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 2);
+    double d3 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 3);
+    if (threadIdx.x == 0) {
+      double* tail = rhs + 6 * (int64_t)g.N;
+      tail[0] = d0; tail[1] = d1; tail[2] = d2; tail[3] = d3;
     }
-    s_last = last;
   }
-  __syncthreads();
-  return s_last != 0;
+  if (id >= 6 * (int64_t)g.N) return;
+  int n = (int)(id / 6), c = (int)(id % 6);
+  double v = 0.0;
+  for (int k = g.node_off[n]; k < g.node_off[n + 1]; ++k) {
+    int code = g.node_list[k];
+    int64_t t = code >> 2;
+    const double* Jp = g.J + t * 72 + 18 * (code & 3);
+    const double* rr = g.res + 3 * t;
+    v += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
+  }
+  rhs[id] = -v;
 }
 
-// sum partial v over nwg workgroups in fixed order (all threads of the last WG get the result)
-__device__ double fixed_order_sum(const double* part, int nwg, int v) {
-  __shared__ double s[kPcgBlock];
-  double acc = 0.0;
-  // thread t sums a contiguous slice, then a fixed-shape tree: deterministic
-  int per = (nwg + blockDim.x - 1) / blockDim.x;
-  int b = threadIdx.x * per, e = min(nwg, b + per);
-  for (int w = b; w < e; ++w) acc += part[4 * w + v];
-  s[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < (unsigned)o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
+// ---------------------------------------------------------------------------- PCG
+// 6x6 Cholesky (packed lower, 21 entries) with compile-time indices (no scratch).
+__device__ __forceinline__ bool chol6(const double* __restrict__ A, double L[21]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      double s = A[i * 6 + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+      if (i == j) {
+        if (!(s > 0.0)) return false;
+        L[i * (i + 1) / 2 + i] = sqrt(s);
+      } else {
+        L[i * (i + 1) / 2 + j] = s / L[j * (j + 1) / 2 + j];
+      }
+    }
   }
-  double r = s[0];
-  __syncthreads();
-  return r;
+  return true;
 }
 
-__device__ __forceinline__ double block_sum(double v) {
-  __shared__ double s[kPcgBlock];
-  s[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < (unsigned)o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
+__device__ __forceinline__ void chol6_solve(const double* __restrict__ L, const double b[6], double x[6]) {
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double s = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= L[i * (i + 1) / 2 + k] * y[k];
+    y[i] = s / L[i * (i + 1) / 2 + i];
   }
-  double r = s[0];
-  __syncthreads();
-  return r;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= L[k * (k + 1) / 2 + i] * x[k];
+    x[i] = s / L[i * (i + 1) / 2 + i];
+  }
 }
 
-// ---- PCG ----
-// prepare: LM damping on the diagonal, block-Jacobi inverse, x=0, r=b, z=D⁻¹r, p(old)=0, beta=0,
-// partials rz & bb.   thread per node.
-__global__ __launch_bounds__(kPcgBlock) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
-                                                         const double* __restrict__ rhs) {
+// LM damping, block Cholesky, x=0, r=b, z=M⁻¹r, p=0; partials: PU[1] = (rz, rr), PB = bb.
+__global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
+                                                   const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; }
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   double rz = 0.0, bb = 0.0;
   if (i < g.N) {
     double* blk = A + 36 * (int64_t)g.map[(int64_t)i * g.N + i];
-    double a[36], inv[36];
-    for (int c = 0; c < 6; ++c) blk[c * 7] += lm;
-    for (int c = 0; c < 36; ++c) { a[c] = blk[c]; inv[c] = (c % 7 == 0) ? 1.0 : 0.0; }
-    // Gauss-Jordan with partial pivoting
-    bool ok = true;
-    for (int c = 0; c < 6; ++c) {
-      int piv = c;
-      double best = fabs(a[c * 6 + c]);
-      for (int rr = c + 1; rr < 6; ++rr)
-        if (fabs(a[rr * 6 + c]) > best) { best = fabs(a[rr * 6 + c]); piv = rr; }
-      if (!(best > 0.0)) { ok = false; break; }
-      if (piv != c)
-        for (int q = 0; q < 6; ++q) {
-          double t0 = a[c * 6 + q]; a[c * 6 + q] = a[piv * 6 + q]; a[piv * 6 + q] = t0;
-          double t1 = inv[c * 6 + q]; inv[c * 6 + q] = inv[piv * 6 + q]; inv[piv * 6 + q] = t1;
-        }
-      double d = 1.0 / a[c * 6 + c];
-      for (int q = 0; q < 6; ++q) { a[c * 6 + q] *= d; inv[c * 6 + q] *= d; }
-      for (int rr = 0; rr < 6; ++rr)
-        if (rr != c) {
-          double f = a[rr * 6 + c];
-          if (f != 0.0)
-            for (int q = 0; q < 6; ++q) { a[rr * 6 + q] -= f * a[c * 6 + q]; inv[rr * 6 + q] -= f * inv[c * 6 + q]; }
-        }
+    double a[36];
+#pragma unroll
+    for (int c = 0; c < 36; ++c) a[c] = blk[c];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) { a[c * 7] += lm; blk[c * 7] = a[c * 7]; }
+    double L[21];
+    bool ok = chol6(a, L);
+    if (!ok) {
+#pragma unroll
+      for (int c = 0; c < 21; ++c) L[c] = 0.0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) L[c * (c + 1) / 2 + c] = 1.0;
     }
-    if (!ok)
-      for (int c = 0; c < 36; ++c) inv[c] = (c % 7 == 0) ? 1.0 : 0.0;
-    double* D = g.Dinv + 36 * (int64_t)i;
-    for (int c = 0; c < 36; ++c) D[c] = inv[c];
-    double rv[6];
+    double* Ld = g.L + 24 * (int64_t)i;
+#pragma unroll
+    for (int c = 0; c < 21; ++c) Ld[c] = L[c];
+    double rv[6], zv[6];
+#pragma unroll
     for (int c = 0; c < 6; ++c) {
       rv[c] = rhs[6 * i + c];
       g.x[6 * i + c] = 0.0;
@@ -429,131 +496,117 @@ __global__ __launch_bounds__(kPcgBlock) void k_pcg_prep(Gn g, double lm, double*
       g.p1[6 * i + c] = 0.0;
       bb += rv[c] * rv[c];
     }
-    for (int c = 0; c < 6; ++c) {
-      double zc = 0.0;
-      for (int q = 0; q < 6; ++q) zc += inv[c * 6 + q] * rv[q];
-      g.z[6 * i + c] = zc;
-      rz += rv[c] * zc;
-    }
+    chol6_solve(L, rv, zv);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) { g.z[6 * i + c] = zv[c]; rz += rv[c] * zv[c]; }
   }
-  double s_rz = block_sum(rz);
-  double s_bb = block_sum(bb);
-  int nwg = gridDim.x;
-  if (threadIdx.x == 0) { g.part[4 * blockIdx.x + 0] = s_rz; g.part[4 * blockIdx.x + 1] = s_bb; }
-  if (last_wg_arrive(g.tickets + 0, nwg)) {
-    double trz = fixed_order_sum(g.part, nwg, 0);
-    double tbb = fixed_order_sum(g.part, nwg, 1);
-    if (threadIdx.x == 0) {
-      g.scal[S_RZ] = trz;
-      g.scal[S_BB] = tbb;
-      g.scal[S_BETA] = 0.0;
-      g.flags[F_DONE] = (tbb == 0.0 || !isfinite(tbb)) ? 1 : 0;
-      if (!isfinite(tbb)) g.flags[F_ILL] = 1;
-      g.flags[F_PCG_IT] = 0;
-    }
+  double s_rz = block_sum(rz), s_bb = block_sum(bb);
+  if (threadIdx.x == 0) {
+    double* PU = g.part_u + 2 * (int64_t)g.nwg_node * 1;  // parity 1 slot
+    PU[2 * blockIdx.x] = s_rz;
+    PU[2 * blockIdx.x + 1] = s_bb;
+    g.part_b[blockIdx.x] = s_bb;
   }
 }
 
-// K1: p_new = z + beta*p_old (on the fly for every column), q = A p_new, partial p·q; last WG: alpha.
-// one wave per block row; lanes stride over the row's blocks.
-__global__ __launch_bounds__(kPcgBlock) void k_pcg_spmv(Gn g, const double* __restrict__ A, int parity) {
+// iteration it: scalars from the previous update; convergence test; p = z + beta p_old (on the fly);
+// q = A p; partial p·q.   One wave per block row; lane = (block-in-group b = lane/6, row rr = lane%6).
+__global__ __launch_bounds__(kBlk) void k_pcg_spmv(Gn g, const double* __restrict__ A, int it) {
   if (g.flags[F_DONE] || g.flags[F_STOPPED]) return;
-  const double* __restrict__ pold = parity ? g.p0 : g.p1;
-  double* __restrict__ pnew = parity ? g.p1 : g.p0;
-  const double beta = g.scal[S_BETA];
+  const double* PUc = g.part_u + 2 * (int64_t)g.nwg_node * ((it - 1) & 1);
+  const double rz = wg_sum_fixed(PUc, g.nwg_node, 2, 0);
+  const double rr = wg_sum_fixed(PUc, g.nwg_node, 2, 1);
+  const double bb = wg_sum_fixed(g.part_b, g.nwg_node, 1, 0);
+  const double tol = g.prm.pcg_tol;
+  if (rr <= tol * tol * bb || rz == 0.0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
+    return;
+  }
+  double beta = 0.0;
+  if (it > 0) {
+    const double* PUo = g.part_u + 2 * (int64_t)g.nwg_node * ((it - 2) & 1);
+    beta = rz / wg_sum_fixed(PUo, g.nwg_node, 2, 0);
+  }
+  const double* __restrict__ pold = (it & 1) ? g.p0 : g.p1;
+  double* __restrict__ pnew = (it & 1) ? g.p1 : g.p0;
+  __shared__ double s_acc[kBlk];
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (kPcgBlock / 64) + (threadIdx.x >> 6);
+  const int wv = threadIdx.x >> 6;
+  const int row = blockIdx.x * kRowsPerWG + wv;
   double pq = 0.0;
-  if (row < g.N) {
-    double acc[6] = {0, 0, 0, 0, 0, 0};
-    int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-    for (int bi = b0 + lane; bi < b1; bi += 64) {
-      int c = g.col[bi];
-      double pv[6];
-      for (int j = 0; j < 6; ++j) pv[j] = g.z[6 * c + j] + beta * pold[6 * c + j];
-      const double* blk = A + 36 * (int64_t)bi;
-      for (int rr = 0; rr < 6; ++rr) {
-        double s = 0.0;
-        for (int j = 0; j < 6; ++j) s += blk[rr * 6 + j] * pv[j];
-        acc[rr] += s;
-      }
+  double acc = 0.0;
+  if (row < g.N && lane < 60) {
+    const int bl = lane / 6, rrw = lane % 6;
+    const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
+    for (int bi = b0 + bl; bi < b1; bi += 10) {
+      const int c = g.col[bi];
+      const double* blk = A + 36 * (int64_t)bi + rrw * 6;
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) s += blk[j] * (g.z[6 * c + j] + beta * pold[6 * c + j]);
+      acc += s;
     }
-    for (int rr = 0; rr < 6; ++rr)
-      for (int off = 32; off > 0; off >>= 1) acc[rr] += __shfl_xor(acc[rr], off, 64);
-    if (lane < 6) {
-      double mine = acc[0];
-      for (int rr = 1; rr < 6; ++rr) if (lane == rr) mine = acc[rr];
-      double pn = g.z[6 * row + lane] + beta * pold[6 * row + lane];
-      pnew[6 * row + lane] = pn;
-      g.q[6 * row + lane] = mine;
-      pq = pn * mine;
-    }
+  }
+  s_acc[threadIdx.x] = acc;
+  __syncthreads();
+  if (row < g.N && lane < 6) {
+    double qv = 0.0;
+#pragma unroll
+    for (int b = 0; b < 10; ++b) qv += s_acc[wv * 64 + b * 6 + lane];
+    double pn = g.z[6 * row + lane] + beta * pold[6 * row + lane];
+    pnew[6 * row + lane] = pn;
+    g.q[6 * row + lane] = qv;
+    pq = pn * qv;
   }
   double s = block_sum(pq);
-  int nwg = gridDim.x;
-  if (threadIdx.x == 0) g.part[4 * blockIdx.x + 0] = s;
-  if (last_wg_arrive(g.tickets + 1, nwg)) {
-    double tpq = fixed_order_sum(g.part, nwg, 0);
-    if (threadIdx.x == 0) {
-      g.scal[S_PQ] = tpq;
-      double rz = g.scal[S_RZ];
-      if (!(tpq > 0.0) || !isfinite(tpq)) {
-        g.flags[F_DONE] = 1;  // breakdown: keep current x
-        g.scal[S_ALPHA] = 0.0;
-        if (!isfinite(tpq)) g.flags[F_ILL] = 1;
-      } else {
-        g.scal[S_ALPHA] = rz / tpq;
-      }
-    }
-  }
+  if (threadIdx.x == 0) g.part_s[blockIdx.x] = s;
 }
 
-// K2: x += a p, r -= a q, z = D⁻¹ r, partial r·z, r·r; last WG: beta, convergence.  thread per node.
-__global__ __launch_bounds__(kPcgBlock) void k_pcg_update(Gn g, int parity) {
+// x += a p, r -= a q, z = M⁻¹ r, partials (r·z, r·r) -> PU[it&1].  thread per node.
+__global__ __launch_bounds__(kBlk) void k_pcg_update(Gn g, int it) {
   if (g.flags[F_DONE] || g.flags[F_STOPPED]) return;
-  const double* __restrict__ p = parity ? g.p1 : g.p0;
-  const double alpha = g.scal[S_ALPHA];
+  const double* PUc = g.part_u + 2 * (int64_t)g.nwg_node * ((it - 1) & 1);
+  const double rz = wg_sum_fixed(PUc, g.nwg_node, 2, 0);
+  const double pq = wg_sum_fixed(g.part_s, g.nwg_row, 1, 0);
+  if (!(pq > 0.0) || !isfinite(pq)) {  // breakdown: keep x
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
+      if (!isfinite(pq)) g.flags[F_ILL] = 1;
+    }
+    return;
+  }
+  const double alpha = rz / pq;
+  const double* __restrict__ p = (it & 1) ? g.p1 : g.p0;
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  double rz = 0.0, rr = 0.0;
+  double rzn = 0.0, rrn = 0.0;
   if (i < g.N) {
-    double rv[6];
+    double rv[6], zv[6];
+#pragma unroll
     for (int c = 0; c < 6; ++c) {
       g.x[6 * i + c] += alpha * p[6 * i + c];
       rv[c] = g.r[6 * i + c] - alpha * g.q[6 * i + c];
       g.r[6 * i + c] = rv[c];
-      rr += rv[c] * rv[c];
+      rrn += rv[c] * rv[c];
     }
-    const double* D = g.Dinv + 36 * (int64_t)i;
-    for (int c = 0; c < 6; ++c) {
-      double zc = 0.0;
-      for (int q = 0; q < 6; ++q) zc += D[c * 6 + q] * rv[q];
-      g.z[6 * i + c] = zc;
-      rz += rv[c] * zc;
-    }
+    double L[21];
+    const double* Ld = g.L + 24 * (int64_t)i;
+#pragma unroll
+    for (int c = 0; c < 21; ++c) L[c] = Ld[c];
+    chol6_solve(L, rv, zv);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) { g.z[6 * i + c] = zv[c]; rzn += rv[c] * zv[c]; }
   }
-  double s_rz = block_sum(rz);
-  double s_rr = block_sum(rr);
-  int nwg = gridDim.x;
-  if (threadIdx.x == 0) { g.part[4 * blockIdx.x + 0] = s_rz; g.part[4 * blockIdx.x + 1] = s_rr; }
-  if (last_wg_arrive(g.tickets + 2, nwg)) {
-    double trz = fixed_order_sum(g.part, nwg, 0);
-    double trr = fixed_order_sum(g.part, nwg, 1);
-    if (threadIdx.x == 0) {
-      double old = g.scal[S_RZ];
-      g.scal[S_BETA] = (old != 0.0) ? trz / old : 0.0;
-      g.scal[S_RZ] = trz;
-      g.scal[S_RR] = trr;
-      g.flags[F_PCG_IT] += 1;
-      g.flags[F_PCG_TOTAL] += 1;
-      double tol = g.prm.pcg_tol;
-      if (!isfinite(trr)) { g.flags[F_ILL] = 1; g.flags[F_DONE] = 1; }
-      else if (trr <= tol * tol * g.scal[S_BB] || trz == 0.0) g.flags[F_DONE] = 1;
-    }
+  double s_rz = block_sum(rzn), s_rr = block_sum(rrn);
+  if (threadIdx.x == 0) {
+    double* PU = g.part_u + 2 * (int64_t)g.nwg_node * (it & 1);
+    PU[2 * blockIdx.x] = s_rz;
+    PU[2 * blockIdx.x + 1] = s_rr;
   }
 }
 
 // After the solve: ill-posed check, loss bookkeeping and early stop (model.py:696-732). Single WG.
-__global__ __launch_bounds__(kPcgBlock) void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log) {
+__global__ __launch_bounds__(kBlk) void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log,
+                                                      int pcg_max) {
   __shared__ int s_bad;
   if (threadIdx.x == 0) s_bad = 0;
   __syncthreads();
@@ -563,6 +616,7 @@ __global__ __launch_bounds__(kPcgBlock) void k_step_decide(Gn g, const double* _
   if (bad) atomicOr(&s_bad, 1);
   __syncthreads();
   if (threadIdx.x != 0) return;
+  if (!g.flags[F_DONE]) g.flags[F_PCG_TOTAL] += pcg_max;
   const double* tail = rhs + 6 * (int64_t)g.N;
   g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
   g.flags[F_APPLY] = 0;
@@ -637,7 +691,6 @@ __global__ void k_reset_flags(Gn g) {
   int i = threadIdx.x;
   if (i < F_COUNT) g.flags[i] = 0;
   if (i < S_COUNT) g.scal[i] = 0.0;
-  if (i < 4) g.tickets[i] = 0;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -650,30 +703,42 @@ static double lm_for_iter(double lm0, int gn_iter) {
 
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
-                  g->map, g->row_ptr, g->col, g->row_cnt, g->R, g->t, g->A_own, g->rhs_own, g->Dinv, g->x, g->r,
-                  g->z, g->p0, g->p1, g->q, g->part, g->scal, g->flags, g->tickets, g->loss_log};
+                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->row_cnt, g->blk_off, g->blk_cnt,
+                  g->blk_list, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->L, g->x,
+                  g->r, g->z, g->p0, g->p1, g->q, g->part_s, g->part_u, g->part_b, g->part_loss, g->scal, g->flags,
+                  g->loss_log};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  if (g->host_flag) (void)hipHostFree(g->host_flag);
+  if (g->host_flags) (void)hipHostFree(g->host_flags);
 }
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
-  const int nwg_node = (g->N + kPcgBlock - 1) / kPcgBlock;
-  const int nwg_row = (g->N + (kPcgBlock / 64) - 1) / (kPcgBlock / 64);
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
-  hipLaunchKernelGGL(k_pcg_prep, dim3(nwg_node), dim3(kPcgBlock), 0, hs, *g, lm, A, rhs);
+  hipLaunchKernelGGL(k_pcg_prep, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
   OFX_LAUNCH_CHECK();
-  const int poll = 8;
-  for (int it = 0; it < g->prm.pcg_max_iter; ++it) {
-    int parity = it & 1;
-    hipLaunchKernelGGL(k_pcg_spmv, dim3(nwg_row), dim3(kPcgBlock), 0, hs, *g, (const double*)A, parity);
-    hipLaunchKernelGGL(k_pcg_update, dim3(nwg_node), dim3(kPcgBlock), 0, hs, *g, parity);
-    OFX_LAUNCH_CHECK();
-    if ((it + 1) % poll == 0 && it + 1 < g->prm.pcg_max_iter) {
-      OFX_HIP(hipMemcpyAsync(g->host_flag, g->flags + F_DONE, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-      OFX_HIP(hipStreamSynchronize(hs));
-      if (*g->host_flag) break;
+  const int max_it = g->prm.pcg_max_iter;
+  int chunk = g->last_pcg > 0 ? ((g->last_pcg + 4 + 7) / 8) * 8 : 64;
+  int it = 0;
+  while (it < max_it) {
+    int n = chunk < max_it - it ? chunk : max_it - it;
+    for (int k = 0; k < n; ++k, ++it) {
+      hipLaunchKernelGGL(k_pcg_spmv, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, (const double*)A, it);
+      hipLaunchKernelGGL(k_pcg_update, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, it);
     }
+    OFX_LAUNCH_CHECK();
+    if (it >= max_it) break;
+    // one extra convergence probe so the final residual test runs on device
+    hipLaunchKernelGGL(k_pcg_spmv, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, (const double*)A, it);
+    OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+    OFX_HIP(hipStreamSynchronize(hs));
+    if (g->host_flags[F_DONE]) {
+      g->last_pcg = g->host_flags[F_PCG_IT];
+      break;
+    }
+    // the probe computed q = A p for iteration `it`; run its update and continue
+    hipLaunchKernelGGL(k_pcg_update, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, it);
+    ++it;
+    chunk = 16;
   }
   return OFX_OK;
 }
@@ -686,27 +751,29 @@ extern "C" {
 
 int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   OFX_CHECK_ARG(handle && max_nodes > 0 && max_matches >= 0, "bad gn_create args");
+  if (max_nodes > 16384) { set_error("max_nodes %d > 16384 (dense NxN slot map)", max_nodes); return OFX_ERR_RANGE; }
   Gn* g = new Gn();
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
   int64_t N = max_nodes, M = max_matches > 0 ? max_matches : 1;
-  int64_t nwg = (N + 3) / 4 + 8;
 #define ALLOC(ptr, n) \
   if (hipMalloc((void**)&(ptr), (size_t)(n) * sizeof(*(ptr))) != hipSuccess) { free_all(g); delete g; set_error("hipMalloc failed"); return OFX_ERR_ALLOC; }
   ALLOC(g->nodes, 3 * N); ALLOC(g->tpos, 3 * N); ALLOC(g->conf, N);
   ALLOC(g->src, 3 * M); ALLOC(g->wts, 4 * M); ALLOC(g->tgt, 3 * M); ALLOC(g->tpx, M); ALLOC(g->tpy, M);
   ALLOC(g->anc, 4 * M);
-  ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N);
+  ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 1);
+  ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
-  ALLOC(g->Dinv, 36 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->z, 6 * N);
+  ALLOC(g->L, 24 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->z, 6 * N);
   ALLOC(g->p0, 6 * N); ALLOC(g->p1, 6 * N); ALLOC(g->q, 6 * N);
-  ALLOC(g->part, 4 * nwg); ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT); ALLOC(g->tickets, 4);
+  int64_t nwg_row = (N + kRowsPerWG - 1) / kRowsPerWG, nwg_node = (N + kBlk - 1) / kBlk;
+  ALLOC(g->part_s, nwg_row); ALLOC(g->part_u, 4 * nwg_node); ALLOC(g->part_b, nwg_node);
+  ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
-  if (hipHostMalloc((void**)&g->host_flag, sizeof(int32_t), 0) != hipSuccess) {
+  if (hipHostMalloc((void**)&g->host_flags, F_COUNT * sizeof(int32_t), 0) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
-  (void)hipMemset(g->tickets, 0, 4 * sizeof(uint32_t));
   *handle = g;
   return OFX_OK;
 }
@@ -735,6 +802,24 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   int N = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
   g->N = N; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
+  g->T = (int64_t)M + (int64_t)N * NB + N;
+  g->nwg_row = (N + kRowsPerWG - 1) / kRowsPerWG;
+  g->nwg_node = (N + kBlk - 1) / kBlk;
+  g->nwg_terms = (int32_t)((g->T + kBlk - 1) / kBlk);
+  // per-solve buffers sized by T
+  if (g->T > g->T_cap) {
+    for (auto pp : {(void**)&g->term_node, (void**)&g->J, (void**)&g->res, (void**)&g->node_list,
+                    (void**)&g->blk_list, (void**)&g->part_loss})
+      if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
+    int64_t c = g->T + g->T / 4 + 64;
+    OFX_HIP(hipMalloc((void**)&g->term_node, 4 * c * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->J, 72 * c * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->res, 3 * c * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->node_list, 4 * c * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->blk_list, 16 * c * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->part_loss, 4 * ((c + kBlk - 1) / kBlk) * sizeof(double)));
+    g->T_cap = c;
+  }
   // edges + weights
   if (g->edges) { OFX_HIP(hipFree(g->edges)); g->edges = nullptr; }
   if (g->ew) { OFX_HIP(hipFree(g->ew)); g->ew = nullptr; }
@@ -761,27 +846,39 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_init_state, dim3(grid_for(N, 256)), dim3(256), 0, hs, pb->prev_rot, pb->prev_trans, N, g->R, g->t);
   hipLaunchKernelGGL(k_reset_flags, dim3(1), dim3(64), 0, hs, *g);
-  // pattern
+  // terms -> block pattern
+  unsigned gT = grid_for(g->T, 256, 1 << 30);
+  hipLaunchKernelGGL(k_term_nodes, dim3(gT), dim3(256), 0, hs, *g);
   OFX_HIP(hipMemsetAsync(g->map, 0, (size_t)N * N * sizeof(int32_t), hs));
-  int64_t nmark = (int64_t)M * 16;
-  if (ne > nmark) nmark = ne;
-  if (N > nmark) nmark = N;
-  hipLaunchKernelGGL(k_mark, dim3(grid_for(nmark, 256, 1 << 30)), dim3(256), 0, hs, N, M, NB, g->anc, g->edges, g->map);
+  hipLaunchKernelGGL(k_mark, dim3(gT), dim3(256), 0, hs, *g);
   hipLaunchKernelGGL(k_row_count, dim3(N), dim3(256), 0, hs, N, g->map, g->row_cnt);
-  hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(1024), 0, hs, N, g->row_cnt, g->row_ptr);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr);
   OFX_LAUNCH_CHECK();
   int32_t nnz = 0;
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
-  if ((int64_t)nnz > g->nnzb_cap) {
-    if (g->col) OFX_HIP(hipFree(g->col));
-    if (g->A_own) OFX_HIP(hipFree(g->A_own));
+  if ((int64_t)nnz + 1 > g->nnzb_cap) {
+    for (auto pp : {(void**)&g->col, (void**)&g->A_own, (void**)&g->blk_off, (void**)&g->blk_cnt})
+      if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     g->nnzb_cap = (int64_t)nnz + nnz / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->col, g->nnzb_cap * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->A_own, g->nnzb_cap * 36 * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->blk_off, (g->nnzb_cap + 1) * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->blk_cnt, (g->nnzb_cap + 1) * sizeof(int32_t)));
   }
   g->nnzb = nnz;
   hipLaunchKernelGGL(k_row_assign, dim3(N), dim3(256), 0, hs, N, g->map, g->row_ptr, g->col);
+  // contribution lists (sorted -> deterministic assembly order)
+  OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
+  OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_pair_count, dim3(gT), dim3(256), 0, hs, *g);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->blk_off);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->node_cnt, g->node_off);
+  OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
+  OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_pair_scatter, dim3(gT), dim3(256), 0, hs, *g);
+  hipLaunchKernelGGL(k_seg_sort, dim3(grid_for(nnz, 256)), dim3(256), 0, hs, (const int32_t*)g->blk_off, (int64_t)nnz, g->blk_list);
+  hipLaunchKernelGGL(k_seg_sort, dim3(grid_for(N, 256)), dim3(256), 0, hs, (const int32_t*)g->node_off, (int64_t)N, g->node_list);
   OFX_LAUNCH_CHECK();
   if (nnz_blocks) *nnz_blocks = nnz;
   g->setup_done = true;
@@ -796,21 +893,14 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   OFX_CHECK_ARG(m0 >= 0 && m1 <= g->M && m0 <= m1, "bad match range [%d,%d) of %d", m0, m1, g->M);
   (void)gn_iter;
   hipStream_t hs = as_stream(s);
-  OFX_HIP(hipMemsetAsync(A, 0, (size_t)g->nnzb * 36 * sizeof(double), hs));
-  OFX_HIP(hipMemsetAsync(rhs, 0, (size_t)(6 * g->N + 4) * sizeof(double), hs));
   DataCoef dc;
   dc.lf = sqrt(g->prm.lambda_flow); dc.ld = sqrt(g->prm.lambda_depth);
+  dc.la = sqrt(g->prm.lambda_arap); dc.lm = sqrt(g->prm.lambda_motion);
   dc.fx = g->fx; dc.fy = g->fy; dc.cx = g->cx; dc.cy = g->cy;
-  Gn gv = *g;
-  if (!(g->tpx && g->M)) { gv.tpx = nullptr; gv.tpy = nullptr; }
-  if (m1 > m0)
-    hipLaunchKernelGGL(k_data, dim3(grid_for((int64_t)(m1 - m0) * 4, 256, 1 << 30)), dim3(256), 0, hs, gv, dc, m0, m1, A, rhs);
-  if (add_reg) {
-    int64_t ne = (int64_t)g->N * g->NB;
-    if (ne > 0)
-      hipLaunchKernelGGL(k_arap, dim3(grid_for(ne, 256, 1 << 30)), dim3(256), 0, hs, gv, sqrt(g->prm.lambda_arap), A, rhs);
-    hipLaunchKernelGGL(k_motion, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, gv, sqrt(g->prm.lambda_motion), A, rhs);
-  }
+  hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
+  if (g->nnzb > 0)
+    hipLaunchKernelGGL(k_blocks, dim3(grid_for(g->nnzb, kBlk / 64, 1 << 30)), dim3(kBlk), 0, hs, *g, A);
+  hipLaunchKernelGGL(k_rhs, dim3(grid_for(6 * (int64_t)g->N, kBlk)), dim3(kBlk), 0, hs, *g, rhs);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }
@@ -822,7 +912,7 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   hipStream_t hs = as_stream(s);
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kPcgBlock), 0, hs, *g, (const double*)rhs, 64);
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlk), 0, hs, *g, (const double*)rhs, 64, g->prm.pcg_max_iter);
   hipLaunchKernelGGL(k_apply, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
@@ -850,10 +940,10 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     if (st) return st;
     st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
     if (st) return st;
-    // stop host loop early once the device has stopped (costs one sync per GN iteration)
-    OFX_HIP(hipMemcpyAsync(g->host_flag, g->flags + F_STOPPED, sizeof(int32_t), hipMemcpyDeviceToHost, as_stream(s)));
+    // the PCG poll of this step already synchronised the stream; read the stop flag cheaply
+    OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, as_stream(s)));
     OFX_HIP(hipStreamSynchronize(as_stream(s)));
-    if (*g->host_flag) break;
+    if (g->host_flags[F_STOPPED]) break;
   }
   return ofx_gn_finish(handle, res, s);
 }

@@ -6,7 +6,7 @@ DeformNet.optimize) over libofx.so: hand-written HIP kernels for gfx950 behind a
 ImportError if it is missing. (`synthetic` and `build` are plain-Python helpers and load nothing.)
 """
 _EXPORTS = {
-    "TSDFVolume": "tsdf", "volume_geometry": "tsdf", "shard_bricks": "tsdf",
+    "TSDFVolume": "tsdf", "volume_geometry": "tsdf", "shard_bricks": "sharding", "match_range": "sharding",
     "WarpField": "warpfield", "EDGraph": "warpfield",
     "GaussNewtonSolver": "registration", "Registration": "registration",
     "FusionPipeline": "pipeline",

@@ -57,8 +57,12 @@ struct Gn {
   // state
   double *R = nullptr, *t = nullptr;
   double *A_own = nullptr, *rhs_own = nullptr;
-  double *L = nullptr, *x = nullptr, *r = nullptr, *z = nullptr, *p0 = nullptr, *p1 = nullptr, *q = nullptr;
-  double *part_s = nullptr, *part_u = nullptr, *part_b = nullptr, *part_loss = nullptr;
+  double *Minv = nullptr, *Bm = nullptr;  // block-Jacobi inverse (N*36), B = A·M⁻¹ (nnzb*36)
+  double *x = nullptr, *r = nullptr, *u = nullptr, *w0 = nullptr, *w1 = nullptr, *zz = nullptr, *qv = nullptr,
+         *sv = nullptr, *pv = nullptr;
+  double *pcg_alpha = nullptr, *pcg_gamma = nullptr;
+  int64_t pcg_cap = 0;
+  double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;
   double* scal = nullptr;
   int32_t* flags = nullptr;
@@ -73,6 +77,7 @@ enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_
 enum { S_LOSS_PREV = 0, S_COUNT = 4 };
 constexpr int kBlk = 256;       // threads per WG
 constexpr int kRowsPerWG = 4;   // SpMV: one wave per block row
+constexpr int kMaxSpmvWG = 128; // bounded grid: fewer partials for the consumer to re-read
 
 // ---------------------------------------------------------------------------- reductions
 __device__ __forceinline__ double block_sum(double v) {
@@ -423,7 +428,12 @@ __global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
 }
 
 // ---------------------------------------------------------------------------- PCG
-// 6x6 Cholesky (packed lower, 21 entries) with compile-time indices (no scratch).
+// Pipelined preconditioned CG (Ghysels & Vanroose 2014): one global reduction per iteration.
+// With block-Jacobi M⁻¹ (node-local) folded into B = A·M⁻¹ (per GN step), n = A·m = A·M⁻¹·w = B·w,
+// so one iteration is ONE kernel: scalars from the previous kernel's partials, SpMV with B, all
+// vector recurrences for the own rows, partial dots for the next iteration.
+
+// 6x6 Cholesky (packed lower, 21 entries, diagonal stored as 1/L_ii) with compile-time indices.
 __device__ __forceinline__ bool chol6(const double* __restrict__ A, double L[21]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
@@ -434,9 +444,9 @@ __device__ __forceinline__ bool chol6(const double* __restrict__ A, double L[21]
       for (int k = 0; k < j; ++k) s -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
       if (i == j) {
         if (!(s > 0.0)) return false;
-        L[i * (i + 1) / 2 + i] = sqrt(s);
+        L[i * (i + 1) / 2 + i] = 1.0 / sqrt(s);   // reciprocal diagonal: the solve multiplies
       } else {
-        L[i * (i + 1) / 2 + j] = s / L[j * (j + 1) / 2 + j];
+        L[i * (i + 1) / 2 + j] = s * L[j * (j + 1) / 2 + j];
       }
     }
   }
@@ -450,157 +460,198 @@ __device__ __forceinline__ void chol6_solve(const double* __restrict__ L, const 
     double s = b[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) s -= L[i * (i + 1) / 2 + k] * y[k];
-    y[i] = s / L[i * (i + 1) / 2 + i];
+    y[i] = s * L[i * (i + 1) / 2 + i];
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     double s = y[i];
 #pragma unroll
     for (int k = i + 1; k < 6; ++k) s -= L[k * (k + 1) / 2 + i] * x[k];
-    x[i] = s / L[i * (i + 1) / 2 + i];
+    x[i] = s * L[i * (i + 1) / 2 + i];
   }
 }
 
-// LM damping, block Cholesky, x=0, r=b, z=M⁻¹r, p=0; partials: PU[1] = (rz, rr), PB = bb.
+// LM damping of the diagonal blocks, explicit block inverse Minv_i, x = 0, r = b, u = M⁻¹ b,
+// recurrence vectors zeroed.  thread per node.
 __global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
                                                    const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; }
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  double rz = 0.0, bb = 0.0;
-  if (i < g.N) {
-    double* blk = A + 36 * (int64_t)g.map[(int64_t)i * g.N + i];
-    double a[36];
+  if (i >= g.N) return;
+  double* blk = A + 36 * (int64_t)g.map[(int64_t)i * g.N + i];
+  double a[36];
 #pragma unroll
-    for (int c = 0; c < 36; ++c) a[c] = blk[c];
+  for (int c = 0; c < 36; ++c) a[c] = blk[c];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) { a[c * 7] += lm; blk[c * 7] = a[c * 7]; }
-    double L[21];
-    bool ok = chol6(a, L);
-    if (!ok) {
+  for (int c = 0; c < 6; ++c) { a[c * 7] += lm; blk[c * 7] = a[c * 7]; }
+  double L[21];
+  bool ok = chol6(a, L);
+  double* Mi = g.Minv + 36 * (int64_t)i;
 #pragma unroll
-      for (int c = 0; c < 21; ++c) L[c] = 0.0;
+  for (int c = 0; c < 6; ++c) {       // column c of the inverse
+    double e[6], col[6];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) L[c * (c + 1) / 2 + c] = 1.0;
+    for (int k = 0; k < 6; ++k) e[k] = (k == c) ? 1.0 : 0.0;
+    if (ok) chol6_solve(L, e, col);
+    else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) col[k] = e[k];
     }
-    double* Ld = g.L + 24 * (int64_t)i;
 #pragma unroll
-    for (int c = 0; c < 21; ++c) Ld[c] = L[c];
-    double rv[6], zv[6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      rv[c] = rhs[6 * i + c];
-      g.x[6 * i + c] = 0.0;
-      g.r[6 * i + c] = rv[c];
-      g.p0[6 * i + c] = 0.0;
-      g.p1[6 * i + c] = 0.0;
-      bb += rv[c] * rv[c];
-    }
-    chol6_solve(L, rv, zv);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) { g.z[6 * i + c] = zv[c]; rz += rv[c] * zv[c]; }
+    for (int k = 0; k < 6; ++k) Mi[k * 6 + c] = col[k];
   }
-  double s_rz = block_sum(rz), s_bb = block_sum(bb);
-  if (threadIdx.x == 0) {
-    double* PU = g.part_u + 2 * (int64_t)g.nwg_node * 1;  // parity 1 slot
-    PU[2 * blockIdx.x] = s_rz;
-    PU[2 * blockIdx.x + 1] = s_bb;
-    g.part_b[blockIdx.x] = s_bb;
+  double b[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) b[c] = rhs[6 * i + c];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    double u = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) u += Mi[c * 6 + k] * b[k];
+    const int64_t o = 6 * (int64_t)i + c;
+    g.x[o] = 0.0; g.r[o] = b[c]; g.u[o] = u;
+    g.zz[o] = 0.0; g.qv[o] = 0.0; g.sv[o] = 0.0; g.pv[o] = 0.0;
   }
 }
 
-// iteration it: scalars from the previous update; convergence test; p = z + beta p_old (on the fly);
-// q = A p; partial p·q.   One wave per block row; lane = (block-in-group b = lane/6, row rr = lane%6).
-__global__ __launch_bounds__(kBlk) void k_pcg_spmv(Gn g, const double* __restrict__ A, int it) {
-  if (g.flags[F_DONE] || g.flags[F_STOPPED]) return;
-  const double* PUc = g.part_u + 2 * (int64_t)g.nwg_node * ((it - 1) & 1);
-  const double rz = wg_sum_fixed(PUc, g.nwg_node, 2, 0);
-  const double rr = wg_sum_fixed(PUc, g.nwg_node, 2, 1);
-  const double bb = wg_sum_fixed(g.part_b, g.nwg_node, 1, 0);
-  const double tol = g.prm.pcg_tol;
-  if (rr <= tol * tol * bb || rz == 0.0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
-    return;
-  }
-  double beta = 0.0;
-  if (it > 0) {
-    const double* PUo = g.part_u + 2 * (int64_t)g.nwg_node * ((it - 2) & 1);
-    beta = rz / wg_sum_fixed(PUo, g.nwg_node, 2, 0);
-  }
-  const double* __restrict__ pold = (it & 1) ? g.p0 : g.p1;
-  double* __restrict__ pnew = (it & 1) ? g.p1 : g.p0;
-  __shared__ double s_acc[kBlk];
+// B_ij = A_ij · Minv_j  (thread per block)
+__global__ __launch_bounds__(kBlk) void k_pcg_bmat(Gn g, const double* __restrict__ A) {
+  if (g.flags[F_STOPPED]) return;
+  int64_t bi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (bi >= g.nnzb) return;
+  const double* Ab = A + 36 * bi;
+  const double* Mj = g.Minv + 36 * (int64_t)g.col[bi];
+  double* Bb = g.Bm + 36 * bi;
+  double a[36], m[36];
+#pragma unroll
+  for (int c = 0; c < 36; ++c) { a[c] = Ab[c]; m[c] = Mj[c]; }
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v += a[r * 6 + k] * m[k * 6 + c];
+      Bb[r * 6 + c] = v;
+    }
+}
+
+// one wave per block row: returns (in lanes 0..5, component = lane) row i of B·v
+__device__ __forceinline__ double bsr_row(const Gn& g, int row, const double* __restrict__ v, double* s_acc) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int row = blockIdx.x * kRowsPerWG + wv;
-  double pq = 0.0;
   double acc = 0.0;
   if (row < g.N && lane < 60) {
-    const int bl = lane / 6, rrw = lane % 6;
+    const int bl = lane / 6, rr = lane % 6;
     const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
     for (int bi = b0 + bl; bi < b1; bi += 10) {
       const int c = g.col[bi];
-      const double* blk = A + 36 * (int64_t)bi + rrw * 6;
+      const double* blk = g.Bm + 36 * (int64_t)bi + rr * 6;
+      const double* vc = v + 6 * (int64_t)c;
       double s = 0.0;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) s += blk[j] * (g.z[6 * c + j] + beta * pold[6 * c + j]);
+      for (int j = 0; j < 6; ++j) s += blk[j] * vc[j];
       acc += s;
     }
   }
   s_acc[threadIdx.x] = acc;
   __syncthreads();
-  if (row < g.N && lane < 6) {
-    double qv = 0.0;
+  double out = 0.0;
+  if (lane < 6) {
 #pragma unroll
-    for (int b = 0; b < 10; ++b) qv += s_acc[wv * 64 + b * 6 + lane];
-    double pn = g.z[6 * row + lane] + beta * pold[6 * row + lane];
-    pnew[6 * row + lane] = pn;
-    g.q[6 * row + lane] = qv;
-    pq = pn * qv;
+    for (int b = 0; b < 10; ++b) out += s_acc[wv * 64 + b * 6 + lane];
   }
-  double s = block_sum(pq);
-  if (threadIdx.x == 0) g.part_s[blockIdx.x] = s;
+  __syncthreads();
+  return out;
 }
 
-// x += a p, r -= a q, z = M⁻¹ r, partials (r·z, r·r) -> PU[it&1].  thread per node.
-__global__ __launch_bounds__(kBlk) void k_pcg_update(Gn g, int it) {
+// w0 = A u0 = B b; partials (γ0 = r·u, δ0 = w·u, r·r) -> PP[0], bb -> PB.
+__global__ __launch_bounds__(kBlk) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
+  if (g.flags[F_STOPPED]) return;
+  __shared__ double s_acc[kBlk];
+  const int lane = threadIdx.x & 63;
+  double ga = 0.0, de = 0.0, rr = 0.0;
+  for (int row0 = blockIdx.x * kRowsPerWG; row0 < g.N; row0 += gridDim.x * kRowsPerWG) {
+    const int row = row0 + (threadIdx.x >> 6);
+    double wv = bsr_row(g, row, rhs, s_acc);
+    if (row < g.N && lane < 6) {
+      const int64_t o = 6 * (int64_t)row + lane;
+      g.w0[o] = wv;
+      double r = g.r[o], u = g.u[o];
+      ga += r * u; de += wv * u; rr += r * r;
+    }
+  }
+  double s0 = block_sum(ga), s1 = block_sum(de), s2 = block_sum(rr);
+  if (threadIdx.x == 0) {
+    double* P = g.part_p + 3 * (int64_t)blockIdx.x;
+    P[0] = s0; P[1] = s1; P[2] = s2;
+    g.part_b[blockIdx.x] = s2;
+  }
+}
+
+// iteration it (reads PP[it&1], W[it&1]; writes PP[(it+1)&1], W[(it+1)&1]).
+__global__ __launch_bounds__(kBlk) void k_pcg_iter(Gn g, int it) {
   if (g.flags[F_DONE] || g.flags[F_STOPPED]) return;
-  const double* PUc = g.part_u + 2 * (int64_t)g.nwg_node * ((it - 1) & 1);
-  const double rz = wg_sum_fixed(PUc, g.nwg_node, 2, 0);
-  const double pq = wg_sum_fixed(g.part_s, g.nwg_row, 1, 0);
-  if (!(pq > 0.0) || !isfinite(pq)) {  // breakdown: keep x
+  const int nw = g.nwg_row;
+  const double* PP = g.part_p + 3 * (int64_t)nw * (it & 1);
+  const double gam = wg_sum_fixed(PP, nw, 3, 0);
+  const double del = wg_sum_fixed(PP, nw, 3, 1);
+  const double rr = wg_sum_fixed(PP, nw, 3, 2);
+  const double bb = wg_sum_fixed(g.part_b, nw, 1, 0);
+  const double tol = g.prm.pcg_tol;
+  if (rr <= tol * tol * bb || gam == 0.0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
+    return;
+  }
+  double beta = 0.0, alpha;
+  if (it == 0) {
+    alpha = gam / del;
+  } else {
+    beta = gam / g.pcg_gamma[it - 1];
+    alpha = gam / (del - beta * gam / g.pcg_alpha[it - 1]);
+  }
+  if (!isfinite(alpha) || !(alpha > 0.0)) {  // breakdown (A SPD => alpha > 0): keep x
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
-      if (!isfinite(pq)) g.flags[F_ILL] = 1;
+      if (!isfinite(alpha)) g.flags[F_ILL] = 1;
     }
     return;
   }
-  const double alpha = rz / pq;
-  const double* __restrict__ p = (it & 1) ? g.p1 : g.p0;
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  double rzn = 0.0, rrn = 0.0;
-  if (i < g.N) {
-    double rv[6], zv[6];
+  if (blockIdx.x == 0 && threadIdx.x == 0) { g.pcg_alpha[it] = alpha; g.pcg_gamma[it] = gam; }
+  const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
+  double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
+  __shared__ double s_acc[kBlk];
+  const int lane = threadIdx.x & 63;
+  double ga = 0.0, de = 0.0, rn = 0.0;
+  for (int row0 = blockIdx.x * kRowsPerWG; row0 < g.N; row0 += gridDim.x * kRowsPerWG) {
+    const int row = row0 + (threadIdx.x >> 6);
+    const double n = bsr_row(g, row, wc, s_acc);       // n = A M⁻¹ w
+    if (row < g.N && lane < 6) {
+      const int64_t o = 6 * (int64_t)row + lane;
+      const double* Mi = g.Minv + 36 * (int64_t)row + 6 * lane;
+      const double* wi = wc + 6 * (int64_t)row;
+      double m = 0.0;
 #pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      g.x[6 * i + c] += alpha * p[6 * i + c];
-      rv[c] = g.r[6 * i + c] - alpha * g.q[6 * i + c];
-      g.r[6 * i + c] = rv[c];
-      rrn += rv[c] * rv[c];
+      for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];    // m = M⁻¹ w (own row)
+      const double w = wc[o];
+      const double zz = n + beta * g.zz[o];
+      const double q = m + beta * g.qv[o];
+      const double s = w + beta * g.sv[o];
+      const double p = g.u[o] + beta * g.pv[o];
+      g.zz[o] = zz; g.qv[o] = q; g.sv[o] = s; g.pv[o] = p;
+      g.x[o] += alpha * p;
+      const double r = g.r[o] - alpha * s;
+      const double u = g.u[o] - alpha * q;
+      const double w2 = w - alpha * zz;
+      g.r[o] = r; g.u[o] = u; wn[o] = w2;
+      ga += r * u; de += w2 * u; rn += r * r;
     }
-    double L[21];
-    const double* Ld = g.L + 24 * (int64_t)i;
-#pragma unroll
-    for (int c = 0; c < 21; ++c) L[c] = Ld[c];
-    chol6_solve(L, rv, zv);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) { g.z[6 * i + c] = zv[c]; rzn += rv[c] * zv[c]; }
   }
-  double s_rz = block_sum(rzn), s_rr = block_sum(rrn);
+  double s0 = block_sum(ga), s1 = block_sum(de), s2 = block_sum(rn);
   if (threadIdx.x == 0) {
-    double* PU = g.part_u + 2 * (int64_t)g.nwg_node * (it & 1);
-    PU[2 * blockIdx.x] = s_rz;
-    PU[2 * blockIdx.x + 1] = s_rr;
+    double* P = g.part_p + 3 * (int64_t)nw * ((it + 1) & 1) + 3 * (int64_t)blockIdx.x;
+    P[0] = s0; P[1] = s1; P[2] = s2;
   }
 }
 
@@ -704,8 +755,9 @@ static double lm_for_iter(double lm0, int gn_iter) {
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->row_cnt, g->blk_off, g->blk_cnt,
-                  g->blk_list, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->L, g->x,
-                  g->r, g->z, g->p0, g->p1, g->q, g->part_s, g->part_u, g->part_b, g->part_loss, g->scal, g->flags,
+                  g->blk_list, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
+                  g->x, g->r, g->u, g->w0, g->w1, g->zz, g->qv, g->sv, g->pv, g->pcg_alpha, g->pcg_gamma,
+                  g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
                   g->loss_log};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -715,29 +767,29 @@ static void free_all(Gn* g) {
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
   hipLaunchKernelGGL(k_pcg_prep, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
+  if (g->nnzb > 0)
+    hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
+  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
   const int max_it = g->prm.pcg_max_iter;
-  int chunk = g->last_pcg > 0 ? ((g->last_pcg + 4 + 7) / 8) * 8 : 64;
+  int chunk = g->last_pcg > 0 ? ((g->last_pcg + 2 + 7) / 8) * 8 : 64;
   int it = 0;
   while (it < max_it) {
     int n = chunk < max_it - it ? chunk : max_it - it;
-    for (int k = 0; k < n; ++k, ++it) {
-      hipLaunchKernelGGL(k_pcg_spmv, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, (const double*)A, it);
-      hipLaunchKernelGGL(k_pcg_update, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, it);
-    }
+    for (int k = 0; k < n; ++k, ++it)
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, it);
     OFX_LAUNCH_CHECK();
-    if (it >= max_it) break;
-    // one extra convergence probe so the final residual test runs on device
-    hipLaunchKernelGGL(k_pcg_spmv, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, (const double*)A, it);
+    // convergence probe: k_pcg_iter(it) tests |r| first and only iterates if not converged
+    if (it < max_it) {
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, it);
+      ++it;
+    }
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
     OFX_HIP(hipStreamSynchronize(hs));
     if (g->host_flags[F_DONE]) {
       g->last_pcg = g->host_flags[F_PCG_IT];
       break;
     }
-    // the probe computed q = A p for iteration `it`; run its update and continue
-    hipLaunchKernelGGL(k_pcg_update, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, it);
-    ++it;
     chunk = 16;
   }
   return OFX_OK;
@@ -764,10 +816,10 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 1);
   ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
-  ALLOC(g->L, 24 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->z, 6 * N);
-  ALLOC(g->p0, 6 * N); ALLOC(g->p1, 6 * N); ALLOC(g->q, 6 * N);
-  int64_t nwg_row = (N + kRowsPerWG - 1) / kRowsPerWG, nwg_node = (N + kBlk - 1) / kBlk;
-  ALLOC(g->part_s, nwg_row); ALLOC(g->part_u, 4 * nwg_node); ALLOC(g->part_b, nwg_node);
+  ALLOC(g->Minv, 36 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->u, 6 * N);
+  ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N); ALLOC(g->zz, 6 * N); ALLOC(g->qv, 6 * N); ALLOC(g->sv, 6 * N);
+  ALLOC(g->pv, 6 * N);
+  ALLOC(g->part_p, 6 * kMaxSpmvWG); ALLOC(g->part_b, kMaxSpmvWG);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
@@ -803,7 +855,15 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   g->N = N; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
   g->T = (int64_t)M + (int64_t)N * NB + N;
+  if (prm->pcg_max_iter + 1 > g->pcg_cap) {
+    if (g->pcg_alpha) OFX_HIP(hipFree(g->pcg_alpha));
+    if (g->pcg_gamma) OFX_HIP(hipFree(g->pcg_gamma));
+    g->pcg_cap = prm->pcg_max_iter + 1;
+    OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
+  }
   g->nwg_row = (N + kRowsPerWG - 1) / kRowsPerWG;
+  if (g->nwg_row > kMaxSpmvWG) g->nwg_row = kMaxSpmvWG;
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T
@@ -858,11 +918,12 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
-    for (auto pp : {(void**)&g->col, (void**)&g->A_own, (void**)&g->blk_off, (void**)&g->blk_cnt})
+    for (auto pp : {(void**)&g->col, (void**)&g->A_own, (void**)&g->Bm, (void**)&g->blk_off, (void**)&g->blk_cnt})
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     g->nnzb_cap = (int64_t)nnz + nnz / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->col, g->nnzb_cap * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->A_own, g->nnzb_cap * 36 * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->Bm, g->nnzb_cap * 36 * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->blk_off, (g->nnzb_cap + 1) * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_cnt, (g->nnzb_cap + 1) * sizeof(int32_t)));
   }

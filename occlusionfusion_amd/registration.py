@@ -18,6 +18,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr, stream_ptr, byref
+from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
                    lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=1000, pcg_tol=1e-8)
@@ -146,7 +147,7 @@ class GaussNewtonSolver:
         call("ofx_gn_setup", self._h, byref(pb), byref(prm), byref(nnz), stream_ptr())
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
-        m0, m1 = (M * rank) // world, (M * (rank + 1)) // world
+        m0, m1 = match_range(M, rank, world)
         A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=self.device)
         rhs = torch.empty(6 * N + 4, dtype=torch.float64, device=self.device)
         for it in range(int(self.params["num_iter"])):

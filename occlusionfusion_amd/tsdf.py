@@ -16,6 +16,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr, stream_ptr, byref
+from .sharding import shard_bricks  # noqa: F401  (re-exported: reference-style import path)
 
 log = logging.getLogger(__name__)
 TRUNC_MARGIN = 0.04  # tsdf.py:127
@@ -48,13 +49,6 @@ def volume_geometry(bbox, max_depth, cam_intr, voxel_dim=None, voxel_size=None):
         raise ValueError("fopt needs voxel_dim or voxel_size")
     vol_bnds[:, 1] = vol_bnds[:, 0] + vol_dim * vs
     return vol_bnds, vol_dim.astype(np.int64), vs, vol_bnds[:, 0].astype(np.float32)
-
-
-def shard_bricks(n_bricks_x, rank, world):
-    """Contiguous x-slab of bricks for `rank` of `world` (spatial volume sharding)."""
-    base, rem = divmod(n_bricks_x, world)
-    x0 = rank * base + min(rank, rem)
-    return x0, x0 + base + (1 if rank < rem else 0)
 
 
 class TSDFVolume:

@@ -1,0 +1,120 @@
+"""CPU, world_size 2 over gloo: the two multi-GPU data paths, with the oracle doing the math.
+
+1. Volume sharding: each rank fuses its x-slab of bricks (sharding.shard_bricks); all_gather of the
+   slabs equals the single-process volume bit for bit (voxels are independent, no halo).
+2. Match-sharded GN: each rank linearises its match range (sharding.match_range), rank 0 adds the
+   ARAP + motion rows; all_reduce(sum) of (A, b, loss²) equals the full system.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # surface worker failures to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return out
+
+
+def volume_shard_job(rank, world):
+    from oracle import fusion_oracle as fo
+    from occlusionfusion_amd.sharding import shard_bricks
+    g = np.load(os.path.join(ROOT, "tests/golden/integrate_small.npz"))
+    dims = g["dims"]
+    nbx = (int(dims[0]) + 7) // 8
+    x0, x1 = shard_bricks(nbx, rank, world)
+    lo, hi = 8 * x0, min(8 * x1, int(dims[0]))
+    world_pts = fo.world_points(g["origin"], dims, float(g["voxel_size"])).reshape(int(dims[0]), -1, 3)[lo:hi]
+    pts = world_pts.reshape(-1, 3)
+    V = pts.shape[0]
+    t, w, c = np.ones(V, np.float32), np.zeros(V, np.float32), np.zeros(V, np.float32)
+    intr = tuple(g["intr"])
+    fo.integrate(t, w, c, pts, np.ones(V, bool), fo.depth_of(g["im0"]), fo.pack_color(g["im0"]), intr)
+    a, ww, v = fo.skin(pts, g["nodes"], float(g["node_coverage"]))
+    x = fo.ed_warp(pts, a, ww, v, g["R"], g["T"], g["nodes"])
+    fo.integrate(t, w, c, x, v, fo.depth_of(g["im1"]), fo.pack_color(g["im1"]), intr)
+    # gather variable-size slabs (pad to the largest)
+    n = torch.tensor([V])
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    mx = int(max(s.item() for s in sizes))
+    buf = torch.zeros(3, mx)
+    buf[0, :V], buf[1, :V], buf[2, :V] = torch.from_numpy(t), torch.from_numpy(w), torch.from_numpy(c)
+    outs = [torch.zeros(3, mx) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    full = torch.cat([o[:, :int(s.item())] for o, s in zip(outs, sizes)], 1).numpy()
+    ok = (np.array_equal(full[0], g["tsdf1"]) and np.array_equal(full[1], g["weight1"])
+          and np.array_equal(full[2], g["color1"]))
+    return bool(ok)
+
+
+def gn_shard_job(rank, world):
+    from oracle import fusion_oracle as fo
+    from occlusionfusion_amd.sharding import match_range
+    g = np.load(os.path.join(ROOT, "tests/golden/gn_small.npz"))
+    sel = slice(0, 200)
+    M = 200
+    N = len(g["nodes"])
+    rng = np.random.default_rng(1)
+    R = fo.angle_axis_to_rotation_matrix(rng.normal(0, 0.01, (N, 3)))
+    t = rng.normal(0, 0.005, (N, 3))
+    m0, m1 = match_range(M, rank, world)
+    args = (g["nodes"], g["edges"], g["tpos"], g["conf"])
+    loc = fo.gn_system(*args, g["src"][m0:m1], g["anchors"][m0:m1], g["weights"][m0:m1], g["tgt"][m0:m1], g["intr"],
+                       R, t, lm_factor=0.0, include_data=True, include_reg=(rank == 0))
+    A = torch.from_numpy(loc["A"])
+    b = torch.from_numpy(loc["b"])
+    l2 = torch.tensor([loc["loss2"]], dtype=torch.float64)
+    for x in (A, b, l2):
+        dist.all_reduce(x)
+    full = fo.gn_system(*args, g["src"][sel], g["anchors"][sel], g["weights"][sel], g["tgt"][sel], g["intr"], R, t,
+                        lm_factor=0.0)
+    return bool(np.allclose(A.numpy(), full["A"], rtol=1e-12, atol=1e-12)
+                and np.allclose(b.numpy(), full["b"], rtol=1e-12, atol=1e-14)
+                and abs(l2.item() - full["loss2"]) <= 1e-12 * max(1.0, full["loss2"]))
+
+
+@pytest.mark.slow
+def test_volume_sharding_world2_equals_full():
+    out = _run(volume_shard_job)
+    assert out == {0: True, 1: True}, out
+
+
+def test_match_sharded_gn_allreduce_world2_equals_full():
+    out = _run(gn_shard_job)
+    assert out == {0: True, 1: True}, out

@@ -1,0 +1,90 @@
+"""CPU: host-side logic of the product (geometry, sharding, synthetic inputs, solver defaults)."""
+import numpy as np
+import pytest
+
+from oracle import fusion_oracle as fo
+
+
+@pytest.mark.parametrize("kw", [dict(voxel_size=0.01), dict(voxel_size=0.004), dict(voxel_dim=128),
+                                dict(voxel_dim=[64, 80, 96])])
+def test_volume_geometry_matches_reference_restatement(kw):
+    from occlusionfusion_amd.tsdf import volume_geometry
+    args = ((100, 50, 500, 400), 2.3, (525.0, 525.0, 319.5, 223.5))
+    vb, dim, vs, origin = volume_geometry(*args, **kw)
+    ovb, odim, ovs, oorigin, _ = fo.volume_geometry(*args, **kw)
+    np.testing.assert_array_equal(vb, ovb)
+    np.testing.assert_array_equal(dim, odim)
+    assert vs == ovs
+    np.testing.assert_array_equal(origin, oorigin)
+
+
+@pytest.mark.parametrize("n,world", [(64, 1), (64, 2), (64, 8), (9, 4), (3, 8)])
+def test_shard_bricks_partition(n, world):
+    from occlusionfusion_amd.sharding import shard_bricks
+    parts = [shard_bricks(n, r, world) for r in range(world)]
+    assert parts[0][0] == 0 and parts[-1][1] == n
+    for (a0, a1), (b0, b1) in zip(parts, parts[1:]):
+        assert a1 == b0 and a0 <= a1
+    sizes = [b - a for a, b in parts]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_match_range_partition():
+    from occlusionfusion_amd.sharding import match_range
+    for M, W in [(10000, 8), (7, 3), (0, 2)]:
+        rs = [match_range(M, r, W) for r in range(W)]
+        assert rs[0][0] == 0 and rs[-1][1] == M
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+def test_synthetic_graph_properties():
+    from occlusionfusion_amd import synthetic as S
+    cam = S.bench_camera(4)
+    d = S.SphereScene().render(cam, 0, np.random.default_rng(0))
+    pts = S.backproject(d, cam)
+    cov = 0.08
+    nodes = S.sample_nodes(pts, cov, 0)
+    dd = np.sqrt(((nodes[:, None] - nodes[None]) ** 2).sum(-1)) + np.eye(len(nodes)) * 10
+    assert dd.min() > cov                                    # coverage rule of csrc sample_nodes
+    near = np.sqrt(((pts[:, None] - nodes[None]) ** 2).sum(-1)).min(1)
+    assert near.max() <= cov + 1e-6                          # every surface point is covered
+    e, w = S.euclidean_edges(nodes, 8)
+    assert (e != np.arange(len(nodes))[:, None]).all()
+    assert np.allclose(w[e >= 0], 1 / 8)
+
+
+def test_bench_camera_crop():
+    from occlusionfusion_amd import synthetic as S
+    c = S.bench_camera()
+    assert (c.width, c.height, c.cy) == (640, 448, 223.5)
+
+
+def test_gn_defaults_match_reference_constants():
+    from occlusionfusion_amd.registration import GN_DEFAULTS, MAX_MATCHES_EVAL
+    # model.py:91-114, custom_settings.py:36,41
+    assert GN_DEFAULTS["num_iter"] == 10 and GN_DEFAULTS["lambda_flow"] == 0 and GN_DEFAULTS["lambda_depth"] == 1
+    assert GN_DEFAULTS["lambda_arap"] == 0.5 and GN_DEFAULTS["lambda_motion"] == 1
+    assert GN_DEFAULTS["lm_factor"] == 1e-7 and GN_DEFAULTS["stop_loss_diff"] == 1
+    assert GN_DEFAULTS["use_edge_weighting"] is False and MAX_MATCHES_EVAL == 10000
+    for k, v in fo.GN_DEFAULTS.items():
+        assert GN_DEFAULTS[k] == v
+
+
+def test_c_oracle_matches_numpy_oracle(golden_dir):
+    import os
+    from oracle import cpu_ref
+    g = np.load(os.path.join(golden_dir, "integrate_small.npz"))
+    V = int(np.prod(g["dims"]))
+    t, w, c = np.ones(V, np.float32), np.zeros(V, np.float32), np.zeros(V, np.float32)
+    cpu_ref.integrate(g["dims"], g["origin"], float(g["voxel_size"]), np.arange(V), fo.depth_of(g["im0"]),
+                      fo.pack_color(g["im0"]), g["intr"], t, w, c)
+    np.testing.assert_array_equal(t, g["tsdf0"])
+    world = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))
+    a, ww, v = fo.skin(world, g["nodes"], float(g["node_coverage"]))
+    n = cpu_ref.integrate(g["dims"], g["origin"], float(g["voxel_size"]), np.arange(V), fo.depth_of(g["im1"]),
+                          fo.pack_color(g["im1"]), g["intr"], t, w, c, warp=True, anchors=a, weights=ww, valid=v,
+                          R=g["R"], T=g["T"], nodes=g["nodes"])
+    assert n == int(g["n_updated1"])
+    np.testing.assert_array_equal(t, g["tsdf1"])
+    np.testing.assert_array_equal(w, g["weight1"])
+    np.testing.assert_array_equal(c, g["color1"])

@@ -39,7 +39,8 @@ def test_skin_weights_match_reference_csrc(golden_dir):
     g = _load(golden_dir, "skin_csrc.npz")
     ov, ow = g["oracle_valid"], g["oracle_weights"].astype(np.float64)
     cw = g["csrc_weights"].astype(np.float64)
-    rescaled = ow / ow.sum(1, keepdims=True)          # w/(S+1e-6) renormalised = w/S
+    with np.errstate(invalid="ignore"):
+        rescaled = ow / ow.sum(1, keepdims=True)      # w/(S+1e-6) renormalised = w/S
     np.testing.assert_allclose(rescaled[ov], cw[ov], rtol=2e-5, atol=1e-7)
     assert (g["oracle_anchors"][ov] == g["csrc_anchors"][ov]).mean() > 0.999
 

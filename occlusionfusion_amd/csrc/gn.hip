@@ -76,8 +76,8 @@ enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_
        F_PCG_IT = 7, F_COUNT = 8 };
 enum { S_LOSS_PREV = 0, S_COUNT = 4 };
 constexpr int kBlk = 256;       // threads per WG
-constexpr int kRowsPerWG = 4;   // SpMV: one wave per block row
-constexpr int kMaxSpmvWG = 128; // bounded grid: fewer partials for the consumer to re-read
+constexpr int kRowBlk = 1024;   // PCG row kernels: 16 waves per WG, one block row per wave
+constexpr int kRowsPerWG = kRowBlk / 64;
 
 // ---------------------------------------------------------------------------- reductions
 __device__ __forceinline__ double block_sum(double v) {
@@ -537,15 +537,17 @@ __global__ __launch_bounds__(kBlk) void k_pcg_bmat(Gn g, const double* __restric
     }
 }
 
-// one wave per block row: returns (in lanes 0..5, component = lane) row i of B·v
-__device__ __forceinline__ double bsr_row(const Gn& g, int row, const double* __restrict__ v, double* s_acc) {
+// One wave per block row. Lane = rr*8 + b (rr = block row component 0..5, b = block slot 0..7):
+// lane accumulates B[row][blk][rr][:]·v[col] over blocks b, b+8, ...; a 3-step xor butterfly inside
+// each aligned group of 8 lanes leaves component rr of (B·v)[row] in every lane of group rr.
+// No LDS and no barrier inside the row.
+__device__ __forceinline__ double bsr_row(const Gn& g, int row, const double* __restrict__ v) {
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
   double acc = 0.0;
-  if (row < g.N && lane < 60) {
-    const int bl = lane / 6, rr = lane % 6;
+  if (row < g.N && lane < 48) {
+    const int rr = lane >> 3, bl = lane & 7;
     const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-    for (int bi = b0 + bl; bi < b1; bi += 10) {
+    for (int bi = b0 + bl; bi < b1; bi += 8) {
       const int c = g.col[bi];
       const double* blk = g.Bm + 36 * (int64_t)bi + rr * 6;
       const double* vc = v + 6 * (int64_t)c;
@@ -555,50 +557,123 @@ __device__ __forceinline__ double bsr_row(const Gn& g, int row, const double* __
       acc += s;
     }
   }
-  s_acc[threadIdx.x] = acc;
-  __syncthreads();
-  double out = 0.0;
-  if (lane < 6) {
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  return acc;
+}
+
+// fixed-order sums of up to 4 interleaved partial streams (every thread gets identical bits)
+template <int NV>
+__device__ __forceinline__ void wg_sum4(const double* __restrict__ p, int n, int stride, double out[4]) {
+  constexpr int nv = NV;
+  __shared__ double s_r[4];
+  if (threadIdx.x < 64) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < n; i += 64)
 #pragma unroll
-    for (int b = 0; b < 10; ++b) out += s_acc[wv * 64 + b * 6 + lane];
+      for (int k = 0; k < nv; ++k) a[k] += p[(int64_t)i * stride + k];
+#pragma unroll
+    for (int k = 0; k < nv; ++k)
+      for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int k = 0; k < nv; ++k) s_r[k] = a[k];
   }
   __syncthreads();
-  return out;
+#pragma unroll
+  for (int k = 0; k < nv; ++k) out[k] = s_r[k];
+  __syncthreads();
+}
+
+// fixed-shape WG sum of 3 values (1024 threads): wave butterflies, then wave partials in order
+__device__ __forceinline__ void wg_sum3(double v[3], double out[3]) {
+  __shared__ double s_w[3][kRowBlk / 64];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s_w[k][threadIdx.x >> 6] = v[k];
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double a = 0.0;
+    for (int w = 0; w < nw; ++w) a += s_w[k][w];
+    out[k] = a;
+  }
 }
 
 // w0 = A u0 = B b; partials (γ0 = r·u, δ0 = w·u, r·r) -> PP[0], bb -> PB.
-__global__ __launch_bounds__(kBlk) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
+__global__ __launch_bounds__(kRowBlk) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
-  __shared__ double s_acc[kBlk];
   const int lane = threadIdx.x & 63;
-  double ga = 0.0, de = 0.0, rr = 0.0;
-  for (int row0 = blockIdx.x * kRowsPerWG; row0 < g.N; row0 += gridDim.x * kRowsPerWG) {
-    const int row = row0 + (threadIdx.x >> 6);
-    double wv = bsr_row(g, row, rhs, s_acc);
-    if (row < g.N && lane < 6) {
-      const int64_t o = 6 * (int64_t)row + lane;
-      g.w0[o] = wv;
-      double r = g.r[o], u = g.u[o];
-      ga += r * u; de += wv * u; rr += r * r;
-    }
+  const int row = blockIdx.x * kRowsPerWG + (threadIdx.x >> 6);
+  double v[3] = {0.0, 0.0, 0.0};
+  const double wv = bsr_row(g, row, rhs);
+  if (row < g.N && lane < 48 && (lane & 7) == 0) {
+    const int64_t o = 6 * (int64_t)row + (lane >> 3);
+    g.w0[o] = wv;
+    double r = g.r[o], u = g.u[o];
+    v[0] = r * u; v[1] = wv * u; v[2] = r * r;
   }
-  double s0 = block_sum(ga), s1 = block_sum(de), s2 = block_sum(rr);
+  double s[3];
+  wg_sum3(v, s);
   if (threadIdx.x == 0) {
     double* P = g.part_p + 3 * (int64_t)blockIdx.x;
-    P[0] = s0; P[1] = s1; P[2] = s2;
-    g.part_b[blockIdx.x] = s2;
+    P[0] = s[0]; P[1] = s[1]; P[2] = s[2];
+    g.part_b[blockIdx.x] = s[2];
   }
 }
 
 // iteration it (reads PP[it&1], W[it&1]; writes PP[(it+1)&1], W[(it+1)&1]).
-__global__ __launch_bounds__(kBlk) void k_pcg_iter(Gn g, int it) {
-  if (g.flags[F_DONE] || g.flags[F_STOPPED]) return;
+// Latency schedule: the SpMV chain (row_ptr -> B,col -> w[col]) and the own-row vector loads do not
+// depend on this iteration's scalars, so they are issued first; wave 0 meanwhile loads the partials
+// of the previous kernel; one barrier publishes the scalars; then the recurrences + partial dots.
+__global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
+  __shared__ double s_sc[4];
+  __shared__ int s_stop;
   const int nw = g.nwg_row;
-  const double* PP = g.part_p + 3 * (int64_t)nw * (it & 1);
-  const double gam = wg_sum_fixed(PP, nw, 3, 0);
-  const double del = wg_sum_fixed(PP, nw, 3, 1);
-  const double rr = wg_sum_fixed(PP, nw, 3, 2);
-  const double bb = wg_sum_fixed(g.part_b, nw, 1, 0);
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kRowsPerWG + (threadIdx.x >> 6);
+  const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
+  double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
+  // wave 0: previous partials (γ, δ, r·r) and b·b, plus the stop flags
+  double pa[4] = {0.0, 0.0, 0.0, 0.0};
+  int stop = 0;
+  if (threadIdx.x < 64) {
+    const double* PP = g.part_p + 3 * (int64_t)nw * (it & 1);
+    for (int i = threadIdx.x; i < nw; i += 64) {
+      pa[0] += PP[3 * i]; pa[1] += PP[3 * i + 1]; pa[2] += PP[3 * i + 2]; pa[3] += g.part_b[i];
+    }
+    stop = g.flags[F_DONE] | g.flags[F_STOPPED];
+  }
+  // SpMV n = A M⁻¹ w for this wave's row (independent of the scalars)
+  const double n = bsr_row(g, row, wc);
+  const bool upd = row < g.N && lane < 48 && (lane & 7) == 0;
+  const int c = lane >> 3;
+  const int64_t o = 6 * (int64_t)row + c;
+  double m = 0.0, w = 0.0, zz0 = 0.0, q0 = 0.0, s0 = 0.0, p0 = 0.0, u0 = 0.0, r0 = 0.0;
+  if (upd) {
+    const double* Mi = g.Minv + 36 * (int64_t)row + 6 * c;
+    const double* wi = wc + 6 * (int64_t)row;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];      // m = M⁻¹ w (own row)
+    w = wc[o]; zz0 = g.zz[o]; q0 = g.qv[o]; s0 = g.sv[o]; p0 = g.pv[o]; u0 = g.u[o]; r0 = g.r[o];
+  }
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      for (int off = 32; off > 0; off >>= 1) pa[k] += __shfl_xor(pa[k], off, 64);
+    if (threadIdx.x == 0) {
+      s_sc[0] = pa[0]; s_sc[1] = pa[1]; s_sc[2] = pa[2]; s_sc[3] = pa[3];
+      s_stop = stop;
+    }
+  }
+  __syncthreads();
+  if (s_stop) return;
+  const double gam = s_sc[0], del = s_sc[1], rr = s_sc[2], bb = s_sc[3];
   const double tol = g.prm.pcg_tol;
   if (rr <= tol * tol * bb || gam == 0.0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
@@ -619,39 +694,25 @@ __global__ __launch_bounds__(kBlk) void k_pcg_iter(Gn g, int it) {
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) { g.pcg_alpha[it] = alpha; g.pcg_gamma[it] = gam; }
-  const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
-  double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
-  __shared__ double s_acc[kBlk];
-  const int lane = threadIdx.x & 63;
-  double ga = 0.0, de = 0.0, rn = 0.0;
-  for (int row0 = blockIdx.x * kRowsPerWG; row0 < g.N; row0 += gridDim.x * kRowsPerWG) {
-    const int row = row0 + (threadIdx.x >> 6);
-    const double n = bsr_row(g, row, wc, s_acc);       // n = A M⁻¹ w
-    if (row < g.N && lane < 6) {
-      const int64_t o = 6 * (int64_t)row + lane;
-      const double* Mi = g.Minv + 36 * (int64_t)row + 6 * lane;
-      const double* wi = wc + 6 * (int64_t)row;
-      double m = 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];    // m = M⁻¹ w (own row)
-      const double w = wc[o];
-      const double zz = n + beta * g.zz[o];
-      const double q = m + beta * g.qv[o];
-      const double s = w + beta * g.sv[o];
-      const double p = g.u[o] + beta * g.pv[o];
-      g.zz[o] = zz; g.qv[o] = q; g.sv[o] = s; g.pv[o] = p;
-      g.x[o] += alpha * p;
-      const double r = g.r[o] - alpha * s;
-      const double u = g.u[o] - alpha * q;
-      const double w2 = w - alpha * zz;
-      g.r[o] = r; g.u[o] = u; wn[o] = w2;
-      ga += r * u; de += w2 * u; rn += r * r;
-    }
+  double v[3] = {0.0, 0.0, 0.0};
+  if (upd) {
+    const double zz = n + beta * zz0;
+    const double q = m + beta * q0;
+    const double sv = w + beta * s0;
+    const double p = u0 + beta * p0;
+    g.zz[o] = zz; g.qv[o] = q; g.sv[o] = sv; g.pv[o] = p;
+    g.x[o] += alpha * p;
+    const double r = r0 - alpha * sv;
+    const double u = u0 - alpha * q;
+    const double w2 = w - alpha * zz;
+    g.r[o] = r; g.u[o] = u; wn[o] = w2;
+    v[0] = r * u; v[1] = w2 * u; v[2] = r * r;
   }
-  double s0 = block_sum(ga), s1 = block_sum(de), s2 = block_sum(rn);
+  double s3[3];
+  wg_sum3(v, s3);
   if (threadIdx.x == 0) {
     double* P = g.part_p + 3 * (int64_t)nw * ((it + 1) & 1) + 3 * (int64_t)blockIdx.x;
-    P[0] = s0; P[1] = s1; P[2] = s2;
+    P[0] = s3[0]; P[1] = s3[1]; P[2] = s3[2];
   }
 }
 
@@ -769,7 +830,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   hipLaunchKernelGGL(k_pcg_prep, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
   if (g->nnzb > 0)
     hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
-  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, (const double*)rhs);
+  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
   const int max_it = g->prm.pcg_max_iter;
   int chunk = g->last_pcg > 0 ? ((g->last_pcg + 2 + 7) / 8) * 8 : 64;
@@ -777,11 +838,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   while (it < max_it) {
     int n = chunk < max_it - it ? chunk : max_it - it;
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, it);
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, it);
     OFX_LAUNCH_CHECK();
     // convergence probe: k_pcg_iter(it) tests |r| first and only iterates if not converged
     if (it < max_it) {
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kBlk), 0, hs, *g, it);
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, it);
       ++it;
     }
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
@@ -819,7 +880,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->Minv, 36 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->u, 6 * N);
   ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N); ALLOC(g->zz, 6 * N); ALLOC(g->qv, 6 * N); ALLOC(g->sv, 6 * N);
   ALLOC(g->pv, 6 * N);
-  ALLOC(g->part_p, 6 * kMaxSpmvWG); ALLOC(g->part_b, kMaxSpmvWG);
+  const int64_t max_row_wg = (N + kRowsPerWG - 1) / kRowsPerWG;
+  ALLOC(g->part_p, 6 * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
@@ -863,7 +925,6 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
   g->nwg_row = (N + kRowsPerWG - 1) / kRowsPerWG;
-  if (g->nwg_row > kMaxSpmvWG) g->nwg_row = kMaxSpmvWG;
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T

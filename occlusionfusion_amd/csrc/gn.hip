@@ -27,6 +27,7 @@
 //    workgroup of the NEXT kernel re-derives the same scalars from them in a fixed order (kernel
 //    boundaries give visibility; no fences, no tickets). The host only polls convergence in chunks.
 #include <math.h>
+#include <utility>
 #include <vector>
 
 #include "ofx_common.h"
@@ -51,8 +52,8 @@ struct Gn {
   int64_t T_cap = 0;
   // pattern + contribution lists
   int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;
-  int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr;
-  int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr;
+  int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr, *blk_tmp = nullptr;
+  int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr, *node_tmp = nullptr;
   int64_t nnzb = 0, nnzb_cap = 0;
   // state
   double *R = nullptr, *t = nullptr;
@@ -252,15 +253,20 @@ __global__ void k_pair_scatter(Gn g) {
   }
 }
 
-__global__ void k_seg_sort(const int32_t* __restrict__ off, int64_t nseg, int32_t* __restrict__ list) {
-  int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (s >= nseg) return;
-  int b = off[s], e = off[s + 1];
-  for (int i = b + 1; i < e; ++i) {
-    int v = list[i];
-    int j = i - 1;
-    while (j >= b && list[j] > v) { list[j + 1] = list[j]; --j; }
-    list[j + 1] = v;
+// Deterministic ordering of each segment (values are unique codes): one wave per segment, every
+// lane ranks its entries against the whole segment (independent loads, no serial chain), and
+// scatters them to their rank in `out`.
+__global__ __launch_bounds__(256) void k_seg_rank(const int32_t* __restrict__ off, int64_t nseg,
+                                                  const int32_t* __restrict__ in, int32_t* __restrict__ out) {
+  const int64_t sgm = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (sgm >= nseg) return;
+  const int b = off[sgm], n = off[sgm + 1] - b;
+  for (int k = lane; k < n; k += 64) {
+    const int v = in[b + k];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += in[b + j] < v;
+    out[b + rank] = v;
   }
 }
 
@@ -389,16 +395,27 @@ __global__ __launch_bounds__(kBlk) void k_blocks(Gn g, double* __restrict__ A) {
   const int lane = threadIdx.x & 63;
   if (s >= g.nnzb || lane >= 36) return;
   const int c = lane / 6, j = lane % 6;
-  double v = 0.0;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
   const int b = g.blk_off[s], e = g.blk_off[s + 1];
-  for (int k = b; k < e; ++k) {
-    int code = g.blk_list[k];
-    int64_t t = code >> 4;
+  int k = b;
+  for (; k + 4 <= e; k += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int code = g.blk_list[k + u];
+      const int64_t t = code >> 4;
+      const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
+      const double* Jq = g.J + t * 72 + 18 * (code & 3);
+      v[u] += Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
+    }
+  }
+  for (int u = 0; k < e; ++k, ++u) {
+    const int code = g.blk_list[k];
+    const int64_t t = code >> 4;
     const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
     const double* Jq = g.J + t * 72 + 18 * (code & 3);
-    v += Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
+    v[u] += Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
   }
-  A[s * 36 + lane] = v;
+  A[s * 36 + lane] = (v[0] + v[1]) + (v[2] + v[3]);
 }
 
 // b = -Jᵀr, thread per (node, component); WG 0 also reduces the loss partials into the rhs tail.
@@ -416,15 +433,27 @@ __global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
   }
   if (id >= 6 * (int64_t)g.N) return;
   int n = (int)(id / 6), c = (int)(id % 6);
-  double v = 0.0;
-  for (int k = g.node_off[n]; k < g.node_off[n + 1]; ++k) {
-    int code = g.node_list[k];
-    int64_t t = code >> 2;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  const int b = g.node_off[n], e = g.node_off[n + 1];
+  int k = b;
+  for (; k + 4 <= e; k += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int code = g.node_list[k + u];
+      const int64_t t = code >> 2;
+      const double* Jp = g.J + t * 72 + 18 * (code & 3);
+      const double* rr = g.res + 3 * t;
+      v[u] += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
+    }
+  }
+  for (int u = 0; k < e; ++k, ++u) {
+    const int code = g.node_list[k];
+    const int64_t t = code >> 2;
     const double* Jp = g.J + t * 72 + 18 * (code & 3);
     const double* rr = g.res + 3 * t;
-    v += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
+    v[u] += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
   }
-  rhs[id] = -v;
+  rhs[id] = -((v[0] + v[1]) + (v[2] + v[3]));
 }
 
 // ---------------------------------------------------------------------------- PCG
@@ -649,18 +678,21 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
     }
     stop = g.flags[F_DONE] | g.flags[F_STOPPED];
   }
+  // previous-iteration scalars written by WG 0 of the previous kernel (prefetched before the barrier)
+  const double gam_prev = it > 0 ? g.pcg_gamma[it - 1] : 1.0;
+  const double alpha_prev = it > 0 ? g.pcg_alpha[it - 1] : 1.0;
   // SpMV n = A M⁻¹ w for this wave's row (independent of the scalars)
   const double n = bsr_row(g, row, wc);
   const bool upd = row < g.N && lane < 48 && (lane & 7) == 0;
   const int c = lane >> 3;
   const int64_t o = 6 * (int64_t)row + c;
-  double m = 0.0, w = 0.0, zz0 = 0.0, q0 = 0.0, s0 = 0.0, p0 = 0.0, u0 = 0.0, r0 = 0.0;
+  double m = 0.0, w = 0.0, zz0 = 0.0, q0 = 0.0, s0 = 0.0, p0 = 0.0, u0 = 0.0, r0 = 0.0, x0 = 0.0;
   if (upd) {
     const double* Mi = g.Minv + 36 * (int64_t)row + 6 * c;
     const double* wi = wc + 6 * (int64_t)row;
 #pragma unroll
     for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];      // m = M⁻¹ w (own row)
-    w = wc[o]; zz0 = g.zz[o]; q0 = g.qv[o]; s0 = g.sv[o]; p0 = g.pv[o]; u0 = g.u[o]; r0 = g.r[o];
+    w = wc[o]; zz0 = g.zz[o]; q0 = g.qv[o]; s0 = g.sv[o]; p0 = g.pv[o]; u0 = g.u[o]; r0 = g.r[o]; x0 = g.x[o];
   }
   if (threadIdx.x < 64) {
 #pragma unroll
@@ -683,8 +715,8 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
   if (it == 0) {
     alpha = gam / del;
   } else {
-    beta = gam / g.pcg_gamma[it - 1];
-    alpha = gam / (del - beta * gam / g.pcg_alpha[it - 1]);
+    beta = gam / gam_prev;
+    alpha = gam / (del - beta * gam / alpha_prev);
   }
   if (!isfinite(alpha) || !(alpha > 0.0)) {  // breakdown (A SPD => alpha > 0): keep x
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -701,7 +733,7 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
     const double sv = w + beta * s0;
     const double p = u0 + beta * p0;
     g.zz[o] = zz; g.qv[o] = q; g.sv[o] = sv; g.pv[o] = p;
-    g.x[o] += alpha * p;
+    g.x[o] = x0 + alpha * p;
     const double r = r0 - alpha * sv;
     const double u = u0 - alpha * q;
     const double w2 = w - alpha * zz;
@@ -816,7 +848,7 @@ static double lm_for_iter(double lm0, int gn_iter) {
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->row_cnt, g->blk_off, g->blk_cnt,
-                  g->blk_list, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
+                  g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
                   g->x, g->r, g->u, g->w0, g->w1, g->zz, g->qv, g->sv, g->pv, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
                   g->loss_log};
@@ -847,8 +879,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
     OFX_HIP(hipStreamSynchronize(hs));
-    if (g->host_flags[F_DONE]) {
-      g->last_pcg = g->host_flags[F_PCG_IT];
+    if (g->host_flags[F_DONE] || g->host_flags[F_STOPPED]) {
+      if (g->host_flags[F_DONE]) g->last_pcg = g->host_flags[F_PCG_IT];
       break;
     }
     chunk = 16;
@@ -930,7 +962,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   // per-solve buffers sized by T
   if (g->T > g->T_cap) {
     for (auto pp : {(void**)&g->term_node, (void**)&g->J, (void**)&g->res, (void**)&g->node_list,
-                    (void**)&g->blk_list, (void**)&g->part_loss})
+                    (void**)&g->blk_list, (void**)&g->node_tmp, (void**)&g->blk_tmp, (void**)&g->part_loss})
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     int64_t c = g->T + g->T / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->term_node, 4 * c * sizeof(int32_t)));
@@ -938,6 +970,8 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->res, 3 * c * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->node_list, 4 * c * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_list, 16 * c * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->node_tmp, 4 * c * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->blk_tmp, 16 * c * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->part_loss, 4 * ((c + kBlk - 1) / kBlk) * sizeof(double)));
     g->T_cap = c;
   }
@@ -999,8 +1033,12 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
   OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_pair_scatter, dim3(gT), dim3(256), 0, hs, *g);
-  hipLaunchKernelGGL(k_seg_sort, dim3(grid_for(nnz, 256)), dim3(256), 0, hs, (const int32_t*)g->blk_off, (int64_t)nnz, g->blk_list);
-  hipLaunchKernelGGL(k_seg_sort, dim3(grid_for(N, 256)), dim3(256), 0, hs, (const int32_t*)g->node_off, (int64_t)N, g->node_list);
+  hipLaunchKernelGGL(k_seg_rank, dim3(grid_for(nnz, 4, 1 << 30)), dim3(256), 0, hs, (const int32_t*)g->blk_off, (int64_t)nnz,
+                     (const int32_t*)g->blk_list, g->blk_tmp);
+  hipLaunchKernelGGL(k_seg_rank, dim3(grid_for(N, 4, 1 << 30)), dim3(256), 0, hs, (const int32_t*)g->node_off, (int64_t)N,
+                     (const int32_t*)g->node_list, g->node_tmp);
+  std::swap(g->blk_list, g->blk_tmp);
+  std::swap(g->node_list, g->node_tmp);
   OFX_LAUNCH_CHECK();
   if (nnz_blocks) *nnz_blocks = nnz;
   g->setup_done = true;
@@ -1062,9 +1100,8 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     if (st) return st;
     st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
     if (st) return st;
-    // the PCG poll of this step already synchronised the stream; read the stop flag cheaply
-    OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, as_stream(s)));
-    OFX_HIP(hipStreamSynchronize(as_stream(s)));
+    // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
+    // decision: a stop costs at most one extra (no-op) linearisation instead of a sync per step
     if (g->host_flags[F_STOPPED]) break;
   }
   return ofx_gn_finish(handle, res, s);

@@ -1,0 +1,121 @@
+"""GPU, full benchmark size (512³ @4 mm, ~2k nodes, 10k matches): size-independent properties.
+
+* integrate: a uniform sample of voxels (plus every voxel of a few skinned bricks) after the source
+  frame and one warped frame equals the oracle run on exactly those voxels (voxels are independent,
+  so the oracle needs only the sampled positions) — bit-exact.
+* skin: listed-brick cull is conservative (no valid voxel outside the list) and the sampled voxels'
+  anchors/weights/valid equal the oracle's.
+* GN at 2k nodes: tol 1e-6 vs 1e-10 inner solves agree within the 1e-5 transform bar; repeated
+  solves are bitwise identical (deterministic assembly and reductions).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fusion_oracle as fo
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def seq():
+    from occlusionfusion_amd import synthetic as S
+    return S.SyntheticSequence.build(2000, seed=3)
+
+
+@pytest.fixture(scope="module")
+def pipe(seq, cuda):
+    from occlusionfusion_amd.pipeline import FusionPipeline
+    D, vs = 512, 0.004
+    p = FusionPipeline(seq, (-D * vs / 2, -D * vs / 2, 0.5), vs, (D, D, D), device=cuda)
+    f0 = p.prepare(0)
+    p.integrate_source(f0)
+    return p
+
+
+def test_full_size_integrate_matches_oracle_on_samples(pipe, seq):
+    vol = pipe.vol
+    D = int(vol._vol_dim[0])
+    V = D ** 3
+    rng = np.random.default_rng(0)
+    cache = pipe.wf.skin_tsdf_cache()
+    blist = cache.brick_list.cpu().numpy()[:cache.n_list]
+    # all voxels of 8 listed bricks + 200k uniform voxels
+    vox = [rng.choice(V, 200000, replace=False)]
+    nb = D // 8
+    for b in blist[rng.choice(len(blist), 8, replace=False)]:
+        bx, by, bz = b // (nb * nb), (b // nb) % nb, b % nb
+        ii, jj, kk = np.meshgrid(np.arange(8) + 8 * bx, np.arange(8) + 8 * by, np.arange(8) + 8 * bz, indexing="ij")
+        vox.append((ii * D * D + jj * D + kk).reshape(-1))
+    vox = np.unique(np.concatenate(vox))
+    i, r = vox // (D * D), vox % (D * D)
+    j, k = r // D, r % D
+    o = vol._vol_origin.astype(np.float64)
+    vs = np.float64(vol._voxel_size)
+    pts = np.stack([(o[q] + vs * ax.astype(np.float32).astype(np.float64)) for q, ax in enumerate((i, j, k))],
+                   1).astype(np.float32)
+    intr = pipe.intr
+    f0 = pipe.prepare(0)
+    im0 = f0.im.cpu().numpy()
+    n = len(vox)
+    t, w, c = np.ones(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    fo.integrate(t, w, c, pts, np.ones(n, bool), fo.depth_of(im0), fo.pack_color(im0), intr)
+    T0, C0, W0 = (x.reshape(-1)[vox] for x in vol.get_volume())
+    np.testing.assert_array_equal(T0, t)
+    np.testing.assert_array_equal(W0, w)
+    np.testing.assert_array_equal(C0, c)
+    # warped frame with the solver's transforms
+    f1 = pipe.prepare(1)
+    pipe.step(f1, 1)
+    R = pipe.prev_rot.cpu().numpy()
+    Tt = pipe.prev_trans.cpu().numpy()
+    a, ww, v = fo.skin(pts, seq.nodes, seq.node_coverage)
+    x = fo.ed_warp(pts, a, ww, v, R, Tt, seq.nodes)
+    im1 = f1.im.cpu().numpy()
+    fo.integrate(t, w, c, x, v, fo.depth_of(im1), fo.pack_color(im1), intr)
+    T1, C1, W1 = (x_.reshape(-1)[vox] for x_ in vol.get_volume())
+    np.testing.assert_array_equal(T1, t)
+    np.testing.assert_array_equal(W1, w)
+    np.testing.assert_array_equal(C1, c)
+    assert (w > 1).sum() > 1000          # the warped frame really integrated skinned voxels
+
+
+def test_full_size_skin_cull_is_conservative(pipe, seq):
+    """Any voxel near >= K nodes lies in a listed brick: check sampled voxels' validity vs oracle."""
+    vol = pipe.vol
+    D = int(vol._vol_dim[0])
+    rng = np.random.default_rng(1)
+    vox = rng.choice(D ** 3, 100000, replace=False)
+    i, r = vox // (D * D), vox % (D * D)
+    j, k = r // D, r % D
+    o = vol._vol_origin.astype(np.float64)
+    vs = np.float64(vol._voxel_size)
+    pts = np.stack([(o[q] + vs * ax.astype(np.float32).astype(np.float64)) for q, ax in enumerate((i, j, k))],
+                   1).astype(np.float32)
+    oa, ow, ov = fo.skin(pts, seq.nodes, seq.node_coverage)
+    cache = pipe.wf.skin_tsdf_cache()
+    listed = np.zeros((D // 8) ** 3, bool)
+    listed[cache.brick_list.cpu().numpy()[:cache.n_list]] = True
+    nb = D // 8
+    brick = (i // 8) * nb * nb + (j // 8) * nb + (k // 8)
+    assert not (ov & ~listed[brick]).any()
+    a, w, v = pipe.wf.skin(pts)
+    np.testing.assert_array_equal(v, ov)
+    np.testing.assert_array_equal(a[ov], oa[ov])
+    np.testing.assert_array_equal(w[ov], ow[ov])
+
+
+def test_gn_2k_nodes_tolerance_and_determinism(pipe, cuda):
+    from occlusionfusion_amd import GaussNewtonSolver
+    f = pipe.prepare(3)
+    args = (pipe.nodes_t, pipe.edges_t, pipe.ew_t, f.tpos, f.conf, f.src, f.anchors, f.weights, f.tgt, pipe.intr)
+    tight = GaussNewtonSolver(len(pipe.seq.nodes), 10000, pcg_tol=1e-10).optimize(*args)
+    s = GaussNewtonSolver(len(pipe.seq.nodes), 10000)
+    a = s.optimize(*args)
+    b = s.optimize(*args)
+    assert a["valid_solve"] == 1 and tight["valid_solve"] == 1
+    assert torch.equal(a["node_translations"], b["node_translations"])
+    assert torch.equal(a["node_rotations"], b["node_rotations"])
+    dt = (a["node_translations"] - tight["node_translations"]).abs().max().item()
+    dr = (a["node_rotations"] - tight["node_rotations"]).abs().max().item()
+    assert dt < 1e-5 and dr < 1e-5, (dt, dr)

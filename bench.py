@@ -90,7 +90,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     marks = []
-    pipe.vol.n_updated.zero_()
+    upd = []
+    pipe.solver.timing(True)               # arm hipEvent timing of the PCG loops (same stream)
     t0 = time.perf_counter()
     for t in range(1 + a.warmup, total):
         e0, e1, e2 = ev(), ev(), ev()
@@ -99,6 +100,7 @@ def main():
         e1.record()
         pipe.integrate(frames[t], t, count_updates=True)
         e2.record()
+        upd.append(pipe.vol.n_updated[:cache.n_list].sum())   # device-side sum, read after timing
         marks.append((e0, e1, e2, out))
     torch.cuda.synchronize()
     if dist:
@@ -109,12 +111,14 @@ def main():
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    pcg_ms, pcg_launches, _ = pipe.solver.timing(False)
+    N_, M_, nnzb, _T = pipe.solver.info()
     t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
     t_int = np.array([m[1].elapsed_time(m[2]) for m in marks]) * 1e-3
     pcg = [int(m[3]["_status"][2].item()) for m in marks]
     gn_it = [int(m[3]["_status"][1].item()) for m in marks]
     valid = [int(m[3]["_status"][0].item()) for m in marks]
-    U = int(pipe.vol.n_updated.item()) / a.steps
+    U = float(np.mean([int(u.item()) for u in upd]))
 
     frames_done = a.steps * (world if a.mode == "replicas" else 1)
     value = frames_done / elapsed
@@ -124,6 +128,11 @@ def main():
     B = cache.n_list * 512 * 8 + n_skin_valid * 24 + U * 16
     t_int_avg = float(np.mean(t_int))
     achieved = B / t_int_avg
+    # k_pcg_iter algorithmic bytes per launch: B = A·M⁻¹ blocks (288 B) + column ids (4 B) per block;
+    # per node: row_ptr, gathered w (48 B), M⁻¹ row block (288 B), 7 vectors read + 8 written (6 f64 each)
+    B_pcg = nnzb * 292 + N_ * (4 + 48 + 288 + 15 * 48)
+    t_pcg = pcg_ms * 1e-3 / max(1, pcg_launches)
+    ach_pcg = B_pcg / t_pcg
     res = {
         "metric": "fusion frames/sec (warp+integrate+solve), 640x480 depth -> 512^3 TSDF",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -137,10 +146,16 @@ def main():
         "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * t_int_avg,
                          "pcg_iters_per_frame": float(np.mean(pcg)), "gn_iters": float(np.mean(gn_it)),
                          "valid_solves": int(np.sum(valid))},
-        "roofline": {"kernel": "k_integrate<true> (fused warp+integrate)", "bound": "hbm", "achieved": achieved / 1e9,
-                     "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": achieved / PEAK_HBM, "traffic": None,
-                     "bytes_per_launch": B, "listed_bricks": cache.n_list, "skin_valid_voxels": n_skin_valid,
-                     "updated_voxels": U},
+        "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: BSR SpMV + recurrences)", "bound": "hbm",
+                     "achieved": ach_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": ach_pcg / PEAK_HBM,
+                     "traffic": None, "bytes_per_launch": B_pcg, "avg_launch_us": 1e6 * t_pcg,
+                     "launches_per_frame": pcg_launches / a.steps, "nnz_blocks": nnzb,
+                     "note": "dominant kernel by time; latency-bound (launch + 3 dependent round trips)"},
+        "roofline_integrate": {"kernel": "k_integrate<true> (fused warp+integrate)", "bound": "hbm",
+                               "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                               "frac": achieved / PEAK_HBM, "traffic": None, "bytes_per_launch": B,
+                               "avg_launch_us": 1e6 * t_int_avg, "listed_bricks": cache.n_list,
+                               "skin_valid_voxels": n_skin_valid, "updated_voxels": U},
     }
     if rank == 0 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(pipe, frames[total - 1], total - 1, a)

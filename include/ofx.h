@@ -108,12 +108,13 @@ int ofx_pack_nodes(const float* R, const float* T, const float* g, int32_t n_nod
 /* Fused warp + integrate of one frame into the shard.
  *   warp = 0 : source frame — every voxel, world position, no skin (tsdf.py:395-398)
  *   warp = 1 : bricks in brick_list, ED-warped positions, skin-valid voxels only (tsdf.py:401,464)
- * color_im / color may be NULL (no colour integration). n_updated (device u64) may be NULL. */
+ * color_im / color may be NULL (no colour integration). n_updated (device u32, one entry per launched
+ * brick: n_list when warp, all shard bricks otherwise) receives per-brick update counts, may be NULL. */
 int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
                   int32_t warp, const float* packed_nodes, int32_t n_nodes, int32_t k,
                   const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
                   double obs_weight, float* tsdf, float* weight, float* color,
-                  unsigned long long* n_updated, ofx_stream_t s);
+                  uint32_t* n_updated, ofx_stream_t s);
 
 /* ED warp of points: out = Σ w (R(x-g)+g+t) for valid points, x otherwise.
  * normals = 1: WarpField.deform_normals semantics (R only, renormalised). valid may be NULL (all valid). */
@@ -168,6 +169,12 @@ typedef struct ofx_gn_result {
 } ofx_gn_result;
 
 int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle);
+/* Profiling hook: returns (and resets) the device time of the PCG iteration loops recorded since the
+ * last call (hipEvents on the solve stream; synchronises on them), the number of k_pcg_iter launches
+ * and of timed solves; `enable` switches recording for the following steps. */
+int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves);
+/* info (host int64[4]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms] of the last setup */
+int ofx_gn_info(void* handle, int64_t* info);
 int ofx_gn_destroy(void* handle);
 /* Upload + build the block-sparse JᵀJ pattern (co-anchored node pairs, edges, diagonal).
  * Synchronises the stream once to size the pattern; *nnz_blocks receives the block count. */

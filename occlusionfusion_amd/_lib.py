@@ -62,6 +62,8 @@ _SIGS = {
     "ofx_visibility": [P, c_int64, P, P, c_double, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],
+    "ofx_gn_timing": [P, c_int32, P, P, P],
+    "ofx_gn_info": [P, P],
     "ofx_gn_setup": [P, P, P, P, P],
     "ofx_gn_linearize": [P, c_int32, c_int32, c_int32, c_int32, P, P, P],
     "ofx_gn_step": [P, c_int32, P, P, P],

@@ -71,6 +71,10 @@ struct Gn {
   int32_t* host_flags = nullptr;  // pinned
   int last_pcg = 0;
   bool setup_done = false;
+  // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  int64_t n_iter_launches = 0;
 };
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
@@ -864,6 +868,12 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
   hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (g->timing) {
+    OFX_HIP(hipEventCreate(&e0));
+    OFX_HIP(hipEventCreate(&e1));
+    OFX_HIP(hipEventRecord(e0, hs));
+  }
   const int max_it = g->prm.pcg_max_iter;
   int chunk = g->last_pcg > 0 ? ((g->last_pcg + 2 + 7) / 8) * 8 : 64;
   int it = 0;
@@ -871,12 +881,15 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     int n = chunk < max_it - it ? chunk : max_it - it;
     for (int k = 0; k < n; ++k, ++it)
       hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, it);
+    g->n_iter_launches += n;
     OFX_LAUNCH_CHECK();
     // convergence probe: k_pcg_iter(it) tests |r| first and only iterates if not converged
     if (it < max_it) {
       hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, it);
       ++it;
+      ++g->n_iter_launches;
     }
+    if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
     OFX_HIP(hipStreamSynchronize(hs));
     if (g->host_flags[F_DONE] || g->host_flags[F_STOPPED]) {
@@ -885,6 +898,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     chunk = 16;
   }
+  if (g->timing) g->ev.emplace_back(e0, e1);
   return OFX_OK;
 }
 
@@ -921,6 +935,34 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
   *handle = g;
+  return OFX_OK;
+}
+
+int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g, "null handle");
+  double ms = 0.0;
+  for (auto& e : g->ev) {
+    float t = 0.f;
+    OFX_HIP(hipEventSynchronize(e.second));
+    OFX_HIP(hipEventElapsedTime(&t, e.first, e.second));
+    ms += t;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (pcg_ms) *pcg_ms = ms;
+  if (iter_launches) *iter_launches = g->n_iter_launches;
+  if (n_solves) *n_solves = (int64_t)g->ev.size();
+  g->ev.clear();
+  g->n_iter_launches = 0;
+  g->timing = enable != 0;
+  return OFX_OK;
+}
+
+int ofx_gn_info(void* handle, int64_t* info) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && info, "null handle/info");
+  info[0] = g->N; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T;
   return OFX_OK;
 }
 

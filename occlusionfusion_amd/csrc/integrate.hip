@@ -96,11 +96,14 @@ __device__ __forceinline__ int update_voxel(const CamD& c, const float* __restri
   return 1;
 }
 
-__device__ __forceinline__ void count_updates(int n, unsigned long long* counter) {
-  if (!counter) return;
-  // wave64 reduction then one atomic per wave
+// per-workgroup (= per-brick) update count, plain store: no contended atomics in the hot kernel
+__device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
+  if (!counts) return;
+  __shared__ int s_w[4];
   for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
-  if ((threadIdx.x & 63) == 0 && n) atomicAdd(counter, (unsigned long long)n);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = (uint32_t)(s_w[0] + s_w[1] + s_w[2] + s_w[3]);
 }
 
 template <bool WARP>
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const fl
                                                     const ushort4* __restrict__ anchors,
                                                     const float4* __restrict__ weights, double trunc, double obs,
                                                     float* __restrict__ tsdf, float* __restrict__ weight,
-                                                    float* __restrict__ color, unsigned long long* counter) {
+                                                    float* __restrict__ color, uint32_t* counter) {
   const int64_t slot = blockIdx.x;
   const int64_t b = WARP ? (int64_t)list[slot] : slot;
   int64_t bz = b % g.nbz;
@@ -208,7 +211,7 @@ extern "C" {
 int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
                   int32_t warp, const float* packed_nodes, int32_t n_nodes, int32_t k, const int32_t* brick_list,
                   int32_t n_list, const uint16_t* anchors, const float* weights, double obs_weight, float* tsdf,
-                  float* weight, float* color, unsigned long long* n_updated, ofx_stream_t s) {
+                  float* weight, float* color, uint32_t* n_updated, ofx_stream_t s) {
   BrickGeom g;
   int st = make_geom(desc, &g);
   if (st) return st;

@@ -11,6 +11,7 @@
   matches, one all-reduce (sum) of the block-sparse accumulators per GN iteration, identical solve
   on every rank.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -53,6 +54,18 @@ class GaussNewtonSolver:
             except Exception:
                 pass
             self._h = None
+
+    def timing(self, enable=True):
+        """(pcg_ms, k_pcg_iter launches, timed PCG solves) recorded since the last call; then (re)arm."""
+        ms, n, ns = _lib.c_double(), _lib.c_int64(), _lib.c_int64()
+        call("ofx_gn_timing", self._h, 1 if enable else 0, byref(ms), byref(n), byref(ns))
+        return ms.value, n.value, ns.value
+
+    def info(self):
+        """[n_nodes, n_matches, JᵀJ block count, residual terms] of the last solve's setup."""
+        arr = (ctypes.c_int64 * 4)()
+        call("ofx_gn_info", self._h, arr)
+        return list(arr)
 
     def _params(self):
         p = _lib.GnParams()

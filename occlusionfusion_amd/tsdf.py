@@ -103,7 +103,7 @@ class TSDFVolume:
         self.tsdf_b = torch.empty(self.n_slots, **kw)
         self.weight_b = torch.empty(self.n_slots, **kw)
         self.color_b = torch.empty(self.n_slots, **kw)
-        self.n_updated = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.n_updated = torch.zeros(max(1, self.n_bricks), dtype=torch.int32, device=self.device)  # per brick
         self.with_color = True
         call("ofx_volume_reset", byref(self.desc), ptr(self.tsdf_b), ptr(self.weight_b), ptr(self.color_b), stream_ptr())
         self.warpfield = None

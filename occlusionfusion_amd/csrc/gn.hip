@@ -27,6 +27,7 @@
 //    workgroup of the NEXT kernel re-derives the same scalars from them in a fixed order (kernel
 //    boundaries give visibility; no fences, no tickets). The host only polls convergence in chunks.
 #include <math.h>
+#include <stdlib.h>
 #include <utility>
 #include <vector>
 
@@ -69,7 +70,8 @@ struct Gn {
   int32_t* flags = nullptr;
   double* loss_log = nullptr;
   int32_t* host_flags = nullptr;  // pinned
-  int last_pcg = 0;
+  int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
+  int row_waves = kRowsPerWG;
   bool setup_done = false;
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
   bool timing = false;
@@ -642,7 +644,7 @@ __device__ __forceinline__ void wg_sum3(double v[3], double out[3]) {
 __global__ __launch_bounds__(kRowBlk) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * kRowsPerWG + (threadIdx.x >> 6);
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   double v[3] = {0.0, 0.0, 0.0};
   const double wv = bsr_row(g, row, rhs);
   if (row < g.N && lane < 48 && (lane & 7) == 0) {
@@ -669,7 +671,7 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
   __shared__ int s_stop;
   const int nw = g.nwg_row;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * kRowsPerWG + (threadIdx.x >> 6);
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
   double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
   // wave 0: previous partials (γ, δ, r·r) and b·b, plus the stop flags
@@ -866,7 +868,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   hipLaunchKernelGGL(k_pcg_prep, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
   if (g->nnzb > 0)
     hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
-  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, (const double*)rhs);
+  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g->timing) {
@@ -875,17 +877,18 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     OFX_HIP(hipEventRecord(e0, hs));
   }
   const int max_it = g->prm.pcg_max_iter;
-  int chunk = g->last_pcg > 0 ? ((g->last_pcg + 2 + 7) / 8) * 8 : 64;
+  const int lp = g->last_pcg[gn_iter & 63];
+  int chunk = lp > 0 ? ((lp + 1 + 3) / 4) * 4 : 64;
   int it = 0;
   while (it < max_it) {
     int n = chunk < max_it - it ? chunk : max_it - it;
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, it);
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, it);
     g->n_iter_launches += n;
     OFX_LAUNCH_CHECK();
     // convergence probe: k_pcg_iter(it) tests |r| first and only iterates if not converged
     if (it < max_it) {
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(kRowBlk), 0, hs, *g, it);
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, it);
       ++it;
       ++g->n_iter_launches;
     }
@@ -893,7 +896,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
     OFX_HIP(hipStreamSynchronize(hs));
     if (g->host_flags[F_DONE] || g->host_flags[F_STOPPED]) {
-      if (g->host_flags[F_DONE]) g->last_pcg = g->host_flags[F_PCG_IT];
+      if (g->host_flags[F_DONE]) g->last_pcg[gn_iter & 63] = g->host_flags[F_PCG_IT];
       break;
     }
     chunk = 16;
@@ -998,7 +1001,12 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
-  g->nwg_row = (N + kRowsPerWG - 1) / kRowsPerWG;
+  {
+    const char* e = getenv("OFX_PCG_WAVES");     // tuning knob: waves (block rows) per PCG workgroup
+    int w = e ? atoi(e) : kRowsPerWG;
+    g->row_waves = (w == 4 || w == 8 || w == 16) ? w : kRowsPerWG;
+  }
+  g->nwg_row = (N + g->row_waves - 1) / g->row_waves;
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T

@@ -131,7 +131,8 @@ typedef struct ofx_gn_params {
   int32_t num_iter;          /* 10 (model.py:91) */
   int32_t use_edge_weighting;/* 0 (custom_settings.py:41) */
   int32_t pcg_max_iter;      /* inner PCG cap */
-  int32_t _pad;
+  int32_t pcg_warm;          /* 1: start each GN step's PCG from the Galerkin projection of b onto the
+                                last 4 GN-step solutions (A-norm optimal in that span); 0: x0 = 0 */
   double lambda_flow;        /* 0   (model.py:96) — squared weights, sqrt taken inside (model.py:374-377) */
   double lambda_depth;       /* 1   (model.py:101) */
   double lambda_arap;        /* 0.5 (model.py:105) */
@@ -175,6 +176,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle);
 int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves);
 /* info (host int64[4]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms] of the last setup */
 int ofx_gn_info(void* handle, int64_t* info);
+/* Per-GN-step statistics of the last solve: out (host f64[3*cap]) = [PCG iterations, |b|², loss] per
+ * step (zeros for steps that did not run); synchronous D2H copy, at most 64 steps. */
+int ofx_gn_stats(void* handle, double* out, int32_t cap);
 int ofx_gn_destroy(void* handle);
 /* Upload + build the block-sparse JᵀJ pattern (co-anchored node pairs, edges, diagonal).
  * Synchronises the stream once to size the pattern; *nnz_blocks receives the block count. */

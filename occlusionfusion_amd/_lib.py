@@ -27,7 +27,7 @@ class Camera(ctypes.Structure):
 
 
 class GnParams(ctypes.Structure):
-    _fields_ = [("num_iter", c_int32), ("use_edge_weighting", c_int32), ("pcg_max_iter", c_int32), ("_pad", c_int32),
+    _fields_ = [("num_iter", c_int32), ("use_edge_weighting", c_int32), ("pcg_max_iter", c_int32), ("pcg_warm", c_int32),
                 ("lambda_flow", c_double), ("lambda_depth", c_double), ("lambda_arap", c_double),
                 ("lambda_motion", c_double), ("lm_factor", c_double), ("stop_loss_diff", c_double),
                 ("pcg_tol", c_double)]
@@ -64,6 +64,7 @@ _SIGS = {
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
+    "ofx_gn_stats": [P, P, c_int32],
     "ofx_gn_setup": [P, P, P, P, P],
     "ofx_gn_linearize": [P, c_int32, c_int32, c_int32, c_int32, P, P, P],
     "ofx_gn_step": [P, c_int32, P, P, P],

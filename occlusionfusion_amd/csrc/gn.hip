@@ -22,10 +22,12 @@
 //    pairs). Per solve, each block gets a sorted list of the (term, p, q) products that land on it,
 //    so assembly is a deterministic gather: one wave per block, lane = block entry (k_blocks); the
 //    rhs is the same per node entry (k_rhs). No atomics -> bitwise reproducible A and b.
-//  * PCG: 2 kernels per iteration (p-update fused into SpMV; axpy + block-Cholesky preconditioner
-//    + dots). Scalars never leave the device: each kernel writes per-workgroup partial sums and every
-//    workgroup of the NEXT kernel re-derives the same scalars from them in a fixed order (kernel
-//    boundaries give visibility; no fences, no tickets). The host only polls convergence in chunks.
+//  * PCG: pipelined (Ghysels-Vanroose) on the right-preconditioned operator B = A·M⁻¹ (M = block
+//    Jacobi, explicit 6x6 inverses), ONE kernel per iteration: SpMV + all recurrences + the three
+//    dot products. Scalars never leave the device: each launch writes per-workgroup partial sums and
+//    every workgroup of the NEXT launch re-derives the same scalars from them in a fixed order
+//    (kernel boundaries give visibility; no fences, no tickets, no atomics). The host only polls
+//    convergence in chunks sized from the previous frame's count for the same GN step.
 #include <math.h>
 #include <stdlib.h>
 #include <utility>
@@ -36,6 +38,11 @@
 namespace ofx {
 
 // --------------------------------------------------------------------------------------------
+constexpr int kBlk = 256;       // threads per WG
+constexpr int kRowBlk = 1024;   // PCG row kernels: 16 waves per WG, one block row per wave
+constexpr int kRowsPerWG = kRowBlk / 64;
+constexpr int kProj = 4;      // warm start: Galerkin projection on the last kProj GN-step solutions
+
 struct Gn {
   int max_nodes = 0, max_matches = 0;
   int N = 0, M = 0, NB = 0;
@@ -69,6 +76,12 @@ struct Gn {
   double* scal = nullptr;
   int32_t* flags = nullptr;
   double* loss_log = nullptr;
+  double* stat = nullptr;         // kMaxLog x [pcg iterations, |b|², loss] of the last solve
+  // Galerkin warm start over the last kProj GN-step solutions of this solve (ring of kProj x 6N each):
+  // xh = previous solutions, xmh = M·xh, th = A·xh
+  double *xh = nullptr, *xmh = nullptr, *th = nullptr;
+  int n_prev = 0;                 // valid entries of the ring for the current step
+  int warm_now = 0;               // this step starts from the projected x0             // PCG stop test against max(|b|, |b| of GN step 0) instead of |b|
   int32_t* host_flags = nullptr;  // pinned
   int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
   int row_waves = kRowsPerWG;
@@ -82,9 +95,7 @@ struct Gn {
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_COUNT = 8 };
 enum { S_LOSS_PREV = 0, S_COUNT = 4 };
-constexpr int kBlk = 256;       // threads per WG
-constexpr int kRowBlk = 1024;   // PCG row kernels: 16 waves per WG, one block row per wave
-constexpr int kRowsPerWG = kRowBlk / 64;
+constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 
 // ---------------------------------------------------------------------------- reductions
 __device__ __forceinline__ double block_sum(double v) {
@@ -322,61 +333,75 @@ __device__ void deformed_point(const Gn& g, int64_t m, double p[3]) {
   }
 }
 
-// One thread per term: residual triple + 3x6 Jacobian block of each of its nodes; loss partials.
+// Four threads per term (t = id/4, slot k = id%4): slot k writes the 3x6 Jacobian block of the
+// term's k-th node; slot 0 also writes the residual triple and the loss partials. Data slots each
+// recompute the deformed point (identical bits) so the four anchor Jacobians run in parallel.
 // Terms outside this rank's share (data matches outside [m0,m1), regularisers when !add_reg) are
 // written as exact zeros so the fixed contribution lists stay valid.
 __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m1, int add_reg) {
-  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t t = id >> 2;
+  const int k = (int)(id & 3);
   double r[3] = {0.0, 0.0, 0.0};
   double l2[3] = {0.0, 0.0, 0.0};
   double bad = 0.0;
   if (t < g.T) {
-    double* J = g.J + t * 72;
+    double* J = g.J + t * 72 + 18 * k;
     if (t < g.M) {
       if (t >= m0 && t < m1) {
         double p[3];
         deformed_point(g, t, p);
         double zinv = 1.0 / (p[2] + 1e-7);
-        double tpx = g.tpx[t], tpy = g.tpy[t];
-        r[0] = dc.lf * (dc.fx * p[0] * zinv + dc.cx - tpx) + dc.ld * (p[0] - g.tgt[3 * t]);
-        r[1] = dc.lf * (dc.fy * p[1] * zinv + dc.cy - tpy) + dc.ld * (p[1] - g.tgt[3 * t + 1]);
-        r[2] = dc.ld * (p[2] - g.tgt[3 * t + 2]);
-        for (int k = 0; k < 4; ++k) data_jacobian(g, dc, t, k, p, zinv, J + 18 * k);
-        l2[0] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        data_jacobian(g, dc, t, k, p, zinv, J);
+        if (k == 0) {
+          double tpx = g.tpx[t], tpy = g.tpy[t];
+          r[0] = dc.lf * (dc.fx * p[0] * zinv + dc.cx - tpx) + dc.ld * (p[0] - g.tgt[3 * t]);
+          r[1] = dc.lf * (dc.fy * p[1] * zinv + dc.cy - tpy) + dc.ld * (p[1] - g.tgt[3 * t + 1]);
+          r[2] = dc.ld * (p[2] - g.tgt[3 * t + 2]);
+          l2[0] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        }
       } else {
-        for (int c = 0; c < 72; ++c) J[c] = 0.0;
+#pragma unroll
+        for (int c = 0; c < 18; ++c) J[c] = 0.0;
       }
     } else if (t < g.M + (int64_t)g.N * g.NB) {
-      int64_t e = t - g.M;
-      int j = g.edges[e];
-      if (j >= 0) {
+      const int64_t e = t - g.M;
+      const int j = g.edges[e];
+      if (j >= 0 && k < 2) {
         if (add_reg) {
-          int i = (int)(e / g.NB);
-          double s = dc.la * g.ew[e];
-          const double* Ri = g.R + 9 * (int64_t)i;
-          const double* gi = g.nodes + 3 * (int64_t)i;
-          const double* gj = g.nodes + 3 * (int64_t)j;
-          const double* ti = g.t + 3 * (int64_t)i;
-          const double* tj = g.t + 3 * (int64_t)j;
-          double e0 = gj[0] - gi[0], e1 = gj[1] - gi[1], e2 = gj[2] - gi[2];
-          double d0 = Ri[0] * e0 + Ri[1] * e1 + Ri[2] * e2;
-          double d1 = Ri[3] * e0 + Ri[4] * e1 + Ri[5] * e2;
-          double d2 = Ri[6] * e0 + Ri[7] * e1 + Ri[8] * e2;
-          r[0] = s * (d0 + gi[0] + ti[0] - (gj[0] + tj[0]));
-          r[1] = s * (d1 + gi[1] + ti[1] - (gj[1] + tj[1]));
-          r[2] = s * (d2 + gi[2] + ti[2] - (gj[2] + tj[2]));
-          // node i: [-s[d]x | s I] ; node j: [0 | -s I]
-          const double Ji[18] = {0.0, s * d2, -s * d1, s, 0, 0, -s * d2, 0.0, s * d0, 0, s, 0, s * d1, -s * d0, 0.0, 0, 0, s};
-          for (int c = 0; c < 18; ++c) J[c] = Ji[c];
-          for (int c = 0; c < 18; ++c) J[18 + c] = 0.0;
-          J[18 + 3] = -s; J[18 + 10] = -s; J[18 + 17] = -s;
-          l2[1] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+          const int i = (int)(e / g.NB);
+          const double s = dc.la * g.ew[e];
+          if (k == 0) {
+            const double* Ri = g.R + 9 * (int64_t)i;
+            const double* gi = g.nodes + 3 * (int64_t)i;
+            const double* gj = g.nodes + 3 * (int64_t)j;
+            const double* ti = g.t + 3 * (int64_t)i;
+            const double* tj = g.t + 3 * (int64_t)j;
+            double e0 = gj[0] - gi[0], e1 = gj[1] - gi[1], e2 = gj[2] - gi[2];
+            double d0 = Ri[0] * e0 + Ri[1] * e1 + Ri[2] * e2;
+            double d1 = Ri[3] * e0 + Ri[4] * e1 + Ri[5] * e2;
+            double d2 = Ri[6] * e0 + Ri[7] * e1 + Ri[8] * e2;
+            r[0] = s * (d0 + gi[0] + ti[0] - (gj[0] + tj[0]));
+            r[1] = s * (d1 + gi[1] + ti[1] - (gj[1] + tj[1]));
+            r[2] = s * (d2 + gi[2] + ti[2] - (gj[2] + tj[2]));
+            // node i: [-s[d]x | s I]
+            const double Ji[18] = {0.0, s * d2, -s * d1, s, 0, 0, -s * d2, 0.0, s * d0, 0, s, 0, s * d1, -s * d0, 0.0, 0, 0, s};
+#pragma unroll
+            for (int c = 0; c < 18; ++c) J[c] = Ji[c];
+            l2[1] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+          } else {  // node j: [0 | -s I]
+#pragma unroll
+            for (int c = 0; c < 18; ++c) J[c] = 0.0;
+            J[3] = -s; J[10] = -s; J[17] = -s;
+          }
         } else {
-          for (int c = 0; c < 36; ++c) J[c] = 0.0;
+#pragma unroll
+          for (int c = 0; c < 18; ++c) J[c] = 0.0;
         }
       }
-    } else {
-      int i = (int)(t - g.M - (int64_t)g.N * g.NB);
+    } else if (k == 0) {
+      const int i = (int)(t - g.M - (int64_t)g.N * g.NB);
+#pragma unroll
       for (int c = 0; c < 18; ++c) J[c] = 0.0;
       if (add_reg) {
         double c = dc.lm * g.conf[i];
@@ -385,8 +410,10 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
         l2[2] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
       }
     }
-    g.res[3 * t] = r[0]; g.res[3 * t + 1] = r[1]; g.res[3 * t + 2] = r[2];
-    bad = (isfinite(l2[0]) && isfinite(l2[1]) && isfinite(l2[2])) ? 0.0 : 1.0;
+    if (k == 0) {
+      g.res[3 * t] = r[0]; g.res[3 * t + 1] = r[1]; g.res[3 * t + 2] = r[2];
+      bad = (isfinite(l2[0]) && isfinite(l2[1]) && isfinite(l2[2])) ? 0.0 : 1.0;
+    }
   }
   double s0 = block_sum(l2[0]), s1 = block_sum(l2[1]), s2 = block_sum(l2[2]), s3 = block_sum(bad);
   if (threadIdx.x == 0) {
@@ -395,38 +422,41 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
   }
 }
 
-// One wave per JᵀJ block: lane (c,j) sums its entry over the block's sorted (term,p,q) list.
+__device__ __forceinline__ double blk_entry(const Gn& g, int code, int c, int j) {
+  const int64_t t = code >> 4;
+  const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
+  const double* Jq = g.J + t * 72 + 18 * (code & 3);
+  return Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
+}
+
+// One wave per JᵀJ block: lane (c,j) sums its entry over the block's sorted (term,p,q) list,
+// 8 independent accumulators (8 list entries in flight per lane).
 __global__ __launch_bounds__(kBlk) void k_blocks(Gn g, double* __restrict__ A) {
   const int64_t s = blockIdx.x * (int64_t)(kBlk / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (s >= g.nnzb || lane >= 36) return;
   const int c = lane / 6, j = lane % 6;
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  double v[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   const int b = g.blk_off[s], e = g.blk_off[s + 1];
   int k = b;
-  for (; k + 4 <= e; k += 4) {
+  for (; k + 8 <= e; k += 8) {
+    int code[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int code = g.blk_list[k + u];
-      const int64_t t = code >> 4;
-      const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
-      const double* Jq = g.J + t * 72 + 18 * (code & 3);
-      v[u] += Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
-    }
+    for (int u = 0; u < 8; ++u) code[u] = g.blk_list[k + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] += blk_entry(g, code[u], c, j);
   }
-  for (int u = 0; k < e; ++k, ++u) {
-    const int code = g.blk_list[k];
-    const int64_t t = code >> 4;
-    const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
-    const double* Jq = g.J + t * 72 + 18 * (code & 3);
-    v[u] += Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
-  }
-  A[s * 36 + lane] = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+  for (int u = 0; u < 7; ++u)
+    if (k + u < e) v[u] += blk_entry(g, g.blk_list[k + u], c, j);
+  A[s * 36 + lane] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 }
 
-// b = -Jᵀr, thread per (node, component); WG 0 also reduces the loss partials into the rhs tail.
+// b = -Jᵀr: one wave per node, lane = slot*6 + c (10 slots); slot s sums list entries s, s+10, ...
+// and lane c combines the 10 slots in fixed order. WG 0 also reduces the loss partials into the
+// rhs tail.
+constexpr int kRhsSlots = 10;
 __global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
-  int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (blockIdx.x == 0) {
     double d0 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 0);
     double d1 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 1);
@@ -437,29 +467,26 @@ __global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
       tail[0] = d0; tail[1] = d1; tail[2] = d2; tail[3] = d3;
     }
   }
-  if (id >= 6 * (int64_t)g.N) return;
-  int n = (int)(id / 6), c = (int)(id % 6);
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
-  const int b = g.node_off[n], e = g.node_off[n + 1];
-  int k = b;
-  for (; k + 4 <= e; k += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int code = g.node_list[k + u];
+  const int n = blockIdx.x * (kBlk / 64) + (threadIdx.x >> 6);
+  if (n >= g.N) return;
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / 6, c = lane % 6;
+  double v = 0.0;
+  if (slot < kRhsSlots) {
+    const int b = g.node_off[n], e = g.node_off[n + 1];
+#pragma unroll 2
+    for (int k = b + slot; k < e; k += kRhsSlots) {
+      const int code = g.node_list[k];
       const int64_t t = code >> 2;
       const double* Jp = g.J + t * 72 + 18 * (code & 3);
       const double* rr = g.res + 3 * t;
-      v[u] += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
+      v += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
     }
   }
-  for (int u = 0; k < e; ++k, ++u) {
-    const int code = g.node_list[k];
-    const int64_t t = code >> 2;
-    const double* Jp = g.J + t * 72 + 18 * (code & 3);
-    const double* rr = g.res + 3 * t;
-    v[u] += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
-  }
-  rhs[id] = -((v[0] + v[1]) + (v[2] + v[3]));
+  double tot = 0.0;
+#pragma unroll
+  for (int q = 0; q < kRhsSlots; ++q) tot += __shfl(v, q * 6 + c);
+  if (lane < 6) rhs[6 * (int64_t)n + c] = -tot;
 }
 
 // ---------------------------------------------------------------------------- PCG
@@ -507,69 +534,68 @@ __device__ __forceinline__ void chol6_solve(const double* __restrict__ L, const 
 }
 
 // LM damping of the diagonal blocks, explicit block inverse Minv_i, x = 0, r = b, u = M⁻¹ b,
-// recurrence vectors zeroed.  thread per node.
+// recurrence vectors zeroed.  8 lanes per node: every lane factors the 6x6 block (identical bits),
+// lane c < 6 solves column c of the inverse and owns component c of the vectors.
 __global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
                                                    const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; }
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int i = (int)(tid >> 3), c = (int)(tid & 7);
   if (i >= g.N) return;
   double* blk = A + 36 * (int64_t)g.map[(int64_t)i * g.N + i];
   double a[36];
 #pragma unroll
-  for (int c = 0; c < 36; ++c) a[c] = blk[c];
+  for (int q = 0; q < 36; ++q) a[q] = blk[q];
 #pragma unroll
-  for (int c = 0; c < 6; ++c) { a[c * 7] += lm; blk[c * 7] = a[c * 7]; }
+  for (int q = 0; q < 6; ++q) a[q * 7] += lm;
+  if (c >= 6) return;
+  blk[c * 7] = a[c * 7];
   double L[21];
   bool ok = chol6(a, L);
+  double e[6], col[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) e[k] = (k == c) ? 1.0 : 0.0;
+  if (ok) chol6_solve(L, e, col);
+  else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) col[k] = e[k];
+  }
   double* Mi = g.Minv + 36 * (int64_t)i;
 #pragma unroll
-  for (int c = 0; c < 6; ++c) {       // column c of the inverse
-    double e[6], col[6];
+  for (int k = 0; k < 6; ++k) Mi[k * 6 + c] = col[k];
+  // u_c = (M⁻¹ b)_c = Σ_k Minv[c][k] b_k = Σ_k col_k-of-row... M⁻¹ is symmetric: row c = column c
+  double u = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) e[k] = (k == c) ? 1.0 : 0.0;
-    if (ok) chol6_solve(L, e, col);
-    else {
+  for (int k = 0; k < 6; ++k) u += col[k] * rhs[6 * i + k];
+  const int64_t o = 6 * (int64_t)i + c;
+  if (g.warm_now) {           // Galerkin start on span of the previous solutions: M·x_j
+    for (int j = 0; j < g.n_prev; ++j) {
+      const double* xj = g.xh + (int64_t)j * 6 * g.N + 6 * (int64_t)i;
+      double m = 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) col[k] = e[k];
+      for (int k = 0; k < 6; ++k) m += a[c * 6 + k] * xj[k];
+      g.xmh[(int64_t)j * 6 * g.N + o] = m;
     }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Mi[k * 6 + c] = col[k];
+  } else {
+    g.x[o] = 0.0; g.r[o] = rhs[o]; g.u[o] = u;
   }
-  double b[6];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) b[c] = rhs[6 * i + c];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-    double u = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) u += Mi[c * 6 + k] * b[k];
-    const int64_t o = 6 * (int64_t)i + c;
-    g.x[o] = 0.0; g.r[o] = b[c]; g.u[o] = u;
-    g.zz[o] = 0.0; g.qv[o] = 0.0; g.sv[o] = 0.0; g.pv[o] = 0.0;
-  }
+  g.zz[o] = 0.0; g.qv[o] = 0.0; g.sv[o] = 0.0; g.pv[o] = 0.0;
 }
 
-// B_ij = A_ij · Minv_j  (thread per block)
+// B_ij = A_ij · Minv_j : one thread per output entry (36 per block)
 __global__ __launch_bounds__(kBlk) void k_pcg_bmat(Gn g, const double* __restrict__ A) {
   if (g.flags[F_STOPPED]) return;
-  int64_t bi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t bi = tid / 36;
+  const int e = (int)(tid % 36), r = e / 6, c = e % 6;
   if (bi >= g.nnzb) return;
-  const double* Ab = A + 36 * bi;
+  const double* Ar = A + 36 * bi + 6 * r;
   const double* Mj = g.Minv + 36 * (int64_t)g.col[bi];
-  double* Bb = g.Bm + 36 * bi;
-  double a[36], m[36];
+  double v = 0.0;
 #pragma unroll
-  for (int c = 0; c < 36; ++c) { a[c] = Ab[c]; m[c] = Mj[c]; }
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      double v = 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) v += a[r * 6 + k] * m[k * 6 + c];
-      Bb[r * 6 + c] = v;
-    }
+  for (int k = 0; k < 6; ++k) v += Ar[k] * Mj[k * 6 + c];
+  g.Bm[36 * bi + e] = v;
 }
 
 // One wave per block row. Lane = rr*8 + b (rr = block row component 0..5, b = block slot 0..7):
@@ -640,25 +666,177 @@ __device__ __forceinline__ void wg_sum3(double v[3], double out[3]) {
   }
 }
 
-// w0 = A u0 = B b; partials (γ0 = r·u, δ0 = w·u, r·r) -> PP[0], bb -> PB.
+// Galerkin warm start, pass 1: t_j = A x_j = B (M x_j) for the n_prev stored solutions (own rows)
+// and per-WG partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
+constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
+__device__ __forceinline__ int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
+
+__global__ __launch_bounds__(kRowBlk) void k_pcg_proj(Gn g, const double* __restrict__ rhs) {
+  if (g.flags[F_STOPPED]) return;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int np = g.n_prev;
+  const int64_t stride = 6 * (int64_t)g.N;
+  double t[kProj];
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) t[j] = j < np ? bsr_row(g, row, g.xmh + j * stride) : 0.0;
+  double v[kProjP];
+#pragma unroll
+  for (int k = 0; k < kProjP; ++k) v[k] = 0.0;
+  if (row < g.N && lane < 48 && (lane & 7) == 0) {
+    const int64_t o = 6 * (int64_t)row + (lane >> 3);
+    const double b = rhs[o];
+    double x[kProj];
+#pragma unroll
+    for (int j = 0; j < kProj; ++j) {
+      x[j] = j < np ? g.xh[j * stride + o] : 0.0;
+      if (j < np) g.th[j * stride + o] = t[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kProj; ++j) {
+#pragma unroll
+      for (int i = 0; i <= j; ++i) v[tri(i, j)] = x[i] * t[j];
+      v[kProj * (kProj + 1) / 2 + j] = x[j] * b;
+    }
+  }
+  __shared__ double s_w[kProjP][kRowBlk / 64];
+#pragma unroll
+  for (int k = 0; k < kProjP; ++k)
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < kProjP; ++k) s_w[k][threadIdx.x >> 6] = v[k];
+  __syncthreads();
+  if (threadIdx.x < kProjP) {
+    double acc = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) acc += s_w[threadIdx.x][w];
+    g.part_p[kProjP * (int64_t)blockIdx.x + threadIdx.x] = acc;
+  }
+}
+
+// Galerkin warm start, pass 2: every WG re-derives G and f from the partials (fixed order, identical
+// bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get c = 0), and
+// sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0.
+__global__ __launch_bounds__(kRowBlk) void k_pcg_proj2(Gn g, const double* __restrict__ rhs) {
+  if (g.flags[F_STOPPED]) return;
+  __shared__ double s_c[kProj];
+  const int np = g.n_prev;
+  if (threadIdx.x < 64) {
+    double p[kProjP];
+#pragma unroll
+    for (int k = 0; k < kProjP; ++k) p[k] = 0.0;
+    for (int i = threadIdx.x; i < g.nwg_row; i += 64)
+#pragma unroll
+      for (int k = 0; k < kProjP; ++k) p[k] += g.part_p[kProjP * (int64_t)i + k];
+#pragma unroll
+    for (int k = 0; k < kProjP; ++k)
+      for (int o = 32; o > 0; o >>= 1) p[k] += __shfl_xor(p[k], o, 64);
+    if (threadIdx.x == 0) {
+      // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
+      double L[kProj][kProj], y[kProj], c[kProj];
+      bool use[kProj];
+#pragma unroll
+      for (int j = 0; j < kProj; ++j) {
+        use[j] = false; y[j] = 0.0; c[j] = 0.0;
+#pragma unroll
+        for (int i = 0; i < kProj; ++i) L[j][i] = 0.0;
+      }
+      for (int j = 0; j < np; ++j) {
+        double d = p[tri(j, j)];
+        for (int k = 0; k < j; ++k) if (use[k]) d -= L[j][k] * L[j][k];
+        if (!(d > 1e-10 * p[tri(j, j)]) || !(p[tri(j, j)] > 0.0)) continue;   // dependent / degenerate
+        use[j] = true;
+        const double ljj = sqrt(d);
+        L[j][j] = ljj;
+        for (int i = j + 1; i < np; ++i) {
+          double sdot = p[tri(j, i)];
+          for (int k = 0; k < j; ++k) if (use[k]) sdot -= L[i][k] * L[j][k];
+          L[i][j] = sdot / ljj;
+        }
+      }
+      for (int j = 0; j < np; ++j) {
+        if (!use[j]) continue;
+        double sdot = p[kProj * (kProj + 1) / 2 + j];
+        for (int k = 0; k < j; ++k) if (use[k]) sdot -= L[j][k] * y[k];
+        y[j] = sdot / L[j][j];
+      }
+      for (int j = np - 1; j >= 0; --j) {
+        if (!use[j]) continue;
+        double sdot = y[j];
+        for (int k = j + 1; k < np; ++k) if (use[k]) sdot -= L[k][j] * c[k];
+        c[j] = sdot / L[j][j];
+      }
+      bool fin = true;
+      for (int j = 0; j < kProj; ++j) fin = fin && isfinite(c[j]);
+      for (int j = 0; j < kProj; ++j) s_c[j] = fin ? c[j] : 0.0;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t stride = 6 * (int64_t)g.N;
+  double rv = 0.0;
+  if (row < g.N && lane < 6) {
+    const int64_t o = 6 * (int64_t)row + lane;
+    double xv = 0.0;
+    rv = rhs[o];
+    for (int j = 0; j < np; ++j) {
+      xv += s_c[j] * g.xh[j * stride + o];
+      rv -= s_c[j] * g.th[j * stride + o];
+    }
+    g.x[o] = xv;
+    g.r[o] = rv;
+  }
+  double rk[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) rk[k] = __shfl(rv, k, 64);
+  if (row < g.N && lane < 6) {
+    const double* Mi = g.Minv + 36 * (int64_t)row + 6 * lane;
+    double u = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) u += Mi[k] * rk[k];
+    g.u[6 * (int64_t)row + lane] = u;
+  }
+}
+
+// fixed-shape WG sum of 4 values (1024 threads): wave butterflies, then wave partials in order
+__device__ __forceinline__ void wg_sum4v(double v[4], double out[4]) {
+  __shared__ double s_w4[4][kRowBlk / 64];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_w4[k][threadIdx.x >> 6] = v[k];
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double a = 0.0;
+    for (int w = 0; w < nw; ++w) a += s_w4[k][w];
+    out[k] = a;
+  }
+}
+
+// w0 = A u0 = B r0; partials (γ0 = r·u, δ0 = w·u, r·r) -> PP[0], b·b -> PB.
 __global__ __launch_bounds__(kRowBlk) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  double v[3] = {0.0, 0.0, 0.0};
-  const double wv = bsr_row(g, row, rhs);
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  const double wv = bsr_row(g, row, g.r);
   if (row < g.N && lane < 48 && (lane & 7) == 0) {
     const int64_t o = 6 * (int64_t)row + (lane >> 3);
     g.w0[o] = wv;
-    double r = g.r[o], u = g.u[o];
-    v[0] = r * u; v[1] = wv * u; v[2] = r * r;
+    double r = g.r[o], u = g.u[o], b = rhs[o];
+    v[0] = r * u; v[1] = wv * u; v[2] = r * r; v[3] = b * b;
   }
-  double s[3];
-  wg_sum3(v, s);
+  double s[4];
+  wg_sum4v(v, s);
   if (threadIdx.x == 0) {
     double* P = g.part_p + 3 * (int64_t)blockIdx.x;
     P[0] = s[0]; P[1] = s[1]; P[2] = s[2];
-    g.part_b[blockIdx.x] = s[2];
+    g.part_b[blockIdx.x] = s[3];
   }
 }
 
@@ -711,7 +889,8 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
   }
   __syncthreads();
   if (s_stop) return;
-  const double gam = s_sc[0], del = s_sc[1], rr = s_sc[2], bb = s_sc[3];
+  const double gam = s_sc[0], del = s_sc[1], rr = s_sc[2];
+  const double bb = s_sc[3];
   const double tol = g.prm.pcg_tol;
   if (rr <= tol * tol * bb || gam == 0.0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
@@ -754,24 +933,25 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
   }
 }
 
-// After the solve: ill-posed check, loss bookkeeping and early stop (model.py:696-732). Single WG.
-__global__ __launch_bounds__(kBlk) void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log,
-                                                      int pcg_max) {
-  __shared__ int s_bad;
-  if (threadIdx.x == 0) s_bad = 0;
-  __syncthreads();
-  if (g.flags[F_STOPPED]) return;
-  int bad = 0;
-  for (int i = threadIdx.x; i < 6 * g.N; i += blockDim.x) bad |= !isfinite(g.x[i]);
-  if (bad) atomicOr(&s_bad, 1);
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+// After the solve: ill-posed check, loss bookkeeping and early stop (model.py:696-732). One thread.
+// A non-finite solve shows up as a non-finite alpha/pq in k_pcg_iter, which sets F_ILL.
+__global__ void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log, int pcg_max, int gn_iter) {
+  if (threadIdx.x != 0 || g.flags[F_STOPPED]) return;
   if (!g.flags[F_DONE]) g.flags[F_PCG_TOTAL] += pcg_max;
+  {
+    double bb = 0.0;
+    for (int i = 0; i < g.nwg_row; ++i) bb += g.part_b[i];
+    if (gn_iter < kMaxLog) {
+      g.stat[3 * gn_iter + 0] = g.flags[F_DONE] ? (double)g.flags[F_PCG_IT] : (double)pcg_max;
+      g.stat[3 * gn_iter + 1] = bb;
+      const double* tl = rhs + 6 * (int64_t)g.N;
+      g.stat[3 * gn_iter + 2] = sqrt(tl[0] + tl[1] + tl[2]);
+    }
+  }
   const double* tail = rhs + 6 * (int64_t)g.N;
   g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
   g.flags[F_APPLY] = 0;
-  if (s_bad || g.flags[F_ILL]) {
-    g.flags[F_ILL] = 1;
+  if (g.flags[F_ILL]) {
     g.flags[F_STOPPED] = 1;
     return;
   }
@@ -841,6 +1021,7 @@ __global__ void k_reset_flags(Gn g) {
   int i = threadIdx.x;
   if (i < F_COUNT) g.flags[i] = 0;
   if (i < S_COUNT) g.scal[i] = 0.0;
+  for (int j = i; j < 3 * kMaxLog; j += blockDim.x) g.stat[j] = 0.0;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -857,7 +1038,7 @@ static void free_all(Gn* g) {
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
                   g->x, g->r, g->u, g->w0, g->w1, g->zz, g->qv, g->sv, g->pv, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log};
+                  g->loss_log, g->stat, g->xh, g->xmh, g->th};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -865,9 +1046,21 @@ static void free_all(Gn* g) {
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
-  hipLaunchKernelGGL(k_pcg_prep, dim3(g->nwg_node), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
+  g->warm_now = 0;
+  if (g->prm.pcg_warm && gn_iter > 0) {   // ring slot (k-1) mod kProj <- x_{k-1}
+    const int slot = (gn_iter - 1) % kProj;
+    OFX_HIP(hipMemcpyAsync(g->xh + (int64_t)slot * 6 * g->N, g->x, 6 * (size_t)g->N * sizeof(double),
+                           hipMemcpyDeviceToDevice, hs));
+    g->n_prev = gn_iter < kProj ? gn_iter : kProj;
+    g->warm_now = 1;
+  }
+  hipLaunchKernelGGL(k_pcg_prep, dim3(grid_for(8 * (int64_t)g->N, kBlk)), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
   if (g->nnzb > 0)
-    hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
+    hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(36 * g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
+  if (g->warm_now) {
+    hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
+    hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
+  }
   hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -929,10 +1122,11 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->Minv, 36 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->u, 6 * N);
   ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N); ALLOC(g->zz, 6 * N); ALLOC(g->qv, 6 * N); ALLOC(g->sv, 6 * N);
   ALLOC(g->pv, 6 * N);
-  const int64_t max_row_wg = (N + kRowsPerWG - 1) / kRowsPerWG;
-  ALLOC(g->part_p, 6 * max_row_wg); ALLOC(g->part_b, max_row_wg);
+  ALLOC(g->xh, kProj * 6 * N); ALLOC(g->xmh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
+  const int64_t max_row_wg = (N + 3) / 4;   // smallest PCG workgroup: 4 rows (OFX_PCG_WAVES)
+  ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
-  ALLOC(g->loss_log, 4 * 64); ALLOC(g->rhs_own, 6 * N + 4);
+  ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
   if (hipHostMalloc((void**)&g->host_flags, F_COUNT * sizeof(int32_t), 0) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
@@ -966,6 +1160,14 @@ int ofx_gn_info(void* handle, int64_t* info) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && info, "null handle/info");
   info[0] = g->N; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T;
+  return OFX_OK;
+}
+
+int ofx_gn_stats(void* handle, double* out, int32_t cap) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && out && cap >= 0, "bad gn_stats args");
+  int n = cap < kMaxLog ? cap : kMaxLog;
+  if (n > 0) OFX_HIP(hipMemcpy(out, g->stat, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
   return OFX_OK;
 }
 
@@ -1008,7 +1210,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   }
   g->nwg_row = (N + g->row_waves - 1) / g->row_waves;
   g->nwg_node = (N + kBlk - 1) / kBlk;
-  g->nwg_terms = (int32_t)((g->T + kBlk - 1) / kBlk);
+  g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T
   if (g->T > g->T_cap) {
     for (auto pp : {(void**)&g->term_node, (void**)&g->J, (void**)&g->res, (void**)&g->node_list,
@@ -1022,7 +1224,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->blk_list, 16 * c * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->node_tmp, 4 * c * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_tmp, 16 * c * sizeof(int32_t)));
-    OFX_HIP(hipMalloc((void**)&g->part_loss, 4 * ((c + kBlk - 1) / kBlk) * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->part_loss, 4 * ((4 * c + kBlk - 1) / kBlk) * sizeof(double)));
     g->T_cap = c;
   }
   // edges + weights
@@ -1110,7 +1312,7 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
   if (g->nnzb > 0)
     hipLaunchKernelGGL(k_blocks, dim3(grid_for(g->nnzb, kBlk / 64, 1 << 30)), dim3(kBlk), 0, hs, *g, A);
-  hipLaunchKernelGGL(k_rhs, dim3(grid_for(6 * (int64_t)g->N, kBlk)), dim3(kBlk), 0, hs, *g, rhs);
+  hipLaunchKernelGGL(k_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, rhs);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }
@@ -1122,7 +1324,7 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   hipStream_t hs = as_stream(s);
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(kBlk), 0, hs, *g, (const double*)rhs, 64, g->prm.pcg_max_iter);
+  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(64), 0, hs, *g, (const double*)rhs, 64, g->prm.pcg_max_iter, gn_iter);
   hipLaunchKernelGGL(k_apply, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g);
   OFX_LAUNCH_CHECK();
   return OFX_OK;

@@ -22,7 +22,8 @@ from ._lib import call, ptr, stream_ptr, byref
 from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
-                   lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=1000, pcg_tol=1e-7)
+                   lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=1000, pcg_tol=1e-7,
+                   pcg_warm=True)
 MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
 
 
@@ -67,12 +68,20 @@ class GaussNewtonSolver:
         call("ofx_gn_info", self._h, arr)
         return list(arr)
 
+    def stats(self):
+        """Per GN step of the last solve: (PCG iterations, |b|², loss) rows; steps that did not run are 0."""
+        n = int(self.params["num_iter"])
+        arr = (ctypes.c_double * (3 * max(1, n)))()
+        call("ofx_gn_stats", self._h, arr, n)
+        return np.array(arr[:3 * n], dtype=np.float64).reshape(n, 3)
+
     def _params(self):
         p = _lib.GnParams()
         q = self.params
         p.num_iter = int(q["num_iter"])
         p.use_edge_weighting = int(bool(q["use_edge_weighting"]))
         p.pcg_max_iter = int(q["pcg_max_iter"])
+        p.pcg_warm = int(bool(q["pcg_warm"]))
         p.lambda_flow, p.lambda_depth = float(q["lambda_flow"]), float(q["lambda_depth"])
         p.lambda_arap, p.lambda_motion = float(q["lambda_arap"]), float(q["lambda_motion"])
         p.lm_factor, p.stop_loss_diff, p.pcg_tol = float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"])

@@ -39,8 +39,6 @@ namespace ofx {
 
 // --------------------------------------------------------------------------------------------
 constexpr int kBlk = 256;       // threads per WG
-constexpr int kRowBlk = 1024;   // PCG row kernels: 16 waves per WG, one block row per wave
-constexpr int kRowsPerWG = kRowBlk / 64;
 constexpr int kProj = 4;      // warm start: Galerkin projection on the last kProj GN-step solutions
 
 struct Gn {
@@ -67,12 +65,12 @@ struct Gn {
   double *R = nullptr, *t = nullptr;
   double *A_own = nullptr, *rhs_own = nullptr;
   double *Minv = nullptr, *Bm = nullptr;  // block-Jacobi inverse (N*36), B = A·M⁻¹ (nnzb*36)
-  double *x = nullptr, *r = nullptr, *u = nullptr, *w0 = nullptr, *w1 = nullptr, *zz = nullptr, *qv = nullptr,
-         *sv = nullptr, *pv = nullptr;
+  double *st = nullptr;          // PCG recurrence state, 6N records of 8 (see the PCG layout note)
+  double *w0 = nullptr, *w1 = nullptr;
   double *pcg_alpha = nullptr, *pcg_gamma = nullptr;
   int64_t pcg_cap = 0;
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
-  int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;
+  int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
   double* scal = nullptr;
   int32_t* flags = nullptr;
   double* loss_log = nullptr;
@@ -84,7 +82,6 @@ struct Gn {
   int warm_now = 0;               // this step starts from the projected x0             // PCG stop test against max(|b|, |b| of GN step 0) instead of |b|
   int32_t* host_flags = nullptr;  // pinned
   int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
-  int row_waves = kRowsPerWG;
   bool setup_done = false;
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
   bool timing = false;
@@ -94,7 +91,7 @@ struct Gn {
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_COUNT = 8 };
-enum { S_LOSS_PREV = 0, S_COUNT = 4 };
+enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
 constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 
 // ---------------------------------------------------------------------------- reductions
@@ -533,9 +530,111 @@ __device__ __forceinline__ void chol6_solve(const double* __restrict__ L, const 
   }
 }
 
-// LM damping of the diagonal blocks, explicit block inverse Minv_i, x = 0, r = b, u = M⁻¹ b,
-// recurrence vectors zeroed.  8 lanes per node: every lane factors the 6x6 block (identical bits),
-// lane c < 6 solves column c of the inverse and owns component c of the vectors.
+// ---- PCG layout. st: per node i and component c an 8-double record [x r u z q s p -] at
+// st[(6i+c)*8], so one lane's whole recurrence state is 64 contiguous bytes (4 x 16-B accesses);
+// w0/w1 (6N) double-buffer the SpMV input. Row kernels run one wave per workgroup (no barriers):
+// lane = (row r of kRW, slot q of kSL); slot q multiplies whole 6x6 blocks q, q+kSL, ... of its
+// row, DPP butterflies sum the row's slots; lanes q < 6 own component q of the row's vectors.
+// Scalars travel as per-wave partials (SoA [stream][wave]); every wave of the next launch re-sums
+// them in the same fixed order.
+enum { V_X = 0, V_R = 1, V_U = 2, V_Z = 3, V_Q = 4, V_S = 5, V_P = 6, V_N = 8 };
+constexpr int kRW = 4;          // block rows per wave
+constexpr int kSL = 64 / kRW;   // lanes (block slots) per row
+
+template <int CTL>
+__device__ __forceinline__ double dpp_mov(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// Sum over each aligned 16-lane row; every lane of the row ends with identical bits.
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_mov<0x141>(x);   // row_half_mirror
+  x += dpp_mov<0x140>(x);   // row_mirror
+  return x;
+}
+__device__ __forceinline__ double read_lane(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+// Full-wave sum, fixed order, uniform result. Call from wave-uniform control flow.
+__device__ __forceinline__ double wave_sum(double x) {
+  x = row16_sum(x);
+  return (read_lane(x, 0) + read_lane(x, 16)) + (read_lane(x, 32) + read_lane(x, 48));
+}
+// Σ_i p[k*nw + i] for K streams; U loads per lane issued up front; uniform result.
+template <int K, int U>
+__device__ __forceinline__ void sum_streams(const double* __restrict__ p, int nw, double out[K]) {
+  const int lane = threadIdx.x & 63;
+  double a[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = lane + 64 * u;
+      t[u] = i < nw ? p[(int64_t)k * nw + i] : 0.0;
+    }
+#pragma unroll
+    for (int w = 1; w < U; w <<= 1)
+#pragma unroll
+      for (int u = 0; u + w < U; u += 2 * w) t[u] += t[u + w];
+    a[k] = t[0];
+  }
+  for (int i = lane + 64 * U; i < nw; i += 64)
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += p[(int64_t)k * nw + i];
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = wave_sum(a[k]);
+}
+// n[c] without a dynamically indexed array (which the compiler would put in scratch): masked sum,
+// exact for finite n (x·1 + 0 terms); a non-finite component poisons the row, as it would anyway.
+__device__ __forceinline__ double pick6(const double n[6], int c) {
+  double v = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v += n[i] * (c == i ? 1.0 : 0.0);
+  return v;
+}
+// (B v)_row summed over the row's kSL lanes: every lane of the row gets all 6 components.
+__device__ __forceinline__ void row_spmv(const Gn& g, int row, int q, const double* __restrict__ v, double n[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) n[i] = 0.0;
+  if (row < g.N) {
+    const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
+    for (int bi = b0 + q; bi < b1; bi += kSL) {
+      const double2* blk = reinterpret_cast<const double2*>(g.Bm + 36 * (int64_t)bi);
+      const double2* vc = reinterpret_cast<const double2*>(v + 6 * (int64_t)g.col[bi]);
+      double x[6];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { const double2 t = vc[j]; x[2 * j] = t.x; x[2 * j + 1] = t.y; }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+        n[i] += ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) n[i] = row16_sum(n[i]);
+}
+__device__ __forceinline__ void load_rec(const double* __restrict__ st, int64_t o, double v[V_N]) {
+  const double2* p = reinterpret_cast<const double2*>(st + V_N * o);
+#pragma unroll
+  for (int k = 0; k < V_N / 2; ++k) { const double2 t = p[k]; v[2 * k] = t.x; v[2 * k + 1] = t.y; }
+}
+__device__ __forceinline__ void store_rec(double* __restrict__ st, int64_t o, const double v[V_N]) {
+  double2* p = reinterpret_cast<double2*>(st + V_N * o);
+#pragma unroll
+  for (int k = 0; k < V_N / 2; ++k) p[k] = make_double2(v[2 * k], v[2 * k + 1]);
+}
+
+// LM damping of the diagonal blocks, explicit block inverse Minv_i; cold start: x = 0, r = b,
+// u = M⁻¹ b, z = q = s = p = 0 (and w1 = r for k_pcg_w0's gather); warm start: M·x_j of the stored
+// solutions (the state follows in k_pcg_proj2). 8 lanes per node: every lane factors the 6x6 block
+// (identical bits), lane c < 6 solves column c of the inverse and owns component c.
 __global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
                                                    const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
@@ -550,7 +649,10 @@ __global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __re
 #pragma unroll
   for (int q = 0; q < 6; ++q) a[q * 7] += lm;
   if (c >= 6) return;
-  blk[c * 7] = a[c * 7];
+  double dg = a[0];
+#pragma unroll
+  for (int q = 1; q < 6; ++q) dg = (c == q) ? a[q * 7] : dg;
+  blk[c * 7] = dg;
   double L[21];
   bool ok = chol6(a, L);
   double e[6], col[6];
@@ -564,23 +666,31 @@ __global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __re
   double* Mi = g.Minv + 36 * (int64_t)i;
 #pragma unroll
   for (int k = 0; k < 6; ++k) Mi[k * 6 + c] = col[k];
-  // u_c = (M⁻¹ b)_c = Σ_k Minv[c][k] b_k = Σ_k col_k-of-row... M⁻¹ is symmetric: row c = column c
-  double u = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) u += col[k] * rhs[6 * i + k];
   const int64_t o = 6 * (int64_t)i + c;
   if (g.warm_now) {           // Galerkin start on span of the previous solutions: M·x_j
+    double arow[6];           // row c of the damped diagonal block (register select, no scratch)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) arow[k] = a[k];
+#pragma unroll
+    for (int cc = 1; cc < 6; ++cc)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) arow[k] = (c == cc) ? a[cc * 6 + k] : arow[k];
     for (int j = 0; j < g.n_prev; ++j) {
       const double* xj = g.xh + (int64_t)j * 6 * g.N + 6 * (int64_t)i;
       double m = 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) m += a[c * 6 + k] * xj[k];
+      for (int k = 0; k < 6; ++k) m += arow[k] * xj[k];
       g.xmh[(int64_t)j * 6 * g.N + o] = m;
     }
   } else {
-    g.x[o] = 0.0; g.r[o] = rhs[o]; g.u[o] = u;
+    // u_c = (M⁻¹ b)_c; M⁻¹ is symmetric, so row c = column c
+    double u = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) u += col[k] * rhs[6 * i + k];
+    double v[V_N] = {0.0, rhs[o], u, 0.0, 0.0, 0.0, 0.0, 0.0};
+    store_rec(g.st, o, v);
+    g.w1[o] = rhs[o];
   }
-  g.zz[o] = 0.0; g.qv[o] = 0.0; g.sv[o] = 0.0; g.pv[o] = 0.0;
 }
 
 // B_ij = A_ij · Minv_j : one thread per output entry (36 per block)
@@ -598,97 +708,62 @@ __global__ __launch_bounds__(kBlk) void k_pcg_bmat(Gn g, const double* __restric
   g.Bm[36 * bi + e] = v;
 }
 
-// One wave per block row. Lane = rr*8 + b (rr = block row component 0..5, b = block slot 0..7):
-// lane accumulates B[row][blk][rr][:]·v[col] over blocks b, b+8, ...; a 3-step xor butterfly inside
-// each aligned group of 8 lanes leaves component rr of (B·v)[row] in every lane of group rr.
-// No LDS and no barrier inside the row.
-__device__ __forceinline__ double bsr_row(const Gn& g, int row, const double* __restrict__ v) {
-  const int lane = threadIdx.x & 63;
-  double acc = 0.0;
-  if (row < g.N && lane < 48) {
-    const int rr = lane >> 3, bl = lane & 7;
-    const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-    for (int bi = b0 + bl; bi < b1; bi += 8) {
-      const int c = g.col[bi];
-      const double* blk = g.Bm + 36 * (int64_t)bi + rr * 6;
-      const double* vc = v + 6 * (int64_t)c;
-      double s = 0.0;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) s += blk[j] * vc[j];
-      acc += s;
-    }
-  }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  return acc;
-}
-
-// fixed-order sums of up to 4 interleaved partial streams (every thread gets identical bits)
-template <int NV>
-__device__ __forceinline__ void wg_sum4(const double* __restrict__ p, int n, int stride, double out[4]) {
-  constexpr int nv = NV;
-  __shared__ double s_r[4];
-  if (threadIdx.x < 64) {
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = threadIdx.x; i < n; i += 64)
-#pragma unroll
-      for (int k = 0; k < nv; ++k) a[k] += p[(int64_t)i * stride + k];
-#pragma unroll
-    for (int k = 0; k < nv; ++k)
-      for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
-    if (threadIdx.x == 0)
-#pragma unroll
-      for (int k = 0; k < nv; ++k) s_r[k] = a[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < nv; ++k) out[k] = s_r[k];
-  __syncthreads();
-}
-
-// fixed-shape WG sum of 3 values (1024 threads): wave butterflies, then wave partials in order
-__device__ __forceinline__ void wg_sum3(double v[3], double out[3]) {
-  __shared__ double s_w[3][kRowBlk / 64];
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) s_w[k][threadIdx.x >> 6] = v[k];
-  __syncthreads();
-  const int nw = blockDim.x >> 6;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    double a = 0.0;
-    for (int w = 0; w < nw; ++w) a += s_w[k][w];
-    out[k] = a;
-  }
-}
-
 // Galerkin warm start, pass 1: t_j = A x_j = B (M x_j) for the n_prev stored solutions (own rows)
-// and per-WG partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
+// and per-wave partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
 constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
-__device__ __forceinline__ int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
+__device__ __forceinline__ constexpr int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
 
-__global__ __launch_bounds__(kRowBlk) void k_pcg_proj(Gn g, const double* __restrict__ rhs) {
+__global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x;
+  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int np = g.n_prev;
   const int64_t stride = 6 * (int64_t)g.N;
-  double t[kProj];
+  double n[kProj][6];
 #pragma unroll
-  for (int j = 0; j < kProj; ++j) t[j] = j < np ? bsr_row(g, row, g.xmh + j * stride) : 0.0;
+  for (int j = 0; j < kProj; ++j)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) n[j][i] = 0.0;
+  if (row < g.N) {
+    const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
+    for (int bi = b0 + q; bi < b1; bi += kSL) {
+      const double* blk = g.Bm + 36 * (int64_t)bi;
+      const int64_t cc = 6 * (int64_t)g.col[bi];
+      double bk[36];
+#pragma unroll
+      for (int k = 0; k < 36; ++k) bk[k] = blk[k];
+#pragma unroll
+      for (int j = 0; j < kProj; ++j) {
+        if (j < np) {
+          const double* vc = g.xmh + j * stride + cc;
+          double x[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) x[k] = vc[k];
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) t += bk[6 * i + k] * x[k];
+            n[j][i] += t;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kProj; ++j)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) n[j][i] = row16_sum(n[j][i]);
   double v[kProjP];
 #pragma unroll
   for (int k = 0; k < kProjP; ++k) v[k] = 0.0;
-  if (row < g.N && lane < 48 && (lane & 7) == 0) {
-    const int64_t o = 6 * (int64_t)row + (lane >> 3);
+  if (row < g.N && q < 6) {
+    const int64_t o = 6 * (int64_t)row + q;
     const double b = rhs[o];
-    double x[kProj];
+    double x[kProj], t[kProj];
 #pragma unroll
     for (int j = 0; j < kProj; ++j) {
+      t[j] = pick6(n[j], q);
       x[j] = j < np ? g.xh[j * stride + o] : 0.0;
       if (j < np) g.th[j * stride + o] = t[j];
     }
@@ -699,201 +774,164 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_proj(Gn g, const double* __rest
       v[kProj * (kProj + 1) / 2 + j] = x[j] * b;
     }
   }
-  __shared__ double s_w[kProjP][kRowBlk / 64];
 #pragma unroll
-  for (int k = 0; k < kProjP; ++k)
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-  if ((threadIdx.x & 63) == 0)
+  for (int k = 0; k < kProjP; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < kProjP; ++k) s_w[k][threadIdx.x >> 6] = v[k];
-  __syncthreads();
-  if (threadIdx.x < kProjP) {
-    double acc = 0.0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) acc += s_w[threadIdx.x][w];
-    g.part_p[kProjP * (int64_t)blockIdx.x + threadIdx.x] = acc;
-  }
+    for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nwg_row + blockIdx.x] = v[k];
 }
 
-// Galerkin warm start, pass 2: every WG re-derives G and f from the partials (fixed order, identical
-// bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get c = 0), and
-// sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0.
-__global__ __launch_bounds__(kRowBlk) void k_pcg_proj2(Gn g, const double* __restrict__ rhs) {
+// Galerkin warm start, pass 2: every wave re-derives G and f from the partials (fixed order,
+// identical bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get
+// c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0, z = q = s = p = 0, w1 = r0.
+__global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
-  __shared__ double s_c[kProj];
+  const int lane = threadIdx.x;
+  const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const int np = g.n_prev;
-  if (threadIdx.x < 64) {
-    double p[kProjP];
+  double p[kProjP];
+  sum_streams<kProjP, 8>(g.part_p, g.nwg_row, p);
+  // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
+  double L[kProj][kProj], y[kProj], c[kProj];
+  bool use[kProj];
 #pragma unroll
-    for (int k = 0; k < kProjP; ++k) p[k] = 0.0;
-    for (int i = threadIdx.x; i < g.nwg_row; i += 64)
+  for (int j = 0; j < kProj; ++j) {
+    use[j] = false; y[j] = 0.0; c[j] = 0.0;
 #pragma unroll
-      for (int k = 0; k < kProjP; ++k) p[k] += g.part_p[kProjP * (int64_t)i + k];
+    for (int i = 0; i < kProj; ++i) L[j][i] = 0.0;
+  }
 #pragma unroll
-    for (int k = 0; k < kProjP; ++k)
-      for (int o = 32; o > 0; o >>= 1) p[k] += __shfl_xor(p[k], o, 64);
-    if (threadIdx.x == 0) {
-      // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
-      double L[kProj][kProj], y[kProj], c[kProj];
-      bool use[kProj];
+  for (int j = 0; j < kProj; ++j) {
+    if (j >= np) continue;
+    double d = p[tri(j, j)];
 #pragma unroll
-      for (int j = 0; j < kProj; ++j) {
-        use[j] = false; y[j] = 0.0; c[j] = 0.0;
+    for (int k = 0; k < j; ++k) if (use[k]) d -= L[j][k] * L[j][k];
+    if (!(d > 1e-10 * p[tri(j, j)]) || !(p[tri(j, j)] > 0.0)) continue;   // dependent / degenerate
+    use[j] = true;
+    const double ljj = sqrt(d);
+    L[j][j] = ljj;
 #pragma unroll
-        for (int i = 0; i < kProj; ++i) L[j][i] = 0.0;
-      }
-      for (int j = 0; j < np; ++j) {
-        double d = p[tri(j, j)];
-        for (int k = 0; k < j; ++k) if (use[k]) d -= L[j][k] * L[j][k];
-        if (!(d > 1e-10 * p[tri(j, j)]) || !(p[tri(j, j)] > 0.0)) continue;   // dependent / degenerate
-        use[j] = true;
-        const double ljj = sqrt(d);
-        L[j][j] = ljj;
-        for (int i = j + 1; i < np; ++i) {
-          double sdot = p[tri(j, i)];
-          for (int k = 0; k < j; ++k) if (use[k]) sdot -= L[i][k] * L[j][k];
-          L[i][j] = sdot / ljj;
-        }
-      }
-      for (int j = 0; j < np; ++j) {
-        if (!use[j]) continue;
-        double sdot = p[kProj * (kProj + 1) / 2 + j];
-        for (int k = 0; k < j; ++k) if (use[k]) sdot -= L[j][k] * y[k];
-        y[j] = sdot / L[j][j];
-      }
-      for (int j = np - 1; j >= 0; --j) {
-        if (!use[j]) continue;
-        double sdot = y[j];
-        for (int k = j + 1; k < np; ++k) if (use[k]) sdot -= L[k][j] * c[k];
-        c[j] = sdot / L[j][j];
-      }
-      bool fin = true;
-      for (int j = 0; j < kProj; ++j) fin = fin && isfinite(c[j]);
-      for (int j = 0; j < kProj; ++j) s_c[j] = fin ? c[j] : 0.0;
+    for (int i = j + 1; i < kProj; ++i) {
+      if (i >= np) continue;
+      double sd = p[tri(j, i)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) if (use[k]) sd -= L[i][k] * L[j][k];
+      L[i][j] = sd / ljj;
     }
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) {
+    if (!use[j]) continue;
+    double sd = p[kProj * (kProj + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) if (use[k]) sd -= L[j][k] * y[k];
+    y[j] = sd / L[j][j];
+  }
+#pragma unroll
+  for (int j = kProj - 1; j >= 0; --j) {
+    if (!use[j]) continue;
+    double sd = y[j];
+#pragma unroll
+    for (int k = j + 1; k < kProj; ++k) if (use[k]) sd -= L[k][j] * c[k];
+    c[j] = sd / L[j][j];
+  }
+  bool fin = true;
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) fin = fin && isfinite(c[j]);
   const int64_t stride = 6 * (int64_t)g.N;
-  double rv = 0.0;
-  if (row < g.N && lane < 6) {
-    const int64_t o = 6 * (int64_t)row + lane;
-    double xv = 0.0;
+  const bool own = row < g.N && q < 6;
+  const int64_t o = 6 * (int64_t)row + q;
+  double xv = 0.0, rv = 0.0;
+  if (own) {
     rv = rhs[o];
-    for (int j = 0; j < np; ++j) {
-      xv += s_c[j] * g.xh[j * stride + o];
-      rv -= s_c[j] * g.th[j * stride + o];
-    }
-    g.x[o] = xv;
-    g.r[o] = rv;
+#pragma unroll
+    for (int j = 0; j < kProj; ++j)
+      if (j < np && fin) { xv += c[j] * g.xh[j * stride + o]; rv -= c[j] * g.th[j * stride + o]; }
   }
   double rk[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) rk[k] = __shfl(rv, k, 64);
-  if (row < g.N && lane < 6) {
-    const double* Mi = g.Minv + 36 * (int64_t)row + 6 * lane;
+  for (int k = 0; k < 6; ++k) rk[k] = __shfl(rv, r * kSL + k, 64);
+  if (own) {
+    const double* Mi = g.Minv + 36 * (int64_t)row + 6 * q;
     double u = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) u += Mi[k] * rk[k];
-    g.u[6 * (int64_t)row + lane] = u;
+    double v[V_N] = {xv, rv, u, 0.0, 0.0, 0.0, 0.0, 0.0};
+    store_rec(g.st, o, v);
+    g.w1[o] = rv;
   }
 }
 
-// fixed-shape WG sum of 4 values (1024 threads): wave butterflies, then wave partials in order
-__device__ __forceinline__ void wg_sum4v(double v[4], double out[4]) {
-  __shared__ double s_w4[4][kRowBlk / 64];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s_w4[k][threadIdx.x >> 6] = v[k];
-  __syncthreads();
-  const int nw = blockDim.x >> 6;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    double a = 0.0;
-    for (int w = 0; w < nw; ++w) a += s_w4[k][w];
-    out[k] = a;
-  }
-}
-
-// w0 = A u0 = B r0; partials (γ0 = r·u, δ0 = w·u, r·r) -> PP[0], b·b -> PB.
-__global__ __launch_bounds__(kRowBlk) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
+// w0 = A u0 = B r0 (r0 gathered from w1); per-wave partials (γ0 = r·u, δ0 = w·u, r·r) -> parity 0,
+// b·b -> part_b.
+__global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
-  const double wv = bsr_row(g, row, g.r);
-  if (row < g.N && lane < 48 && (lane & 7) == 0) {
-    const int64_t o = 6 * (int64_t)row + (lane >> 3);
-    g.w0[o] = wv;
-    double r = g.r[o], u = g.u[o], b = rhs[o];
-    v[0] = r * u; v[1] = wv * u; v[2] = r * r; v[3] = b * b;
+  const int lane = threadIdx.x;
+  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
+  double n[6];
+  row_spmv(g, row, q, g.w1, n);
+  double d[4] = {0.0, 0.0, 0.0, 0.0};
+  if (row < g.N && q < 6) {
+    const int64_t o = 6 * (int64_t)row + q;
+    const double w = pick6(n, q);
+    g.w0[o] = w;
+    double v[V_N];
+    load_rec(g.st, o, v);
+    const double b = rhs[o];
+    d[0] = v[V_R] * v[V_U]; d[1] = w * v[V_U]; d[2] = v[V_R] * v[V_R]; d[3] = b * b;
   }
-  double s[4];
-  wg_sum4v(v, s);
-  if (threadIdx.x == 0) {
-    double* P = g.part_p + 3 * (int64_t)blockIdx.x;
-    P[0] = s[0]; P[1] = s[1]; P[2] = s[2];
-    g.part_b[blockIdx.x] = s[3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = wave_sum(d[k]);
+  if (lane == 0) {
+    const int nw = g.nwg_row;
+    g.part_p[blockIdx.x] = d[0]; g.part_p[nw + blockIdx.x] = d[1]; g.part_p[2 * nw + blockIdx.x] = d[2];
+    g.part_b[blockIdx.x] = d[3];
   }
 }
 
-// iteration it (reads PP[it&1], W[it&1]; writes PP[(it+1)&1], W[(it+1)&1]).
-// Latency schedule: the SpMV chain (row_ptr -> B,col -> w[col]) and the own-row vector loads do not
-// depend on this iteration's scalars, so they are issued first; wave 0 meanwhile loads the partials
-// of the previous kernel; one barrier publishes the scalars; then the recurrences + partial dots.
-__global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
-  __shared__ double s_sc[4];
-  __shared__ int s_stop;
+// Iteration it (reads partials parity it&1 and w[it&1]; writes parity (it+1)&1 and w[(it+1)&1]).
+// Everything this launch needs — previous partials, own-row state, M⁻¹ row, B blocks, w gather —
+// is loaded up front; the scalars are uniform per wave, so there is no barrier at all.
+__global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
+  const int lane = threadIdx.x;
+  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int nw = g.nwg_row;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
   double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
-  // wave 0: previous partials (γ, δ, r·r) and b·b, plus the stop flags
-  double pa[4] = {0.0, 0.0, 0.0, 0.0};
-  int stop = 0;
-  if (threadIdx.x < 64) {
-    const double* PP = g.part_p + 3 * (int64_t)nw * (it & 1);
-    for (int i = threadIdx.x; i < nw; i += 64) {
-      pa[0] += PP[3 * i]; pa[1] += PP[3 * i + 1]; pa[2] += PP[3 * i + 2]; pa[3] += g.part_b[i];
-    }
-    stop = g.flags[F_DONE] | g.flags[F_STOPPED];
-  }
-  // previous-iteration scalars written by WG 0 of the previous kernel (prefetched before the barrier)
+  const int stop = g.flags[F_DONE] | g.flags[F_STOPPED];
   const double gam_prev = it > 0 ? g.pcg_gamma[it - 1] : 1.0;
   const double alpha_prev = it > 0 ? g.pcg_alpha[it - 1] : 1.0;
-  // SpMV n = A M⁻¹ w for this wave's row (independent of the scalars)
-  const double n = bsr_row(g, row, wc);
-  const bool upd = row < g.N && lane < 48 && (lane & 7) == 0;
-  const int c = lane >> 3;
-  const int64_t o = 6 * (int64_t)row + c;
-  double m = 0.0, w = 0.0, zz0 = 0.0, q0 = 0.0, s0 = 0.0, p0 = 0.0, u0 = 0.0, r0 = 0.0, x0 = 0.0;
-  if (upd) {
-    const double* Mi = g.Minv + 36 * (int64_t)row + 6 * c;
-    const double* wi = wc + 6 * (int64_t)row;
+  const double bb_stored = g.scal[S_BB];
+  const bool own = row < g.N && q < 6;
+  const int64_t o = 6 * (int64_t)row + q;
+  double v[V_N], m = 0.0, w = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];      // m = M⁻¹ w (own row)
-    w = wc[o]; zz0 = g.zz[o]; q0 = g.qv[o]; s0 = g.sv[o]; p0 = g.pv[o]; u0 = g.u[o]; r0 = g.r[o]; x0 = g.x[o];
-  }
-  if (threadIdx.x < 64) {
+  for (int k = 0; k < V_N; ++k) v[k] = 0.0;
+  if (own) {
+    load_rec(g.st, o, v);
+    const double2* Mi = reinterpret_cast<const double2*>(g.Minv + 36 * (int64_t)row + 6 * q);
+    const double2* wi = reinterpret_cast<const double2*>(wc + 6 * (int64_t)row);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      for (int off = 32; off > 0; off >>= 1) pa[k] += __shfl_xor(pa[k], off, 64);
-    if (threadIdx.x == 0) {
-      s_sc[0] = pa[0]; s_sc[1] = pa[1]; s_sc[2] = pa[2]; s_sc[3] = pa[3];
-      s_stop = stop;
-    }
+    for (int k = 0; k < 3; ++k) { const double2 a = Mi[k], b = wi[k]; m += a.x * b.x + a.y * b.y; }
+    w = wc[o];
   }
-  __syncthreads();
-  if (s_stop) return;
-  const double gam = s_sc[0], del = s_sc[1], rr = s_sc[2];
-  const double bb = s_sc[3];
+  double pa[3];
+  sum_streams<3, 16>(g.part_p + 3 * (int64_t)nw * (it & 1), nw, pa);
+  double bb = bb_stored;
+  if (it == 0) {
+    double t[1];
+    sum_streams<1, 16>(g.part_b, nw, t);
+    bb = t[0];
+  }
+  double n[6];
+  row_spmv(g, row, q, wc, n);
+  if (stop) return;
+  const double gam = pa[0], del = pa[1], rr = pa[2];
   const double tol = g.prm.pcg_tol;
+  const bool lead = blockIdx.x == 0 && lane == 0;
+  if (it == 0 && lead) g.scal[S_BB] = bb;
   if (rr <= tol * tol * bb || gam == 0.0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
+    if (lead) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
     return;
   }
   double beta = 0.0, alpha;
@@ -904,32 +942,33 @@ __global__ __launch_bounds__(kRowBlk) void k_pcg_iter(Gn g, int it) {
     alpha = gam / (del - beta * gam / alpha_prev);
   }
   if (!isfinite(alpha) || !(alpha > 0.0)) {  // breakdown (A SPD => alpha > 0): keep x
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (lead) {
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
       if (!isfinite(alpha)) g.flags[F_ILL] = 1;
     }
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) { g.pcg_alpha[it] = alpha; g.pcg_gamma[it] = gam; }
-  double v[3] = {0.0, 0.0, 0.0};
-  if (upd) {
-    const double zz = n + beta * zz0;
-    const double q = m + beta * q0;
-    const double sv = w + beta * s0;
-    const double p = u0 + beta * p0;
-    g.zz[o] = zz; g.qv[o] = q; g.sv[o] = sv; g.pv[o] = p;
-    g.x[o] = x0 + alpha * p;
-    const double r = r0 - alpha * sv;
-    const double u = u0 - alpha * q;
+  if (lead) { g.pcg_alpha[it] = alpha; g.pcg_gamma[it] = gam; }
+  double d[3] = {0.0, 0.0, 0.0};
+  if (own) {
+    const double nc = pick6(n, q);
+    const double zz = nc + beta * v[V_Z];
+    const double qq = m + beta * v[V_Q];
+    const double sv = w + beta * v[V_S];
+    const double p = v[V_U] + beta * v[V_P];
+    const double r = v[V_R] - alpha * sv;
+    const double u = v[V_U] - alpha * qq;
     const double w2 = w - alpha * zz;
-    g.r[o] = r; g.u[o] = u; wn[o] = w2;
-    v[0] = r * u; v[1] = w2 * u; v[2] = r * r;
+    const double nv[V_N] = {v[V_X] + alpha * p, r, u, zz, qq, sv, p, 0.0};
+    store_rec(g.st, o, nv);
+    wn[o] = w2;
+    d[0] = r * u; d[1] = w2 * u; d[2] = r * r;
   }
-  double s3[3];
-  wg_sum3(v, s3);
-  if (threadIdx.x == 0) {
-    double* P = g.part_p + 3 * (int64_t)nw * ((it + 1) & 1) + 3 * (int64_t)blockIdx.x;
-    P[0] = s3[0]; P[1] = s3[1]; P[2] = s3[2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
+  if (lane == 0) {
+    double* P = g.part_p + 3 * (int64_t)nw * ((it + 1) & 1);
+    P[blockIdx.x] = d[0]; P[nw + blockIdx.x] = d[1]; P[2 * nw + blockIdx.x] = d[2];
   }
 }
 
@@ -976,10 +1015,18 @@ __global__ void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_l
 }
 
 // kornia 0.7.0 angle_axis_to_rotation_matrix + left-multiplicative update (model.py:744-748).
-__global__ void k_apply(Gn g) {
+// xsave (nullable): ring slot receiving this step's solution for the next steps' warm start.
+__global__ void k_apply(Gn g, double* __restrict__ xsave) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.N || !g.flags[F_APPLY] || g.flags[F_STOPPED]) return;
-  double a0 = g.x[6 * i], a1 = g.x[6 * i + 1], a2 = g.x[6 * i + 2];
+  if (i >= g.N) return;
+  double x[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) x[c] = g.st[V_N * (6 * (int64_t)i + c) + V_X];
+  if (xsave)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) xsave[6 * (int64_t)i + c] = x[c];
+  if (!g.flags[F_APPLY] || g.flags[F_STOPPED]) return;
+  double a0 = x[0], a1 = x[1], a2 = x[2];
   double th2 = a0 * a0 + a1 * a1 + a2 * a2;
   double Ri[9];
   if (th2 > 1e-6) {
@@ -997,7 +1044,7 @@ __global__ void k_apply(Gn g) {
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c) Rn[3 * r + c] = Ri[3 * r] * R[c] + Ri[3 * r + 1] * R[3 + c] + Ri[3 * r + 2] * R[6 + c];
   for (int c = 0; c < 9; ++c) R[c] = Rn[c];
-  for (int c = 0; c < 3; ++c) g.t[3 * i + c] += g.x[6 * i + 3 + c];
+  for (int c = 0; c < 3; ++c) g.t[3 * i + c] += x[3 + c];
 }
 
 __global__ void k_finish(Gn g, float* __restrict__ rot, float* __restrict__ trans, int32_t* __restrict__ status,
@@ -1036,7 +1083,7 @@ static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->row_cnt, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
-                  g->x, g->r, g->u, g->w0, g->w1, g->zz, g->qv, g->sv, g->pv, g->pcg_alpha, g->pcg_gamma,
+                  g->st, g->w0, g->w1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
                   g->loss_log, g->stat, g->xh, g->xmh, g->th};
   for (void* p : ptrs)
@@ -1047,10 +1094,7 @@ static void free_all(Gn* g) {
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
   g->warm_now = 0;
-  if (g->prm.pcg_warm && gn_iter > 0) {   // ring slot (k-1) mod kProj <- x_{k-1}
-    const int slot = (gn_iter - 1) % kProj;
-    OFX_HIP(hipMemcpyAsync(g->xh + (int64_t)slot * 6 * g->N, g->x, 6 * (size_t)g->N * sizeof(double),
-                           hipMemcpyDeviceToDevice, hs));
+  if (g->prm.pcg_warm && gn_iter > 0) {   // k_apply of the previous steps filled the ring
     g->n_prev = gn_iter < kProj ? gn_iter : kProj;
     g->warm_now = 1;
   }
@@ -1058,10 +1102,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   if (g->nnzb > 0)
     hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(36 * g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
   if (g->warm_now) {
-    hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
-    hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
+    hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
   }
-  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, (const double*)rhs);
+  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g->timing) {
@@ -1076,12 +1120,12 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   while (it < max_it) {
     int n = chunk < max_it - it ? chunk : max_it - it;
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, it);
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64), 0, hs, *g, it);
     g->n_iter_launches += n;
     OFX_LAUNCH_CHECK();
     // convergence probe: k_pcg_iter(it) tests |r| first and only iterates if not converged
     if (it < max_it) {
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64 * g->row_waves), 0, hs, *g, it);
+      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64), 0, hs, *g, it);
       ++it;
       ++g->n_iter_launches;
     }
@@ -1119,11 +1163,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 1);
   ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
-  ALLOC(g->Minv, 36 * N); ALLOC(g->x, 6 * N); ALLOC(g->r, 6 * N); ALLOC(g->u, 6 * N);
-  ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N); ALLOC(g->zz, 6 * N); ALLOC(g->qv, 6 * N); ALLOC(g->sv, 6 * N);
-  ALLOC(g->pv, 6 * N);
+  ALLOC(g->Minv, 36 * N); ALLOC(g->st, V_N * 6 * N); ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N);
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->xmh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
-  const int64_t max_row_wg = (N + 3) / 4;   // smallest PCG workgroup: 4 rows (OFX_PCG_WAVES)
+  const int64_t max_row_wg = (N + kRW - 1) / kRW;
   ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->rhs_own, 6 * N + 4);
@@ -1203,12 +1245,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
-  {
-    const char* e = getenv("OFX_PCG_WAVES");     // tuning knob: waves (block rows) per PCG workgroup
-    int w = e ? atoi(e) : kRowsPerWG;
-    g->row_waves = (w == 4 || w == 8 || w == 16) ? w : kRowsPerWG;
-  }
-  g->nwg_row = (N + g->row_waves - 1) / g->row_waves;
+  g->nwg_row = (N + kRW - 1) / kRW;
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T
@@ -1325,7 +1362,8 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
   hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(64), 0, hs, *g, (const double*)rhs, 64, g->prm.pcg_max_iter, gn_iter);
-  hipLaunchKernelGGL(k_apply, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g);
+  double* xsave = g->prm.pcg_warm ? g->xh + (int64_t)(gn_iter % kProj) * 6 * g->N : nullptr;
+  hipLaunchKernelGGL(k_apply, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g, xsave);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

@@ -1,0 +1,470 @@
+// Latency micro-benchmark for the PCG iteration kernel structure (tuning tool, not product code).
+// Synthetic block-sparse pattern shaped like the GN system (N block rows of 6x6 f64, ~12 blocks
+// per row). Each variant is launched back-to-back ITERS times on one stream; reports us/launch.
+//
+//   hipcc -O3 --offload-arch=gfx950 -o /tmp/pcg_micro tools/pcg_micro.hip && /tmp/pcg_micro
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+constexpr int N = 2073, ITERS = 2000;
+constexpr int RPW = 16;   // rows (waves) per WG
+
+struct Sys {
+  int *row_ptr, *col, *tpos;
+  double *B, *wv0, *wv1, *wg0, *wg1, *vec, *part, *Minv;
+  int nw, nnzb;
+  double *rec, *partw;   // AoS node state (N x 48: 8 vectors x 6), per-wave partials (2 x 3 x nwaves)
+  int nwaves;
+};
+
+__device__ __forceinline__ double red8(double a) {
+  a += __shfl_xor(a, 1, 64); a += __shfl_xor(a, 2, 64); a += __shfl_xor(a, 4, 64);
+  return a;
+}
+
+__global__ __launch_bounds__(1024) void k_empty(Sys s, int it) {
+  if (it < 0) s.part[0] = 1.0;
+}
+
+// wave 0 loads the previous partials, barrier, thread 0 writes a new partial
+__global__ __launch_bounds__(1024) void k_partials(Sys s, int it) {
+  __shared__ double sh;
+  if (threadIdx.x < 64) {
+    const double* P = s.part + 3 * s.nw * (it & 1);
+    double a = 0.0;
+    for (int i = threadIdx.x; i < s.nw; i += 64) a += P[3 * i] + P[3 * i + 1] + P[3 * i + 2];
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (threadIdx.x == 0) sh = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double* P = s.part + 3 * s.nw * ((it + 1) & 1) + 3 * blockIdx.x;
+    P[0] = sh * 1e-9; P[1] = 0.0; P[2] = 0.0;
+  }
+}
+
+// one dependent trip: every thread loads one double and stores it
+__global__ __launch_bounds__(1024) void k_copy(Sys s, int it) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 6 * N) ((it & 1) ? s.wv0 : s.wv1)[i] = ((it & 1) ? s.wv1 : s.wv0)[i] + 1e-9;
+}
+// two dependent trips: load an index, then the value
+__global__ __launch_bounds__(1024) void k_copy2(Sys s, int it) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 6 * N) {
+    int j = s.col[i % s.nnzb];
+    ((it & 1) ? s.wv0 : s.wv1)[i] = ((it & 1) ? s.wv1 : s.wv0)[6 * j + (i % 6)] + 1e-9;
+  }
+}
+
+// the shape of the current k_pcg_iter: row_ptr -> (col, B) -> w[col] gather, own-row vectors,
+// partials, recurrences, 3 WG sums, partial write. XCD0 = only WGs with blockIdx % 8 == 0 work.
+// F_ELL: row blocks at fixed offsets (no row_ptr trip; synthetic, assumes <= 13 blocks/row, padding
+// reads real neighbours' data); F_PRE: own-row vectors loaded before the SpMV, SpMV slots unrolled x2;
+// F_FAKEW: vector writes predicated off at run time (computation kept); F_MINW: only w written.
+enum { F_ELL = 1, F_PRE = 2, F_FAKEW = 4, F_MINW = 8, F_SMALLB = 16, F_F32B = 32, F_SMALLW = 64 };
+template <bool PUSH, bool XCD0, int F = 0>
+__global__ __launch_bounds__(1024) void k_iter(Sys s, int it) {
+  int wgid = blockIdx.x;
+  if (XCD0) { if (wgid & 7) return; wgid >>= 3; }
+  __shared__ double s_sc[3];
+  __shared__ double s_w[3][RPW];
+  const int lane = threadIdx.x & 63;
+  const int row = wgid * RPW + (threadIdx.x >> 6);
+  const double* wc = (it & 1) ? s.wv1 : s.wv0;
+  double* wn = (it & 1) ? s.wv0 : s.wv1;
+  const double* gc = (it & 1) ? s.wg1 : s.wg0;
+  double* gn = (it & 1) ? s.wg0 : s.wg1;
+  double pa[3] = {0.0, 0.0, 0.0};
+  if (threadIdx.x < 64) {
+    const double* P = s.part + 3 * s.nw * (it & 1);
+    for (int i = threadIdx.x; i < s.nw; i += 64) { pa[0] += P[3 * i]; pa[1] += P[3 * i + 1]; pa[2] += P[3 * i + 2]; }
+  }
+  const int rr = lane >> 3, bl = lane & 7;
+  const bool upd = row < N && lane < 48 && bl == 0;
+  const int64_t o = 6 * (int64_t)row + rr;
+  double m = 0.0, v[8], wown = 0.0;
+  for (int k = 0; k < 8; ++k) v[k] = 0.0;
+  if ((F & F_PRE) && upd) {
+    const double* Mi = s.Minv + 36 * (int64_t)row + 6 * rr;
+    const double* wi = wc + 6 * (int64_t)row;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = s.vec[(int64_t)k * 6 * N + o];
+    wown = wc[o];
+  }
+  double acc = 0.0;
+  int b0 = 0, b1 = 0;
+  if (row < N && lane < 48) {
+    if (F & F_ELL) { b0 = row * 12; b1 = b0 + 12; if (b1 > s.nnzb) b1 = s.nnzb; }
+    else { b0 = s.row_ptr[row]; b1 = s.row_ptr[row + 1]; }
+    if (F & F_PRE) {
+      for (int bi = b0 + bl; bi < b1; bi += 16) {
+        const bool two = bi + 8 < b1;
+        const double* blk = s.B + 36 * (int64_t)bi + rr * 6;
+        const double* blk2 = s.B + 36 * (int64_t)(two ? bi + 8 : bi) + rr * 6;
+        const double* vc = PUSH ? gc + 6 * (int64_t)bi : wc + 6 * (int64_t)s.col[bi];
+        const double* vc2 = PUSH ? gc + 6 * (int64_t)(two ? bi + 8 : bi) : wc + 6 * (int64_t)s.col[two ? bi + 8 : bi];
+        double t = 0.0, t2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) { t += blk[j] * vc[j]; t2 += blk2[j] * vc2[j]; }
+        acc += t + (two ? t2 : 0.0);
+      }
+    } else {
+      for (int bi = b0 + bl; bi < b1; bi += 8) {
+        const int bb = (F & F_SMALLB) ? (bi & 255) : bi;
+        const double* blk = s.B + 36 * (int64_t)bb + rr * 6;
+        const float* blkf = (const float*)s.B + 36 * (int64_t)bb + rr * 6;
+        const int cc = (F & F_SMALLW) ? (bi & 63) : s.col[bi];
+        const double* vc = PUSH ? gc + 6 * (int64_t)bi : wc + 6 * (int64_t)cc;
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) t += ((F & F_F32B) ? (double)blkf[j] : blk[j]) * vc[j];
+        acc += t;
+      }
+    }
+  }
+  acc = red8(acc);
+  if (!(F & F_PRE) && upd) {
+    const double* Mi = s.Minv + 36 * (int64_t)row + 6 * rr;
+    const double* wi = wc + 6 * (int64_t)row;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = s.vec[(int64_t)k * 6 * N + o];
+    wown = wc[o];
+  }
+  if (threadIdx.x < 64) {
+    for (int k = 0; k < 3; ++k)
+      for (int off = 32; off > 0; off >>= 1) pa[k] += __shfl_xor(pa[k], off, 64);
+    if (threadIdx.x == 0) { s_sc[0] = pa[0]; s_sc[1] = pa[1]; s_sc[2] = pa[2]; }
+  }
+  __syncthreads();
+  const double al = 1e-3 + 1e-12 * s_sc[0], be = 1e-3 + 1e-12 * s_sc[1];
+  const bool dow = !(F & F_FAKEW) || s_sc[2] == 12345.0;
+  double d[3] = {0.0, 0.0, 0.0};
+  double w2 = 0.0;
+  if (upd) {
+    const double zz = acc + be * v[0], q = m + be * v[1], sv = v[2] + be * v[3], p = v[4] + be * v[5];
+    const double r = v[6] - al * sv, u = v[7] - al * q;
+    w2 = 0.5 * (wown - al * zz);
+    if (dow && !(F & F_MINW)) {
+      s.vec[o] = zz; s.vec[6 * N + o] = q; s.vec[3 * 6 * N + o] = sv; s.vec[5 * 6 * N + o] = p;
+      s.vec[6 * 6 * N + o] = r; s.vec[7 * 6 * N + o] = u;
+    }
+    if (dow) wn[o] = w2;
+    d[0] = r * u; d[1] = w2 * u; d[2] = r * r;
+  }
+  if (PUSH) {   // scatter own w2 into the gathered slots of every block in this column
+    double wk[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) wk[k] = __shfl(w2, 8 * k, 64);
+    if (row < N && lane < 48) {
+      for (int bi = b0 + bl; bi < b1; bi += 8) gn[6 * (int64_t)s.tpos[bi] + rr] = wk[rr];
+    }
+  }
+  for (int k = 0; k < 3; ++k)
+    for (int off = 32; off > 0; off >>= 1) d[k] += __shfl_xor(d[k], off, 64);
+  if (lane == 0) for (int k = 0; k < 3; ++k) s_w[k][threadIdx.x >> 6] = d[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double* P = s.part + 3 * s.nw * ((it + 1) & 1) + 3 * wgid;
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+      for (int w = 0; w < RPW; ++w) a += s_w[k][w];
+      P[k] = a * 1e-30;
+    }
+  }
+}
+
+// cumulative build-up of the iteration: S=1 partials; 2 + row_ptr trip; 3 + SpMV gather; 4 + own
+// vectors and recurrence writes; 5 + second WG reduction (= full iteration)
+template <int S>
+__global__ __launch_bounds__(1024) void k_step(Sys s, int it) {
+  __shared__ double s_sc[3];
+  __shared__ double s_w[3][RPW];
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * RPW + (threadIdx.x >> 6);
+  const double* wc = (it & 1) ? s.wv1 : s.wv0;
+  double* wn = (it & 1) ? s.wv0 : s.wv1;
+  double pa[3] = {0.0, 0.0, 0.0};
+  if (threadIdx.x < 64) {
+    const double* P = s.part + 3 * s.nw * (it & 1);
+    for (int i = threadIdx.x; i < s.nw; i += 64) { pa[0] += P[3 * i]; pa[1] += P[3 * i + 1]; pa[2] += P[3 * i + 2]; }
+  }
+  const int rr = lane >> 3, bl = lane & 7;
+  double acc = 0.0;
+  if (S >= 2 && row < N && lane < 48) {
+    const int b0 = s.row_ptr[row], b1 = s.row_ptr[row + 1];
+    if (S == 2) acc = b1 - b0;
+    if (S >= 3)
+      for (int bi = b0 + bl; bi < b1; bi += 8) {
+        const double* blk = s.B + 36 * (int64_t)bi + rr * 6;
+        const double* vc = wc + 6 * (int64_t)s.col[bi];
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) t += blk[j] * vc[j];
+        acc += t;
+      }
+  }
+  if (S >= 3) acc = red8(acc);
+  const bool upd = row < N && lane < 48 && bl == 0;
+  const int64_t o = 6 * (int64_t)row + rr;
+  double m = 0.0, v[8], wown = 0.0;
+  for (int k = 0; k < 8; ++k) v[k] = 0.0;
+  if (S >= 4 && upd) {
+    const double* Mi = s.Minv + 36 * (int64_t)row + 6 * rr;
+    const double* wi = wc + 6 * (int64_t)row;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = s.vec[(int64_t)k * 6 * N + o];
+    wown = wc[o];
+  }
+  if (threadIdx.x < 64) {
+    for (int k = 0; k < 3; ++k)
+      for (int off = 32; off > 0; off >>= 1) pa[k] += __shfl_xor(pa[k], off, 64);
+    if (threadIdx.x == 0) { s_sc[0] = pa[0]; s_sc[1] = pa[1]; s_sc[2] = pa[2]; }
+  }
+  __syncthreads();
+  const double al = 1e-3 + 1e-12 * s_sc[0], be = 1e-3 + 1e-12 * s_sc[1];
+  double d[3] = {0.0, 0.0, 0.0};
+  if (upd) {
+    if (S < 4) wn[o] = 1e-3 * (acc + al);
+    else {
+      const double zz = acc + be * v[0], q = m + be * v[1], sv = v[2] + be * v[3], p = v[4] + be * v[5];
+      const double r = v[6] - al * sv, u = v[7] - al * q;
+      const double w2 = 0.5 * (wown - al * zz);
+      s.vec[o] = zz; s.vec[6 * N + o] = q; s.vec[3 * 6 * N + o] = sv; s.vec[5 * 6 * N + o] = p;
+      s.vec[6 * 6 * N + o] = r; s.vec[7 * 6 * N + o] = u; wn[o] = w2;
+      d[0] = r * u; d[1] = w2 * u; d[2] = r * r;
+    }
+  }
+  if (S >= 5) {
+    for (int k = 0; k < 3; ++k)
+      for (int off = 32; off > 0; off >>= 1) d[k] += __shfl_xor(d[k], off, 64);
+    if (lane == 0) for (int k = 0; k < 3; ++k) s_w[k][threadIdx.x >> 6] = d[k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* P = s.part + 3 * s.nw * ((it + 1) & 1) + 3 * blockIdx.x;
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+      if (S >= 5) for (int w = 0; w < RPW; ++w) a += s_w[k][w];
+      P[k] = a * 1e-30 + 1e-30 * s_sc[k];
+    }
+  }
+}
+
+// Restructured iteration: RW rows per wave (lane = (row r, slot q), SL = 64/RW slots per row), one
+// wave per WG (no barriers), each lane multiplies a whole 6x6 block; per-row 6-vector via xor
+// butterflies over the SL slot lanes; own-row state in an AoS record (8 vectors x 6 per node);
+// per-wave partials; every wave re-derives the scalars from the previous launch's per-wave partials.
+__device__ __forceinline__ double dpp_d(double x, int ctrlsel) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  switch (ctrlsel) {
+    case 0: lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false); break;
+    case 1: lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false); break;
+    case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false); break;
+    default: lo = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xF, 0xF, false); break;
+  }
+  return __hiloint2double(hi, lo);
+}
+// sum over aligned groups of G lanes (G = 2,4,8,16), result in every lane of the group
+template <int G>
+__device__ __forceinline__ double group_sum(double x) {
+  x += dpp_d(x, 0);
+  if (G >= 4) x += dpp_d(x, 1);
+  if (G >= 8) x += dpp_d(x, 2);
+  if (G >= 16) x += dpp_d(x, 3);
+  return x;
+}
+// full wave sum (fixed order): row sums by DPP, then the 4 row totals via readlane
+__device__ __forceinline__ double wave_sum(double x) {
+  x = group_sum<16>(x);
+  const double a = __shfl(x, 0, 64), b = __shfl(x, 16, 64), c = __shfl(x, 32, 64), d = __shfl(x, 48, 64);
+  return (a + b) + (c + d);
+}
+
+template <int RW, int V = 0>
+__global__ __launch_bounds__(64) void k_iterw(Sys s, int it) {
+  constexpr int SL = 64 / RW;
+  const int lane = threadIdx.x;
+  const int r = lane / SL, q = lane % SL;
+  const int row = blockIdx.x * RW + r;
+  const double* wc = (it & 1) ? s.wv1 : s.wv0;
+  double* wn = (it & 1) ? s.wv0 : s.wv1;
+  // scalars: previous per-wave partials
+  double pa[3] = {0.0, 0.0, 0.0};
+  if (V == 0) {
+    const double* P = s.partw + 3 * (int64_t)s.nwaves * (it & 1);
+    for (int i = lane; i < s.nwaves; i += 64) { pa[0] += P[3 * i]; pa[1] += P[3 * i + 1]; pa[2] += P[3 * i + 2]; }
+  } else {   // SoA partials [3][nwaves], all loads issued up front (nwaves <= 64*8)
+    const double* P = s.partw + 3 * (int64_t)s.nwaves * (it & 1);
+    double t[3][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = lane + 64 * u;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) t[k][u] = i < s.nwaves ? P[k * s.nwaves + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pa[k] = ((t[k][0] + t[k][1]) + (t[k][2] + t[k][3])) + ((t[k][4] + t[k][5]) + (t[k][6] + t[k][7]));
+  }
+  // own-row state: lane (r, c<6) holds component c of the 8 vectors
+  const bool own = row < N && q < 6;
+  double v[8], m = 0.0;
+  for (int k = 0; k < 8; ++k) v[k] = 0.0;
+  if (own) {
+    const double* R = s.rec + 48 * (int64_t)row + q;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = R[6 * k];
+    const double* Mi = s.Minv + 36 * (int64_t)row + 6 * q;
+    const double* wi = wc + 6 * (int64_t)row;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) m += Mi[k] * wi[k];
+  }
+  // SpMV: lane (r, q) takes blocks q, q+SL, ... of row r
+  double n[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (row < N) {
+    const int b0 = s.row_ptr[row], b1 = s.row_ptr[row + 1];
+    for (int bi = b0 + q; bi < b1; bi += SL) {
+      const double* blk = s.B + 36 * (int64_t)bi;
+      const double* vc = wc + 6 * (int64_t)s.col[bi];
+      double x[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) x[j] = vc[j];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) t += blk[6 * i + j] * x[j];
+        n[i] += t;
+      }
+    }
+  }
+  if (V >= 2) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) n[i] = group_sum<SL>(n[i]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pa[k] = wave_sum(pa[k]);
+  } else {
+#pragma unroll
+    for (int off = 1; off < SL; off <<= 1)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) n[i] += __shfl_xor(n[i], off, 64);
+    for (int k = 0; k < 3; ++k)
+      for (int off = 32; off > 0; off >>= 1) pa[k] += __shfl_xor(pa[k], off, 64);
+  }
+  const double al = 1e-3 + 1e-12 * pa[0], be = 1e-3 + 1e-12 * pa[1];
+  double nc = n[0];
+#pragma unroll
+  for (int i = 1; i < 6; ++i) nc = (q == i) ? n[i] : nc;
+  double d[3] = {0.0, 0.0, 0.0};
+  if (own) {
+    const double zz = nc + be * v[3], qq = m + be * v[4], sv = v[0] + be * v[5], p = v[2] + be * v[6];
+    const double rr = v[1] - al * sv, u = v[2] - al * qq;
+    const double w2 = 0.5 * (v[0] - al * zz);
+    double* R = s.rec + 48 * (int64_t)row + q;
+    R[6 * 1] = rr; R[6 * 2] = u; R[6 * 3] = zz; R[6 * 4] = qq; R[6 * 5] = sv; R[6 * 6] = p; R[6 * 7] = v[7] + al * p;
+    wn[6 * (int64_t)row + q] = w2;
+    d[0] = rr * u; d[1] = w2 * u; d[2] = rr * rr;
+  }
+  if (V >= 2) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
+  } else {
+    for (int k = 0; k < 3; ++k)
+      for (int off = 32; off > 0; off >>= 1) d[k] += __shfl_xor(d[k], off, 64);
+  }
+  if (lane == 0) {
+    double* P = s.partw + 3 * (int64_t)s.nwaves * ((it + 1) & 1);
+    if (V == 0) { P += 3 * blockIdx.x; P[0] = d[0] * 1e-30; P[1] = d[1] * 1e-30; P[2] = d[2] * 1e-30; }
+    else { P[blockIdx.x] = d[0] * 1e-30; P[s.nwaves + blockIdx.x] = d[1] * 1e-30; P[2 * s.nwaves + blockIdx.x] = d[2] * 1e-30; }
+  }
+}
+
+template <typename F>
+static double timeit(F launch) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  for (int i = 0; i < 50; ++i) launch(i);
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < ITERS; ++i) launch(i);
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipGetLastError());
+  return 1e3 * ms / ITERS;
+}
+
+int main() {
+  // grid-surface graph 46 x 46 (cropped to N): 8-neighbourhood + 4 two-hop axis neighbours
+  const int G = 46;
+  std::vector<std::vector<int>> adj(N);
+  for (int i = 0; i < N; ++i) {
+    int x = i % G, y = i / G;
+    for (int dy = -2; dy <= 2; ++dy)
+      for (int dx = -2; dx <= 2; ++dx) {
+        bool keep = (abs(dx) <= 1 && abs(dy) <= 1) || (dx == 0 && abs(dy) == 2) || (dy == 0 && abs(dx) == 2);
+        int xx = x + dx, yy = y + dy, j = yy * G + xx;
+        if (keep && xx >= 0 && xx < G && yy >= 0 && j < N && j >= 0) adj[i].push_back(j);
+      }
+  }
+  std::vector<int> rp(N + 1, 0), cl, tp;
+  for (int i = 0; i < N; ++i) { rp[i + 1] = rp[i] + (int)adj[i].size(); for (int j : adj[i]) cl.push_back(j); }
+  const int nnzb = rp[N];
+  tp.resize(nnzb);
+  for (int i = 0; i < N; ++i)
+    for (int k = rp[i]; k < rp[i + 1]; ++k) {      // position of block (j,i) for block (i,j)
+      int j = cl[k];
+      for (int q = rp[j]; q < rp[j + 1]; ++q) if (cl[q] == i) tp[k] = q;
+    }
+  printf("N=%d nnzb=%d (%.1f blocks/row)\n", N, nnzb, (double)nnzb / N);
+  Sys s{};
+  s.nnzb = nnzb;
+  s.nw = (N + RPW - 1) / RPW;
+  CK(hipMalloc(&s.row_ptr, (N + 1) * 4)); CK(hipMalloc(&s.col, nnzb * 4)); CK(hipMalloc(&s.tpos, nnzb * 4));
+  CK(hipMemcpy(s.row_ptr, rp.data(), (N + 1) * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(s.col, cl.data(), nnzb * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(s.tpos, tp.data(), nnzb * 4, hipMemcpyHostToDevice));
+  std::vector<double> hb((size_t)nnzb * 36);
+  for (size_t i = 0; i < hb.size(); ++i) hb[i] = 1e-3 * ((i * 2654435761u) % 1000) / 1000.0;
+  CK(hipMalloc(&s.B, hb.size() * 8)); CK(hipMemcpy(s.B, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMalloc(&s.Minv, (size_t)N * 36 * 8)); CK(hipMemset(s.Minv, 0, (size_t)N * 36 * 8));
+  for (double** p : {&s.wv0, &s.wv1}) { CK(hipMalloc(p, 6 * N * 8)); CK(hipMemset(*p, 0, 6 * N * 8)); }
+  for (double** p : {&s.wg0, &s.wg1}) { CK(hipMalloc(p, (size_t)6 * nnzb * 8)); CK(hipMemset(*p, 0, (size_t)6 * nnzb * 8)); }
+  CK(hipMalloc(&s.vec, (size_t)8 * 6 * N * 8)); CK(hipMemset(s.vec, 0, (size_t)8 * 6 * N * 8));
+  CK(hipMalloc(&s.part, (size_t)6 * s.nw * 8)); CK(hipMemset(s.part, 0, (size_t)6 * s.nw * 8));
+  const dim3 g(s.nw), g8(8 * s.nw), b(1024);
+  CK(hipMalloc(&s.rec, (size_t)48 * N * 8)); CK(hipMemset(s.rec, 0, (size_t)48 * N * 8));
+  CK(hipMalloc(&s.partw, (size_t)6 * N * 8)); CK(hipMemset(s.partw, 0, (size_t)6 * N * 8));
+  printf("empty          %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_empty, g, b, 0, 0, s, i); }));
+  printf("empty 64thr    %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_empty, g, dim3(64), 0, 0, s, i); }));
+  printf("partials       %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_partials, g, b, 0, 0, s, i); }));
+  auto run = [&](const char* name, void (*k)(Sys, int)) {
+    printf("%-16s %7.2f us\n", name, timeit([&](int i) { hipLaunchKernelGGL(k, g, b, 0, 0, s, i); }));
+  };
+  auto runw = [&](const char* name, void (*k)(Sys, int), int rw) {
+    s.nwaves = (N + rw - 1) / rw;
+    printf("%-16s %7.2f us\n", name, timeit([&](int i) { hipLaunchKernelGGL(k, dim3(s.nwaves), dim3(64), 0, 0, s, i); }));
+  };
+  for (int rep = 0; rep < 2; ++rep) {
+    run("iter base", k_iter<false, false, 0>);
+    runw("iterw RW=8", k_iterw<8, 0>, 8);
+    runw("iterw8 soa", k_iterw<8, 1>, 8);
+    runw("iterw8 soa dpp", k_iterw<8, 2>, 8);
+    runw("iterw16 soa dpp", k_iterw<16, 2>, 16);
+    runw("iterw4 soa dpp", k_iterw<4, 2>, 4);
+  }
+  printf("copy 1 trip      %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_copy, g, b, 0, 0, s, i); }));
+  printf("copy 2 trips     %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_copy2, g, b, 0, 0, s, i); }));
+  return 0;
+}

@@ -92,6 +92,7 @@ def main():
     marks = []
     upd = []
     pipe.solver.timing(True)               # arm hipEvent timing of the PCG loops (same stream)
+    pipe.vol.kernel_timer = []             # hipEvents around each warped integrate launch
     t0 = time.perf_counter()
     for t in range(1 + a.warmup, total):
         e0, e1, e2 = ev(), ev(), ev()
@@ -119,15 +120,18 @@ def main():
     gn_it = [int(m[3]["_status"][1].item()) for m in marks]
     valid = [int(m[3]["_status"][0].item()) for m in marks]
     U = float(np.mean([int(u.item()) for u in upd]))
+    t_kint = float(np.mean([a.elapsed_time(b) for a, b in pipe.vol.kernel_timer])) * 1e-3
+    pipe.vol.kernel_timer = None
 
     frames_done = a.steps * (world if a.mode == "replicas" else 1)
     value = frames_done / elapsed
-    # algorithmic bytes of one integrate launch: anchors 8 B per voxel of every
-    # listed brick; weights 16 B + tsdf/weight 8 B read per skin-valid voxel; per updated voxel
-    # tsdf/weight write 8 B + colour read+write 8 B.
-    B = cache.n_list * 512 * 8 + n_skin_valid * 24 + U * 16
+    # algorithmic bytes of one integrate launch: palette-rank anchors 4 B per voxel
+    # of every listed brick + the brick's palette (64 x u16 + count); weights 16 B + tsdf/weight 8 B read
+    # per skin-valid voxel; per updated voxel tsdf/weight write 8 B + colour read+write 8 B. Node records
+    # and the depth/colour images are L2-resident and not counted.
+    B = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
     t_int_avg = float(np.mean(t_int))
-    achieved = B / t_int_avg
+    achieved = B / t_kint
     # k_pcg_iter algorithmic bytes per launch: B = A·M⁻¹ blocks (288 B) + column ids (4 B) per block;
     # per node: row_ptr, gathered w (48 B), M⁻¹ row block (288 B), 7 vectors read + 8 written (6 f64 each)
     B_pcg = nnzb * 292 + N_ * (4 + 48 + 288 + 15 * 48)
@@ -150,11 +154,11 @@ def main():
                      "achieved": ach_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": ach_pcg / PEAK_HBM,
                      "traffic": None, "bytes_per_launch": B_pcg, "avg_launch_us": 1e6 * t_pcg,
                      "launches_per_frame": pcg_launches / a.steps, "nnz_blocks": nnzb,
-                     "note": "dominant kernel by time; latency-bound (launch + 3 dependent round trips)"},
-        "roofline_integrate": {"kernel": "k_integrate<true> (fused warp+integrate)", "bound": "hbm",
+                     "note": "dominant kernel by time; latency-bound (one launch per iteration: launch + gather chain)"},
+        "roofline_integrate": {"kernel": "k_integrate<true,true> (fused warp+integrate, LDS node palette)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                "frac": achieved / PEAK_HBM, "traffic": None, "bytes_per_launch": B,
-                               "avg_launch_us": 1e6 * t_int_avg, "listed_bricks": cache.n_list,
+                               "avg_launch_us": 1e6 * t_kint, "listed_bricks": cache.n_list,
                                "skin_valid_voxels": n_skin_valid, "updated_voxels": U},
     }
     if rank == 0 and not a.no_cpu_baseline:

@@ -91,6 +91,13 @@ int ofx_skin_volume_bricks(const ofx_volume_desc* desc, const float* nodes, int3
 int ofx_skin_volume(const ofx_volume_desc* desc, const float* nodes, int32_t n_nodes, double node_coverage,
                     int32_t k, const int32_t* brick_list, int32_t n_list, uint16_t* anchors, float* weights,
                     ofx_stream_t s);
+/* Node palette of the bricked skin cache (MI355X-specific, no reference twin): per listed brick the
+ * ascending distinct anchors of its skin-valid voxels, pal_ids u16[n_list*OFX_PALETTE], count
+ * pal_n i32[n_list] (> OFX_PALETTE: overflow, palette unused), and per voxel the anchors as palette
+ * ranks local_anchors u8[n_list*512*4] (0xFF: skin-invalid voxel / unused slot). */
+#define OFX_PALETTE 64
+int ofx_skin_palette(const uint16_t* anchors, int32_t n_list, int32_t k, int32_t n_nodes, uint16_t* pal_ids,
+                     int32_t* pal_n, uint8_t* local_anchors, ofx_stream_t s);
 /* Skinning of arbitrary points: anchors int32[P*K] (-1 beyond 4σ), weights f32[P*K], valid u8[P] */
 int ofx_skin_points(const float* points, int64_t n_points, const float* nodes, int32_t n_nodes,
                     double node_coverage, int32_t k, int32_t* anchors, float* weights, uint8_t* valid,
@@ -115,6 +122,16 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
                   const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
                   double obs_weight, float* tsdf, float* weight, float* color,
                   uint32_t* n_updated, ofx_stream_t s);
+
+/* ofx_integrate (warp = 1) with the skin cache's node palette (ofx_skin_palette): each brick's node
+ * records are staged once in LDS. Bit-identical results; bricks with pal_n > OFX_PALETTE fall back
+ * to the global anchors. */
+int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth,
+                          const float* color_im, const float* packed_nodes, int32_t n_nodes, int32_t k,
+                          const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
+                          const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
+                          double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
+                          ofx_stream_t s);
 
 /* ED warp of points: out = Σ w (R(x-g)+g+t) for valid points, x otherwise.
  * normals = 1: WarpField.deform_normals semantics (R only, renormalised). valid may be NULL (all valid). */

@@ -54,10 +54,12 @@ _SIGS = {
     "ofx_pack_color": [P, c_int32, c_int32, P, P],
     "ofx_skin_volume_bricks": [P, P, c_int32, c_double, c_int32, P, P, P],
     "ofx_skin_volume": [P, P, c_int32, c_double, c_int32, P, c_int32, P, P, P],
+    "ofx_skin_palette": [P, c_int32, c_int32, c_int32, P, P, P, P],
     "ofx_skin_points": [P, c_int64, P, c_int32, c_double, c_int32, P, P, P, P],
     "ofx_skin_volume_to_dense": [P, P, c_int32, P, P, c_int32, P, P, P, P],
     "ofx_pack_nodes": [P, P, P, c_int32, P, P],
     "ofx_integrate": [P, P, P, P, c_int32, P, c_int32, c_int32, P, c_int32, P, P, c_double, P, P, P, P, P],
+    "ofx_integrate_palette": [P, P, P, P, P, c_int32, c_int32, P, c_int32, P, P, P, P, P, c_double, P, P, P, P, P],
     "ofx_deform_points": [P, c_int64, P, P, P, c_int32, P, c_int32, c_int32, P, P],
     "ofx_visibility": [P, c_int64, P, P, c_double, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
@@ -89,6 +91,9 @@ def _load():
 
 lib = _load()
 EXPORTED = tuple(_SIGS) + ("ofx_last_error",)
+
+
+PALETTE = 64   # OFX_PALETTE (include/ofx.h)
 
 
 class OfxError(RuntimeError):

@@ -95,6 +95,30 @@ enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
 constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 
 // ---------------------------------------------------------------------------- reductions
+template <int CTL>
+__device__ __forceinline__ double dpp_mov(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// Sum over each aligned 16-lane row; every lane of the row ends with identical bits.
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_mov<0x141>(x);   // row_half_mirror
+  x += dpp_mov<0x140>(x);   // row_mirror
+  return x;
+}
+__device__ __forceinline__ double read_lane(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+// Full-wave sum, fixed order, uniform result. Call from wave-uniform control flow.
+__device__ __forceinline__ double wave_sum(double x) {
+  x = row16_sum(x);
+  return (read_lane(x, 0) + read_lane(x, 16)) + (read_lane(x, 32) + read_lane(x, 48));
+}
 __device__ __forceinline__ double block_sum(double v) {
   __shared__ double s[kBlk];
   s[threadIdx.x] = v;
@@ -419,34 +443,42 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
   }
 }
 
-__device__ __forceinline__ double blk_entry(const Gn& g, int code, int c, int j) {
-  const int64_t t = code >> 4;
-  const double* Jp = g.J + t * 72 + 18 * ((code >> 2) & 3);
-  const double* Jq = g.J + t * 72 + 18 * (code & 3);
-  return Jp[c] * Jq[j] + Jp[6 + c] * Jq[6 + j] + Jp[12 + c] * Jq[12 + j];
-}
-
-// One wave per JᵀJ block: lane (c,j) sums its entry over the block's sorted (term,p,q) list,
-// 8 independent accumulators (8 list entries in flight per lane).
+// JᵀJ blocks: 16 lanes per block, 4 blocks per wave; lane q takes list entries q, q+16, ... of its
+// block, loads both 3x6 Jacobian blocks of the entry whole (16-B accesses) and accumulates the full
+// 6x6 product; 16-lane DPP sums (fixed pairing) finish the block and lane 0 of the group stores it.
+// Deterministic; forward declared helpers live in the PCG section.
 __global__ __launch_bounds__(kBlk) void k_blocks(Gn g, double* __restrict__ A) {
-  const int64_t s = blockIdx.x * (int64_t)(kBlk / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (s >= g.nnzb || lane >= 36) return;
-  const int c = lane / 6, j = lane % 6;
-  double v[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  const int b = g.blk_off[s], e = g.blk_off[s + 1];
-  int k = b;
-  for (; k + 8 <= e; k += 8) {
-    int code[8];
+  const int64_t s = blockIdx.x * (int64_t)(kBlk / 16) + (threadIdx.x >> 4);
+  const int q = threadIdx.x & 15;
+  double acc[36];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) code[u] = g.blk_list[k + u];
+  for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+  if (s < g.nnzb) {
+    const int b = g.blk_off[s], e = g.blk_off[s + 1];
+    for (int k = b + q; k < e; k += 16) {
+      const int code = g.blk_list[k];
+      const int64_t t = code >> 4;
+      const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * ((code >> 2) & 3));
+      const double2* Jq = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code & 3));
+      double P[18], Q[18];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] += blk_entry(g, code[u], c, j);
+      for (int u = 0; u < 9; ++u) {
+        const double2 x = Jp[u], y = Jq[u];
+        P[2 * u] = x.x; P[2 * u + 1] = x.y; Q[2 * u] = y.x; Q[2 * u + 1] = y.y;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc[6 * c + j] += P[c] * Q[j] + P[6 + c] * Q[6 + j] + P[12 + c] * Q[12 + j];
+    }
   }
 #pragma unroll
-  for (int u = 0; u < 7; ++u)
-    if (k + u < e) v[u] += blk_entry(g, g.blk_list[k + u], c, j);
-  A[s * 36 + lane] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  for (int k = 0; k < 36; ++k) acc[k] = row16_sum(acc[k]);
+  if (s < g.nnzb && q == 0) {
+    double2* out = reinterpret_cast<double2*>(A + 36 * s);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) out[k] = make_double2(acc[2 * k], acc[2 * k + 1]);
+  }
 }
 
 // b = -Jᵀr: one wave per node, lane = slot*6 + c (10 slots); slot s sums list entries s, s+10, ...
@@ -541,54 +573,43 @@ enum { V_X = 0, V_R = 1, V_U = 2, V_Z = 3, V_Q = 4, V_S = 5, V_P = 6, V_N = 8 };
 constexpr int kRW = 4;          // block rows per wave
 constexpr int kSL = 64 / kRW;   // lanes (block slots) per row
 
-template <int CTL>
-__device__ __forceinline__ double dpp_mov(double x) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-// Sum over each aligned 16-lane row; every lane of the row ends with identical bits.
-__device__ __forceinline__ double row16_sum(double x) {
-  x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
-  x += dpp_mov<0x4E>(x);    // quad_perm [2,3,0,1]
-  x += dpp_mov<0x141>(x);   // row_half_mirror
-  x += dpp_mov<0x140>(x);   // row_mirror
-  return x;
-}
-__device__ __forceinline__ double read_lane(double x, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-  return __hiloint2double(hi, lo);
-}
-// Full-wave sum, fixed order, uniform result. Call from wave-uniform control flow.
-__device__ __forceinline__ double wave_sum(double x) {
-  x = row16_sum(x);
-  return (read_lane(x, 0) + read_lane(x, 16)) + (read_lane(x, 32) + read_lane(x, 48));
-}
-// Σ_i p[k*nw + i] for K streams; U loads per lane issued up front; uniform result.
+// Σ_i p[k*nw + i] for K streams, in two phases so the loads can be issued early: load_streams puts
+// U entries per lane in registers, reduce_streams adds the tail (nw > 64U) and sums in a fixed
+// order; uniform result in every lane.
 template <int K, int U>
-__device__ __forceinline__ void sum_streams(const double* __restrict__ p, int nw, double out[K]) {
+__device__ __forceinline__ void load_streams(const double* __restrict__ p, int nw, double t[K][U]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = lane + 64 * u;
+      t[k][u] = i < nw ? p[(int64_t)k * nw + i] : 0.0;
+    }
+}
+template <int K, int U>
+__device__ __forceinline__ void reduce_streams(const double* __restrict__ p, int nw, double t[K][U], double out[K]) {
   const int lane = threadIdx.x & 63;
   double a[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    double t[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = lane + 64 * u;
-      t[u] = i < nw ? p[(int64_t)k * nw + i] : 0.0;
-    }
 #pragma unroll
     for (int w = 1; w < U; w <<= 1)
 #pragma unroll
-      for (int u = 0; u + w < U; u += 2 * w) t[u] += t[u + w];
-    a[k] = t[0];
+      for (int u = 0; u + w < U; u += 2 * w) t[k][u] += t[k][u + w];
+    a[k] = t[k][0];
   }
   for (int i = lane + 64 * U; i < nw; i += 64)
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] += p[(int64_t)k * nw + i];
 #pragma unroll
   for (int k = 0; k < K; ++k) out[k] = wave_sum(a[k]);
+}
+template <int K, int U>
+__device__ __forceinline__ void sum_streams(const double* __restrict__ p, int nw, double out[K]) {
+  double t[K][U];
+  load_streams<K, U>(p, nw, t);
+  reduce_streams<K, U>(p, nw, t, out);
 }
 // n[c] without a dynamically indexed array (which the compiler would put in scratch): masked sum,
 // exact for finite n (x·1 + 0 terms); a non-finite component poisons the row, as it would anyway.
@@ -599,11 +620,12 @@ __device__ __forceinline__ double pick6(const double n[6], int c) {
   return v;
 }
 // (B v)_row summed over the row's kSL lanes: every lane of the row gets all 6 components.
-__device__ __forceinline__ void row_spmv(const Gn& g, int row, int q, const double* __restrict__ v, double n[6]) {
+// [b0, b1) = the row's block range (empty for padding rows).
+__device__ __forceinline__ void row_spmv(const Gn& g, int b0, int b1, int q, const double* __restrict__ v,
+                                         double n[6]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) n[i] = 0.0;
-  if (row < g.N) {
-    const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
+  {
     for (int bi = b0 + q; bi < b1; bi += kSL) {
       const double2* blk = reinterpret_cast<const double2*>(g.Bm + 36 * (int64_t)bi);
       const double2* vc = reinterpret_cast<const double2*>(v + 6 * (int64_t)g.col[bi]);
@@ -869,7 +891,8 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
   const int lane = threadIdx.x;
   const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   double n[6];
-  row_spmv(g, row, q, g.w1, n);
+  const int b0 = row < g.N ? g.row_ptr[row] : 0, b1 = row < g.N ? g.row_ptr[row + 1] : 0;
+  row_spmv(g, b0, b1, q, g.w1, n);
   double d[4] = {0.0, 0.0, 0.0, 0.0};
   if (row < g.N && q < 6) {
     const int64_t o = 6 * (int64_t)row + q;
@@ -898,34 +921,50 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
   const int nw = g.nwg_row;
   const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
   double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
+  // 1. issue every independent load: stop flags and scalars (scalar loads), previous partials,
+  //    own-row state, M⁻¹ row, own w, the row's block range
   const int stop = g.flags[F_DONE] | g.flags[F_STOPPED];
   const double gam_prev = it > 0 ? g.pcg_gamma[it - 1] : 1.0;
   const double alpha_prev = it > 0 ? g.pcg_alpha[it - 1] : 1.0;
   const double bb_stored = g.scal[S_BB];
+  double tp[3][16], tb[1][16];
+  load_streams<3, 16>(g.part_p + 3 * (int64_t)nw * (it & 1), nw, tp);
+  if (it == 0) load_streams<1, 16>(g.part_b, nw, tb);
   const bool own = row < g.N && q < 6;
   const int64_t o = 6 * (int64_t)row + q;
-  double v[V_N], m = 0.0, w = 0.0;
+  double v[V_N], mi[6], wi[6], w = 0.0;
 #pragma unroll
   for (int k = 0; k < V_N; ++k) v[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { mi[k] = 0.0; wi[k] = 0.0; }
   if (own) {
     load_rec(g.st, o, v);
     const double2* Mi = reinterpret_cast<const double2*>(g.Minv + 36 * (int64_t)row + 6 * q);
-    const double2* wi = reinterpret_cast<const double2*>(wc + 6 * (int64_t)row);
+    const double2* wr = reinterpret_cast<const double2*>(wc + 6 * (int64_t)row);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { const double2 a = Mi[k], b = wi[k]; m += a.x * b.x + a.y * b.y; }
+    for (int k = 0; k < 3; ++k) {
+      const double2 a = Mi[k], b = wr[k];
+      mi[2 * k] = a.x; mi[2 * k + 1] = a.y; wi[2 * k] = b.x; wi[2 * k + 1] = b.y;
+    }
     w = wc[o];
   }
+  const int b0 = row < g.N ? g.row_ptr[row] : 0, b1 = row < g.N ? g.row_ptr[row + 1] : 0;
+  // 2. after convergence the remaining launches of the chunk end here (one scalar round trip)
+  if (stop) return;
+  // 3. SpMV n = B w (gather chain), then the scalars from the partials (long arrived)
+  double n[6];
+  row_spmv(g, b0, b1, q, wc, n);
   double pa[3];
-  sum_streams<3, 16>(g.part_p + 3 * (int64_t)nw * (it & 1), nw, pa);
+  reduce_streams<3, 16>(g.part_p + 3 * (int64_t)nw * (it & 1), nw, tp, pa);
   double bb = bb_stored;
   if (it == 0) {
     double t[1];
-    sum_streams<1, 16>(g.part_b, nw, t);
+    reduce_streams<1, 16>(g.part_b, nw, tb, t);
     bb = t[0];
   }
-  double n[6];
-  row_spmv(g, row, q, wc, n);
-  if (stop) return;
+  double m = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) m += mi[k] * wi[k];
   const double gam = pa[0], del = pa[1], rr = pa[2];
   const double tol = g.prm.pcg_tol;
   const bool lead = blockIdx.x == 0 && lane == 0;
@@ -974,12 +1013,15 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
 
 // After the solve: ill-posed check, loss bookkeeping and early stop (model.py:696-732). One thread.
 // A non-finite solve shows up as a non-finite alpha/pq in k_pcg_iter, which sets F_ILL.
-__global__ void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log, int pcg_max, int gn_iter) {
-  if (threadIdx.x != 0 || g.flags[F_STOPPED]) return;
+__global__ __launch_bounds__(64) void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log, int pcg_max,
+                                                     int gn_iter) {
+  if (g.flags[F_STOPPED]) return;
+  double bbv[1];
+  sum_streams<1, 16>(g.part_b, g.nwg_row, bbv);
+  if (threadIdx.x != 0) return;
   if (!g.flags[F_DONE]) g.flags[F_PCG_TOTAL] += pcg_max;
   {
-    double bb = 0.0;
-    for (int i = 0; i < g.nwg_row; ++i) bb += g.part_b[i];
+    const double bb = bbv[0];
     if (gn_iter < kMaxLog) {
       g.stat[3 * gn_iter + 0] = g.flags[F_DONE] ? (double)g.flags[F_PCG_IT] : (double)pcg_max;
       g.stat[3 * gn_iter + 1] = bb;
@@ -1113,9 +1155,12 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     OFX_HIP(hipEventCreate(&e1));
     OFX_HIP(hipEventRecord(e0, hs));
   }
+  // Launch in chunks and poll the flags between chunks. Launch `it` tests convergence of the state
+  // after `it` iterations, and launches after convergence end after one scalar load, so the first
+  // chunk covers the previous solve's count for this GN step plus a small margin.
   const int max_it = g->prm.pcg_max_iter;
   const int lp = g->last_pcg[gn_iter & 63];
-  int chunk = lp > 0 ? ((lp + 1 + 3) / 4) * 4 : 64;
+  int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
     int n = chunk < max_it - it ? chunk : max_it - it;
@@ -1123,12 +1168,6 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64), 0, hs, *g, it);
     g->n_iter_launches += n;
     OFX_LAUNCH_CHECK();
-    // convergence probe: k_pcg_iter(it) tests |r| first and only iterates if not converged
-    if (it < max_it) {
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64), 0, hs, *g, it);
-      ++it;
-      ++g->n_iter_launches;
-    }
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
     OFX_HIP(hipStreamSynchronize(hs));
@@ -1136,7 +1175,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       if (g->host_flags[F_DONE]) g->last_pcg[gn_iter & 63] = g->host_flags[F_PCG_IT];
       break;
     }
-    chunk = 16;
+    chunk = 8;
   }
   if (g->timing) g->ev.emplace_back(e0, e1);
   return OFX_OK;
@@ -1348,7 +1387,7 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   dc.fx = g->fx; dc.fy = g->fy; dc.cx = g->cx; dc.cy = g->cy;
   hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
   if (g->nnzb > 0)
-    hipLaunchKernelGGL(k_blocks, dim3(grid_for(g->nnzb, kBlk / 64, 1 << 30)), dim3(kBlk), 0, hs, *g, A);
+    hipLaunchKernelGGL(k_blocks, dim3(grid_for(g->nnzb, kBlk / 16, 1 << 30)), dim3(kBlk), 0, hs, *g, A);
   hipLaunchKernelGGL(k_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, rhs);
   OFX_LAUNCH_CHECK();
   return OFX_OK;

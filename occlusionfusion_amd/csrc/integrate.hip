@@ -106,15 +106,21 @@ __device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
   if (threadIdx.x == 0) counts[blockIdx.x] = (uint32_t)(s_w[0] + s_w[1] + s_w[2] + s_w[3]);
 }
 
-template <bool WARP>
+// PAL: node records of the brick's palette staged in LDS once per workgroup; voxel anchors are
+// palette ranks (uint8). A brick whose palette overflowed (pal_n > kPal) uses the global anchors.
+template <bool WARP, bool PAL>
 __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const float* __restrict__ depth,
                                                     const float* __restrict__ color_im,
                                                     const float4* __restrict__ nodes, int K,
                                                     const int32_t* __restrict__ list,
                                                     const ushort4* __restrict__ anchors,
-                                                    const float4* __restrict__ weights, double trunc, double obs,
+                                                    const float4* __restrict__ weights,
+                                                    const uint16_t* __restrict__ pal_ids,
+                                                    const int32_t* __restrict__ pal_n,
+                                                    const uchar4* __restrict__ local, double trunc, double obs,
                                                     float* __restrict__ tsdf, float* __restrict__ weight,
                                                     float* __restrict__ color, uint32_t* counter) {
+  __shared__ float4 s_node[PAL ? 4 * kPal : 1];
   const int64_t slot = blockIdx.x;
   const int64_t b = WARP ? (int64_t)list[slot] : slot;
   int64_t bz = b % g.nbz;
@@ -122,6 +128,14 @@ __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const fl
   int64_t by = r % g.nby;
   int64_t bx = r / g.nby + g.bx0;
   const int i0 = (int)bx * kBrick, j0 = (int)by * kBrick, k0 = (int)bz * kBrick;
+  bool use_pal = false;
+  if (PAL) {
+    const int pn = pal_n[slot];
+    use_pal = pn <= kPal;
+    if (use_pal && (int)threadIdx.x < 4 * pn)
+      s_node[threadIdx.x] = nodes[4 * (int64_t)pal_ids[slot * kPal + (threadIdx.x >> 2)] + (threadIdx.x & 3)];
+    __syncthreads();
+  }
   int n_upd = 0;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -133,12 +147,20 @@ __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const fl
     float z = vox2world(g.oz, g.vs, k);
     if (WARP) {
       const int64_t si = slot * kBrickVox + l;
-      ushort4 a = anchors[si];
-      int ids[4] = {a.x, a.y, a.z, a.w};
-      if (ids[K - 1] == kNoAnchor) continue;  // skin-invalid voxel: never integrated after the source frame
+      int ids[4];
+      if (PAL && use_pal) {
+        const uchar4 a = local[si];
+        ids[0] = a.x; ids[1] = a.y; ids[2] = a.z; ids[3] = a.w;
+        if (ids[K - 1] == kNoLocal) continue;   // skin-invalid voxel: never integrated after the source frame
+      } else {
+        const ushort4 a = anchors[si];
+        ids[0] = a.x; ids[1] = a.y; ids[2] = a.z; ids[3] = a.w;
+        if (ids[K - 1] == kNoAnchor) continue;
+      }
       float4 ww = weights[si];
       float w[4] = {ww.x, ww.y, ww.z, ww.w};
-      ed_warp(nodes, ids, w, K, x, y, z);
+      if (PAL && use_pal) ed_warp(s_node, ids, w, K, x, y, z);
+      else ed_warp(nodes, ids, w, K, x, y, z);
     }
     n_upd += update_voxel(c, depth, color_im, trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
   }
@@ -221,18 +243,45 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
   CamD c = make_cam(cam);
   hipStream_t hs = as_stream(s);
   if (!warp) {
-    hipLaunchKernelGGL(k_integrate<false>, dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth, color_im,
-                       (const float4*)nullptr, 1, (const int32_t*)nullptr, (const ushort4*)nullptr,
-                       (const float4*)nullptr, desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+    hipLaunchKernelGGL((k_integrate<false, false>), dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth,
+                       color_im, (const float4*)nullptr, 1, (const int32_t*)nullptr, (const ushort4*)nullptr,
+                       (const float4*)nullptr, (const uint16_t*)nullptr, (const int32_t*)nullptr,
+                       (const uchar4*)nullptr, desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
   } else {
     OFX_CHECK_ARG(k >= 1 && k <= 4 && n_nodes >= k, "bad k/n_nodes");
     OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
     if (n_list == 0) return OFX_OK;
     OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights, "null warp buffer");
-    hipLaunchKernelGGL(k_integrate<true>, dim3((unsigned)n_list), dim3(256), 0, hs, g, c, depth, color_im,
+    hipLaunchKernelGGL((k_integrate<true, false>), dim3((unsigned)n_list), dim3(256), 0, hs, g, c, depth, color_im,
                        (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors, (const float4*)weights,
+                       (const uint16_t*)nullptr, (const int32_t*)nullptr, (const uchar4*)nullptr,
                        desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
   }
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth,
+                          const float* color_im, const float* packed_nodes, int32_t n_nodes, int32_t k,
+                          const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
+                          const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
+                          double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
+                          ofx_stream_t s) {
+  BrickGeom g;
+  int st = make_geom(desc, &g);
+  if (st) return st;
+  OFX_CHECK_ARG(cam && depth, "null camera/depth");
+  OFX_CHECK_ARG(cam->width > 0 && cam->height > 0, "bad camera size");
+  OFX_CHECK_ARG((color == nullptr) == (color_im == nullptr), "color and color_im must both be set or both NULL");
+  OFX_CHECK_ARG(k >= 1 && k <= 4 && n_nodes >= k, "bad k/n_nodes");
+  OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
+  if (n_list == 0) return OFX_OK;
+  OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights && pal_ids && pal_n && local_anchors,
+                "null warp/palette buffer");
+  hipLaunchKernelGGL((k_integrate<true, true>), dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_cam(cam),
+                     depth, color_im, (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors,
+                     (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,
+                     obs_weight, tsdf, weight, color, n_updated);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

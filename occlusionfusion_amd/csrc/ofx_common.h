@@ -36,6 +36,8 @@ void set_error(const char* fmt, ...);
 constexpr int kBrick = 8;            // brick edge (voxels)
 constexpr int kBrickVox = 512;       // voxels per brick
 constexpr uint16_t kNoAnchor = 0xFFFF;
+constexpr int kPal = 64;             // node palette entries per brick (skin cache, integrate)
+constexpr uint8_t kNoLocal = 0xFF;   // palette-local anchor of a skin-invalid voxel
 
 // Brick geometry of one shard. Bricks are numbered brick-major in C order over the shard:
 // b = ((bx - bx0) * nby + by) * nbz + bz ; voxel within brick l = (lx*8 + ly)*8 + lz.

@@ -209,6 +209,73 @@ __global__ __launch_bounds__(256) void k_skin_volume(BrickGeom g, const float* _
   }
 }
 
+// ---- per-brick node palette of the skin cache ----
+// Distinct anchors of the brick's skin-valid voxels, ascending node id (LDS bitmap over node ids +
+// block scan of popcounts); each voxel's anchors re-expressed as palette ranks (uint8, kNoLocal for
+// skin-invalid voxels and unused slots). pal_n > kPal marks an overflowing brick (palette unused).
+__global__ __launch_bounds__(256) void k_skin_palette(const ushort4* __restrict__ anchors, int K, int n_nodes,
+                                                       uint16_t* __restrict__ pal_ids, int32_t* __restrict__ pal_n,
+                                                       uchar4* __restrict__ local) {
+  __shared__ uint32_t s_bits[2048];
+  __shared__ int s_pre[2048 + 1];
+  __shared__ int s_tsum[256];
+  const int64_t slot = blockIdx.x;
+  const int nw = (n_nodes + 31) >> 5;
+  for (int i = threadIdx.x; i < nw; i += 256) s_bits[i] = 0u;
+  __syncthreads();
+  int ids[2][4];
+  bool val[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const ushort4 a = anchors[slot * kBrickVox + threadIdx.x + 256 * h];
+    ids[h][0] = a.x; ids[h][1] = a.y; ids[h][2] = a.z; ids[h][3] = a.w;
+    val[h] = ids[h][K - 1] != kNoAnchor;
+    if (val[h])
+      for (int s = 0; s < K; ++s) atomicOr(&s_bits[ids[h][s] >> 5], 1u << (ids[h][s] & 31));
+  }
+  __syncthreads();
+  // exclusive prefix of word popcounts: contiguous chunk per thread, then a 256-entry scan
+  const int chunk = (nw + 255) / 256;
+  const int w0 = threadIdx.x * chunk, w1 = min(nw, w0 + chunk);
+  int tsum = 0;
+  for (int w = w0; w < w1; ++w) tsum += __popc(s_bits[w]);
+  s_tsum[threadIdx.x] = tsum;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int v = threadIdx.x >= off ? s_tsum[threadIdx.x - off] : 0;
+    __syncthreads();
+    s_tsum[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = s_tsum[threadIdx.x] - tsum;
+  for (int w = w0; w < w1; ++w) {
+    s_pre[w] = run;
+    const uint32_t bits = s_bits[w];
+    uint32_t m = bits;
+    int r = run;
+    while (m) {
+      const int bit = __ffs(m) - 1;
+      if (r < kPal) pal_ids[slot * kPal + r] = (uint16_t)(w * 32 + bit);
+      ++r;
+      m &= m - 1;
+    }
+    run += __popc(bits);
+  }
+  if (threadIdx.x == 255) pal_n[slot] = s_tsum[255];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint8_t o[4] = {kNoLocal, kNoLocal, kNoLocal, kNoLocal};
+    if (val[h])
+      for (int s = 0; s < K; ++s) {
+        const int id = ids[h][s];
+        const int rk = s_pre[id >> 5] + __popc(s_bits[id >> 5] & ((1u << (id & 31)) - 1u));
+        o[s] = rk < kPal ? (uint8_t)rk : kNoLocal;
+      }
+    local[slot * kBrickVox + threadIdx.x + 256 * h] = make_uchar4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // ---- per-point k-NN (all nodes) ----
 __global__ __launch_bounds__(256) void k_skin_points(const float* __restrict__ pts, int64_t n_pts,
                                                       const float* __restrict__ nodes, int n_nodes, float cutoff,
@@ -331,6 +398,18 @@ int ofx_skin_volume(const ofx_volume_desc* desc, const float* nodes, int32_t n_n
   SkinConsts c = skin_consts(node_coverage);
   hipLaunchKernelGGL(k_skin_volume, dim3(n_list), dim3(256), 0, as_stream(s), g, nodes, n_nodes, c.cull_r2, c.cutoff,
                      c.denom, k, brick_list, (ushort4*)anchors, (float4*)weights);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_skin_palette(const uint16_t* anchors, int32_t n_list, int32_t k, int32_t n_nodes, uint16_t* pal_ids,
+                     int32_t* pal_n, uint8_t* local_anchors, ofx_stream_t s) {
+  OFX_CHECK_ARG(k >= 1 && k <= 4 && n_nodes >= k && n_list >= 0, "bad k/n_nodes/n_list");
+  if (n_nodes > 65535) { set_error("n_nodes %d exceeds 65535 (palette bitmap)", n_nodes); return OFX_ERR_RANGE; }
+  if (n_list == 0) return OFX_OK;
+  OFX_CHECK_ARG(anchors && pal_ids && pal_n && local_anchors, "null buffer");
+  hipLaunchKernelGGL(k_skin_palette, dim3(n_list), dim3(256), 0, as_stream(s), (const ushort4*)anchors, k, n_nodes,
+                     pal_ids, pal_n, (uchar4*)local_anchors);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

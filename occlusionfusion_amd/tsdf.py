@@ -105,6 +105,8 @@ class TSDFVolume:
         self.color_b = torch.empty(self.n_slots, **kw)
         self.n_updated = torch.zeros(max(1, self.n_bricks), dtype=torch.int32, device=self.device)  # per brick
         self.with_color = True
+        self.kernel_timer = None   # list -> (start, end) torch events around each warped integrate launch
+        self.use_palette = True    # warped integrate through the skin cache's LDS node palette
         call("ofx_volume_reset", byref(self.desc), ptr(self.tsdf_b), ptr(self.weight_b), ptr(self.color_b), stream_ptr())
         self.warpfield = None
         self._world_pts = None
@@ -164,9 +166,23 @@ class TSDFVolume:
                 raise RuntimeError("non-source frame integrate needs tsdf.warpfield (WarpField) to be set")
             cache = self.warpfield.skin_tsdf_cache()
             nodes = self.warpfield.packed_nodes()
-            call("ofx_integrate", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, 1, ptr(nodes),
-                 self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
-                 ptr(cache.weights), float(obs_weight), ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu, stream_ptr())
+            timer = self.kernel_timer
+            if timer is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            if self.use_palette and cache.pal_n is not None:
+                call("ofx_integrate_palette", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, ptr(nodes),
+                     self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
+                     ptr(cache.weights), ptr(cache.pal_ids), ptr(cache.pal_n), ptr(cache.local), float(obs_weight),
+                     ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu, stream_ptr())
+            else:
+                call("ofx_integrate", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, 1, ptr(nodes),
+                     self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
+                     ptr(cache.weights), float(obs_weight), ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu,
+                     stream_ptr())
+            if timer is not None:
+                e1.record()
+                timer.append((e0, e1))
 
     # ------------------------------------------------------------------ readback
     def _dense(self, t):

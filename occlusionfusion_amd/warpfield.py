@@ -44,6 +44,9 @@ class SkinCache:
     anchors: torch.Tensor      # uint16 as int16 storage [n_list*512*4]
     weights: torch.Tensor      # f32 [n_list*512*4]
     k: int
+    pal_ids: torch.Tensor = None   # int16 storage of u16 [n_list*PALETTE] node palette per brick
+    pal_n: torch.Tensor = None     # int32 [n_list] distinct anchors per brick (> PALETTE: overflow)
+    local: torch.Tensor = None     # uint8 [n_list*512*4] anchors as palette ranks (0xFF invalid)
 
 
 def _t(x, device, dtype):
@@ -159,7 +162,13 @@ class WarpField:
             weights = torch.empty(max(1, n_list) * 512 * 4, dtype=torch.float32, device=self.device)
             call("ofx_skin_volume", byref(t.desc), ptr(self.nodes_t), self.num_nodes, self.node_coverage, K, ptr(blist),
                  n_list, ptr(anchors), ptr(weights), stream_ptr())
-            self._cache = SkinCache(blist[:max(1, n_list)], n_list, anchors, weights, K)
+            P = _lib.PALETTE
+            pal_ids = torch.empty(max(1, n_list) * P, dtype=torch.int16, device=self.device)
+            pal_n = torch.empty(max(1, n_list), dtype=torch.int32, device=self.device)
+            local = torch.empty(max(1, n_list) * 512 * 4, dtype=torch.uint8, device=self.device)
+            call("ofx_skin_palette", ptr(anchors), n_list, K, self.num_nodes, ptr(pal_ids), ptr(pal_n), ptr(local),
+                 stream_ptr())
+            self._cache = SkinCache(blist[:max(1, n_list)], n_list, anchors, weights, K, pal_ids, pal_n, local)
         return self._cache
 
     def skin_tsdf(self):

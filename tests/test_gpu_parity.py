@@ -89,6 +89,46 @@ def test_integrate_source_and_warped_frames_bitexact(cuda, golden_dir):
     np.testing.assert_array_equal(c, g["color1"].reshape(D))
 
 
+def test_skin_palette_and_fallback(cuda, golden_dir):
+    """Node palette = ascending distinct anchors of each brick's skin-valid voxels, local ranks map back
+    to the anchors; palette path, forced-overflow fallback and global path integrate identically."""
+    from occlusionfusion_amd import WarpField, _lib
+    g = _g(golden_dir, "integrate_small.npz")
+    P = _lib.PALETTE
+    vols = []
+    for mode in ("palette", "overflow", "global"):
+        vol = _small_volume(g)
+        vol.integrate({"im": g["im0"], "id": 0})
+        wf = WarpField(_graph(g), vol)
+        c = wf.skin_tsdf_cache()
+        if mode == "palette":
+            K = c.k
+            an = c.anchors.view(torch.uint16).cpu().numpy().astype(np.int64).reshape(c.n_list, 512, 4)[:, :, :K]
+            loc = c.local.cpu().numpy().reshape(c.n_list, 512, 4)[:, :, :K].astype(np.int64)
+            pid = c.pal_ids.view(torch.uint16).cpu().numpy().astype(np.int64).reshape(c.n_list, P)
+            pn = c.pal_n.cpu().numpy()
+            assert pn.max() <= P
+            for b in range(c.n_list):
+                valid = an[b, :, K - 1] != 0xFFFF
+                uniq = np.unique(an[b][valid])
+                assert pn[b] == len(uniq)
+                np.testing.assert_array_equal(pid[b, :pn[b]], uniq)
+                np.testing.assert_array_equal(pid[b][loc[b][valid]], an[b][valid])
+                assert (loc[b][~valid] == 0xFF).all()
+        elif mode == "overflow":
+            c.pal_n[::2] = P + 1          # every other brick takes the global-anchor fallback
+        else:
+            vol.use_palette = False
+        wf.frame_id = 1
+        wf.set_node_transforms(g["R"], g["T"])
+        vol.integrate({"im": g["im1"], "id": 1})
+        vols.append(vol.get_volume())
+    D = tuple(g["dims"])
+    for v in vols:
+        for i, key in enumerate(("tsdf1", "color1", "weight1")):
+            np.testing.assert_array_equal(v[i], g[key].reshape(D))
+
+
 def test_sharded_volume_equals_full(cuda, golden_dir):
     """Spatial x-slab sharding (3 shards in one process) reproduces the full volume exactly."""
     from occlusionfusion_amd import WarpField

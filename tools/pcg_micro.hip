@@ -19,6 +19,11 @@ struct Sys {
   int nw, nnzb;
   double *rec, *partw;   // AoS node state (N x 48: 8 vectors x 6), per-wave partials (2 x 3 x nwaves)
   int nwaves;
+  // slot layout (4 rows x 16 slots per wave, 1 round): Bs (nslot x 36), cols (nslot), ws0/ws1 (nslot x 6
+  // pushed w), dst (nslot): slot receiving this slot's row w (transposed block position)
+  double *Bs, *ws0, *ws1;
+  int *dst;
+  unsigned* bar;   // grid barrier: [0] arrivals, [1] generation, [2] timeout flag
 };
 
 __device__ __forceinline__ double red8(double a) {
@@ -389,6 +394,163 @@ __global__ __launch_bounds__(64) void k_iterw(Sys s, int it) {
   }
 }
 
+// Slot-layout iteration: every load address is static (no row_ptr / col chain): lane (r, q) of
+// wave w owns slot (w*64 + lane) holding block (row, j) and the pushed copy of w_j; after the
+// update each lane pushes its row's new w into the transposed block's slot of the next buffer.
+template <bool PUSHW>
+__global__ __launch_bounds__(64) void k_iters(Sys s, int it) {
+  const int lane = threadIdx.x;
+  const int r = lane / 16, q = lane % 16;
+  const int row = blockIdx.x * 4 + r;
+  const int64_t slot = (int64_t)blockIdx.x * 64 + lane;
+  const double* wc = (it & 1) ? s.wv1 : s.wv0;
+  double* wn = (it & 1) ? s.wv0 : s.wv1;
+  const double* gc = (it & 1) ? s.ws1 : s.ws0;
+  double* gn = (it & 1) ? s.ws0 : s.ws1;
+  double t[3][16];
+  {
+    const double* P = s.partw + 3 * (int64_t)s.nwaves * (it & 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) { const int i = lane + 64 * u; t[k][u] = i < s.nwaves ? P[k * s.nwaves + i] : 0.0; }
+  }
+  const bool own = row < N && q < 6;
+  double v[8], mi[6], wi[6];
+  for (int k = 0; k < 8; ++k) v[k] = 0.0;
+  for (int k = 0; k < 6; ++k) { mi[k] = 0.0; wi[k] = 0.0; }
+  if (own) {
+    const double2* R = reinterpret_cast<const double2*>(s.rec + 48 * (int64_t)row + 8 * q);
+    for (int k = 0; k < 4; ++k) { double2 a = R[k]; v[2 * k] = a.x; v[2 * k + 1] = a.y; }
+    const double2* Mi = reinterpret_cast<const double2*>(s.Minv + 36 * (int64_t)row + 6 * q);
+    const double2* wr = reinterpret_cast<const double2*>(wc + 6 * (int64_t)row);
+    for (int k = 0; k < 3; ++k) { double2 a = Mi[k], b = wr[k]; mi[2 * k] = a.x; mi[2 * k + 1] = a.y; wi[2 * k] = b.x; wi[2 * k + 1] = b.y; }
+  }
+  // one static block per lane
+  double n[6];
+  {
+    const double2* blk = reinterpret_cast<const double2*>(s.Bs + 36 * slot);
+    const double2* vc = reinterpret_cast<const double2*>(PUSHW ? gc + 6 * slot : wc + 6 * (int64_t)s.col[slot % s.nnzb]);
+    double x[6];
+    for (int j = 0; j < 3; ++j) { double2 a = vc[j]; x[2 * j] = a.x; x[2 * j + 1] = a.y; }
+    for (int i = 0; i < 6; ++i) {
+      double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+      n[i] = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+    }
+  }
+  const int dslot = PUSHW ? s.dst[slot] : 0;
+  for (int i = 0; i < 6; ++i) n[i] = group_sum<16>(n[i]);
+  double pa[3];
+  for (int k = 0; k < 3; ++k) {
+    for (int w = 1; w < 16; w <<= 1)
+      for (int u = 0; u + w < 16; u += 2 * w) t[k][u] += t[k][u + w];
+    pa[k] = wave_sum(t[k][0]);
+  }
+  const double al = 1e-3 + 1e-12 * pa[0], be = 1e-3 + 1e-12 * pa[1];
+  double nc = 0.0, m = 0.0;
+  for (int i = 0; i < 6; ++i) { nc += n[i] * (q == i ? 1.0 : 0.0); m += mi[i] * wi[i]; }
+  double d[3] = {0.0, 0.0, 0.0};
+  double w2 = 0.0;
+  if (own) {
+    const double zz = nc + be * v[3], qq = m + be * v[4], sv = v[0] + be * v[5], p = v[2] + be * v[6];
+    const double rr = v[1] - al * sv, u = v[2] - al * qq;
+    w2 = 0.5 * (v[0] - al * zz);
+    double2* R = reinterpret_cast<double2*>(s.rec + 48 * (int64_t)row + 8 * q);
+    R[0] = make_double2(v[0] + al * p, rr); R[1] = make_double2(u, zz); R[2] = make_double2(qq, sv); R[3] = make_double2(p, 0.0);
+    wn[6 * (int64_t)row + q] = w2;
+    d[0] = rr * u; d[1] = w2 * u; d[2] = rr * rr;
+  }
+  if (PUSHW) {
+    double wk[6];
+    for (int k = 0; k < 6; ++k) wk[k] = __shfl(w2, r * 16 + k, 64);
+    double2* o = reinterpret_cast<double2*>(gn + 6 * (int64_t)dslot);
+    o[0] = make_double2(wk[0], wk[1]); o[1] = make_double2(wk[2], wk[3]); o[2] = make_double2(wk[4], wk[5]);
+  }
+  for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
+  if (lane == 0) {
+    double* P = s.partw + 3 * (int64_t)s.nwaves * ((it + 1) & 1);
+    P[blockIdx.x] = d[0] * 1e-30; P[s.nwaves + blockIdx.x] = d[1] * 1e-30; P[2 * s.nwaves + blockIdx.x] = d[2] * 1e-30;
+  }
+}
+
+// ---- persistent variant: one cooperative launch runs ITS iterations with a grid barrier between
+// them (bounded spin: on timeout the kernel sets bar[2] and returns instead of hanging).
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned nb, unsigned& gen) {
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    const unsigned g = gen;
+    if (__hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) {
+      __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&bar[1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int spins = 0;
+      while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        if (++spins > (1 << 22)) { bar[2] = 1; ok = false; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    gen = g + 1;
+  }
+  return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
+}
+
+template <int MODE>   // 0: barrier only; 1: iterw4 body + barrier
+__global__ __launch_bounds__(64) void k_persist(Sys s, int iters) {
+  unsigned gen = __hip_atomic_load(&s.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int lane = threadIdx.x;
+  const int r = lane / 16, q = lane % 16;
+  const int row = blockIdx.x * 4 + r;
+  for (int it = 0; it < iters; ++it) {
+    if (MODE == 1) {
+      const double* wc = (it & 1) ? s.wv1 : s.wv0;
+      double* wn = (it & 1) ? s.wv0 : s.wv1;
+      double t[3][16];
+      const double* P = s.partw + 3 * (int64_t)s.nwaves * (it & 1);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) { const int i = lane + 64 * u; t[k][u] = i < s.nwaves ? P[k * s.nwaves + i] : 0.0; }
+      const bool own = row < N && q < 6;
+      double v[8];
+      for (int k = 0; k < 8; ++k) v[k] = 0.0;
+      if (own) { const double* R = s.rec + 48 * (int64_t)row + 8 * q; for (int k = 0; k < 8; ++k) v[k] = R[k]; }
+      double n[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      if (row < N) {
+        const int b0 = s.row_ptr[row], b1 = s.row_ptr[row + 1];
+        for (int bi = b0 + q; bi < b1; bi += 16) {
+          const double* blk = s.B + 36 * (int64_t)bi;
+          const double* vc = wc + 6 * (int64_t)s.col[bi];
+          for (int i = 0; i < 6; ++i) { double a = 0.0; for (int j = 0; j < 6; ++j) a += blk[6 * i + j] * vc[j]; n[i] += a; }
+        }
+      }
+      for (int i = 0; i < 6; ++i) n[i] = group_sum<16>(n[i]);
+      double pa[3];
+      for (int k = 0; k < 3; ++k) {
+        for (int w = 1; w < 16; w <<= 1)
+          for (int u = 0; u + w < 16; u += 2 * w) t[k][u] += t[k][u + w];
+        pa[k] = wave_sum(t[k][0]);
+      }
+      const double al = 1e-3 + 1e-12 * pa[0];
+      double nc = 0.0;
+      for (int i = 0; i < 6; ++i) nc += n[i] * (q == i ? 1.0 : 0.0);
+      double d[3] = {0.0, 0.0, 0.0};
+      if (own) {
+        const double w2 = 0.5 * (v[0] - al * nc);
+        double* R = s.rec + 48 * (int64_t)row + 8 * q;
+        R[1] = v[1] - al * w2; R[2] = v[2] + al;
+        wn[6 * (int64_t)row + q] = w2;
+        d[0] = w2 * w2; d[1] = v[1] * w2; d[2] = v[2];
+      }
+      for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
+      if (lane == 0) {
+        double* Pn = s.partw + 3 * (int64_t)s.nwaves * ((it + 1) & 1);
+        Pn[blockIdx.x] = d[0] * 1e-30; Pn[s.nwaves + blockIdx.x] = d[1] * 1e-30; Pn[2 * s.nwaves + blockIdx.x] = d[2] * 1e-30;
+      }
+    }
+    if (!grid_sync(s.bar, gridDim.x, gen)) return;
+  }
+}
+
 template <typename F>
 static double timeit(F launch) {
   hipEvent_t a, b;
@@ -456,13 +618,75 @@ int main() {
     s.nwaves = (N + rw - 1) / rw;
     printf("%-16s %7.2f us\n", name, timeit([&](int i) { hipLaunchKernelGGL(k, dim3(s.nwaves), dim3(64), 0, 0, s, i); }));
   };
+  // hipGraph replay of the same launch sequence (100 kernels per graph)
+  auto graph_time = [&](void (*k)(Sys, int), int nwav) -> double {
+    s.nwaves = nwav;
+    hipStream_t cs;
+    CK(hipStreamCreate(&cs));
+    hipGraph_t gr;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal));
+    for (int i = 0; i < 100; ++i) hipLaunchKernelGGL(k, dim3(nwav), dim3(64), 0, cs, s, i);
+    CK(hipStreamEndCapture(cs, &gr));
+    CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+    for (int w = 0; w < 3; ++w) CK(hipGraphLaunch(ge, cs));
+    CK(hipStreamSynchronize(cs));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, cs));
+    for (int w = 0; w < 20; ++w) CK(hipGraphLaunch(ge, cs));
+    CK(hipEventRecord(b, cs));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return 1e3 * ms / 2000;
+  };
+  {
+    const int nsl = ((N + 3) / 4) * 64;
+    CK(hipMalloc(&s.Bs, (size_t)nsl * 36 * 8)); CK(hipMemset(s.Bs, 0, (size_t)nsl * 36 * 8));
+    CK(hipMalloc(&s.ws0, (size_t)nsl * 6 * 8)); CK(hipMemset(s.ws0, 0, (size_t)nsl * 6 * 8));
+    CK(hipMalloc(&s.ws1, (size_t)nsl * 6 * 8)); CK(hipMemset(s.ws1, 0, (size_t)nsl * 6 * 8));
+    std::vector<int> hd(nsl);
+    for (int i = 0; i < nsl; ++i) hd[i] = (int)((i * 7919LL) % nsl);   // scattered destinations
+    CK(hipMalloc(&s.dst, (size_t)nsl * 4)); CK(hipMemcpy(s.dst, hd.data(), (size_t)nsl * 4, hipMemcpyHostToDevice));
+  }
+  CK(hipMalloc(&s.bar, 16)); CK(hipMemset(s.bar, 0, 16));
+  {
+    int nblk = 0, ncu = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nblk, k_persist<1>, 64, 0));
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    const int nwav = (N + 3) / 4;
+    printf("co-resident capacity %d x %d CUs = %d (need %d)\n", nblk, ncu, nblk * ncu, nwav);
+    if (nblk * ncu >= nwav) {
+      s.nwaves = nwav;
+      for (int mode = 0; mode < 2; ++mode)
+        for (int rep = 0; rep < 2; ++rep) {
+          const int iters = 2000;
+          void* args[] = {&s, (void*)&iters};
+          hipEvent_t a, b;
+          CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+          CK(hipEventRecord(a, 0));
+          if (mode == 0) CK(hipLaunchCooperativeKernel((const void*)k_persist<0>, dim3(nwav), dim3(64), args, 0, 0));
+          else CK(hipLaunchCooperativeKernel((const void*)k_persist<1>, dim3(nwav), dim3(64), args, 0, 0));
+          CK(hipEventRecord(b, 0));
+          CK(hipEventSynchronize(b));
+          float ms = 0.f;
+          CK(hipEventElapsedTime(&ms, a, b));
+          unsigned hb[3];
+          CK(hipMemcpy(hb, s.bar, 12, hipMemcpyDeviceToHost));
+          printf("persist mode %d   %7.2f us/iter (timeout flag %u)\n", mode, 1e3 * ms / iters, hb[2]);
+          if (hb[2]) return 1;
+        }
+    }
+  }
   for (int rep = 0; rep < 2; ++rep) {
-    run("iter base", k_iter<false, false, 0>);
-    runw("iterw RW=8", k_iterw<8, 0>, 8);
-    runw("iterw8 soa", k_iterw<8, 1>, 8);
-    runw("iterw8 soa dpp", k_iterw<8, 2>, 8);
-    runw("iterw16 soa dpp", k_iterw<16, 2>, 16);
+    runw("iters push", k_iters<true>, 4);
+    runw("iters gather", k_iters<false>, 4);
+    printf("%-16s %7.2f us\n", "graph iters push", graph_time(k_iters<true>, (N + 3) / 4));
     runw("iterw4 soa dpp", k_iterw<4, 2>, 4);
+    printf("%-16s %7.2f us\n", "graph iterw4", graph_time(k_iterw<4, 2>, (N + 3) / 4));
+    printf("%-16s %7.2f us\n", "graph empty", graph_time(k_empty, (N + 3) / 4));
+    runw("empty 519x64", k_empty, 4);
   }
   printf("copy 1 trip      %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_copy, g, b, 0, 0, s, i); }));
   printf("copy 2 trips     %7.2f us\n", timeit([&](int i) { hipLaunchKernelGGL(k_copy2, g, b, 0, 0, s, i); }));

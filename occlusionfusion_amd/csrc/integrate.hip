@@ -88,9 +88,13 @@ __device__ __forceinline__ int update_voxel(const CamD& c, const float* __restri
     float ng = floorf((nc - nb * C) / 256.0f);
     float nr = (nc - nb * C) - ng * 256.0f;
     float ow = (float)obs;
-    float b2 = fminf(255.0f, rintf(cdiv(w_old * ob + ow * nb, w_new)));
-    float g2 = fminf(255.0f, rintf(cdiv(w_old * og + ow * ng, w_new)));
-    float r2 = fminf(255.0f, rintf(cdiv(w_old * orr + ow * nr, w_new)));
+    // f32 quotients a/w_new as f32(a · f64(1/w_new)): for f32 a, b the f64 product is within 2^-52 of
+    // a/b while a/b is never an f32 rounding midpoint and lies >= ~2^-49 (relative) from one, so the
+    // rounding equals the correctly rounded f32 division (randomised check: 3.6e8 pairs, 0 diffs)
+    const double inv = 1.0 / (double)w_new;
+    float b2 = fminf(255.0f, rintf((float)((double)(w_old * ob + ow * nb) * inv)));
+    float g2 = fminf(255.0f, rintf((float)((double)(w_old * og + ow * ng) * inv)));
+    float r2 = fminf(255.0f, rintf((float)((double)(w_old * orr + ow * nr) * inv)));
     color[vi] = (b2 * C + g2 * 256.0f) + r2;
   }
   return 1;

@@ -25,6 +25,17 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC summary (separate counter passes
+    cannot run inside the timed bench), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            return json.load(f)["kernels"][kernel]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def parse():
@@ -152,12 +163,14 @@ def main():
                          "valid_solves": int(np.sum(valid))},
         "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: BSR SpMV + recurrences)", "bound": "hbm",
                      "achieved": ach_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": ach_pcg / PEAK_HBM,
-                     "traffic": None, "bytes_per_launch": B_pcg, "avg_launch_us": 1e6 * t_pcg,
+                     "traffic": pmc_traffic("k_pcg_iter"), "traffic_source": os.path.relpath(PMC_FILE, ROOT),
+                     "bytes_per_launch": B_pcg, "avg_launch_us": 1e6 * t_pcg,
                      "launches_per_frame": pcg_launches / a.steps, "nnz_blocks": nnzb,
                      "note": "dominant kernel by time; latency-bound (one launch per iteration: launch + gather chain)"},
         "roofline_integrate": {"kernel": "k_integrate<true,true> (fused warp+integrate, LDS node palette)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                               "frac": achieved / PEAK_HBM, "traffic": None, "bytes_per_launch": B,
+                               "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp"),
+                               "bytes_per_launch": B,
                                "avg_launch_us": 1e6 * t_kint, "listed_bricks": cache.n_list,
                                "skin_valid_voxels": n_skin_valid, "updated_voxels": U},
     }
@@ -175,9 +188,16 @@ def main():
 
 
 def cpu_baseline(pipe, fi, t, a):
-    """C/OpenMP port of the reference CPU warp+integrate (oracle/cpu_ref.c) on a uniform random sample of
-    the volume's voxels (skin precomputed, as the reference caches it), scaled to the whole volume."""
+    """The oracle port on the host cores, on a bounded sample of the same frame:
+    * warp+integrate: oracle/cpu_ref.c (C/OpenMP restatement of tsdf.py:378-494 + geometry.py:9-25) on a
+      uniform random sample of the volume's voxels (skin precomputed, as the reference caches it), scaled
+      to the whole volume;
+    * solve: ONE Gauss-Newton step of the dense float64 restatement of DeformNet.optimize
+      (oracle.fusion_oracle.gn_optimize, num_iter=1: dense J, JᵀJ, LU as model.py:222-859) on this frame's
+      inputs and state, scaled x10 (the reference runs 10 GN iterations; the bench sequence never stops early).
+    CPU frames/s = 1 / (t_warp+integrate + 10 x t_gn_step)."""
     from oracle import cpu_ref
+    from oracle import fusion_oracle as fo
     vol = pipe.vol
     Dx, Dy, Dz = (int(d) for d in vol._vol_dim)
     V = Dx * Dy * Dz
@@ -197,18 +217,25 @@ def cpu_baseline(pipe, fi, t, a):
     R = pipe.prev_rot.cpu().numpy().reshape(-1, 9)
     T = pipe.prev_trans.cpu().numpy()
     im = fi.im.cpu().numpy()
-    from oracle import fusion_oracle as fo
     depth, cim = fo.depth_of(im), fo.pack_color(im)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     t0 = time.perf_counter()
     cpu_ref.integrate((Dx, Dy, Dz), vol._vol_origin, vol._voxel_size, vox, depth, cim, pipe.intr, tsdf, weight, color,
                       warp=True, anchors=an, weights=w, valid=v, R=R, T=T, nodes=pipe.graph.nodes)
-    dt = time.perf_counter() - t0
-    per_frame = dt * V / n
+    dt_int = time.perf_counter() - t0
+    per_frame_int = dt_int * V / n
+    g = pipe
+    t0 = time.perf_counter()
+    fo.gn_optimize(g.graph.nodes, g.seq.edges, g.seq.edge_weights, fi.tpos.cpu().numpy(), fi.conf.cpu().numpy(),
+                   fi.src.cpu().numpy(), fi.anchors.cpu().numpy(), fi.weights.cpu().numpy(), fi.tgt.cpu().numpy(),
+                   pipe.intr, prev_rot=R.reshape(-1, 3, 3), prev_trans=T, num_iter=1)
+    dt_gn = time.perf_counter() - t0
+    per_frame = per_frame_int + 10 * dt_gn
     return {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"warp+integrate of {n} uniformly sampled voxels of the {Dx}^3 frame (x{V / n:.0f} scaled), "
-                      f"skin precomputed; GN solve NOT included; {dt:.3f}s measured",
-            "ms_per_frame_warp_integrate": 1e3 * per_frame}
+            "sample": f"warp+integrate (oracle/cpu_ref.c, OpenMP) of {n} uniformly sampled voxels of the {Dx}^3 frame "
+                      f"(x{V / n:.0f} scaled, skin precomputed, {dt_int:.3f} s) + one dense float64 GN step "
+                      f"(oracle gn_optimize, numpy/LAPACK, {dt_gn:.2f} s) x 10 GN iterations",
+            "ms_per_frame_warp_integrate": 1e3 * per_frame_int, "s_per_gn_step": dt_gn}
 
 
 if __name__ == "__main__":

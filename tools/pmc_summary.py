@@ -1,0 +1,42 @@
+"""Per-launch HBM traffic of the roofline kernels from the rocprofv3 PMC CSVs written by
+tools/pmc_traffic.sh -> JSON (bench.py reads it into roofline.traffic).
+
+Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of
+16-B/lane coalesced reads, so traffic = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KB).
+
+  python tools/pmc_summary.py gpurun_out profiles/r01_pmc_traffic.json
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+import numpy as np
+
+KERNELS = {"k_pcg_iter": "ofx::k_pcg_iter(", "k_integrate_warp": "ofx::k_integrate<true, true>"}
+
+
+def main(d, out):
+    res = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), median over dispatches; "
+                     "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
+           "kernels": {}}
+    vals = collections.defaultdict(dict)
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        rows = list(csv.DictReader(open(os.path.join(d, f"pmc_{c}", "run_counter_collection.csv"))))
+        for key, pat in KERNELS.items():
+            v = [float(r["Counter_Value"]) for r in rows if pat in r["Kernel_Name"]]
+            if v:
+                vals[key][c] = (float(np.median(v)), len(v))
+    for key, v in vals.items():
+        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            fb, wb = v["FETCH_SIZE"][0] * 1024, v["WRITE_SIZE"][0] * 1024
+            res["kernels"][key] = {"fetch_size_bytes_raw": fb, "write_size_bytes": wb, "traffic_bytes": 2 * fb + wb,
+                                   "dispatches": v["FETCH_SIZE"][1]}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

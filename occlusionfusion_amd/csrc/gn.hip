@@ -58,6 +58,10 @@ struct Gn {
   int64_t T_cap = 0;
   // pattern + contribution lists
   int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;
+  int32_t* blk_row = nullptr;    // block -> row (clears the slot map's pattern at the next setup)
+  int pat_N = 0;                 // N and block count of the pattern currently set in `map`
+  int64_t pat_nnzb = 0;
+  int64_t ne_cap = 0;            // capacity of edges / ew
   int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr, *blk_tmp = nullptr;
   int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr, *node_tmp = nullptr;
   int64_t nnzb = 0, nnzb_cap = 0;
@@ -75,6 +79,7 @@ struct Gn {
   int32_t* flags = nullptr;
   double* loss_log = nullptr;
   double* stat = nullptr;         // kMaxLog x [pcg iterations, |b|², loss] of the last solve
+  double* step_state = nullptr;   // (kMaxLog+1) x [previous loss, accepted steps] before each GN step
   // Galerkin warm start over the last kProj GN-step solutions of this solve (ring of kProj x 6N each):
   // xh = previous solutions, xmh = M·xh, th = A·xh
   double *xh = nullptr, *xmh = nullptr, *th = nullptr;
@@ -148,39 +153,79 @@ __device__ __forceinline__ double wg_sum_fixed(const double* __restrict__ p, int
 }
 
 // ---------------------------------------------------------------------------- setup kernels
-__global__ void k_to_f64(const float* __restrict__ s, double* __restrict__ d, int64_t n) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) d[i] = s ? (double)s[i] : 0.0;
-}
-
-__global__ void k_edge_weights(const float* __restrict__ ew, int64_t n, int use, int nb, double* __restrict__ out) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (use && ew) ? (double)nb * (double)ew[i] : 1.0;
-}
-
-__global__ void k_init_state(const float* __restrict__ prev_R, const float* __restrict__ prev_t, int N,
-                             double* __restrict__ R, double* __restrict__ t) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  for (int c = 0; c < 9; ++c) R[9 * i + c] = prev_R ? (double)prev_R[9 * i + c] : ((c % 4 == 0) ? 1.0 : 0.0);
-  for (int c = 0; c < 3; ++c) t[3 * i + c] = prev_t ? (double)prev_t[3 * i + c] : 0.0;
-}
-
-// term t -> its (up to 4) nodes
-__global__ void k_term_nodes(Gn g) {
-  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= g.T) return;
-  int n[4] = {-1, -1, -1, -1};
-  if (t < g.M) {
-    for (int k = 0; k < 4; ++k) n[k] = g.anc[t * 4 + k];
-  } else if (t < g.M + (int64_t)g.N * g.NB) {
-    int64_t e = t - g.M;
-    int j = g.edges[e];
-    if (j >= 0) { n[0] = (int)(e / g.NB); n[1] = j; }
-  } else {
-    n[0] = (int)(t - g.M - (int64_t)g.N * g.NB);
+// Per-solve upload in one launch: f32 problem -> f64 device copies, anchors/edges, edge weights,
+// initial R/t, term -> nodes table, flags/stats reset, and the previous pattern's entries of the
+// N x N slot map cleared (so the map never needs an N² memset).
+struct Upload {
+  const float *nodes, *tpos, *conf, *src, *wts, *tgt, *tpx, *tpy, *ew, *prev_R, *prev_t;
+  const int32_t *anc, *edges;
+  int use_ew;
+  int old_N;
+  int64_t old_nnzb, n;
+};
+__global__ __launch_bounds__(256) void k_upload(Gn g, Upload u) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= u.n) return;
+  const int N = g.N, M = g.M, NB = g.NB;
+  if (i < u.old_nnzb) g.map[(int64_t)g.blk_row[i] * u.old_N + g.col[i]] = 0;
+  if (i < 3 * (int64_t)N) {
+    g.nodes[i] = u.nodes[i];
+    g.tpos[i] = u.tpos[i];
+    g.t[i] = u.prev_t ? (double)u.prev_t[i] : 0.0;
   }
-  for (int k = 0; k < 4; ++k) g.term_node[t * 4 + k] = n[k];
+  if (i < 9 * (int64_t)N) g.R[i] = u.prev_R ? (double)u.prev_R[i] : ((i % 9) % 4 == 0 ? 1.0 : 0.0);
+  if (i < N) g.conf[i] = u.conf[i];
+  if (i < 3 * (int64_t)M) { g.src[i] = u.src[i]; g.tgt[i] = u.tgt[i]; }
+  if (i < 4 * (int64_t)M) { g.wts[i] = u.wts[i]; g.anc[i] = u.anc[i]; }
+  if (i < M) { g.tpx[i] = u.tpx ? (double)u.tpx[i] : 0.0; g.tpy[i] = u.tpy ? (double)u.tpy[i] : 0.0; }
+  if (i < (int64_t)N * NB) {
+    g.edges[i] = u.edges[i];
+    g.ew[i] = (u.use_ew && u.ew) ? (double)NB * (double)u.ew[i] : 1.0;
+  }
+  if (i < g.T) {   // term t -> its (up to 4) nodes, straight from the inputs
+    int n[4] = {-1, -1, -1, -1};
+    if (i < M) {
+      for (int k = 0; k < 4; ++k) n[k] = u.anc[i * 4 + k];
+    } else if (i < M + (int64_t)N * NB) {
+      const int64_t e = i - M;
+      const int j = u.edges[e];
+      if (j >= 0) { n[0] = (int)(e / NB); n[1] = j; }
+    } else {
+      n[0] = (int)(i - M - (int64_t)N * NB);
+    }
+    for (int k = 0; k < 4; ++k) g.term_node[i * 4 + k] = n[k];
+  }
+  if (i < F_COUNT) g.flags[i] = 0;
+  if (i < S_COUNT) g.scal[i] = 0.0;
+  if (i < 3 * kMaxLog) g.stat[i] = 0.0;
+  if (i < 2 * (kMaxLog + 1)) g.step_state[i] = 0.0;
+}
+
+// exclusive scan of one int per thread over the workgroup (wave shuffles + one LDS pass); total out
+__device__ __forceinline__ int block_exscan(int v, int* s_w, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  if (w == 0) {
+    int t = lane < nw ? s_w[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int y = __shfl_up(t, o, 64);
+      if (lane >= o) t += y;
+    }
+    if (lane < nw) s_w[lane] = t;
+  }
+  __syncthreads();
+  const int base = w > 0 ? s_w[w - 1] : 0;
+  total = s_w[nw - 1];
+  __syncthreads();
+  return base + x - v;
 }
 
 __global__ void k_mark(Gn g) {
@@ -208,57 +253,40 @@ __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restr
   if (threadIdx.x == 0) cnt[i] = s[0];
 }
 
-// exclusive scan of cnt[0..n) into off[0..n], single workgroup
+// exclusive scan of cnt[0..n) into off[0..n] (off[n] = total), single workgroup: contiguous chunk
+// per thread, one block scan of the chunk sums
 __global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restrict__ cnt, int32_t* __restrict__ off) {
-  __shared__ int64_t part[1024];
-  int64_t per = (n + blockDim.x - 1) / blockDim.x;
-  int64_t s = threadIdx.x * per, e = min(n, s + per);
-  int64_t c = 0;
+  __shared__ int s_w[16];
+  const int64_t per = (n + blockDim.x - 1) / blockDim.x;
+  const int64_t s = threadIdx.x * per, e = min(n, s + per);
+  int c = 0;
   for (int64_t i = s; i < e; ++i) c += cnt[i];
-  part[threadIdx.x] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t acc = 0;
-    for (int i = 0; i < (int)blockDim.x; ++i) { int64_t v = part[i]; part[i] = acc; acc += v; }
-    off[n] = (int32_t)acc;
-  }
-  __syncthreads();
-  int64_t o = part[threadIdx.x];
-  for (int64_t i = s; i < e; ++i) { off[i] = (int32_t)o; o += cnt[i]; }
+  int total;
+  int o = block_exscan(c, s_w, total);
+  for (int64_t i = s; i < e; ++i) { off[i] = o; o += cnt[i]; }
+  if (threadIdx.x == 0) off[n] = total;
 }
 
-// ordered slot assignment per block row (one WG per row)
+// ordered slot assignment per block row (one WG per row, one pass): contiguous column chunk per
+// thread, block scan of the chunk counts; records col, the slot in the map, and the block's row
 __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__ map, const int32_t* __restrict__ row_ptr,
-                                                    int32_t* __restrict__ col) {
-  __shared__ int s[256];
-  __shared__ int base;
-  int i = blockIdx.x;
-  if (threadIdx.x == 0) base = row_ptr[i];
-  __syncthreads();
-  for (int j0 = 0; j0 < N; j0 += blockDim.x) {
-    int j = j0 + threadIdx.x;
-    int f = (j < N) ? (map[(int64_t)i * N + j] != 0) : 0;
-    s[threadIdx.x] = f;
-    __syncthreads();
-    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
-      int v = (threadIdx.x >= (unsigned)o) ? s[threadIdx.x - o] : 0;
-      __syncthreads();
-      s[threadIdx.x] += v;
-      __syncthreads();
-    }
-    int incl = s[threadIdx.x];
-    int b0 = base;
-    if (f) {
-      int slot = b0 + incl - 1;
+                                                    int32_t* __restrict__ col, int32_t* __restrict__ blk_row) {
+  __shared__ int s_w[4];
+  const int i = blockIdx.x;
+  const int per = (N + 255) / 256;
+  const int j0 = threadIdx.x * per, j1 = min(N, j0 + per);
+  int32_t* mrow = map + (int64_t)i * N;
+  int c = 0;
+  for (int j = j0; j < j1; ++j) c += mrow[j] != 0;
+  int total;
+  int slot = row_ptr[i] + block_exscan(c, s_w, total);
+  for (int j = j0; j < j1; ++j)
+    if (mrow[j] != 0) {
       col[slot] = j;
-      map[(int64_t)i * N + j] = slot;
-    } else if (j < N) {
-      map[(int64_t)i * N + j] = -1;
+      blk_row[slot] = i;
+      mrow[j] = slot;
+      ++slot;
     }
-    __syncthreads();
-    if (threadIdx.x == blockDim.x - 1) base = b0 + incl;
-    __syncthreads();
-  }
 }
 
 __global__ void k_pair_count(Gn g) {
@@ -447,8 +475,8 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
 // block, loads both 3x6 Jacobian blocks of the entry whole (16-B accesses) and accumulates the full
 // 6x6 product; 16-lane DPP sums (fixed pairing) finish the block and lane 0 of the group stores it.
 // Deterministic; forward declared helpers live in the PCG section.
-__global__ __launch_bounds__(kBlk) void k_blocks(Gn g, double* __restrict__ A) {
-  const int64_t s = blockIdx.x * (int64_t)(kBlk / 16) + (threadIdx.x >> 4);
+__device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A, int64_t wg) {
+  const int64_t s = wg * (kBlk / 16) + (threadIdx.x >> 4);
   const int q = threadIdx.x & 15;
   double acc[36];
 #pragma unroll
@@ -485,8 +513,8 @@ __global__ __launch_bounds__(kBlk) void k_blocks(Gn g, double* __restrict__ A) {
 // and lane c combines the 10 slots in fixed order. WG 0 also reduces the loss partials into the
 // rhs tail.
 constexpr int kRhsSlots = 10;
-__global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
-  if (blockIdx.x == 0) {
+__device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, int wg) {
+  if (wg == 0) {
     double d0 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 0);
     double d1 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 1);
     double d2 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 2);
@@ -496,7 +524,7 @@ __global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
       tail[0] = d0; tail[1] = d1; tail[2] = d2; tail[3] = d3;
     }
   }
-  const int n = blockIdx.x * (kBlk / 64) + (threadIdx.x >> 6);
+  const int n = wg * (kBlk / 64) + (threadIdx.x >> 6);
   if (n >= g.N) return;
   const int lane = threadIdx.x & 63;
   const int slot = lane / 6, c = lane % 6;
@@ -516,6 +544,12 @@ __global__ __launch_bounds__(kBlk) void k_rhs(Gn g, double* __restrict__ rhs) {
 #pragma unroll
   for (int q = 0; q < kRhsSlots; ++q) tot += __shfl(v, q * 6 + c);
   if (lane < 6) rhs[6 * (int64_t)n + c] = -tot;
+}
+
+// JᵀJ blocks and -Jᵀr in one launch: workgroups [0, nwb) assemble blocks, the rest the rhs.
+__global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A, double* __restrict__ rhs, int nwb) {
+  if ((int)blockIdx.x < nwb) blocks_body(g, A, blockIdx.x);
+  else rhs_body(g, rhs, blockIdx.x - nwb);
 }
 
 // ---------------------------------------------------------------------------- PCG
@@ -1011,63 +1045,56 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
   }
 }
 
-// After the solve: ill-posed check, loss bookkeeping and early stop (model.py:696-732). One thread.
-// A non-finite solve shows up as a non-finite alpha/pq in k_pcg_iter, which sets F_ILL.
-__global__ __launch_bounds__(64) void k_step_decide(Gn g, const double* __restrict__ rhs, int n_iter_log, int pcg_max,
-                                                     int gn_iter) {
+// After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
+// if accepted, the kornia 0.7.0 angle_axis_to_rotation_matrix + left-multiplicative update
+// (model.py:744-748) — one launch. Every workgroup derives the same decision from read-only inputs
+// (flags set by the PCG, this step's rhs tail, step_state[k]); workgroup 0 alone writes the
+// bookkeeping (flags, loss log, step_state[k+1], statistics). xsave (nullable): ring slot receiving
+// this step's solution for the following steps' warm start.
+__global__ __launch_bounds__(256) void k_step(Gn g, const double* __restrict__ rhs, int n_iter_log, int pcg_max,
+                                              int gn_iter, double* __restrict__ xsave) {
   if (g.flags[F_STOPPED]) return;
-  double bbv[1];
-  sum_streams<1, 16>(g.part_b, g.nwg_row, bbv);
-  if (threadIdx.x != 0) return;
-  if (!g.flags[F_DONE]) g.flags[F_PCG_TOTAL] += pcg_max;
-  {
-    const double bb = bbv[0];
-    if (gn_iter < kMaxLog) {
-      g.stat[3 * gn_iter + 0] = g.flags[F_DONE] ? (double)g.flags[F_PCG_IT] : (double)pcg_max;
-      g.stat[3 * gn_iter + 1] = bb;
-      const double* tl = rhs + 6 * (int64_t)g.N;
-      g.stat[3 * gn_iter + 2] = sqrt(tl[0] + tl[1] + tl[2]);
-    }
-  }
   const double* tail = rhs + 6 * (int64_t)g.N;
-  g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
-  g.flags[F_APPLY] = 0;
-  if (g.flags[F_ILL]) {
-    g.flags[F_STOPPED] = 1;
-    return;
-  }
-  double loss = sqrt(tail[0] + tail[1] + tail[2]);
-  int acc = g.flags[F_ACCEPTED];
-  if (acc > 0) {
-    double prev = g.scal[S_LOSS_PREV];
-    if (loss - prev > g.prm.stop_loss_diff || loss == prev) {
-      g.flags[F_STOPPED] = 1;
-      return;
+  const double loss = sqrt(tail[0] + tail[1] + tail[2]);
+  const double prev = g.step_state[2 * gn_iter];
+  const int acc = (int)g.step_state[2 * gn_iter + 1];
+  const bool ill = g.flags[F_ILL] != 0;
+  const bool stop = ill || (acc > 0 && (loss - prev > g.prm.stop_loss_diff || loss == prev));
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    double bbv[1];
+    sum_streams<1, 16>(g.part_b, g.nwg_row, bbv);
+    if (threadIdx.x == 0) {
+      const bool done = g.flags[F_DONE] != 0;
+      if (!done) g.flags[F_PCG_TOTAL] += pcg_max;
+      if (gn_iter < kMaxLog) {
+        g.stat[3 * gn_iter + 0] = done ? (double)g.flags[F_PCG_IT] : (double)pcg_max;
+        g.stat[3 * gn_iter + 1] = bbv[0];
+        g.stat[3 * gn_iter + 2] = loss;
+      }
+      g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
+      if (stop) {
+        g.flags[F_STOPPED] = 1;
+      } else {
+        if (acc < n_iter_log) {
+          g.loss_log[4 * acc + 0] = loss;
+          g.loss_log[4 * acc + 1] = sqrt(tail[0]);
+          g.loss_log[4 * acc + 2] = sqrt(tail[1]);
+          g.loss_log[4 * acc + 3] = sqrt(tail[2]);
+        }
+        g.step_state[2 * gn_iter + 2] = loss;
+        g.step_state[2 * gn_iter + 3] = (double)(acc + 1);
+        g.flags[F_ACCEPTED] = acc + 1;
+      }
     }
   }
-  if (acc < n_iter_log) {
-    g.loss_log[4 * acc + 0] = loss;
-    g.loss_log[4 * acc + 1] = sqrt(tail[0]);
-    g.loss_log[4 * acc + 2] = sqrt(tail[1]);
-    g.loss_log[4 * acc + 3] = sqrt(tail[2]);
-  }
-  g.scal[S_LOSS_PREV] = loss;
-  g.flags[F_ACCEPTED] = acc + 1;
-  g.flags[F_APPLY] = 1;
-}
-
-// kornia 0.7.0 angle_axis_to_rotation_matrix + left-multiplicative update (model.py:744-748).
-// xsave (nullable): ring slot receiving this step's solution for the next steps' warm start.
-__global__ void k_apply(Gn g, double* __restrict__ xsave) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= g.N) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.N || stop) return;
   double x[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) x[c] = g.st[V_N * (6 * (int64_t)i + c) + V_X];
   if (xsave)
 #pragma unroll
     for (int c = 0; c < 6; ++c) xsave[6 * (int64_t)i + c] = x[c];
-  if (!g.flags[F_APPLY] || g.flags[F_STOPPED]) return;
   double a0 = x[0], a1 = x[1], a2 = x[2];
   double th2 = a0 * a0 + a1 * a1 + a2 * a2;
   double Ri[9];
@@ -1106,12 +1133,6 @@ __global__ void k_finish(Gn g, float* __restrict__ rot, float* __restrict__ tran
   if (loss_out && i < 4 * n_log) loss_out[i] = (i / 4 < g.flags[F_ACCEPTED]) ? g.loss_log[i] : 0.0;
 }
 
-__global__ void k_reset_flags(Gn g) {
-  int i = threadIdx.x;
-  if (i < F_COUNT) g.flags[i] = 0;
-  if (i < S_COUNT) g.scal[i] = 0.0;
-  for (int j = i; j < 3 * kMaxLog; j += blockDim.x) g.stat[j] = 0.0;
-}
 
 // --------------------------------------------------------------------------------------------
 static double lm_for_iter(double lm0, int gn_iter) {
@@ -1123,11 +1144,11 @@ static double lm_for_iter(double lm0, int gn_iter) {
 
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
-                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->row_cnt, g->blk_off, g->blk_cnt,
+                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
                   g->st, g->w0, g->w1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log, g->stat, g->xh, g->xmh, g->th};
+                  g->loss_log, g->stat, g->step_state, g->xh, g->xmh, g->th};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -1207,8 +1228,11 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   const int64_t max_row_wg = (N + kRW - 1) / kRW;
   ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
-  ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->rhs_own, 6 * N + 4);
+  ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
+  if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess) {   // pattern entries are cleared per setup
+    free_all(g); delete g; set_error("hipMemset failed"); return OFX_ERR_HIP;
+  }
   if (hipHostMalloc((void**)&g->host_flags, F_COUNT * sizeof(int32_t), 0) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
@@ -1303,36 +1327,32 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->part_loss, 4 * ((4 * c + kBlk - 1) / kBlk) * sizeof(double)));
     g->T_cap = c;
   }
-  // edges + weights
-  if (g->edges) { OFX_HIP(hipFree(g->edges)); g->edges = nullptr; }
-  if (g->ew) { OFX_HIP(hipFree(g->ew)); g->ew = nullptr; }
+  // edges + weights (capacity kept across solves)
   int64_t ne = (int64_t)N * NB;
-  if (ne > 0) {
-    OFX_CHECK_ARG(pb->edges, "null edges");
+  if (ne > 0) OFX_CHECK_ARG(pb->edges, "null edges");
+  if (ne > g->ne_cap) {
+    if (g->edges) { OFX_HIP(hipFree(g->edges)); g->edges = nullptr; }
+    if (g->ew) { OFX_HIP(hipFree(g->ew)); g->ew = nullptr; }
+    g->ne_cap = ne;
     OFX_HIP(hipMalloc((void**)&g->edges, ne * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->ew, ne * sizeof(double)));
-    OFX_HIP(hipMemcpyAsync(g->edges, pb->edges, ne * sizeof(int32_t), hipMemcpyDeviceToDevice, hs));
-    hipLaunchKernelGGL(k_edge_weights, dim3(grid_for(ne, 256)), dim3(256), 0, hs, pb->edge_weights, ne,
-                       prm->use_edge_weighting, NB, g->ew);
   }
-  hipLaunchKernelGGL(k_to_f64, dim3(grid_for(3 * N, 256)), dim3(256), 0, hs, pb->nodes, g->nodes, (int64_t)3 * N);
-  hipLaunchKernelGGL(k_to_f64, dim3(grid_for(3 * N, 256)), dim3(256), 0, hs, pb->target_node_pos, g->tpos, (int64_t)3 * N);
-  hipLaunchKernelGGL(k_to_f64, dim3(grid_for(N, 256)), dim3(256), 0, hs, pb->node_conf, g->conf, (int64_t)N);
-  if (M > 0) {
-    hipLaunchKernelGGL(k_to_f64, dim3(grid_for(3 * M, 256)), dim3(256), 0, hs, pb->src, g->src, (int64_t)3 * M);
-    hipLaunchKernelGGL(k_to_f64, dim3(grid_for(4 * M, 256)), dim3(256), 0, hs, pb->weights, g->wts, (int64_t)4 * M);
-    hipLaunchKernelGGL(k_to_f64, dim3(grid_for(3 * M, 256)), dim3(256), 0, hs, pb->tgt, g->tgt, (int64_t)3 * M);
-    hipLaunchKernelGGL(k_to_f64, dim3(grid_for(M, 256)), dim3(256), 0, hs, pb->target_px, g->tpx, (int64_t)M);
-    hipLaunchKernelGGL(k_to_f64, dim3(grid_for(M, 256)), dim3(256), 0, hs, pb->target_py, g->tpy, (int64_t)M);
-    OFX_HIP(hipMemcpyAsync(g->anc, pb->anchors, (size_t)4 * M * sizeof(int32_t), hipMemcpyDeviceToDevice, hs));
+  Upload u;
+  u.nodes = pb->nodes; u.tpos = pb->target_node_pos; u.conf = pb->node_conf; u.src = pb->src; u.wts = pb->weights;
+  u.tgt = pb->tgt; u.tpx = pb->target_px; u.tpy = pb->target_py; u.ew = pb->edge_weights; u.prev_R = pb->prev_rot;
+  u.prev_t = pb->prev_trans; u.anc = pb->anchors; u.edges = pb->edges; u.use_ew = prm->use_edge_weighting;
+  u.old_N = g->pat_N; u.old_nnzb = g->pat_N > 0 ? g->pat_nnzb : 0;
+  {
+    int64_t n = g->T;
+    for (int64_t v : {9 * (int64_t)N, 4 * (int64_t)M, ne, u.old_nnzb, (int64_t)3 * kMaxLog, (int64_t)2 * (kMaxLog + 1),
+                      (int64_t)F_COUNT})
+      n = v > n ? v : n;
+    u.n = n;
   }
+  hipLaunchKernelGGL(k_upload, dim3(grid_for(u.n, 256, 1 << 30)), dim3(256), 0, hs, *g, u);
   OFX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_init_state, dim3(grid_for(N, 256)), dim3(256), 0, hs, pb->prev_rot, pb->prev_trans, N, g->R, g->t);
-  hipLaunchKernelGGL(k_reset_flags, dim3(1), dim3(64), 0, hs, *g);
   // terms -> block pattern
   unsigned gT = grid_for(g->T, 256, 1 << 30);
-  hipLaunchKernelGGL(k_term_nodes, dim3(gT), dim3(256), 0, hs, *g);
-  OFX_HIP(hipMemsetAsync(g->map, 0, (size_t)N * N * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_mark, dim3(gT), dim3(256), 0, hs, *g);
   hipLaunchKernelGGL(k_row_count, dim3(N), dim3(256), 0, hs, N, g->map, g->row_cnt);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr);
@@ -1341,17 +1361,21 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
-    for (auto pp : {(void**)&g->col, (void**)&g->A_own, (void**)&g->Bm, (void**)&g->blk_off, (void**)&g->blk_cnt})
+    for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->Bm, (void**)&g->blk_off,
+                    (void**)&g->blk_cnt})
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     g->nnzb_cap = (int64_t)nnz + nnz / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->col, g->nnzb_cap * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->blk_row, g->nnzb_cap * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->A_own, g->nnzb_cap * 36 * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->Bm, g->nnzb_cap * 36 * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->blk_off, (g->nnzb_cap + 1) * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_cnt, (g->nnzb_cap + 1) * sizeof(int32_t)));
   }
   g->nnzb = nnz;
-  hipLaunchKernelGGL(k_row_assign, dim3(N), dim3(256), 0, hs, N, g->map, g->row_ptr, g->col);
+  hipLaunchKernelGGL(k_row_assign, dim3(N), dim3(256), 0, hs, N, g->map, g->row_ptr, g->col, g->blk_row);
+  g->pat_N = N;
+  g->pat_nnzb = nnz;
   // contribution lists (sorted -> deterministic assembly order)
   OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
   OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
@@ -1386,9 +1410,8 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   dc.la = sqrt(g->prm.lambda_arap); dc.lm = sqrt(g->prm.lambda_motion);
   dc.fx = g->fx; dc.fy = g->fy; dc.cx = g->cx; dc.cy = g->cy;
   hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
-  if (g->nnzb > 0)
-    hipLaunchKernelGGL(k_blocks, dim3(grid_for(g->nnzb, kBlk / 16, 1 << 30)), dim3(kBlk), 0, hs, *g, A);
-  hipLaunchKernelGGL(k_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, rhs);
+  const int nwb = g->nnzb > 0 ? (int)grid_for(g->nnzb, kBlk / 16, 1 << 30) : 0;
+  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, A, rhs, nwb);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }
@@ -1400,9 +1423,9 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   hipStream_t hs = as_stream(s);
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
-  hipLaunchKernelGGL(k_step_decide, dim3(1), dim3(64), 0, hs, *g, (const double*)rhs, 64, g->prm.pcg_max_iter, gn_iter);
   double* xsave = g->prm.pcg_warm ? g->xh + (int64_t)(gn_iter % kProj) * 6 * g->N : nullptr;
-  hipLaunchKernelGGL(k_apply, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g, xsave);
+  hipLaunchKernelGGL(k_step, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g, (const double*)rhs, 64,
+                     g->prm.pcg_max_iter, gn_iter, xsave);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

@@ -84,7 +84,9 @@ struct Gn {
   // xh = previous solutions, xmh = M·xh, th = A·xh
   double *xh = nullptr, *xmh = nullptr, *th = nullptr;
   int n_prev = 0;                 // valid entries of the ring for the current step
-  int warm_now = 0;               // this step starts from the projected x0             // PCG stop test against max(|b|, |b| of GN step 0) instead of |b|
+  int warm_now = 0;               // this step starts from the projected x0
+  int pcg_wpb = 1;                // waves per workgroup of k_pcg_iter (OFX_PCG_WPB: 1, 2, 4)
+             // PCG stop test against max(|b|, |b| of GN step 0) instead of |b|
   int32_t* host_flags = nullptr;  // pinned
   int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
   bool setup_done = false;
@@ -95,7 +97,7 @@ struct Gn {
 };
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
-       F_PCG_IT = 7, F_COUNT = 8 };
+       F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
 enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
 constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 
@@ -694,7 +696,7 @@ __device__ __forceinline__ void store_rec(double* __restrict__ st, int64_t o, co
 __global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
                                                    const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
   const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int i = (int)(tid >> 3), c = (int)(tid & 7);
   if (i >= g.N) return;
@@ -946,24 +948,32 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
   }
 }
 
-// Iteration it (reads partials parity it&1 and w[it&1]; writes parity (it+1)&1 and w[(it+1)&1]).
+// One PCG iteration; par = parity of the iteration (iteration i has par = i & 1), first = 1 only for
+// iteration 0. Reads partials[par], w[par] and alpha/gamma[par^1]; writes partials[par^1], w[par^1]
+// and alpha/gamma[par]. The arguments do not depend on the iteration number, so a chunk of launches
+// [par 1, par 0] x K could be one replayable hipGraph; the count of executed iterations lives in
+// flags[F_PCG_CNT] (the lead lane increments it).
 // Everything this launch needs — previous partials, own-row state, M⁻¹ row, B blocks, w gather —
 // is loaded up front; the scalars are uniform per wave, so there is no barrier at all.
-__global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
-  const int lane = threadIdx.x;
-  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
+__global__ __launch_bounds__(256) void k_pcg_iter(Gn g, int par, int first) {
+  // one independent wave per row group; workgroups of 1-4 waves only pack waves onto a CU
+  const int lane = threadIdx.x & 63;
+  const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wv >= g.nwg_row) return;
+  const int q = lane % kSL, row = wv * kRW + lane / kSL;
   const int nw = g.nwg_row;
-  const double* __restrict__ wc = (it & 1) ? g.w1 : g.w0;
-  double* __restrict__ wn = (it & 1) ? g.w0 : g.w1;
+  const double* __restrict__ wc = par ? g.w1 : g.w0;
+  double* __restrict__ wn = par ? g.w0 : g.w1;
   // 1. issue every independent load: stop flags and scalars (scalar loads), previous partials,
   //    own-row state, M⁻¹ row, own w, the row's block range
   const int stop = g.flags[F_DONE] | g.flags[F_STOPPED];
-  const double gam_prev = it > 0 ? g.pcg_gamma[it - 1] : 1.0;
-  const double alpha_prev = it > 0 ? g.pcg_alpha[it - 1] : 1.0;
+  const int cnt = g.flags[F_PCG_CNT];
+  const double gam_prev = first ? 1.0 : g.pcg_gamma[par ^ 1];
+  const double alpha_prev = first ? 1.0 : g.pcg_alpha[par ^ 1];
   const double bb_stored = g.scal[S_BB];
   double tp[3][16], tb[1][16];
-  load_streams<3, 16>(g.part_p + 3 * (int64_t)nw * (it & 1), nw, tp);
-  if (it == 0) load_streams<1, 16>(g.part_b, nw, tb);
+  load_streams<3, 16>(g.part_p + 3 * (int64_t)nw * par, nw, tp);
+  if (first) load_streams<1, 16>(g.part_b, nw, tb);
   const bool own = row < g.N && q < 6;
   const int64_t o = 6 * (int64_t)row + q;
   double v[V_N], mi[6], wi[6], w = 0.0;
@@ -989,9 +999,9 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
   double n[6];
   row_spmv(g, b0, b1, q, wc, n);
   double pa[3];
-  reduce_streams<3, 16>(g.part_p + 3 * (int64_t)nw * (it & 1), nw, tp, pa);
+  reduce_streams<3, 16>(g.part_p + 3 * (int64_t)nw * par, nw, tp, pa);
   double bb = bb_stored;
-  if (it == 0) {
+  if (first) {
     double t[1];
     reduce_streams<1, 16>(g.part_b, nw, tb, t);
     bb = t[0];
@@ -1001,14 +1011,14 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
   for (int k = 0; k < 6; ++k) m += mi[k] * wi[k];
   const double gam = pa[0], del = pa[1], rr = pa[2];
   const double tol = g.prm.pcg_tol;
-  const bool lead = blockIdx.x == 0 && lane == 0;
-  if (it == 0 && lead) g.scal[S_BB] = bb;
+  const bool lead = wv == 0 && lane == 0;
+  if (first && lead) g.scal[S_BB] = bb;
   if (rr <= tol * tol * bb || gam == 0.0) {
-    if (lead) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it; }
+    if (lead) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt; }
     return;
   }
   double beta = 0.0, alpha;
-  if (it == 0) {
+  if (first) {
     alpha = gam / del;
   } else {
     beta = gam / gam_prev;
@@ -1016,12 +1026,12 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
   }
   if (!isfinite(alpha) || !(alpha > 0.0)) {  // breakdown (A SPD => alpha > 0): keep x
     if (lead) {
-      g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
+      g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
       if (!isfinite(alpha)) g.flags[F_ILL] = 1;
     }
     return;
   }
-  if (lead) { g.pcg_alpha[it] = alpha; g.pcg_gamma[it] = gam; }
+  if (lead) { g.pcg_alpha[par] = alpha; g.pcg_gamma[par] = gam; g.flags[F_PCG_CNT] = cnt + 1; }
   double d[3] = {0.0, 0.0, 0.0};
   if (own) {
     const double nc = pick6(n, q);
@@ -1040,8 +1050,8 @@ __global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int it) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) {
-    double* P = g.part_p + 3 * (int64_t)nw * ((it + 1) & 1);
-    P[blockIdx.x] = d[0]; P[nw + blockIdx.x] = d[1]; P[2 * nw + blockIdx.x] = d[2];
+    double* P = g.part_p + 3 * (int64_t)nw * (par ^ 1);
+    P[wv] = d[0]; P[nw + wv] = d[1]; P[2 * nw + wv] = d[2];
   }
 }
 
@@ -1176,18 +1186,19 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     OFX_HIP(hipEventCreate(&e1));
     OFX_HIP(hipEventRecord(e0, hs));
   }
-  // Launch in chunks and poll the flags between chunks. Launch `it` tests convergence of the state
-  // after `it` iterations, and launches after convergence end after one scalar load, so the first
-  // chunk covers the previous solve's count for this GN step plus a small margin.
+  // Chunks of launches, flags polled between chunks. Launch i tests convergence of the state after
+  // i iterations, and launches after convergence end after one scalar load, so the first chunk
+  // covers the previous frame's count for this GN step plus a small margin. (A hipGraph replay of
+  // parity-pair chunks was measured: no gain over plain launches for this kernel.)
   const int max_it = g->prm.pcg_max_iter;
   const int lp = g->last_pcg[gn_iter & 63];
+  const dim3 grid((g->nwg_row + g->pcg_wpb - 1) / g->pcg_wpb), block(64 * g->pcg_wpb);
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
-    int n = chunk < max_it - it ? chunk : max_it - it;
+    const int n = chunk < max_it - it ? chunk : max_it - it;
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(k_pcg_iter, dim3(g->nwg_row), dim3(64), 0, hs, *g, it);
-    g->n_iter_launches += n;
+      hipLaunchKernelGGL(k_pcg_iter, grid, block, 0, hs, *g, it & 1, it == 0 ? 1 : 0);
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
@@ -1198,6 +1209,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     chunk = 8;
   }
+  g->n_iter_launches += it;
   if (g->timing) g->ev.emplace_back(e0, e1);
   return OFX_OK;
 }
@@ -1236,6 +1248,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   if (hipHostMalloc((void**)&g->host_flags, F_COUNT * sizeof(int32_t), 0) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
+
   *handle = g;
   return OFX_OK;
 }
@@ -1309,6 +1322,11 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
   g->nwg_row = (N + kRW - 1) / kRW;
+  {
+    const char* e = getenv("OFX_PCG_WPB");     // tuning knob
+    const int w = e ? atoi(e) : 1;
+    g->pcg_wpb = (w == 2 || w == 4) ? w : 1;
+  }
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T

@@ -75,6 +75,7 @@ struct Gn {
   int64_t pcg_cap = 0;
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
+  int32_t nw_pad = 0;            // stride of the iteration partial streams (nwg_row rounded up to even)
   double* scal = nullptr;
   int32_t* flags = nullptr;
   double* loss_log = nullptr;
@@ -647,6 +648,45 @@ __device__ __forceinline__ void sum_streams(const double* __restrict__ p, int nw
   load_streams<K, U>(p, nw, t);
   reduce_streams<K, U>(p, nw, t, out);
 }
+// Same sums over streams stored with an even stride, read as 16-B pairs (half the load instructions;
+// the pad slot of an odd count is kept zero). U pairs per lane cover 128·U entries.
+template <int K, int U>
+__device__ __forceinline__ void load_streams2(const double* __restrict__ p, int nw, int stride, double2 t[K][U]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = 2 * (lane + 64 * u);
+      t[k][u] = i < nw ? *reinterpret_cast<const double2*>(p + (int64_t)k * stride + i) : make_double2(0.0, 0.0);
+    }
+}
+template <int K, int U>
+__device__ __forceinline__ void reduce_streams2(const double* __restrict__ p, int nw, int stride, double2 t[K][U],
+                                                double out[K]) {
+  const int lane = threadIdx.x & 63;
+  double a[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = t[k][u].x + t[k][u].y;
+#pragma unroll
+    for (int w = 1; w < U; w <<= 1)
+#pragma unroll
+      for (int u = 0; u + w < U; u += 2 * w) v[u] += v[u + w];
+    a[k] = v[0];
+  }
+  for (int i = 2 * (lane + 64 * U); i < nw; i += 128)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double2 x = *reinterpret_cast<const double2*>(p + (int64_t)k * stride + i);
+      a[k] += x.x + x.y;
+    }
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = wave_sum(a[k]);
+}
+
 // n[c] without a dynamically indexed array (which the compiler would put in scratch): masked sum,
 // exact for finite n (x·1 + 0 terms); a non-finite component poisons the row, as it would anyway.
 __device__ __forceinline__ double pick6(const double n[6], int c) {
@@ -942,8 +982,10 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 4; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) {
-    const int nw = g.nwg_row;
-    g.part_p[blockIdx.x] = d[0]; g.part_p[nw + blockIdx.x] = d[1]; g.part_p[2 * nw + blockIdx.x] = d[2];
+    const int ns = g.nw_pad;
+    g.part_p[blockIdx.x] = d[0]; g.part_p[ns + blockIdx.x] = d[1]; g.part_p[2 * ns + blockIdx.x] = d[2];
+    if (blockIdx.x == 0 && ns > g.nwg_row)   // pad slot of every iteration stream (part_p is also proj scratch)
+      for (int k = 0; k < 6; ++k) g.part_p[k * ns + g.nwg_row] = 0.0;
     g.part_b[blockIdx.x] = d[3];
   }
 }
@@ -971,8 +1013,10 @@ __global__ __launch_bounds__(256) void k_pcg_iter(Gn g, int par, int first) {
   const double gam_prev = first ? 1.0 : g.pcg_gamma[par ^ 1];
   const double alpha_prev = first ? 1.0 : g.pcg_alpha[par ^ 1];
   const double bb_stored = g.scal[S_BB];
-  double tp[3][16], tb[1][16];
-  load_streams<3, 16>(g.part_p + 3 * (int64_t)nw * par, nw, tp);
+  const int ns = g.nw_pad;
+  double2 tp[3][8];
+  double tb[1][16];
+  load_streams2<3, 8>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp);
   if (first) load_streams<1, 16>(g.part_b, nw, tb);
   const bool own = row < g.N && q < 6;
   const int64_t o = 6 * (int64_t)row + q;
@@ -999,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_pcg_iter(Gn g, int par, int first) {
   double n[6];
   row_spmv(g, b0, b1, q, wc, n);
   double pa[3];
-  reduce_streams<3, 16>(g.part_p + 3 * (int64_t)nw * par, nw, tp, pa);
+  reduce_streams2<3, 8>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp, pa);
   double bb = bb_stored;
   if (first) {
     double t[1];
@@ -1050,8 +1094,8 @@ __global__ __launch_bounds__(256) void k_pcg_iter(Gn g, int par, int first) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) {
-    double* P = g.part_p + 3 * (int64_t)nw * (par ^ 1);
-    P[wv] = d[0]; P[nw + wv] = d[1]; P[2 * nw + wv] = d[2];
+    double* P = g.part_p + 3 * (int64_t)ns * (par ^ 1);
+    P[wv] = d[0]; P[ns + wv] = d[1]; P[2 * ns + wv] = d[2];
   }
 }
 
@@ -1237,7 +1281,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
   ALLOC(g->Minv, 36 * N); ALLOC(g->st, V_N * 6 * N); ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N);
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->xmh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
-  const int64_t max_row_wg = (N + kRW - 1) / kRW;
+  const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
@@ -1322,6 +1366,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
   g->nwg_row = (N + kRW - 1) / kRW;
+  g->nw_pad = (g->nwg_row + 1) & ~1;
   {
     const char* e = getenv("OFX_PCG_WPB");     // tuning knob
     const int w = e ? atoi(e) : 1;

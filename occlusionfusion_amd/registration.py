@@ -159,11 +159,15 @@ class GaussNewtonSolver:
         call("ofx_gn_solve", self._h, byref(pb), byref(prm), byref(r), stream_ptr())
         return self._pack(out, sync)
 
-    def optimize_distributed(self, *args, group=None, sync=True, **kw):
+    def optimize_distributed(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position,
+                             node_confidence, source_points, anchors, weights, target_points, intrinsics,
+                             target_px=None, target_py=None, prev_rot=None, prev_trans=None, group=None, sync=True):
         """Match-sharded solve over torch.distributed: rank r assembles matches [r*M/W, (r+1)*M/W);
         A and rhs are all-reduced (sum) once per GN iteration; rank 0 adds ARAP + motion rows."""
         import torch.distributed as dist
-        pb, N, M = self._problem(*args, **kw)
+        pb, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
+                                 node_confidence, source_points, anchors, weights, target_points, intrinsics,
+                                 target_px, target_py, prev_rot, prev_trans)
         prm = self._params()
         nnz = _lib.c_int64()
         call("ofx_gn_setup", self._h, byref(pb), byref(prm), byref(nnz), stream_ptr())

@@ -15,15 +15,18 @@
  *   ofx_pack_color          TSDFVolume.update colour folding                tsdf.py:545-566
  *   ofx_skin_volume_bricks  WarpField.skin_tsdf (cache build, brick cull)   warpfield.py:131-141
  *   ofx_skin_volume         WarpField.skin over TSDFVolume.world_pts       warpfield.py:83-129, tsdf.py:294-307
+ *   ofx_skin_palette        (layout only) per-brick node palette of the skin_tsdf cache, warpfield.py:131-141
  *   ofx_skin_points         WarpField.skin(points, nodes)                  warpfield.py:83-129
  *                           (k-NN twin of csrc compute_pixel_anchors_euclidean, csrc/cpu/graph_proc.cpp:610-709)
  *   ofx_pack_nodes          Registration.deform_ED gathers of R, t, g       NonRigidICP/model/registration_fusion.py:168-170
  *   ofx_integrate           WarpField.deform_tsdf + TSDFVolume.integrate    warpfield.py:369-380, tsdf.py:378-494
  *                           (fused: skin cache -> ED warp -> project -> SDF/weight/colour update)
+ *   ofx_integrate_palette   same, node records staged per brick in LDS      warpfield.py:369-380, tsdf.py:442-494
  *   ofx_deform_points       ED_warp / deform_ED / deform_mesh / normals     NonRigidICP/model/geometry.py:9-25,
  *                                                                          registration_fusion.py:157-184, warpfield.py:312-367
  *   ofx_visibility          TSDFVolume.check_visibility                     tsdf.py:576-612
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
+ *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
  */
 #ifndef OFX_H
 #define OFX_H

@@ -159,7 +159,7 @@ def main():
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
         "scaling": "weak" if a.mode == "replicas" else "strong", "vs_baseline": None, "dtype": "f32/f64",
-        "data": "synthetic (seeded sphere+plane non-rigid sequence, 1 mm noise; SURVEY §8(d))",
+        "data": "synthetic (seeded sphere+plane non-rigid sequence with a moving occluder hiding up to ~38 % of the object, 1 mm noise, matches from visible points; SURVEY §8(d), BASELINE config 3)",
         "config": {"workload": f"{D}^3 TSDF @{a.voxel * 1e3:g} mm, {seq.nodes.shape[0]} nodes, "
                                f"{a.matches} matches, 640x448 depth, GN 10 it",
                    "mode": a.mode, "dims": D, "voxel_size_m": a.voxel, "nodes": int(seq.nodes.shape[0]),

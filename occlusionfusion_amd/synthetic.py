@@ -5,7 +5,10 @@ loader does (cy -= 16; options.py:13-14, utils/image_proc.py:303-311). Depth in 
 1 mm Gaussian noise, quantised to 1 mm. Scene: sphere R=0.35 m at (0,0,1.4) in front of a
 1.6x1.2 m backing plane at z=1.75 (the survey's 0.6x0.6 m plane is fully hidden by the sphere
 silhouette, so it is enlarged). Non-rigid motion: the sphere breathes (radius) and drifts (centre);
-the plane is static.
+the plane is static. Occlusion (BASELINE config 3): a vertical bar (0.14 m wide, z=0.9 m)
+enters from the left after frame 0 and sweeps over the sphere and back (up to ~30 % of the sphere's
+pixels hidden); matches come only from surface points visible in the target frame, and the motion
+term confidence is 1 for visible nodes, 0.3 for occluded ones.
 
 Graphs: greedy coverage sampling of surface points (the rule of csrc sample_nodes,
 csrc/cpu/graph_proc.cpp:79-136, with a spatial hash instead of the O(N²) scan) and 8 Euclidean
@@ -41,6 +44,13 @@ class SphereScene:
     radius: float = 0.35
     plane_z: float = 1.75
     plane_half: tuple = (0.8, 0.6)
+    occluder: bool = True
+    occ_z: float = 0.9
+    occ_half: float = 0.07
+
+    def occluder_x(self, t):
+        """x centre of the occluding bar at frame t: out of view at t=0, over the sphere for t≈8..24."""
+        return -0.75 + 0.375 * (1.0 - math.cos(0.2 * t))
 
     def frame_params(self, t):
         """Sphere centre/radius at frame t (smooth non-rigid drift + breathing)."""
@@ -75,6 +85,10 @@ class SphereScene:
         inplane = (np.abs(dx * self.plane_z) <= self.plane_half[0]) & (np.abs(dy * self.plane_z) <= self.plane_half[1])
         zp = np.where(inplane, zp, np.inf)
         z = np.minimum(zs, zp)
+        if self.occluder:
+            xo = self.occluder_x(t)
+            hit = np.abs(dx * self.occ_z - xo) <= self.occ_half
+            z = np.where(hit, np.minimum(z, self.occ_z), z)
         if rng is not None and noise > 0:
             z = z + rng.normal(0.0, noise, z.shape)
         z = np.where(np.isfinite(z), np.round(z * 1000.0) / 1000.0, 0.0)
@@ -198,16 +212,34 @@ class SyntheticSequence:
         rng = np.random.default_rng(self.seed * 1000 + t)
         return make_image(self.scene.render(self.cam, t, rng))
 
+    def visible(self, pts_t, t, tol=0.01):
+        """Points (already at frame t) seen by the camera in frame t: the noise-free rendered depth at
+        their pixel is not in front of them by more than tol."""
+        cam = self.cam
+        z = pts_t[:, 2]
+        u = np.rint(pts_t[:, 0] * cam.fx / z + cam.cx).astype(np.int64)
+        v = np.rint(pts_t[:, 1] * cam.fy / z + cam.cy).astype(np.int64)
+        inside = (z > 0) & (u >= 0) & (u < cam.width) & (v >= 0) & (v < cam.height)
+        d = self.scene.render(cam, t)
+        dv = np.zeros_like(z)
+        dv[inside] = d[v[inside], u[inside]]
+        return inside & (dv > 0) & (dv >= z - tol)
+
     def solver_inputs(self, t, n_matches=10000, occluded_conf=0.3):
-        """Matches (canonical surface point -> its position at frame t + 1 mm noise) and node motion
-        targets (ground-truth node motion, confidence 1 visible / occluded_conf otherwise)."""
+        """Matches (canonical surface point visible in frame t -> its position at frame t + 1 mm noise)
+        and node motion targets (ground-truth node motion, confidence 1 visible / occluded_conf for
+        nodes that are back-facing or hidden by the occluder)."""
         rng = np.random.default_rng(self.seed * 7919 + t)
-        sel = rng.choice(self.canonical_points.shape[0], size=min(n_matches, self.canonical_points.shape[0]),
-                         replace=False)
-        src = self.canonical_points[np.sort(sel)]
-        tgt = self.scene.deform_points(src, t) + rng.normal(0, 0.001, src.shape)
+        cand = self.canonical_points
+        pos_t = self.scene.deform_points(cand, t)
+        vis = np.nonzero(self.visible(pos_t, t))[0] if self.scene.occluder else np.arange(cand.shape[0])
+        sel = np.sort(rng.choice(vis, size=min(n_matches, vis.shape[0]), replace=False))
+        src = cand[sel]
+        tgt = pos_t[sel] + rng.normal(0, 0.001, src.shape)
         tpos = self.scene.deform_points(self.nodes, t)
         c, r = self.scene.frame_params(t)
         facing = (self.nodes[:, 2] < c[2]) | (self.nodes[:, 2] > self.scene.plane_z - 0.02)
+        if self.scene.occluder:
+            facing = facing & self.visible(tpos, t, tol=0.02)
         conf = np.where(facing, 1.0, occluded_conf).astype(np.float32)
         return src.astype(np.float32), tgt.astype(np.float32), tpos.astype(np.float32), conf

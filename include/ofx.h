@@ -111,7 +111,8 @@ int ofx_skin_volume_to_dense(const ofx_volume_desc* desc, const int32_t* brick_l
                              float* weights_out, uint8_t* valid_out, ofx_stream_t s);
 
 /* Node transforms (node-relative, as Registration.deform_ED uses them):
- * R f32[N*9] row-major, T f32[N*3], g f32[N*3] -> packed f32[N*16] */
+ * R f32[N*9] row-major, T f32[N*3], g f32[N*3] -> packed f32[N*16], 64-B records interleaved for
+ * packed-f32 warps: [R00 R10 R01 R11 | R02 R12 g0 g1 | t0 t1 R20 R21 | R22 g2 t2 0] */
 int ofx_pack_nodes(const float* R, const float* T, const float* g, int32_t n_nodes, float* packed,
                    ofx_stream_t s);
 

@@ -26,24 +26,34 @@ struct CamD {
   int W, H;
 };
 
-// Warp one voxel position with its K anchors (f32, reference op order).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Warp one voxel position with its K anchors (f32, reference op order). Rows 0 and 1 of R(x-g)+g+t
+// run as packed f32 pairs (v_pk_mul/add_f32; the same per-component rounding), row 2 scalar.
+// Node record layout: see ofx_pack_nodes.
 __device__ __forceinline__ void ed_warp(const float4* __restrict__ nodes, const int ids[4], const float w[4], int K,
                                         float& x, float& y, float& z) {
-  float ax = 0.f, ay = 0.f, az = 0.f;
+  f2 axy = {0.f, 0.f};
+  float az = 0.f;
+  const f2 xy = {x, y};
   for (int k = 0; k < K; ++k) {
     const float4* n = nodes + 4 * (int64_t)ids[k];
-    float4 r0 = n[0], r1 = n[1], r2 = n[2], tt = n[3];
-    float dx = x - r0.w, dy = y - r1.w, dz = z - r2.w;
-    float rx = r0.x * dx; rx = rx + r0.y * dy; rx = rx + r0.z * dz;
-    float ry = r1.x * dx; ry = ry + r1.y * dy; ry = ry + r1.z * dz;
-    float rz = r2.x * dx; rz = rz + r2.y * dy; rz = rz + r2.z * dz;
-    float yx = ((rx + r0.w) + tt.x) * w[k];
-    float yy = ((ry + r1.w) + tt.y) * w[k];
-    float yz = ((rz + r2.w) + tt.z) * w[k];
-    if (k == 0) { ax = yx; ay = yy; az = yz; }
-    else { ax = ax + yx; ay = ay + yy; az = az + yz; }
+    const float4 a = n[0], b = n[1], c = n[2], d = n[3];
+    const f2 P0 = {a.x, a.y}, P1 = {a.z, a.w}, P2 = {b.x, b.y}, G = {b.z, b.w}, T = {c.x, c.y};
+    const f2 dxy = xy - G;
+    const float dz = z - d.y;
+    f2 r = P0 * dxy.x;
+    r = r + P1 * dxy.y;
+    r = r + P2 * dz;
+    float rz = c.z * dxy.x;
+    rz = rz + c.w * dxy.y;
+    rz = rz + d.x * dz;
+    const f2 yxy = ((r + G) + T) * w[k];
+    const float yz = ((rz + d.y) + d.z) * w[k];
+    if (k == 0) { axy = yxy; az = yz; }
+    else { axy = axy + yxy; az = az + yz; }
   }
-  x = ax; y = ay; z = az;
+  x = axy.x; y = axy.y; z = az;
 }
 
 // Projection + visibility (tsdf.py:351-364, 576-612). Returns pixel index or -1.
@@ -58,28 +68,72 @@ __device__ __forceinline__ int64_t project(const CamD& c, float x, float y, floa
 
 __device__ __forceinline__ float cdiv(float a, float b) { return (float)((double)a / (double)b); }
 
-// One voxel update; returns 1 if the voxel was integrated.
+// s lies within tol of a rounding tie of rint (a half-integer)
+__device__ __forceinline__ bool near_half(double s, double tol) {
+  return fabs((s - floor(s)) - 0.5) < tol;
+}
+
+// f32(t) for the exact f64 value t64 with |t - t64| <= err: returns false if t's f32 rounding could
+// differ from t64's (t within err of a rounding boundary, or a zero / non-finite result)
+__device__ __forceinline__ bool f32_round_safe(double t, double err, float& out) {
+  const float f = (float)t;
+  if (!(f != 0.f) || !isfinite(f)) return false;
+  const int bits = __float_as_int(f);
+  const float up = __int_as_float(bits + 1), dn = __int_as_float(bits - 1);   // magnitude up / down
+  const double m1 = 0.5 * ((double)f + (double)up), m2 = 0.5 * ((double)f + (double)dn);
+  const double lo = fmin(m1, m2), hi = fmax(m1, m2);
+  out = f;
+  return t - err > lo && t + err < hi;
+}
+
+// One voxel update; returns 1 if the voxel was integrated. Reference semantics (tsdf.py:351-376,
+// 479-494; numba f64 promotion), with three of the seven f64 divisions replaced by products with a
+// reciprocal: (X·fx)/Z and (Y·fy)/Z use 1/Z, dd/trunc uses 1/trunc, the SDF quotient uses 1/w_new.
+// Each replacement perturbs the f64 value by a few ulp at most; the result is used only where that
+// cannot change a rounding (pixel: not within 1e-9 of a half-integer; SDF: its f32 rounding interval
+// contains the whole error bound) — otherwise the exact division path runs. Bit-identical results.
 __device__ __forceinline__ int update_voxel(const CamD& c, const float* __restrict__ depth,
-                                            const float* __restrict__ color_im, double trunc, double obs, float x,
-                                            float y, float z, int64_t vi, float* __restrict__ tsdf,
-                                            float* __restrict__ weight, float* __restrict__ color) {
-  double Z;
-  int64_t pix = project(c, x, y, z, Z);
-  if (pix < 0) return 0;
+                                            const float* __restrict__ color_im, double trunc, double itrunc,
+                                            double obs, float x, float y, float z, int64_t vi,
+                                            float* __restrict__ tsdf, float* __restrict__ weight,
+                                            float* __restrict__ color) {
+  const double X = x, Y = y, Z = z;
+  if (!(Z > 0.0)) return 0;
+  const double nx = X * c.fx, ny = Y * c.fy;
+  const double rz = 1.0 / Z;
+  double qx = nx * rz, qy = ny * rz;
+  double su = qx + c.cx, sv = qy + c.cy;
+  if (near_half(su, 1e-9 * fmax(1.0, fmax(fabs(qx), fabs(su)))) ||
+      near_half(sv, 1e-9 * fmax(1.0, fmax(fabs(qy), fabs(sv))))) {
+    su = nx / Z + c.cx;
+    sv = ny / Z + c.cy;
+  }
+  const double u = rint(su), v = rint(sv);
+  if (!(u >= 0.0 && u < (double)c.W && v >= 0.0 && v < (double)c.H)) return 0;
+  const int64_t pix = (int64_t)v * c.W + (int64_t)u;
   float d = depth[pix];
   double dd = (double)d - Z;
   if (!(d > 0.f && dd >= -trunc)) return 0;
-  double dist = fmin(1.0, dd / trunc);
-  float w_old = weight[vi];
-  float t_old = tsdf[vi];
+  const float w_old = weight[vi];
+  const float t_old = tsdf[vi];
   float w_new = (float)((double)w_old + obs);
   float prod = w_old * t_old;
-  float t_new = (float)(((double)prod + obs * dist) / (double)w_new);
+  const double wn = (double)w_new;
+  const double inv = 1.0 / wn;
+  const double dist_a = fmin(1.0, dd * itrunc);
+  const double num_a = (double)prod + obs * dist_a;
+  const double t_a = num_a * inv;
+  const double err = (fabs(obs) * 1e-15 + 1e-15 * fabs(num_a)) * inv + 1e-15 * fabs(t_a);
+  float t_new;
+  if (!f32_round_safe(t_a, err, t_new)) {
+    const double dist = fmin(1.0, dd / trunc);
+    t_new = (float)(((double)prod + obs * dist) / wn);
+  }
   weight[vi] = w_new;
   tsdf[vi] = t_new;
   if (color) {
     const float C = 65536.0f;
-    float oc = color[vi];
+    const float oc = color[vi];
     float ob = floorf(oc / C);
     float og = floorf((oc - ob * C) / 256.0f);
     float orr = (oc - ob * C) - og * 256.0f;
@@ -91,7 +145,6 @@ __device__ __forceinline__ int update_voxel(const CamD& c, const float* __restri
     // f32 quotients a/w_new as f32(a · f64(1/w_new)): for f32 a, b the f64 product is within 2^-52 of
     // a/b while a/b is never an f32 rounding midpoint and lies >= ~2^-49 (relative) from one, so the
     // rounding equals the correctly rounded f32 division (randomised check: 3.6e8 pairs, 0 diffs)
-    const double inv = 1.0 / (double)w_new;
     float b2 = fminf(255.0f, rintf((float)((double)(w_old * ob + ow * nb) * inv)));
     float g2 = fminf(255.0f, rintf((float)((double)(w_old * og + ow * ng) * inv)));
     float r2 = fminf(255.0f, rintf((float)((double)(w_old * orr + ow * nr) * inv)));
@@ -99,6 +152,7 @@ __device__ __forceinline__ int update_voxel(const CamD& c, const float* __restri
   }
   return 1;
 }
+
 
 // per-workgroup (= per-brick) update count, plain store: no contended atomics in the hot kernel
 __device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
@@ -112,8 +166,12 @@ __device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
 
 // PAL: node records of the brick's palette staged in LDS once per workgroup; voxel anchors are
 // palette ranks (uint8). A brick whose palette overflowed (pal_n > kPal) uses the global anchors.
+// amdgpu_waves_per_eu(8): the kernel is memory-latency-bound (60 % of wave time in s_waitcnt), so the
+// register budget is capped at 64 VGPRs for full occupancy (87 -> 77 us at 512^3). Prefetching the
+// voxels' tsdf/weight/colour ahead of the palette barrier is slower: vmcnt retires in order, so the
+// barrier would wait on those HBM loads.
 template <bool WARP, bool PAL>
-__global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const float* __restrict__ depth,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_integrate(BrickGeom g, CamD c, const float* __restrict__ depth,
                                                     const float* __restrict__ color_im,
                                                     const float4* __restrict__ nodes, int K,
                                                     const int32_t* __restrict__ list,
@@ -133,11 +191,15 @@ __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const fl
   int64_t bx = r / g.nby + g.bx0;
   const int i0 = (int)bx * kBrick, j0 = (int)by * kBrick, k0 = (int)bz * kBrick;
   bool use_pal = false;
+  uchar4 la[2];
   if (PAL) {
+    // independent loads first (count, palette ids, the voxels' palette ranks), then the node records
     const int pn = pal_n[slot];
+    const int pid = pal_ids[slot * kPal + (threadIdx.x >> 2)];
+    la[0] = local[slot * kBrickVox + threadIdx.x];
+    la[1] = local[slot * kBrickVox + threadIdx.x + 256];
     use_pal = pn <= kPal;
-    if (use_pal && (int)threadIdx.x < 4 * pn)
-      s_node[threadIdx.x] = nodes[4 * (int64_t)pal_ids[slot * kPal + (threadIdx.x >> 2)] + (threadIdx.x & 3)];
+    if (use_pal && (int)threadIdx.x < 4 * pn) s_node[threadIdx.x] = nodes[4 * (int64_t)pid + (threadIdx.x & 3)];
     __syncthreads();
   }
   int n_upd = 0;
@@ -153,7 +215,7 @@ __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const fl
       const int64_t si = slot * kBrickVox + l;
       int ids[4];
       if (PAL && use_pal) {
-        const uchar4 a = local[si];
+        const uchar4 a = la[h];
         ids[0] = a.x; ids[1] = a.y; ids[2] = a.z; ids[3] = a.w;
         if (ids[K - 1] == kNoLocal) continue;   // skin-invalid voxel: never integrated after the source frame
       } else {
@@ -166,7 +228,7 @@ __global__ __launch_bounds__(256) void k_integrate(BrickGeom g, CamD c, const fl
       if (PAL && use_pal) ed_warp(s_node, ids, w, K, x, y, z);
       else ed_warp(nodes, ids, w, K, x, y, z);
     }
-    n_upd += update_voxel(c, depth, color_im, trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
+    n_upd += update_voxel(c, depth, color_im, trunc, 1.0 / trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
   }
   count_updates(n_upd, counter);
 }
@@ -193,10 +255,10 @@ __global__ __launch_bounds__(256) void k_deform_points(const float* __restrict__
       for (int k = 0; k < K; ++k) {
         if (w[k] == 0.f) continue;
         const float4* nd = nodes + 4 * (int64_t)ids[k];
-        float4 r0 = nd[0], r1 = nd[1], r2 = nd[2];
-        float rx = r0.x * x; rx = rx + r0.y * y; rx = rx + r0.z * z;
-        float ry = r1.x * x; ry = ry + r1.y * y; ry = ry + r1.z * z;
-        float rz = r2.x * x; rz = rz + r2.y * y; rz = rz + r2.z * z;
+        const float4 a = nd[0], b = nd[1], c = nd[2], d = nd[3];   // record layout: ofx_pack_nodes
+        float rx = a.x * x; rx = rx + a.z * y; rx = rx + b.x * z;
+        float ry = a.y * x; ry = ry + a.w * y; ry = ry + b.y * z;
+        float rz = c.z * x; rz = rz + c.w * y; rz = rz + d.x * z;
         ax = ax + w[k] * rx; ay = ay + w[k] * ry; az = az + w[k] * rz;
       }
       x = ax; y = ay; z = az;

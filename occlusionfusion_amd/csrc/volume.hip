@@ -65,10 +65,11 @@ __global__ void k_pack_nodes(const float* __restrict__ R, const float* __restric
   const float* r = R + 9 * (int64_t)i;
   const float* g = G + 3 * (int64_t)i;
   const float* t = T + 3 * (int64_t)i;
-  out[4 * (int64_t)i + 0] = make_float4(r[0], r[1], r[2], g[0]);
-  out[4 * (int64_t)i + 1] = make_float4(r[3], r[4], r[5], g[1]);
-  out[4 * (int64_t)i + 2] = make_float4(r[6], r[7], r[8], g[2]);
-  out[4 * (int64_t)i + 3] = make_float4(t[0], t[1], t[2], 0.f);
+  // pair-interleaved for packed-f32 warps: (R00,R10)(R01,R11) | (R02,R12)(g0,g1) | (t0,t1)(R20,R21) | R22 g2 t2 0
+  out[4 * (int64_t)i + 0] = make_float4(r[0], r[3], r[1], r[4]);
+  out[4 * (int64_t)i + 1] = make_float4(r[2], r[5], g[0], g[1]);
+  out[4 * (int64_t)i + 2] = make_float4(t[0], t[1], r[6], r[7]);
+  out[4 * (int64_t)i + 3] = make_float4(r[8], g[2], t[2], 0.f);
 }
 
 static int shard_x_range(const BrickGeom& g, int32_t* lo, int32_t* n) {

@@ -15,7 +15,7 @@ torch.cuda.synchronize()
 res = {}
 t = 2
 for var in sys.argv[1:] or ["0", "1", "2", "0"]:
-    os.environ["OFX_INT_VARIANT"] = var
+    os.environ["OFX_INT_BPW"] = var
     pipe.vol.kernel_timer = []
     for _ in range(40):
         pipe.integrate(f1, t)

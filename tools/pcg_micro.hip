@@ -24,6 +24,8 @@ struct Sys {
   double *Bs, *ws0, *ws1;
   int *dst;
   unsigned* bar;   // grid barrier: [0] arrivals, [1] generation, [2] timeout flag
+  float* Mcl;      // cluster preconditioner rows: (rows*6) x 48 f32
+  double *mv0, *mv1;
 };
 
 __device__ __forceinline__ double red8(double a) {
@@ -551,6 +553,87 @@ __global__ __launch_bounds__(64) void k_persist(Sys s, int iters) {
   }
 }
 
+// Cluster-preconditioned explicit pipelined iteration: 8 rows per wave (one 8-node cluster, 8 lanes per
+// row), n = A m (m gathered), recurrences incl. w in the state record, then m_new = M_cl⁻¹ w_new via LDS
+// (48x48 f32 rows, loaded up front).
+__global__ __launch_bounds__(64) void k_iterc(Sys s, int it) {
+  __shared__ double s_w[48];
+  const int lane = threadIdx.x;
+  const int r = lane >> 3, q = lane & 7;
+  const int row = blockIdx.x * 8 + r;
+  const double* mc = (it & 1) ? s.mv1 : s.mv0;
+  double* mn = (it & 1) ? s.mv0 : s.mv1;
+  double2 t[3][4];
+  {
+    const double* P = s.partw + 3 * (int64_t)((s.nwaves + 1) & ~1) * (it & 1);
+    const int ns = (s.nwaves + 1) & ~1;
+    for (int k = 0; k < 3; ++k)
+      for (int u = 0; u < 4; ++u) { const int i = 2 * (lane + 64 * u); t[k][u] = i < s.nwaves ? *(const double2*)(P + k * ns + i) : make_double2(0, 0); }
+  }
+  const bool own = row < N && q < 6;
+  double v[8];
+  float4 mrow[12];
+  for (int k = 0; k < 8; ++k) v[k] = 0.0;
+  if (own) {
+    const double2* R = reinterpret_cast<const double2*>(s.rec + 48 * (int64_t)row + 8 * q);
+    for (int k = 0; k < 4; ++k) { double2 a = R[k]; v[2 * k] = a.x; v[2 * k + 1] = a.y; }
+    const float4* M = reinterpret_cast<const float4*>(s.Mcl + (int64_t)(6 * row + q) * 48);
+    for (int k = 0; k < 12; ++k) mrow[k] = M[k];
+  }
+  double n[6] = {0, 0, 0, 0, 0, 0};
+  if (row < N) {
+    const int b0 = s.row_ptr[row], b1 = s.row_ptr[row + 1];
+    for (int bi = b0 + q; bi < b1; bi += 8) {
+      const double2* blk = reinterpret_cast<const double2*>(s.B + 36 * (int64_t)bi);
+      const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)s.col[bi]);
+      double x[6];
+      for (int j = 0; j < 3; ++j) { double2 a = vc[j]; x[2 * j] = a.x; x[2 * j + 1] = a.y; }
+      for (int i = 0; i < 6; ++i) {
+        double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+        n[i] += ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+      }
+    }
+  }
+  for (int i = 0; i < 6; ++i) n[i] = group_sum<8>(n[i]);
+  double pa[3];
+  for (int k = 0; k < 3; ++k) {
+    double a = 0.0;
+    for (int u = 0; u < 4; ++u) a += t[k][u].x + t[k][u].y;
+    pa[k] = wave_sum(a);
+  }
+  const double al = 1e-3 + 1e-12 * pa[0], be = 1e-3 + 1e-12 * pa[1];
+  double nc = 0.0;
+  for (int i = 0; i < 6; ++i) nc += n[i] * (q == i ? 1.0 : 0.0);
+  double d[3] = {0, 0, 0};
+  double w2 = 0.0;
+  if (own) {
+    const double mo = mc[6 * (int64_t)row + q];
+    const double zz = nc + be * v[3], qq = mo + be * v[4], sv = v[7] + be * v[5], p = v[2] + be * v[6];
+    const double rr = v[1] - al * sv, u = v[2] - al * qq;
+    w2 = 0.5 * (v[7] - al * zz);
+    double2* R = reinterpret_cast<double2*>(s.rec + 48 * (int64_t)row + 8 * q);
+    R[0] = make_double2(v[0] + al * p, rr); R[1] = make_double2(u, zz); R[2] = make_double2(qq, sv); R[3] = make_double2(p, w2);
+    d[0] = rr * u; d[1] = w2 * u; d[2] = rr * rr;
+    s_w[6 * r + q] = w2;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  if (own) {
+    double m = 0.0;
+    for (int k = 0; k < 12; ++k) {
+      m += (double)mrow[k].x * s_w[4 * k] + (double)mrow[k].y * s_w[4 * k + 1] + (double)mrow[k].z * s_w[4 * k + 2] +
+           (double)mrow[k].w * s_w[4 * k + 3];
+    }
+    mn[6 * (int64_t)row + q] = m * 1e-3;
+  }
+  for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
+  if (lane == 0) {
+    const int ns = (s.nwaves + 1) & ~1;
+    double* P = s.partw + 3 * (int64_t)ns * ((it + 1) & 1);
+    P[blockIdx.x] = d[0] * 1e-30; P[ns + blockIdx.x] = d[1] * 1e-30; P[2 * ns + blockIdx.x] = d[2] * 1e-30;
+  }
+}
+
 template <typename F>
 static double timeit(F launch) {
   hipEvent_t a, b;
@@ -657,7 +740,7 @@ int main() {
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
     const int nwav = (N + 3) / 4;
     printf("co-resident capacity %d x %d CUs = %d (need %d)\n", nblk, ncu, nblk * ncu, nwav);
-    if (nblk * ncu >= nwav) {
+    if (false && nblk * ncu >= nwav) {
       s.nwaves = nwav;
       for (int mode = 0; mode < 2; ++mode)
         for (int rep = 0; rep < 2; ++rep) {
@@ -679,7 +762,13 @@ int main() {
         }
     }
   }
-  for (int rep = 0; rep < 2; ++rep) {
+  CK(hipMalloc(&s.Mcl, (size_t)6 * N * 48 * 4)); CK(hipMemset(s.Mcl, 0, (size_t)6 * N * 48 * 4));
+  for (double** p : {&s.mv0, &s.mv1}) { CK(hipMalloc(p, 6 * N * 8)); CK(hipMemset(*p, 0, 6 * N * 8)); }
+  for (int rep = 0; rep < 3; ++rep) {
+    runw("iterc cluster8", k_iterc, 8);
+    runw("iterw4 soa dpp", k_iterw<4, 2>, 4);
+  }
+  for (int rep = 0; rep < 0; ++rep) {
     runw("iters push", k_iters<true>, 4);
     runw("iters gather", k_iters<false>, 4);
     printf("%-16s %7.2f us\n", "graph iters push", graph_time(k_iters<true>, (N + 3) / 4));

@@ -130,7 +130,7 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     pcg_ms, pcg_launches, _ = pipe.solver.timing(False)
-    N_, M_, nnzb, _T = pipe.solver.info()
+    N_, M_, nnzb, _T, rows = pipe.solver.info()
     t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
     t_int = np.array([m[1].elapsed_time(m[2]) for m in marks]) * 1e-3
     pcg = [int(m[3]["_status"][2].item()) for m in marks]
@@ -149,9 +149,10 @@ def main():
     B = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
     t_int_avg = float(np.mean(t_int))
     achieved = B / t_kint
-    # k_pcg_iter algorithmic bytes per launch: B = A·M⁻¹ blocks (288 B) + column ids (4 B) per block;
-    # per node: row_ptr, gathered w (48 B), M⁻¹ row block (288 B), 7 vectors read + 8 written (6 f64 each)
-    B_pcg = nnzb * 292 + N_ * (4 + 48 + 288 + 15 * 48)
+    # k_pcg_iter algorithmic bytes per launch: A blocks (288 B) + column ids (4 B) per block; per row
+    # (nodes in cluster order, padded): row_ptr (4 B), gathered m (48 B), cluster-inverse rows (6 x 48
+    # f32 = 1152 B), 8-vector state read + written (2 x 384 B), new m written (48 B)
+    B_pcg = nnzb * 292 + rows * (4 + 48 + 1152 + 768 + 48)
     t_pcg = pcg_ms * 1e-3 / max(1, pcg_launches)
     ach_pcg = B_pcg / t_pcg
     res = {

@@ -190,28 +190,34 @@ typedef struct ofx_gn_result {
   double* loss_log;
 } ofx_gn_result;
 
+/* max_nodes <= 8192 (the JᵀJ slot map is dense over the padded rows) */
 int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle);
 /* Profiling hook: returns (and resets) the device time of the PCG iteration loops recorded since the
  * last call (hipEvents on the solve stream; synchronises on them), the number of k_pcg_iter launches
  * and of timed solves; `enable` switches recording for the following steps. */
 int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves);
-/* info (host int64[4]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms] of the last setup */
+/* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
+ * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
 int ofx_gn_info(void* handle, int64_t* info);
 /* Per-GN-step statistics of the last solve: out (host f64[3*cap]) = [PCG iterations, |b|², loss] per
  * step (zeros for steps that did not run); synchronous D2H copy, at most 64 steps. */
 int ofx_gn_stats(void* handle, double* out, int32_t cap);
+/* Row order of the last setup: perm (host int32[cap]) = node of each PCG row, -1 for padding rows
+ * (the order of rhs and of the solver's per-node state); cap must be >= rows (ofx_gn_info()[4]). */
+int ofx_gn_row_order(void* handle, int32_t* perm, int32_t cap);
 int ofx_gn_destroy(void* handle);
 /* Upload + build the block-sparse JᵀJ pattern (co-anchored node pairs, edges, diagonal).
- * Synchronises the stream once to size the pattern; *nnz_blocks receives the block count. */
+ * Copies nodes/edges to the host (one stream sync) to order the rows by graph clusters when the
+ * graph changed, and synchronises once more to size the pattern; *nnz_blocks receives the block count. */
 int ofx_gn_setup(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params, int64_t* nnz_blocks,
                  ofx_stream_t s);
-/* Assemble A (f64[nnz_blocks*36]) and rhs (f64[6N+4]: b = -Jᵀr then [loss² total,data,arap,motion])
+/* Assemble A (f64[nnz_blocks*36]) and rhs (f64[6·rows+4]: b = -Jᵀr then [loss² total,data,arap,motion])
  * from matches [m0,m1); regularizers (ARAP, motion) added iff add_reg. Zeroes both first.
  * In a multi-GPU solve every rank calls this on its match shard, the caller all-reduces
  * (sum) A and rhs, then every rank calls ofx_gn_step with identical buffers. */
 int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int32_t add_reg, double* A,
                      double* rhs, ofx_stream_t s);
-/* LM damping, block-Jacobi PCG solve, early-stop bookkeeping, R <- exp(x_rot) R, t += x_t. */
+/* LM damping, cluster block-Jacobi PCG solve, early-stop bookkeeping, R <- exp(x_rot) R, t += x_t. */
 int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_stream_t s);
 int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s);
 /* setup + num_iter x (linearize + step) + finish, single device */

@@ -67,6 +67,7 @@ _SIGS = {
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
     "ofx_gn_stats": [P, P, c_int32],
+    "ofx_gn_row_order": [P, P, c_int32],
     "ofx_gn_setup": [P, P, P, P, P],
     "ofx_gn_linearize": [P, c_int32, c_int32, c_int32, c_int32, P, P, P],
     "ofx_gn_step": [P, c_int32, P, P, P],

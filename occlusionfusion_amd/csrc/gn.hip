@@ -22,14 +22,20 @@
 //    pairs). Per solve, each block gets a sorted list of the (term, p, q) products that land on it,
 //    so assembly is a deterministic gather: one wave per block, lane = block entry (k_blocks); the
 //    rhs is the same per node entry (k_rhs). No atomics -> bitwise reproducible A and b.
-//  * PCG: pipelined (Ghysels-Vanroose) on the right-preconditioned operator B = A·M⁻¹ (M = block
-//    Jacobi, explicit 6x6 inverses), ONE kernel per iteration: SpMV + all recurrences + the three
-//    dot products. Scalars never leave the device: each launch writes per-workgroup partial sums and
-//    every workgroup of the NEXT launch re-derives the same scalars from them in a fixed order
-//    (kernel boundaries give visibility; no fences, no tickets, no atomics). The host only polls
-//    convergence in chunks sized from the previous frame's count for the same GN step.
+//  * Node order: setup groups the nodes into clusters of <= kCS graph neighbours (host BFS over the
+//    ED graph, first-fit packed into groups of exactly kCS rows, padded with decoupled dummy nodes),
+//    and permutes every node-indexed array into that order; k_finish permutes the result back.
+//  * PCG: pipelined (Ghysels-Vanroose) with a cluster block-Jacobi preconditioner (explicit inverse
+//    of each damped 48x48 cluster diagonal block), ONE kernel per iteration: SpMV + all recurrences
+//    + the cluster M⁻¹ (wave-local: one cluster = one wave's rows) + the three dot products. Scalars
+//    never leave the device: each launch writes per-wave partial sums and every wave of the NEXT
+//    launch re-derives the same scalars from them in a fixed order (kernel boundaries give
+//    visibility; no fences, no tickets, no atomics). The host only polls convergence in chunks
+//    sized from the previous frame's count for the same GN step.
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
+#include <algorithm>
 #include <utility>
 #include <vector>
 
@@ -40,10 +46,18 @@ namespace ofx {
 // --------------------------------------------------------------------------------------------
 constexpr int kBlk = 256;       // threads per WG
 constexpr int kProj = 4;      // warm start: Galerkin projection on the last kProj GN-step solutions
+constexpr int kCS = 8;        // nodes per preconditioner cluster (= PCG rows per wave)
+constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² entries
 
 struct Gn {
   int max_nodes = 0, max_matches = 0;
-  int N = 0, M = 0, NB = 0;
+  int N = 0, M = 0, NB = 0;    // N: PCG rows (nodes in cluster order, padded to whole clusters)
+  int N_real = 0;              // caller's node count
+  int max_pad = 0;             // capacity of the node-indexed arrays (2·max_nodes + kCS)
+  int32_t *perm = nullptr;     // row -> caller node (-1: padding), N entries
+  int32_t *iperm = nullptr;    // caller node -> row, N_real entries
+  std::vector<float> h_nodes;          // host copy of the graph the current order was built from
+  std::vector<int32_t> h_edges, h_perm;
   int64_t T = 0;        // terms = M + N*NB + N
   ofx_gn_params prm{};
   float fx = 0, fy = 0, cx = 0, cy = 0;
@@ -68,9 +82,10 @@ struct Gn {
   // state
   double *R = nullptr, *t = nullptr;
   double *A_own = nullptr, *rhs_own = nullptr;
-  double *Minv = nullptr, *Bm = nullptr;  // block-Jacobi inverse (N*36), B = A·M⁻¹ (nnzb*36)
+  float* Mcl = nullptr;           // cluster inverse rows (6N x 6kCS, f32)
+  const double* Aop = nullptr;    // PCG operator (the damped A of the current step)
   double *st = nullptr;          // PCG recurrence state, 6N records of 8 (see the PCG layout note)
-  double *w0 = nullptr, *w1 = nullptr;
+  double *m0 = nullptr, *m1 = nullptr;   // double-buffered m = M⁻¹w (gathered by the SpMV)
   double *pcg_alpha = nullptr, *pcg_gamma = nullptr;
   int64_t pcg_cap = 0;
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
@@ -82,12 +97,10 @@ struct Gn {
   double* stat = nullptr;         // kMaxLog x [pcg iterations, |b|², loss] of the last solve
   double* step_state = nullptr;   // (kMaxLog+1) x [previous loss, accepted steps] before each GN step
   // Galerkin warm start over the last kProj GN-step solutions of this solve (ring of kProj x 6N each):
-  // xh = previous solutions, xmh = M·xh, th = A·xh
-  double *xh = nullptr, *xmh = nullptr, *th = nullptr;
+  // xh = previous solutions, th = A·xh
+  double *xh = nullptr, *th = nullptr;
   int n_prev = 0;                 // valid entries of the ring for the current step
   int warm_now = 0;               // this step starts from the projected x0
-  int pcg_wpb = 1;                // waves per workgroup of k_pcg_iter (OFX_PCG_WPB: 1, 2, 4)
-             // PCG stop test against max(|b|, |b| of GN step 0) instead of |b|
   int32_t* host_flags = nullptr;  // pinned
   int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
   bool setup_done = false;
@@ -166,32 +179,46 @@ struct Upload {
   int old_N;
   int64_t old_nnzb, n;
 };
+// caller node -> row (negative ids stay negative)
+__device__ __forceinline__ int to_row(const Gn& g, int a) { return a >= 0 ? g.iperm[a] : a; }
+// edge k of row i in row numbering (-1: none, also for padding rows)
+__device__ __forceinline__ int edge_row(const Gn& g, const Upload& u, int i, int k) {
+  const int p = g.perm[i];
+  return p >= 0 ? to_row(g, u.edges[(int64_t)p * g.NB + k]) : -1;
+}
 __global__ __launch_bounds__(256) void k_upload(Gn g, Upload u) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= u.n) return;
   const int N = g.N, M = g.M, NB = g.NB;
   if (i < u.old_nnzb) g.map[(int64_t)g.blk_row[i] * u.old_N + g.col[i]] = 0;
-  if (i < 3 * (int64_t)N) {
-    g.nodes[i] = u.nodes[i];
-    g.tpos[i] = u.tpos[i];
-    g.t[i] = u.prev_t ? (double)u.prev_t[i] : 0.0;
+  if (i < 3 * (int64_t)N) {   // padding rows: a node at the origin with confidence 0 and no edges
+    const int p = g.perm[i / 3];
+    const int64_t s = 3 * (int64_t)p + i % 3;
+    g.nodes[i] = p >= 0 ? u.nodes[s] : 0.0;
+    g.tpos[i] = p >= 0 ? u.tpos[s] : 0.0;
+    g.t[i] = (p >= 0 && u.prev_t) ? (double)u.prev_t[s] : 0.0;
   }
-  if (i < 9 * (int64_t)N) g.R[i] = u.prev_R ? (double)u.prev_R[i] : ((i % 9) % 4 == 0 ? 1.0 : 0.0);
-  if (i < N) g.conf[i] = u.conf[i];
+  if (i < 9 * (int64_t)N) {
+    const int p = g.perm[i / 9];
+    g.R[i] = (p >= 0 && u.prev_R) ? (double)u.prev_R[9 * (int64_t)p + i % 9] : ((i % 9) % 4 == 0 ? 1.0 : 0.0);
+  }
+  if (i < N) { const int p = g.perm[i]; g.conf[i] = p >= 0 ? u.conf[p] : 0.0; }
   if (i < 3 * (int64_t)M) { g.src[i] = u.src[i]; g.tgt[i] = u.tgt[i]; }
-  if (i < 4 * (int64_t)M) { g.wts[i] = u.wts[i]; g.anc[i] = u.anc[i]; }
+  if (i < 4 * (int64_t)M) { g.wts[i] = u.wts[i]; g.anc[i] = to_row(g, u.anc[i]); }
   if (i < M) { g.tpx[i] = u.tpx ? (double)u.tpx[i] : 0.0; g.tpy[i] = u.tpy ? (double)u.tpy[i] : 0.0; }
   if (i < (int64_t)N * NB) {
-    g.edges[i] = u.edges[i];
-    g.ew[i] = (u.use_ew && u.ew) ? (double)NB * (double)u.ew[i] : 1.0;
+    const int r = (int)(i / NB), k = (int)(i % NB);
+    const int p = g.perm[r];
+    g.edges[i] = edge_row(g, u, r, k);
+    g.ew[i] = (p >= 0 && u.use_ew && u.ew) ? (double)NB * (double)u.ew[(int64_t)p * NB + k] : 1.0;
   }
-  if (i < g.T) {   // term t -> its (up to 4) nodes, straight from the inputs
+  if (i < g.T) {   // term t -> its (up to 4) rows, straight from the inputs
     int n[4] = {-1, -1, -1, -1};
     if (i < M) {
-      for (int k = 0; k < 4; ++k) n[k] = u.anc[i * 4 + k];
+      for (int k = 0; k < 4; ++k) n[k] = to_row(g, u.anc[i * 4 + k]);
     } else if (i < M + (int64_t)N * NB) {
       const int64_t e = i - M;
-      const int j = u.edges[e];
+      const int j = edge_row(g, u, (int)(e / NB), (int)(e % NB));
       if (j >= 0) { n[0] = (int)(e / NB); n[1] = j; }
     } else {
       n[0] = (int)(i - M - (int64_t)N * NB);
@@ -271,7 +298,8 @@ __global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restr
 }
 
 // ordered slot assignment per block row (one WG per row, one pass): contiguous column chunk per
-// thread, block scan of the chunk counts; records col, the slot in the map, and the block's row
+// thread, block scan of the chunk counts; records col, slot + 1 in the map (0 = not in the
+// pattern), and the block's row
 __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__ map, const int32_t* __restrict__ row_ptr,
                                                     int32_t* __restrict__ col, int32_t* __restrict__ blk_row) {
   __shared__ int s_w[4];
@@ -287,7 +315,7 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
     if (mrow[j] != 0) {
       col[slot] = j;
       blk_row[slot] = i;
-      mrow[j] = slot;
+      mrow[j] = slot + 1;
       ++slot;
     }
 }
@@ -300,7 +328,7 @@ __global__ void k_pair_count(Gn g) {
     if (n[p] < 0) continue;
     atomicAdd(&g.node_cnt[n[p]], 1);
     for (int q = 0; q < 4; ++q)
-      if (n[q] >= 0) atomicAdd(&g.blk_cnt[g.map[(int64_t)n[p] * g.N + n[q]]], 1);
+      if (n[q] >= 0) atomicAdd(&g.blk_cnt[g.map[(int64_t)n[p] * g.N + n[q]] - 1], 1);
   }
 }
 
@@ -315,7 +343,7 @@ __global__ void k_pair_scatter(Gn g) {
     g.node_list[pos] = (int32_t)(t * 4 + p);
     for (int q = 0; q < 4; ++q) {
       if (n[q] < 0) continue;
-      int s = g.map[(int64_t)n[p] * g.N + n[q]];
+      int s = g.map[(int64_t)n[p] * g.N + n[q]] - 1;
       int pb = g.blk_off[s] + atomicAdd(&g.blk_cnt[s], 1);
       g.blk_list[pb] = (int32_t)(t * 16 + p * 4 + q);
     }
@@ -556,59 +584,33 @@ __global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A,
 }
 
 // ---------------------------------------------------------------------------- PCG
-// Pipelined preconditioned CG (Ghysels & Vanroose 2014): one global reduction per iteration.
-// With block-Jacobi M⁻¹ (node-local) folded into B = A·M⁻¹ (per GN step), n = A·m = A·M⁻¹·w = B·w,
-// so one iteration is ONE kernel: scalars from the previous kernel's partials, SpMV with B, all
-// vector recurrences for the own rows, partial dots for the next iteration.
+// Pipelined preconditioned CG (Ghysels & Vanroose 2014): one global reduction per iteration, ONE
+// kernel per iteration. Preconditioner: block Jacobi over clusters of kCS graph-adjacent nodes
+// (48x48 blocks of A; setup orders the nodes so that every cluster is the kRW = kCS rows of one
+// wave, padding clusters with decoupled dummy nodes). The pipelined recurrences need m = M⁻¹w and
+// n = A·m: each launch gathers m (written by the previous launch) for n = A·m, updates its rows,
+// and applies its cluster's M⁻¹ to the new w through LDS — wave-local, so still one launch.
 
-// 6x6 Cholesky (packed lower, 21 entries, diagonal stored as 1/L_ii) with compile-time indices.
-__device__ __forceinline__ bool chol6(const double* __restrict__ A, double L[21]) {
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-#pragma unroll
-    for (int j = 0; j <= i; ++j) {
-      double s = A[i * 6 + j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) s -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
-      if (i == j) {
-        if (!(s > 0.0)) return false;
-        L[i * (i + 1) / 2 + i] = 1.0 / sqrt(s);   // reciprocal diagonal: the solve multiplies
-      } else {
-        L[i * (i + 1) / 2 + j] = s * L[j * (j + 1) / 2 + j];
-      }
-    }
-  }
-  return true;
-}
-
-__device__ __forceinline__ void chol6_solve(const double* __restrict__ L, const double b[6], double x[6]) {
-  double y[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    double s = b[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) s -= L[i * (i + 1) / 2 + k] * y[k];
-    y[i] = s * L[i * (i + 1) / 2 + i];
-  }
-#pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    double s = y[i];
-#pragma unroll
-    for (int k = i + 1; k < 6; ++k) s -= L[k * (k + 1) / 2 + i] * x[k];
-    x[i] = s * L[i * (i + 1) / 2 + i];
-  }
-}
-
-// ---- PCG layout. st: per node i and component c an 8-double record [x r u z q s p -] at
-// st[(6i+c)*8], so one lane's whole recurrence state is 64 contiguous bytes (4 x 16-B accesses);
-// w0/w1 (6N) double-buffer the SpMV input. Row kernels run one wave per workgroup (no barriers):
-// lane = (row r of kRW, slot q of kSL); slot q multiplies whole 6x6 blocks q, q+kSL, ... of its
-// row, DPP butterflies sum the row's slots; lanes q < 6 own component q of the row's vectors.
-// Scalars travel as per-wave partials (SoA [stream][wave]); every wave of the next launch re-sums
-// them in the same fixed order.
-enum { V_X = 0, V_R = 1, V_U = 2, V_Z = 3, V_Q = 4, V_S = 5, V_P = 6, V_N = 8 };
-constexpr int kRW = 4;          // block rows per wave
+// ---- layout. st: per PCG row i and component c an 8-double record [x r u z q s p w] at
+// st[(6i+c)*8] (a lane's whole recurrence state in 4 x 16-B accesses); m0/m1 (6N) double-buffer
+// the gathered m. Row kernels run one wave per workgroup: lane = (row r of kRW, slot q of kSL);
+// slot q multiplies whole 6x6 blocks q, q+kSL, ... of its row, DPP butterflies sum the row's slots;
+// lanes q < 6 own component q of the row's vectors. Mcl: per row/component the f32 row of its
+// cluster's symmetric inverse (48 entries). Scalars travel as per-wave partials (SoA
+// [stream][wave]); every wave of the next launch re-sums them in the same fixed order.
+enum { V_X = 0, V_R = 1, V_U = 2, V_Z = 3, V_Q = 4, V_S = 5, V_P = 6, V_W = 7, V_N = 8 };
+constexpr int kRW = kCS;        // block rows per wave = cluster size
 constexpr int kSL = 64 / kRW;   // lanes (block slots) per row
+constexpr int kCD = 6 * kCS;    // cluster dimension
+static_assert(kCS * kCS == 64, "k_pcg_prep maps the cluster's kCS x kCS node blocks onto one wave");
+
+// Sum over each aligned group of kSL (= 8) lanes; every lane of the group ends with identical bits.
+__device__ __forceinline__ double slot_sum(double x) {
+  x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_mov<0x141>(x);   // row_half_mirror
+  return x;
+}
 
 // Σ_i p[k*nw + i] for K streams, in two phases so the loads can be issued early: load_streams puts
 // U entries per lane in registers, reduce_streams adds the tail (nw > 64U) and sums in a fixed
@@ -695,28 +697,26 @@ __device__ __forceinline__ double pick6(const double n[6], int c) {
   for (int i = 0; i < 6; ++i) v += n[i] * (c == i ? 1.0 : 0.0);
   return v;
 }
-// (B v)_row summed over the row's kSL lanes: every lane of the row gets all 6 components.
+// (A v)_row summed over the row's kSL lanes: every lane of the row gets all 6 components.
 // [b0, b1) = the row's block range (empty for padding rows).
 __device__ __forceinline__ void row_spmv(const Gn& g, int b0, int b1, int q, const double* __restrict__ v,
                                          double n[6]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) n[i] = 0.0;
-  {
-    for (int bi = b0 + q; bi < b1; bi += kSL) {
-      const double2* blk = reinterpret_cast<const double2*>(g.Bm + 36 * (int64_t)bi);
-      const double2* vc = reinterpret_cast<const double2*>(v + 6 * (int64_t)g.col[bi]);
-      double x[6];
+  for (int bi = b0 + q; bi < b1; bi += kSL) {
+    const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)bi);
+    const double2* vc = reinterpret_cast<const double2*>(v + 6 * (int64_t)g.col[bi]);
+    double x[6];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) { const double2 t = vc[j]; x[2 * j] = t.x; x[2 * j + 1] = t.y; }
+    for (int j = 0; j < 3; ++j) { const double2 t = vc[j]; x[2 * j] = t.x; x[2 * j + 1] = t.y; }
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
-        n[i] += ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
-      }
+    for (int i = 0; i < 6; ++i) {
+      const double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+      n[i] += ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 6; ++i) n[i] = row16_sum(n[i]);
+  for (int i = 0; i < 6; ++i) n[i] = slot_sum(n[i]);
 }
 __device__ __forceinline__ void load_rec(const double* __restrict__ st, int64_t o, double v[V_N]) {
   const double2* p = reinterpret_cast<const double2*>(st + V_N * o);
@@ -728,86 +728,119 @@ __device__ __forceinline__ void store_rec(double* __restrict__ st, int64_t o, co
 #pragma unroll
   for (int k = 0; k < V_N / 2; ++k) p[k] = make_double2(v[2 * k], v[2 * k + 1]);
 }
+// The row's (r, c) f32 row of the cluster inverse, 12 x 16-B loads.
+__device__ __forceinline__ void load_mrow(const Gn& g, int64_t o, float4 mr[kCD / 4]) {
+  const float4* p = reinterpret_cast<const float4*>(g.Mcl + o * kCD);
+#pragma unroll
+  for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k];
+}
+// (M⁻¹ v)_(r,c) with v the wave's cluster vector staged in LDS (s_v[6 r' + c'], f64)
+__device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const double* s_v) {
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < kCD / 4; ++k)
+    a += (((double)mr[k].x * s_v[4 * k] + (double)mr[k].y * s_v[4 * k + 1]) +
+          ((double)mr[k].z * s_v[4 * k + 2] + (double)mr[k].w * s_v[4 * k + 3]));
+  return a;
+}
 
-// LM damping of the diagonal blocks, explicit block inverse Minv_i; cold start: x = 0, r = b,
-// u = M⁻¹ b, z = q = s = p = 0 (and w1 = r for k_pcg_w0's gather); warm start: M·x_j of the stored
-// solutions (the state follows in k_pcg_proj2). 8 lanes per node: every lane factors the 6x6 block
-// (identical bits), lane c < 6 solves column c of the inverse and owns component c.
-__global__ __launch_bounds__(kBlk) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
-                                                   const double* __restrict__ rhs) {
+// Per cluster (one wave): LM damping of the cluster's diagonal node blocks (written back to A: the
+// PCG operator is A + λI) and the explicit inverse of the damped 48x48 cluster matrix by in-place
+// Gauss-Jordan (SPD: no pivoting; a non-positive or non-finite pivot falls back to M⁻¹ = I for the
+// cluster), stored as symmetrised f32 rows. Lane (ti, tj) = node block (ti, tj) of the cluster, held
+// in registers for all 48 (unrolled) steps; step k fetches the old row k / column k entries it needs
+// from their owner lanes by cross-lane permutes and the pivot by a lane read — no LDS, no barrier.
+// Cold start also: x = 0, r = b, u = M⁻¹ b, z = q = s = p = w = 0, u -> m1.
+__global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
+                                                 const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
-  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int i = (int)(tid >> 3), c = (int)(tid & 7);
-  if (i >= g.N) return;
-  double* blk = A + 36 * (int64_t)g.map[(int64_t)i * g.N + i];
-  double a[36];
+  const int lane = threadIdx.x;
+  const int base = blockIdx.x * kCS;
+  const int ti = lane / kCS, tj = lane % kCS;
+  const int slot = g.map[(int64_t)(base + ti) * g.N + base + tj] - 1;
+  double a[6][6];
+  {
+    const double2* blk = reinterpret_cast<const double2*>(A + 36 * (int64_t)(slot >= 0 ? slot : 0));
 #pragma unroll
-  for (int q = 0; q < 36; ++q) a[q] = blk[q];
-#pragma unroll
-  for (int q = 0; q < 6; ++q) a[q * 7] += lm;
-  if (c >= 6) return;
-  double dg = a[0];
-#pragma unroll
-  for (int q = 1; q < 6; ++q) dg = (c == q) ? a[q * 7] : dg;
-  blk[c * 7] = dg;
-  double L[21];
-  bool ok = chol6(a, L);
-  double e[6], col[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) e[k] = (k == c) ? 1.0 : 0.0;
-  if (ok) chol6_solve(L, e, col);
-  else {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) col[k] = e[k];
-  }
-  double* Mi = g.Minv + 36 * (int64_t)i;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) Mi[k * 6 + c] = col[k];
-  const int64_t o = 6 * (int64_t)i + c;
-  if (g.warm_now) {           // Galerkin start on span of the previous solutions: M·x_j
-    double arow[6];           // row c of the damped diagonal block (register select, no scratch)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) arow[k] = a[k];
-#pragma unroll
-    for (int cc = 1; cc < 6; ++cc)
-#pragma unroll
-      for (int k = 0; k < 6; ++k) arow[k] = (c == cc) ? a[cc * 6 + k] : arow[k];
-    for (int j = 0; j < g.n_prev; ++j) {
-      const double* xj = g.xh + (int64_t)j * 6 * g.N + 6 * (int64_t)i;
-      double m = 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) m += arow[k] * xj[k];
-      g.xmh[(int64_t)j * 6 * g.N + o] = m;
+    for (int e = 0; e < 18; ++e) {
+      const double2 v = slot >= 0 ? blk[e] : make_double2(0.0, 0.0);
+      a[(2 * e) / 6][(2 * e) % 6] = v.x;
+      a[(2 * e + 1) / 6][(2 * e + 1) % 6] = v.y;
     }
-  } else {
-    // u_c = (M⁻¹ b)_c; M⁻¹ is symmetric, so row c = column c
-    double u = 0.0;
+  }
+  if (ti == tj) {   // diagonal blocks are always in the pattern
 #pragma unroll
-    for (int k = 0; k < 6; ++k) u += col[k] * rhs[6 * i + k];
-    double v[V_N] = {0.0, rhs[o], u, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < 6; ++r) {
+      a[r][r] += lm;
+      A[36 * (int64_t)slot + 7 * r] = a[r][r];
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < kCD; ++k) {
+    const int K = k / 6, kr = k % 6;
+    const double piv = read_lane(a[kr][kr], K * (kCS + 1));
+    bad = bad || !(piv > 0.0) || !isfinite(piv);
+    const double ip = 1.0 / piv;
+    double rk[6], ck[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) rk[c] = __shfl(a[kr][c], K * kCS + tj, 64);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ck[r] = __shfl(a[r][kr], ti * kCS + K, 64);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) rk[c] *= ip;                 // new row k (off the pivot)
+    const bool rowk = ti == K, colk = tj == K;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double upd = a[r][c] - ck[r] * rk[c];
+        double v = upd;
+        if (c == kr) v = colk ? -ck[r] * ip : v;                // column k
+        if (r == kr) v = rowk ? ((c == kr && colk) ? ip : rk[c]) : v;   // row k, pivot
+        a[r][c] = v;
+      }
+  }
+  // symmetrise with the transposed block (lane (tj, ti)), round to f32, store the cluster rows
+  float m[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const double t = __shfl(a[c][r], tj * kCS + ti, 64);
+      m[r][c] = bad ? ((ti == tj && r == c) ? 1.f : 0.f) : (float)(0.5 * (a[r][c] + t));
+    }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float2* row = reinterpret_cast<float2*>(g.Mcl + ((int64_t)(base + ti) * 6 + r) * kCD + 6 * tj);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) row[c] = make_float2(m[r][2 * c], m[r][2 * c + 1]);
+  }
+  if (g.warm_now) return;
+  // cold start: u = M⁻¹ b with the stored (f32) operator; the 8 lanes of a block row sum in fixed order
+  double bj[6], u[6];
+  const double* bc = rhs + 6 * (int64_t)(base + tj);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) bj[c] = bc[c];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) acc += (double)m[r][c] * bj[c];
+    u[r] = slot_sum(acc);
+  }
+  if (tj < 6) {
+    const int64_t o = 6 * (int64_t)(base + ti) + tj;
+    const double uo = pick6(u, tj);
+    const double v[V_N] = {0.0, rhs[o], uo, 0.0, 0.0, 0.0, 0.0, 0.0};
     store_rec(g.st, o, v);
-    g.w1[o] = rhs[o];
+    g.m1[o] = uo;
   }
 }
 
-// B_ij = A_ij · Minv_j : one thread per output entry (36 per block)
-__global__ __launch_bounds__(kBlk) void k_pcg_bmat(Gn g, const double* __restrict__ A) {
-  if (g.flags[F_STOPPED]) return;
-  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t bi = tid / 36;
-  const int e = (int)(tid % 36), r = e / 6, c = e % 6;
-  if (bi >= g.nnzb) return;
-  const double* Ar = A + 36 * bi + 6 * r;
-  const double* Mj = g.Minv + 36 * (int64_t)g.col[bi];
-  double v = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) v += Ar[k] * Mj[k * 6 + c];
-  g.Bm[36 * bi + e] = v;
-}
-
-// Galerkin warm start, pass 1: t_j = A x_j = B (M x_j) for the n_prev stored solutions (own rows)
-// and per-wave partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
+// Galerkin warm start, pass 1: t_j = A x_j for the n_prev stored solutions (own rows) and per-wave
+// partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
 constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
 __device__ __forceinline__ constexpr int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
 
@@ -822,28 +855,26 @@ __global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict_
   for (int j = 0; j < kProj; ++j)
 #pragma unroll
     for (int i = 0; i < 6; ++i) n[j][i] = 0.0;
-  if (row < g.N) {
-    const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-    for (int bi = b0 + q; bi < b1; bi += kSL) {
-      const double* blk = g.Bm + 36 * (int64_t)bi;
-      const int64_t cc = 6 * (int64_t)g.col[bi];
-      double bk[36];
+  const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
+  for (int bi = b0 + q; bi < b1; bi += kSL) {
+    const double* blk = g.Aop + 36 * (int64_t)bi;
+    const int64_t cc = 6 * (int64_t)g.col[bi];
+    double bk[36];
 #pragma unroll
-      for (int k = 0; k < 36; ++k) bk[k] = blk[k];
+    for (int k = 0; k < 36; ++k) bk[k] = blk[k];
 #pragma unroll
-      for (int j = 0; j < kProj; ++j) {
-        if (j < np) {
-          const double* vc = g.xmh + j * stride + cc;
-          double x[6];
+    for (int j = 0; j < kProj; ++j) {
+      if (j < np) {
+        const double* vc = g.xh + j * stride + cc;
+        double x[6];
 #pragma unroll
-          for (int k = 0; k < 6; ++k) x[k] = vc[k];
+        for (int k = 0; k < 6; ++k) x[k] = vc[k];
 #pragma unroll
-          for (int i = 0; i < 6; ++i) {
-            double t = 0.0;
+        for (int i = 0; i < 6; ++i) {
+          double t = 0.0;
 #pragma unroll
-            for (int k = 0; k < 6; ++k) t += bk[6 * i + k] * x[k];
-            n[j][i] += t;
-          }
+          for (int k = 0; k < 6; ++k) t += bk[6 * i + k] * x[k];
+          n[j][i] += t;
         }
       }
     }
@@ -851,11 +882,11 @@ __global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict_
 #pragma unroll
   for (int j = 0; j < kProj; ++j)
 #pragma unroll
-    for (int i = 0; i < 6; ++i) n[j][i] = row16_sum(n[j][i]);
+    for (int i = 0; i < 6; ++i) n[j][i] = slot_sum(n[j][i]);
   double v[kProjP];
 #pragma unroll
   for (int k = 0; k < kProjP; ++k) v[k] = 0.0;
-  if (row < g.N && q < 6) {
+  if (q < 6) {
     const int64_t o = 6 * (int64_t)row + q;
     const double b = rhs[o];
     double x[kProj], t[kProj];
@@ -881,12 +912,18 @@ __global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict_
 
 // Galerkin warm start, pass 2: every wave re-derives G and f from the partials (fixed order,
 // identical bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get
-// c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0, z = q = s = p = 0, w1 = r0.
+// c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0 (cluster, via LDS),
+// z = q = s = p = w = 0, u0 -> m1.
 __global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict__ rhs) {
+  __shared__ double s_v[kCD];
   if (g.flags[F_STOPPED]) return;
   const int lane = threadIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const int np = g.n_prev;
+  const bool own = q < 6;
+  const int64_t o = 6 * (int64_t)row + q;
+  float4 mr[kCD / 4];
+  if (own) load_mrow(g, o, mr);
   double p[kProjP];
   sum_streams<kProjP, 8>(g.part_p, g.nwg_row, p);
   // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
@@ -937,46 +974,47 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict
 #pragma unroll
   for (int j = 0; j < kProj; ++j) fin = fin && isfinite(c[j]);
   const int64_t stride = 6 * (int64_t)g.N;
-  const bool own = row < g.N && q < 6;
-  const int64_t o = 6 * (int64_t)row + q;
   double xv = 0.0, rv = 0.0;
   if (own) {
     rv = rhs[o];
 #pragma unroll
     for (int j = 0; j < kProj; ++j)
       if (j < np && fin) { xv += c[j] * g.xh[j * stride + o]; rv -= c[j] * g.th[j * stride + o]; }
+    s_v[6 * r + q] = rv;
   }
-  double rk[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) rk[k] = __shfl(rv, r * kSL + k, 64);
+  __syncthreads();
   if (own) {
-    const double* Mi = g.Minv + 36 * (int64_t)row + 6 * q;
-    double u = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) u += Mi[k] * rk[k];
-    double v[V_N] = {xv, rv, u, 0.0, 0.0, 0.0, 0.0, 0.0};
+    const double u = apply_mrow(mr, s_v);
+    const double v[V_N] = {xv, rv, u, 0.0, 0.0, 0.0, 0.0, 0.0};
     store_rec(g.st, o, v);
-    g.w1[o] = rv;
+    g.m1[o] = u;
   }
 }
 
-// w0 = A u0 = B r0 (r0 gathered from w1); per-wave partials (γ0 = r·u, δ0 = w·u, r·r) -> parity 0,
-// b·b -> part_b.
+// w0 = A u0 (u0 gathered from m1), m0 = M⁻¹ w0 (cluster, via LDS); per-wave partials
+// (γ0 = r·u, δ0 = w·u, r·r) -> parity 0, b·b -> part_b.
 __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
+  __shared__ double s_v[kCD];
   if (g.flags[F_STOPPED]) return;
   const int lane = threadIdx.x;
-  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
+  const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
+  const bool own = q < 6;
+  const int64_t o = 6 * (int64_t)row + q;
+  float4 mr[kCD / 4];
+  double v[V_N];
+  double b = 0.0;
+  if (own) { load_mrow(g, o, mr); load_rec(g.st, o, v); b = rhs[o]; }
   double n[6];
-  const int b0 = row < g.N ? g.row_ptr[row] : 0, b1 = row < g.N ? g.row_ptr[row + 1] : 0;
-  row_spmv(g, b0, b1, q, g.w1, n);
+  row_spmv(g, g.row_ptr[row], g.row_ptr[row + 1], q, g.m1, n);
+  const double w = pick6(n, q);
+  if (own) s_v[6 * r + q] = w;
+  __syncthreads();
   double d[4] = {0.0, 0.0, 0.0, 0.0};
-  if (row < g.N && q < 6) {
-    const int64_t o = 6 * (int64_t)row + q;
-    const double w = pick6(n, q);
-    g.w0[o] = w;
-    double v[V_N];
-    load_rec(g.st, o, v);
-    const double b = rhs[o];
+  if (own) {
+    const double m = apply_mrow(mr, s_v);
+    v[V_W] = w;
+    store_rec(g.st, o, v);
+    g.m0[o] = m;
     d[0] = v[V_R] * v[V_U]; d[1] = w * v[V_U]; d[2] = v[V_R] * v[V_R]; d[3] = b * b;
   }
 #pragma unroll
@@ -984,75 +1022,63 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
   if (lane == 0) {
     const int ns = g.nw_pad;
     g.part_p[blockIdx.x] = d[0]; g.part_p[ns + blockIdx.x] = d[1]; g.part_p[2 * ns + blockIdx.x] = d[2];
+    g.part_b[blockIdx.x] = d[3];
     if (blockIdx.x == 0 && ns > g.nwg_row)   // pad slot of every iteration stream (part_p is also proj scratch)
       for (int k = 0; k < 6; ++k) g.part_p[k * ns + g.nwg_row] = 0.0;
-    g.part_b[blockIdx.x] = d[3];
   }
 }
 
 // One PCG iteration; par = parity of the iteration (iteration i has par = i & 1), first = 1 only for
-// iteration 0. Reads partials[par], w[par] and alpha/gamma[par^1]; writes partials[par^1], w[par^1]
-// and alpha/gamma[par]. The arguments do not depend on the iteration number, so a chunk of launches
-// [par 1, par 0] x K could be one replayable hipGraph; the count of executed iterations lives in
-// flags[F_PCG_CNT] (the lead lane increments it).
-// Everything this launch needs — previous partials, own-row state, M⁻¹ row, B blocks, w gather —
-// is loaded up front; the scalars are uniform per wave, so there is no barrier at all.
-__global__ __launch_bounds__(256) void k_pcg_iter(Gn g, int par, int first) {
-  // one independent wave per row group; workgroups of 1-4 waves only pack waves onto a CU
-  const int lane = threadIdx.x & 63;
-  const int wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (wv >= g.nwg_row) return;
-  const int q = lane % kSL, row = wv * kRW + lane / kSL;
+// iteration 0. Reads partials[par], m[par] and alpha/gamma[par^1]; writes partials[par^1], m[par^1]
+// and alpha/gamma[par]. The count of executed iterations lives in flags[F_PCG_CNT] (the lead lane
+// increments it). Everything this launch needs — previous partials, own-row state, the cluster
+// inverse row, A blocks, m gather — is loaded up front; the scalars are uniform per wave and the
+// cluster exchange is wave-local, so the only barrier is the single-wave LDS handoff.
+__global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int par, int first) {
+  __shared__ double s_v[kCD];
+  const int lane = threadIdx.x;
+  const int wv = blockIdx.x;
+  const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
   const int nw = g.nwg_row;
-  const double* __restrict__ wc = par ? g.w1 : g.w0;
-  double* __restrict__ wn = par ? g.w0 : g.w1;
+  const double* __restrict__ mc = par ? g.m1 : g.m0;
+  double* __restrict__ mn = par ? g.m0 : g.m1;
   // 1. issue every independent load: stop flags and scalars (scalar loads), previous partials,
-  //    own-row state, M⁻¹ row, own w, the row's block range
+  //    own-row state, cluster-inverse row, own m, the row's block range
   const int stop = g.flags[F_DONE] | g.flags[F_STOPPED];
   const int cnt = g.flags[F_PCG_CNT];
   const double gam_prev = first ? 1.0 : g.pcg_gamma[par ^ 1];
   const double alpha_prev = first ? 1.0 : g.pcg_alpha[par ^ 1];
   const double bb_stored = g.scal[S_BB];
   const int ns = g.nw_pad;
-  double2 tp[3][8];
-  double tb[1][16];
-  load_streams2<3, 8>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp);
-  if (first) load_streams<1, 16>(g.part_b, nw, tb);
-  const bool own = row < g.N && q < 6;
+  double2 tp[3][4];
+  double tb[1][8];
+  load_streams2<3, 4>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp);
+  if (first) load_streams<1, 8>(g.part_b, nw, tb);
+  const bool own = q < 6;
   const int64_t o = 6 * (int64_t)row + q;
-  double v[V_N], mi[6], wi[6], w = 0.0;
+  double v[V_N], m = 0.0;
+  float4 mr[kCD / 4];
 #pragma unroll
   for (int k = 0; k < V_N; ++k) v[k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { mi[k] = 0.0; wi[k] = 0.0; }
   if (own) {
     load_rec(g.st, o, v);
-    const double2* Mi = reinterpret_cast<const double2*>(g.Minv + 36 * (int64_t)row + 6 * q);
-    const double2* wr = reinterpret_cast<const double2*>(wc + 6 * (int64_t)row);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const double2 a = Mi[k], b = wr[k];
-      mi[2 * k] = a.x; mi[2 * k + 1] = a.y; wi[2 * k] = b.x; wi[2 * k + 1] = b.y;
-    }
-    w = wc[o];
+    load_mrow(g, o, mr);
+    m = mc[o];
   }
-  const int b0 = row < g.N ? g.row_ptr[row] : 0, b1 = row < g.N ? g.row_ptr[row + 1] : 0;
+  const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   // 2. after convergence the remaining launches of the chunk end here (one scalar round trip)
   if (stop) return;
-  // 3. SpMV n = B w (gather chain), then the scalars from the partials (long arrived)
+  // 3. SpMV n = A m (gather chain), then the scalars from the partials (long arrived)
   double n[6];
-  row_spmv(g, b0, b1, q, wc, n);
+  row_spmv(g, b0, b1, q, mc, n);
   double pa[3];
-  reduce_streams2<3, 8>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp, pa);
+  reduce_streams2<3, 4>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp, pa);
   double bb = bb_stored;
   if (first) {
     double t[1];
-    reduce_streams<1, 16>(g.part_b, nw, tb, t);
+    reduce_streams<1, 8>(g.part_b, nw, tb, t);
     bb = t[0];
   }
-  double m = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) m += mi[k] * wi[k];
   const double gam = pa[0], del = pa[1], rr = pa[2];
   const double tol = g.prm.pcg_tol;
   const bool lead = wv == 0 && lane == 0;
@@ -1077,20 +1103,23 @@ __global__ __launch_bounds__(256) void k_pcg_iter(Gn g, int par, int first) {
   }
   if (lead) { g.pcg_alpha[par] = alpha; g.pcg_gamma[par] = gam; g.flags[F_PCG_CNT] = cnt + 1; }
   double d[3] = {0.0, 0.0, 0.0};
+  double w2 = 0.0, rn = 0.0, un = 0.0;
+  const double nc = pick6(n, q);
   if (own) {
-    const double nc = pick6(n, q);
     const double zz = nc + beta * v[V_Z];
     const double qq = m + beta * v[V_Q];
-    const double sv = w + beta * v[V_S];
+    const double sv = v[V_W] + beta * v[V_S];
     const double p = v[V_U] + beta * v[V_P];
-    const double r = v[V_R] - alpha * sv;
-    const double u = v[V_U] - alpha * qq;
-    const double w2 = w - alpha * zz;
-    const double nv[V_N] = {v[V_X] + alpha * p, r, u, zz, qq, sv, p, 0.0};
+    rn = v[V_R] - alpha * sv;
+    un = v[V_U] - alpha * qq;
+    w2 = v[V_W] - alpha * zz;
+    const double nv[V_N] = {v[V_X] + alpha * p, rn, un, zz, qq, sv, p, w2};
     store_rec(g.st, o, nv);
-    wn[o] = w2;
-    d[0] = r * u; d[1] = w2 * u; d[2] = r * r;
+    s_v[6 * r + q] = w2;
+    d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
   }
+  __syncthreads();
+  if (own) mn[o] = apply_mrow(mr, s_v);      // m of the next iteration: M⁻¹ w_new, cluster-local
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) {
@@ -1174,9 +1203,10 @@ __global__ void k_finish(Gn g, float* __restrict__ rot, float* __restrict__ tran
                          double* __restrict__ loss_out, int n_log) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = !g.flags[F_ILL] && !g.flags[F_RES_NONFINITE];
-  if (i < g.N) {
-    for (int c = 0; c < 9; ++c) rot[9 * i + c] = valid ? (float)g.R[9 * i + c] : ((c % 4 == 0) ? 1.f : 0.f);
-    for (int c = 0; c < 3; ++c) trans[3 * i + c] = valid ? (float)g.t[3 * i + c] : 0.f;
+  if (i < g.N_real) {   // caller order
+    const int64_t r = g.iperm[i];
+    for (int c = 0; c < 9; ++c) rot[9 * i + c] = valid ? (float)g.R[9 * r + c] : ((c % 4 == 0) ? 1.f : 0.f);
+    for (int c = 0; c < 3; ++c) trans[3 * i + c] = valid ? (float)g.t[3 * r + c] : 0.f;
   }
   if (i == 0 && status) {
     status[0] = valid ? 1 : 0;
@@ -1199,13 +1229,77 @@ static double lm_for_iter(double lm0, int gn_iter) {
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->blk_off, g->blk_cnt,
-                  g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Minv, g->Bm,
-                  g->st, g->w0, g->w1, g->pcg_alpha, g->pcg_gamma,
+                  g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
+                  g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log, g->stat, g->step_state, g->xh, g->xmh, g->th};
+                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->perm, g->iperm};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
+}
+
+// Row order for the cluster preconditioner (host, from the ED graph). Clusters: the lowest
+// unassigned node seeds a cluster that grows breadth-first over graph edges, candidates of each
+// visited node taken nearest-to-seed first, up to kCS members. Groups: clusters first-fit packed by
+// decreasing size into groups of kCS rows, unused rows are padding (-1). perm[row] = node.
+static void order_rows(int N, int NB, const float* nodes, const int32_t* edges, std::vector<int32_t>& perm) {
+  std::vector<int32_t> lab(N, -1), members;
+  std::vector<int32_t> c_off{0};
+  std::vector<int32_t> front, cand;
+  for (int s0 = 0; s0 < N; ++s0) {
+    if (lab[s0] >= 0) continue;
+    const int c = (int)c_off.size() - 1;
+    const size_t first = members.size();
+    lab[s0] = c;
+    members.push_back(s0);
+    front.assign(1, s0);
+    const float* ps = nodes + 3 * (int64_t)s0;
+    auto d2 = [&](int j) {
+      const float* pj = nodes + 3 * (int64_t)j;
+      const double a = (double)pj[0] - ps[0], b = (double)pj[1] - ps[1], e = (double)pj[2] - ps[2];
+      return a * a + b * b + e * e;
+    };
+    for (size_t f = 0; f < front.size() && members.size() - first < (size_t)kCS; ++f) {
+      const int cur = front[f];
+      cand.clear();
+      for (int k = 0; k < NB; ++k) {
+        const int j = edges[(int64_t)cur * NB + k];
+        if (j >= 0 && j < N && lab[j] < 0 && std::find(cand.begin(), cand.end(), j) == cand.end()) cand.push_back(j);
+      }
+      std::sort(cand.begin(), cand.end(), [&](int a, int b) {
+        const double da = d2(a), db = d2(b);
+        return da < db || (da == db && a < b);
+      });
+      for (int j : cand) {
+        if (members.size() - first >= (size_t)kCS) break;
+        lab[j] = c;
+        members.push_back(j);
+        front.push_back(j);
+      }
+    }
+    c_off.push_back((int32_t)members.size());
+  }
+  const int nc = (int)c_off.size() - 1;
+  std::vector<int32_t> order(nc);
+  for (int c = 0; c < nc; ++c) order[c] = c;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return c_off[a + 1] - c_off[a] > c_off[b + 1] - c_off[b]; });
+  std::vector<int32_t> fill;                       // per group
+  std::vector<std::vector<int32_t>> grp;
+  for (int c : order) {
+    const int sz = c_off[c + 1] - c_off[c];
+    size_t k = 0;
+    while (k < fill.size() && fill[k] + sz > kCS) ++k;
+    if (k == fill.size()) { fill.push_back(0); grp.emplace_back(); }
+    fill[k] += sz;
+    grp[k].push_back(c);
+  }
+  perm.assign(grp.size() * kCS, -1);
+  for (size_t k = 0; k < grp.size(); ++k) {
+    int r = (int)k * kCS;
+    for (int c : grp[k])
+      for (int m = c_off[c]; m < c_off[c + 1]; ++m) perm[r++] = members[m];
+  }
 }
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
@@ -1215,9 +1309,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     g->n_prev = gn_iter < kProj ? gn_iter : kProj;
     g->warm_now = 1;
   }
-  hipLaunchKernelGGL(k_pcg_prep, dim3(grid_for(8 * (int64_t)g->N, kBlk)), dim3(kBlk), 0, hs, *g, lm, A, (const double*)rhs);
-  if (g->nnzb > 0)
-    hipLaunchKernelGGL(k_pcg_bmat, dim3(grid_for(36 * g->nnzb, kBlk, 1 << 30)), dim3(kBlk), 0, hs, *g, (const double*)A);
+  g->Aop = A;
+  hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs);
   if (g->warm_now) {
     hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
     hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
@@ -1236,7 +1329,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // parity-pair chunks was measured: no gain over plain launches for this kernel.)
   const int max_it = g->prm.pcg_max_iter;
   const int lp = g->last_pcg[gn_iter & 63];
-  const dim3 grid((g->nwg_row + g->pcg_wpb - 1) / g->pcg_wpb), block(64 * g->pcg_wpb);
+  const dim3 grid(g->nwg_row), block(64);
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
@@ -1266,11 +1359,17 @@ extern "C" {
 
 int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   OFX_CHECK_ARG(handle && max_nodes > 0 && max_matches >= 0, "bad gn_create args");
-  if (max_nodes > 16384) { set_error("max_nodes %d > 16384 (dense NxN slot map)", max_nodes); return OFX_ERR_RANGE; }
+  if (max_nodes > kMaxNodes) {
+    set_error("max_nodes %d > %d (dense slot map over the padded rows)", max_nodes, kMaxNodes);
+    return OFX_ERR_RANGE;
+  }
   Gn* g = new Gn();
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
-  int64_t N = max_nodes, M = max_matches > 0 ? max_matches : 1;
+  // rows: clusters of <= kCS first-fit packed into groups of kCS; at most one group is at most half
+  // full, so rows <= 2·nodes + kCS
+  g->max_pad = 2 * max_nodes + kCS;
+  int64_t N = g->max_pad, M = max_matches > 0 ? max_matches : 1;
 #define ALLOC(ptr, n) \
   if (hipMalloc((void**)&(ptr), (size_t)(n) * sizeof(*(ptr))) != hipSuccess) { free_all(g); delete g; set_error("hipMalloc failed"); return OFX_ERR_ALLOC; }
   ALLOC(g->nodes, 3 * N); ALLOC(g->tpos, 3 * N); ALLOC(g->conf, N);
@@ -1279,8 +1378,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 1);
   ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
-  ALLOC(g->Minv, 36 * N); ALLOC(g->st, V_N * 6 * N); ALLOC(g->w0, 6 * N); ALLOC(g->w1, 6 * N);
-  ALLOC(g->xh, kProj * 6 * N); ALLOC(g->xmh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
+  ALLOC(g->Mcl, 6 * N * kCD); ALLOC(g->st, V_N * 6 * N); ALLOC(g->m0, 6 * N); ALLOC(g->m1, 6 * N);
+  ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
+  ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes);
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
@@ -1321,7 +1421,7 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 int ofx_gn_info(void* handle, int64_t* info) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && info, "null handle/info");
-  info[0] = g->N; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T;
+  info[0] = g->N_real; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T; info[4] = g->N;
   return OFX_OK;
 }
 
@@ -1330,6 +1430,14 @@ int ofx_gn_stats(void* handle, double* out, int32_t cap) {
   OFX_CHECK_ARG(g && out && cap >= 0, "bad gn_stats args");
   int n = cap < kMaxLog ? cap : kMaxLog;
   if (n > 0) OFX_HIP(hipMemcpy(out, g->stat, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+  return OFX_OK;
+}
+
+int ofx_gn_row_order(void* handle, int32_t* perm, int32_t cap) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && g->setup_done && perm, "gn_setup not called / null perm");
+  OFX_CHECK_ARG(cap >= (int)g->h_perm.size(), "cap %d < rows %d", cap, (int)g->h_perm.size());
+  memcpy(perm, g->h_perm.data(), g->h_perm.size() * sizeof(int32_t));
   return OFX_OK;
 }
 
@@ -1354,8 +1462,31 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_CHECK_ARG(prm->num_iter >= 0 && prm->num_iter <= 64, "num_iter must be in [0,64]");
   OFX_CHECK_ARG(prm->pcg_max_iter >= 1, "pcg_max_iter must be >= 1");
   hipStream_t hs = as_stream(s);
-  int N = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
-  g->N = N; g->M = M; g->NB = NB; g->prm = *prm;
+  int N0 = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
+  if ((int64_t)N0 * NB > 0) OFX_CHECK_ARG(pb->edges, "null edges");
+  // row order (cluster preconditioner): rebuilt when the graph differs from the previous solve's
+  {
+    std::vector<float> hn(3 * (size_t)N0);
+    std::vector<int32_t> he((size_t)N0 * NB);
+    OFX_HIP(hipMemcpyAsync(hn.data(), pb->nodes, hn.size() * sizeof(float), hipMemcpyDeviceToHost, hs));
+    if (!he.empty())
+      OFX_HIP(hipMemcpyAsync(he.data(), pb->edges, he.size() * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+    OFX_HIP(hipStreamSynchronize(hs));
+    if (hn != g->h_nodes || he != g->h_edges || g->h_perm.empty()) {
+      order_rows(N0, NB, hn.data(), he.data(), g->h_perm);
+      std::vector<int32_t> ip(N0, -1);
+      for (size_t r = 0; r < g->h_perm.size(); ++r)
+        if (g->h_perm[r] >= 0) ip[g->h_perm[r]] = (int32_t)r;
+      if ((int)g->h_perm.size() > g->max_pad) { set_error("row order overflow"); return OFX_ERR_RANGE; }
+      OFX_HIP(hipMemcpyAsync(g->perm, g->h_perm.data(), g->h_perm.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+      OFX_HIP(hipMemcpyAsync(g->iperm, ip.data(), ip.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+      OFX_HIP(hipStreamSynchronize(hs));   // pageable sources
+      g->h_nodes.swap(hn);
+      g->h_edges.swap(he);
+    }
+  }
+  const int N = (int)g->h_perm.size();
+  g->N = N; g->N_real = N0; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
   g->T = (int64_t)M + (int64_t)N * NB + N;
   if (prm->pcg_max_iter + 1 > g->pcg_cap) {
@@ -1365,13 +1496,8 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
-  g->nwg_row = (N + kRW - 1) / kRW;
+  g->nwg_row = N / kRW;
   g->nw_pad = (g->nwg_row + 1) & ~1;
-  {
-    const char* e = getenv("OFX_PCG_WPB");     // tuning knob
-    const int w = e ? atoi(e) : 1;
-    g->pcg_wpb = (w == 2 || w == 4) ? w : 1;
-  }
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T
@@ -1392,7 +1518,6 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   }
   // edges + weights (capacity kept across solves)
   int64_t ne = (int64_t)N * NB;
-  if (ne > 0) OFX_CHECK_ARG(pb->edges, "null edges");
   if (ne > g->ne_cap) {
     if (g->edges) { OFX_HIP(hipFree(g->edges)); g->edges = nullptr; }
     if (g->ew) { OFX_HIP(hipFree(g->ew)); g->ew = nullptr; }
@@ -1424,14 +1549,13 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
-    for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->Bm, (void**)&g->blk_off,
+    for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->blk_off,
                     (void**)&g->blk_cnt})
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     g->nnzb_cap = (int64_t)nnz + nnz / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->col, g->nnzb_cap * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_row, g->nnzb_cap * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->A_own, g->nnzb_cap * 36 * sizeof(double)));
-    OFX_HIP(hipMalloc((void**)&g->Bm, g->nnzb_cap * 36 * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->blk_off, (g->nnzb_cap + 1) * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_cnt, (g->nnzb_cap + 1) * sizeof(int32_t)));
   }
@@ -1466,6 +1590,7 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   OFX_CHECK_ARG(g && g->setup_done, "gn_setup not called");
   OFX_CHECK_ARG(A && rhs, "null A/rhs");
   OFX_CHECK_ARG(m0 >= 0 && m1 <= g->M && m0 <= m1, "bad match range [%d,%d) of %d", m0, m1, g->M);
+  // A: nnz_blocks x 36 f64, rhs: 6·rows + 4 f64 (rows = ofx_gn_info()[4])
   (void)gn_iter;
   hipStream_t hs = as_stream(s);
   DataCoef dc;

@@ -63,10 +63,17 @@ class GaussNewtonSolver:
         return ms.value, n.value, ns.value
 
     def info(self):
-        """[n_nodes, n_matches, JᵀJ block count, residual terms] of the last solve's setup."""
-        arr = (ctypes.c_int64 * 4)()
+        """[n_nodes, n_matches, JᵀJ block count, residual terms, PCG rows] of the last solve's setup."""
+        arr = (ctypes.c_int64 * 5)()
         call("ofx_gn_info", self._h, arr)
         return list(arr)
+
+    def row_order(self):
+        """PCG row -> node of the last setup (-1: padding row); the order of rhs / the state rows."""
+        rows = self.info()[4]
+        arr = np.empty(rows, np.int32)
+        call("ofx_gn_row_order", self._h, arr.ctypes.data_as(ctypes.c_void_p), rows)
+        return arr
 
     def stats(self):
         """Per GN step of the last solve: (PCG iterations, |b|², loss) rows; steps that did not run are 0."""
@@ -175,7 +182,8 @@ class GaussNewtonSolver:
         rank = dist.get_rank(group)
         m0, m1 = match_range(M, rank, world)
         A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=self.device)
-        rhs = torch.empty(6 * N + 4, dtype=torch.float64, device=self.device)
+        rows = self.info()[4]        # nodes in cluster order, padded (include/ofx.h: ofx_gn_info)
+        rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=self.device)
         for it in range(int(self.params["num_iter"])):
             call("ofx_gn_linearize", self._h, it, m0, m1, 1 if rank == 0 else 0, ptr(A), ptr(rhs), stream_ptr())
             dist.all_reduce(A, group=group)

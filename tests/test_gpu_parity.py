@@ -240,8 +240,12 @@ def test_gn_assembly_matches_dense_system(cuda, golden_dir):
     prm = s._params()
     nnz = _lib.c_int64()
     call("ofx_gn_setup", s._h, byref(pb), byref(prm), byref(nnz), stream_ptr())
+    rows = s.info()[4]
+    perm = s.row_order()
+    assert len(perm) == rows and rows % 8 == 0 and rows <= 2 * N + 8
+    assert sorted(perm[perm >= 0].tolist()) == list(range(N))   # every node exactly once
     A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=cuda)
-    rhs = torch.empty(6 * N + 4, dtype=torch.float64, device=cuda)
+    rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=cuda)
     call("ofx_gn_linearize", s._h, 0, 0, M, 1, ptr(A), ptr(rhs), stream_ptr())
     torch.cuda.synchronize()
     sysd = fo.gn_system(g["nodes"], g["edges"], g["tpos"], g["conf"], g["src"], g["anchors"], g["weights"], g["tgt"],
@@ -256,8 +260,11 @@ def test_gn_assembly_matches_dense_system(cuda, golden_dir):
     assert Ab.shape[0] >= nzmask.sum()
     np.testing.assert_allclose(np.sort(Ab.reshape(-1)), np.sort(np.concatenate(
         [blocks_dense[nzmask].reshape(-1), np.zeros((Ab.shape[0] - nzmask.sum()) * 36)])), rtol=1e-9, atol=1e-12)
-    np.testing.assert_allclose(rhs.cpu().numpy()[:6 * N], bd, rtol=1e-9, atol=1e-12)
-    np.testing.assert_allclose(rhs.cpu().numpy()[6 * N:6 * N + 3].sum(), sysd["loss2"], rtol=1e-9)
+    rb = rhs.cpu().numpy()
+    real = perm >= 0
+    np.testing.assert_allclose(rb[:6 * rows].reshape(rows, 6)[real], bd.reshape(N, 6)[perm[real]], rtol=1e-9, atol=1e-12)
+    assert not rb[:6 * rows].reshape(rows, 6)[~real].any()     # padding rows are decoupled zeros
+    np.testing.assert_allclose(rb[6 * rows:6 * rows + 3].sum(), sysd["loss2"], rtol=1e-9)
 
 
 def test_gn_repeatable(cuda, golden_dir):

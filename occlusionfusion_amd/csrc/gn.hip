@@ -71,7 +71,11 @@ struct Gn {
   double* res = nullptr;         // T*3
   int64_t T_cap = 0;
   // pattern + contribution lists
-  int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;
+  int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;   // row_cnt[N]: max row length
+  int2* wl = nullptr;            // per PCG wave: its first kWL blocks (CSR order) as (col, slot); (-1, 0) = none
+  int max_deg = 0;               // longest block row of the pattern
+  int max_wave = 0;              // most blocks of one PCG wave (kCS rows)
+  int32_t* stopw = nullptr;      // per PCG wave and lane: 1 once the current solve has converged
   int32_t* blk_row = nullptr;    // block -> row (clears the slot map's pattern at the next setup)
   int pat_N = 0;                 // N and block count of the pattern currently set in `map`
   int64_t pat_nnzb = 0;
@@ -96,7 +100,8 @@ struct Gn {
   double* loss_log = nullptr;
   double* stat = nullptr;         // kMaxLog x [pcg iterations, |b|², loss] of the last solve
   double* step_state = nullptr;   // (kMaxLog+1) x [previous loss, accepted steps] before each GN step
-  // Galerkin warm start over the last kProj GN-step solutions of this solve (ring of kProj x 6N each):
+  // Galerkin warm start over the last kProj GN-step solutions of this solve (ring of kProj x 6N each;
+  // the previous frame's solutions were measured not to help its first steps):
   // xh = previous solutions, th = A·xh
   double *xh = nullptr, *th = nullptr;
   int n_prev = 0;                 // valid entries of the ring for the current step
@@ -269,6 +274,8 @@ __global__ void k_mark(Gn g) {
   }
 }
 
+// cnt[i] = blocks of row i; cnt[N] = max over rows (zeroed by the caller); cnt[N + 1] is set later
+// to the longest PCG wave (k_wave_max)
 __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restrict__ map, int32_t* __restrict__ cnt) {
   __shared__ int s[256];
   int i = blockIdx.x;
@@ -280,7 +287,22 @@ __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restr
     if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) cnt[i] = s[0];
+  if (threadIdx.x == 0) { cnt[i] = s[0]; atomicMax(&cnt[N], s[0]); }
+}
+
+// Per PCG wave (kCS consecutive rows = one contiguous CSR range) the (col, slot) of its first kWL
+// blocks, so the iteration reads its gather addresses without the row_ptr -> col chain
+constexpr int kWL = 128;
+__global__ __launch_bounds__(256) void k_wave_max(int nwave, const int32_t* __restrict__ row_ptr, int32_t* __restrict__ out) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < nwave) atomicMax(out, row_ptr[(w + 1) * kCS] - row_ptr[w * kCS]);
+}
+__global__ __launch_bounds__(256) void k_wave_list(Gn g) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= (int64_t)(g.N / kCS) * kWL) return;
+  const int w = (int)(e / kWL), k = (int)(e % kWL);
+  const int b = g.row_ptr[w * kCS] + k;
+  g.wl[e] = b < g.row_ptr[(w + 1) * kCS] ? make_int2(g.col[b], b) : make_int2(-1, 0);
 }
 
 // exclusive scan of cnt[0..n) into off[0..n] (off[n] = total), single workgroup: contiguous chunk
@@ -1010,6 +1032,7 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
   if (own) s_v[6 * r + q] = w;
   __syncthreads();
   double d[4] = {0.0, 0.0, 0.0, 0.0};
+  g.stopw[(int64_t)blockIdx.x * 64 + lane] = 0;
   if (own) {
     const double m = apply_mrow(mr, s_v);
     v[V_W] = w;
@@ -1028,104 +1051,190 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
   }
 }
 
-// One PCG iteration; par = parity of the iteration (iteration i has par = i & 1), first = 1 only for
+// One PCG iteration; par = parity of the iteration (iteration i has par = i & 1), kFirst only for
 // iteration 0. Reads partials[par], m[par] and alpha/gamma[par^1]; writes partials[par^1], m[par^1]
 // and alpha/gamma[par]. The count of executed iterations lives in flags[F_PCG_CNT] (the lead lane
-// increments it). Everything this launch needs — previous partials, own-row state, the cluster
-// inverse row, A blocks, m gather — is loaded up front; the scalars are uniform per wave and the
-// cluster exchange is wave-local, so the only barrier is the single-wave LDS handoff.
-__global__ __launch_bounds__(64) void k_pcg_iter(Gn g, int par, int first) {
+// increments it).
+// Latency structure (one wave per cluster = workgroup): exactly two dependent memory trips, every
+// load unconditional (clamped addresses, masked values) so no branch splits a trip. Trip 1: the
+// wave's block list, previous partials, own-row state, own m, and the cluster inverse straight to
+// LDS (LDS-DMA: no VGPRs held). Trip 2: A blocks and gathered m — lane l multiplies the wave's
+// blocks l and l + 64 (balanced over the cluster's rows, whatever their lengths); the products
+// meet in LDS and each row sums its blocks in CSR order (fixed order: deterministic).
+// Convergence is decided from the partials alone and carried forward through them and a per-lane
+// stop word: a converged (or broken-down) launch copies its wave's partials (rr = 0 on breakdown)
+// into the next parity and sets the stop words, so later launches of the chunk end after trip 1.
+// kWave = false: plain CSR rows (waves of more than kWL blocks or rows longer than kRowMax).
+constexpr int kRowMax = 24;
+template <bool kWave, bool kFirst, int kU>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(Gn g, int par) {
+  constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   __shared__ double s_v[kCD];
+  __shared__ float4 s_m[kCD * kCD / 4];
+  __shared__ double s_prod[kWave ? kWL * 6 : 1];
   const int lane = threadIdx.x;
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
   const int nw = g.nwg_row;
   const double* __restrict__ mc = par ? g.m1 : g.m0;
   double* __restrict__ mn = par ? g.m0 : g.m1;
-  // 1. issue every independent load: stop flags and scalars (scalar loads), previous partials,
-  //    own-row state, cluster-inverse row, own m, the row's block range
-  const int stop = g.flags[F_DONE] | g.flags[F_STOPPED];
-  const int cnt = g.flags[F_PCG_CNT];
-  const double gam_prev = first ? 1.0 : g.pcg_gamma[par ^ 1];
-  const double alpha_prev = first ? 1.0 : g.pcg_alpha[par ^ 1];
-  const double bb_stored = g.scal[S_BB];
   const int ns = g.nw_pad;
-  double2 tp[3][4];
-  double tb[1][8];
-  load_streams2<3, 4>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp);
-  if (first) load_streams<1, 8>(g.part_b, nw, tb);
+  const double* Pc = g.part_p + 3 * (int64_t)ns * par;
+  double* Pn = g.part_p + 3 * (int64_t)ns * (par ^ 1);
   const bool own = q < 6;
-  const int64_t o = 6 * (int64_t)row + q;
-  double v[V_N], m = 0.0;
-  float4 mr[kCD / 4];
-#pragma unroll
-  for (int k = 0; k < V_N; ++k) v[k] = 0.0;
-  if (own) {
-    load_rec(g.st, o, v);
-    load_mrow(g, o, mr);
-    m = mc[o];
+  const int qc = own ? q : 5;
+  const int64_t o = 6 * (int64_t)row + qc;
+  // ---- trip 1 (block list first: trip 2 waits only for it)
+  int2 bl0 = make_int2(-1, 0), bl1 = make_int2(-1, 0);
+  if (kWave) {
+    bl0 = g.wl[(int64_t)wv * kWL + lane];
+    bl1 = g.wl[(int64_t)wv * kWL + 64 + lane];
   }
+  const int stop = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
+  const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-  // 2. after convergence the remaining launches of the chunk end here (one scalar round trip)
+  const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
+#pragma unroll
+  for (int k = 0; k < kMS; ++k)
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + k * 64 + lane), reinterpret_cast<void*>(s_m + k * 64), 16, 0, 0);
+  double v[V_N];
+  load_rec(g.st, o, v);
+  const double m = mc[o];
+  double2 tp[3][kU];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = 2 * (lane + 64 * u);
+      tp[k][u] = *reinterpret_cast<const double2*>(Pc + (int64_t)k * ns + (i < ns ? i : ns - 2));
+    }
+  double tb[kFirst ? 2 * kU : 1];
+  if (kFirst)
+#pragma unroll
+    for (int u = 0; u < 2 * kU; ++u) tb[u] = g.part_b[min(lane + 64 * u, nw - 1)];
+  double own_p[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * ns + wv];
+  const int cnt = g.flags[F_PCG_CNT];
+  const double gam_prev = kFirst ? 1.0 : g.pcg_gamma[par ^ 1];
+  const double alpha_prev = kFirst ? 1.0 : g.pcg_alpha[par ^ 1];
+  const double bb_stored = g.scal[S_BB];
+  // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
+  // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
   if (stop) return;
-  // 3. SpMV n = A m (gather chain), then the scalars from the partials (long arrived)
+  // ---- trip 2: n = A m
   double n[6];
-  row_spmv(g, b0, b1, q, mc, n);
+  if (kWave) {
+    double pr[2][6];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked)
+      const int2 e = j ? bl1 : bl0;
+      const bool ok = e.x >= 0;
+      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e.y);
+      const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(ok ? e.x : 0));
+      double x[6];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { const double2 t = vc[k]; x[2 * k] = t.x; x[2 * k + 1] = t.y; }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+        const double t = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+        pr[j][i] = ok ? t : 0.0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) s_prod[(j * 64 + lane) * 6 + i] = pr[j][i];
+    __syncthreads();
+    // row sums in CSR order (rows of at most kRowMax blocks; unrolled, masked LDS reads)
+    const int lb = b0 - wb0, len = b1 - b0;
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRowMax; ++k) {
+      const double t = s_prod[(lb + (k < len ? k : 0)) * 6 + qc];
+      a += k < len ? t : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) n[i] = i == qc ? a : 0.0;
+  } else {
+    row_spmv(g, b0, b1, q, mc, n);
+  }
+  // ---- scalars
   double pa[3];
-  reduce_streams2<3, 4>(g.part_p + 3 * (int64_t)ns * par, nw, ns, tp, pa);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = 2 * (lane + 64 * u);
+      t += i < nw ? tp[k][u].x + (i + 1 < nw ? tp[k][u].y : 0.0) : 0.0;
+    }
+    pa[k] = wave_sum(t);
+  }
   double bb = bb_stored;
-  if (first) {
-    double t[1];
-    reduce_streams<1, 8>(g.part_b, nw, tb, t);
-    bb = t[0];
+  if (kFirst) {
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < 2 * kU; ++u) t += lane + 64 * u < nw ? tb[u] : 0.0;
+    bb = wave_sum(t);
   }
   const double gam = pa[0], del = pa[1], rr = pa[2];
   const double tol = g.prm.pcg_tol;
   const bool lead = wv == 0 && lane == 0;
-  if (first && lead) g.scal[S_BB] = bb;
-  if (rr <= tol * tol * bb || gam == 0.0) {
-    if (lead) { g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt; }
-    return;
-  }
+  if (kFirst && lead) g.scal[S_BB] = bb;
   double beta = 0.0, alpha;
-  if (first) {
+  if (kFirst) {
     alpha = gam / del;
   } else {
     beta = gam / gam_prev;
     alpha = gam / (del - beta * gam / alpha_prev);
   }
-  if (!isfinite(alpha) || !(alpha > 0.0)) {  // breakdown (A SPD => alpha > 0): keep x
-    if (lead) {
+  const bool conv = rr <= tol * tol * bb || gam == 0.0;
+  if (conv || !isfinite(alpha) || !(alpha > 0.0)) {   // converged, or breakdown (A SPD => alpha > 0): keep x
+    if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
+    g.stopw[(int64_t)wv * 64 + lane] = 1;
+    if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
-      if (!isfinite(alpha)) g.flags[F_ILL] = 1;
+      if (!conv && !isfinite(alpha)) g.flags[F_ILL] = 1;
     }
     return;
   }
   if (lead) { g.pcg_alpha[par] = alpha; g.pcg_gamma[par] = gam; g.flags[F_PCG_CNT] = cnt + 1; }
   double d[3] = {0.0, 0.0, 0.0};
-  double w2 = 0.0, rn = 0.0, un = 0.0;
-  const double nc = pick6(n, q);
-  if (own) {
+  const double nc = pick6(n, qc);
+  {
     const double zz = nc + beta * v[V_Z];
     const double qq = m + beta * v[V_Q];
     const double sv = v[V_W] + beta * v[V_S];
     const double p = v[V_U] + beta * v[V_P];
-    rn = v[V_R] - alpha * sv;
-    un = v[V_U] - alpha * qq;
-    w2 = v[V_W] - alpha * zz;
-    const double nv[V_N] = {v[V_X] + alpha * p, rn, un, zz, qq, sv, p, w2};
-    store_rec(g.st, o, nv);
-    s_v[6 * r + q] = w2;
-    d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
+    const double rn = v[V_R] - alpha * sv;
+    const double un = v[V_U] - alpha * qq;
+    const double w2 = v[V_W] - alpha * zz;
+    if (own) {
+      const double nv[V_N] = {v[V_X] + alpha * p, rn, un, zz, qq, sv, p, w2};
+      store_rec(g.st, o, nv);
+      s_v[6 * r + q] = w2;
+      d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
+    }
   }
   __syncthreads();
-  if (own) mn[o] = apply_mrow(mr, s_v);      // m of the next iteration: M⁻¹ w_new, cluster-local
+  if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (inverse rows staged in LDS)
+    const float4* mrow = s_m + (6 * r + q) * (kCD / 4);
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < kCD / 4; ++k) {
+      const float4 t = mrow[k];
+      a += (((double)t.x * s_v[4 * k] + (double)t.y * s_v[4 * k + 1]) +
+            ((double)t.z * s_v[4 * k + 2] + (double)t.w * s_v[4 * k + 3]));
+    }
+    mn[o] = a;
+  }
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
-  if (lane == 0) {
-    double* P = g.part_p + 3 * (int64_t)ns * (par ^ 1);
-    P[wv] = d[0]; P[ns + wv] = d[1]; P[2 * ns + wv] = d[2];
-  }
+  if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
 }
 
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
@@ -1228,7 +1337,7 @@ static double lm_for_iter(double lm0, int gn_iter) {
 
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
-                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->blk_off, g->blk_cnt,
+                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->stopw, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
@@ -1305,7 +1414,7 @@ static void order_rows(int N, int NB, const float* nodes, const int32_t* edges, 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
   g->warm_now = 0;
-  if (g->prm.pcg_warm && gn_iter > 0) {   // k_apply of the previous steps filled the ring
+  if (g->prm.pcg_warm && gn_iter > 0) {   // k_step of the previous steps filled the ring
     g->n_prev = gn_iter < kProj ? gn_iter : kProj;
     g->warm_now = 1;
   }
@@ -1330,12 +1439,19 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const int max_it = g->prm.pcg_max_iter;
   const int lp = g->last_pcg[gn_iter & 63];
   const dim3 grid(g->nwg_row), block(64);
+  // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width for up to 384 / 2176 waves
+  const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
+  const bool small = g->nwg_row <= 2 * 64 * 3;
+  auto iter0 = wave ? (small ? k_pcg_iter<true, true, 3> : k_pcg_iter<true, true, 17>)
+                    : (small ? k_pcg_iter<false, true, 3> : k_pcg_iter<false, true, 17>);
+  auto iter = wave ? (small ? k_pcg_iter<true, false, 3> : k_pcg_iter<true, false, 17>)
+                   : (small ? k_pcg_iter<false, false, 3> : k_pcg_iter<false, false, 17>);
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(k_pcg_iter, grid, block, 0, hs, *g, it & 1, it == 0 ? 1 : 0);
+      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block, 0, hs, *g, it & 1);
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
@@ -1375,12 +1491,12 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->nodes, 3 * N); ALLOC(g->tpos, 3 * N); ALLOC(g->conf, N);
   ALLOC(g->src, 3 * M); ALLOC(g->wts, 4 * M); ALLOC(g->tgt, 3 * M); ALLOC(g->tpx, M); ALLOC(g->tpy, M);
   ALLOC(g->anc, 4 * M);
-  ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 1);
+  ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 2);
   ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
   ALLOC(g->Mcl, 6 * N * kCD); ALLOC(g->st, V_N * 6 * N); ALLOC(g->m0, 6 * N); ALLOC(g->m1, 6 * N);
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
-  ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes);
+  ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes); ALLOC(g->wl, N / kCS * kWL); ALLOC(g->stopw, N / kCS * 64);
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
@@ -1542,12 +1658,17 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   // terms -> block pattern
   unsigned gT = grid_for(g->T, 256, 1 << 30);
   hipLaunchKernelGGL(k_mark, dim3(gT), dim3(256), 0, hs, *g);
+  OFX_HIP(hipMemsetAsync(g->row_cnt + N, 0, 2 * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_row_count, dim3(N), dim3(256), 0, hs, N, g->map, g->row_cnt);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr);
+  hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
-  int32_t nnz = 0;
+  int32_t nnz = 0, lens[2] = {0, 0};
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipMemcpyAsync(lens, g->row_cnt + N, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
+  g->max_deg = lens[0];
+  g->max_wave = lens[1];
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
     for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->blk_off,
                     (void**)&g->blk_cnt})
@@ -1561,6 +1682,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   }
   g->nnzb = nnz;
   hipLaunchKernelGGL(k_row_assign, dim3(N), dim3(256), 0, hs, N, g->map, g->row_ptr, g->col, g->blk_row);
+  hipLaunchKernelGGL(k_wave_list, dim3(grid_for((int64_t)(N / kCS) * kWL, 256, 1 << 30)), dim3(256), 0, hs, *g);
   g->pat_N = N;
   g->pat_nnzb = nnz;
   // contribution lists (sorted -> deterministic assembly order)
@@ -1591,7 +1713,6 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   OFX_CHECK_ARG(A && rhs, "null A/rhs");
   OFX_CHECK_ARG(m0 >= 0 && m1 <= g->M && m0 <= m1, "bad match range [%d,%d) of %d", m0, m1, g->M);
   // A: nnz_blocks x 36 f64, rhs: 6·rows + 4 f64 (rows = ofx_gn_info()[4])
-  (void)gn_iter;
   hipStream_t hs = as_stream(s);
   DataCoef dc;
   dc.lf = sqrt(g->prm.lambda_flow); dc.ld = sqrt(g->prm.lambda_depth);

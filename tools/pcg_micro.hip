@@ -26,6 +26,10 @@ struct Sys {
   unsigned* bar;   // grid barrier: [0] arrivals, [1] generation, [2] timeout flag
   float* Mcl;      // cluster preconditioner rows: (rows*6) x 48 f32
   double *mv0, *mv1;
+  int* ecol;       // ELL: 16 block slots per row (-1 = empty)
+  double* Bell;    // ELL blocks (N x 16 x 36)
+  int* flags;
+  double* scal;
 };
 
 __device__ __forceinline__ double red8(double a) {
@@ -556,8 +560,14 @@ __global__ __launch_bounds__(64) void k_persist(Sys s, int iters) {
 // Cluster-preconditioned explicit pipelined iteration: 8 rows per wave (one 8-node cluster, 8 lanes per
 // row), n = A m (m gathered), recurrences incl. w in the state record, then m_new = M_cl⁻¹ w_new via LDS
 // (48x48 f32 rows, loaded up front).
-__global__ __launch_bounds__(64) void k_iterc(Sys s, int it) {
+struct SysBig { Sys s; char pad[1024]; };
+template <bool ELL, bool FLAGS, typename SY>
+__global__ __launch_bounds__(64) void k_iterc_t(SY sy, int it) {
+  const Sys& s = reinterpret_cast<const Sys&>(sy);
   __shared__ double s_w[48];
+  int stop = 0, cnt = 0;
+  double gp = 1.0, ap = 1.0;
+  if (FLAGS) { stop = s.flags[0] | s.flags[1]; cnt = s.flags[2]; gp = s.scal[it & 1]; ap = s.scal[2 + (it & 1)]; }
   const int lane = threadIdx.x;
   const int r = lane >> 3, q = lane & 7;
   const int row = blockIdx.x * 8 + r;
@@ -581,7 +591,24 @@ __global__ __launch_bounds__(64) void k_iterc(Sys s, int it) {
     for (int k = 0; k < 12; ++k) mrow[k] = M[k];
   }
   double n[6] = {0, 0, 0, 0, 0, 0};
-  if (row < N) {
+  if (FLAGS && stop) return;
+  if (ELL && row < N) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int64_t e = (int64_t)row * 16 + q + 8 * k;
+      const int c = s.ecol[e];
+      if (c < 0) continue;
+      const double2* blk = reinterpret_cast<const double2*>(s.Bell + 36 * e);
+      const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)c);
+      double x[6];
+      for (int j = 0; j < 3; ++j) { double2 a = vc[j]; x[2 * j] = a.x; x[2 * j + 1] = a.y; }
+      for (int i = 0; i < 6; ++i) {
+        double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+        n[i] += ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+      }
+    }
+  }
+  if (!ELL && row < N) {
     const int b0 = s.row_ptr[row], b1 = s.row_ptr[row + 1];
     for (int bi = b0 + q; bi < b1; bi += 8) {
       const double2* blk = reinterpret_cast<const double2*>(s.B + 36 * (int64_t)bi);
@@ -601,7 +628,13 @@ __global__ __launch_bounds__(64) void k_iterc(Sys s, int it) {
     for (int u = 0; u < 4; ++u) a += t[k][u].x + t[k][u].y;
     pa[k] = wave_sum(a);
   }
-  const double al = 1e-3 + 1e-12 * pa[0], be = 1e-3 + 1e-12 * pa[1];
+  double al = 1e-3 + 1e-12 * pa[0], be = 1e-3 + 1e-12 * pa[1];
+  if (FLAGS) {
+    be = 1e-3 + 1e-12 * (pa[0] / gp);
+    al = 1e-3 + 1e-12 * (pa[0] / (pa[1] - be * pa[0] / ap));
+    if (pa[2] < -1.0) return;
+    if (blockIdx.x == 0 && lane == 0) { s.scal[(it + 1) & 1] = 1.0 + 1e-30 * pa[0]; s.scal[2 + ((it + 1) & 1)] = 1.0 + 1e-30 * al; s.flags[2] = cnt + 1; }
+  }
   double nc = 0.0;
   for (int i = 0; i < 6; ++i) nc += n[i] * (q == i ? 1.0 : 0.0);
   double d[3] = {0, 0, 0};
@@ -764,9 +797,30 @@ int main() {
   }
   CK(hipMalloc(&s.Mcl, (size_t)6 * N * 48 * 4)); CK(hipMemset(s.Mcl, 0, (size_t)6 * N * 48 * 4));
   for (double** p : {&s.mv0, &s.mv1}) { CK(hipMalloc(p, 6 * N * 8)); CK(hipMemset(*p, 0, 6 * N * 8)); }
+  {
+    std::vector<int> ec((size_t)N * 16, -1);
+    for (int i = 0; i < N; ++i)
+      for (int k = rp[i]; k < rp[i + 1]; ++k) ec[(size_t)i * 16 + (k - rp[i])] = cl[k];
+    CK(hipMalloc(&s.ecol, ec.size() * 4)); CK(hipMemcpy(s.ecol, ec.data(), ec.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMalloc(&s.Bell, (size_t)N * 16 * 36 * 8)); CK(hipMemset(s.Bell, 0, (size_t)N * 16 * 36 * 8));
+    CK(hipMalloc(&s.flags, 64)); CK(hipMemset(s.flags, 0, 64));
+    CK(hipMalloc(&s.scal, 64)); CK(hipMemset(s.scal, 0, 64));
+  }
+  SysBig sb{};
+  sb.s = s;
+  auto runc = [&](const char* name, auto k, auto arg) {
+    s.nwaves = (N + 7) / 8;
+    sb.s = s;
+    printf("%-16s %7.2f us\n", name, timeit([&](int i) { hipLaunchKernelGGL(k, dim3(s.nwaves), dim3(64), 0, 0, arg, i); }));
+  };
   for (int rep = 0; rep < 3; ++rep) {
-    runw("iterc cluster8", k_iterc, 8);
-    runw("iterw4 soa dpp", k_iterw<4, 2>, 4);
+    s.nwaves = (N + 7) / 8; sb.s = s;
+    runc("iterc csr", k_iterc_t<false, false, Sys>, s);
+    runc("iterc ell", k_iterc_t<true, false, Sys>, s);
+    runc("iterc csr+flags", k_iterc_t<false, true, Sys>, s);
+    runc("iterc ell+flags", k_iterc_t<true, true, Sys>, s);
+    runc("iterc csr+fl+big", k_iterc_t<false, true, SysBig>, sb);
+    runc("iterc ell+fl+big", k_iterc_t<true, true, SysBig>, sb);
   }
   for (int rep = 0; rep < 0; ++rep) {
     runw("iters push", k_iters<true>, 4);

@@ -106,7 +106,8 @@ struct Gn {
   double *xh = nullptr, *th = nullptr;
   int n_prev = 0;                 // valid entries of the ring for the current step
   int warm_now = 0;               // this step starts from the projected x0
-  int32_t* host_flags = nullptr;  // pinned
+  int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED] mirrored by the kernels
+  int32_t* hflags = nullptr;      // its device address (system-scope stores: no copy kernel per poll)
   int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
   bool setup_done = false;
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
@@ -118,6 +119,10 @@ struct Gn {
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
 enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
+enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_COUNT = 4 };
+__device__ __forceinline__ void host_flag(const int32_t* hf, int k, int v) {
+  __hip_atomic_store(const_cast<int32_t*>(hf) + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 
 // ---------------------------------------------------------------------------- reductions
@@ -231,6 +236,7 @@ __global__ __launch_bounds__(256) void k_upload(Gn g, Upload u) {
     for (int k = 0; k < 4; ++k) g.term_node[i * 4 + k] = n[k];
   }
   if (i < F_COUNT) g.flags[i] = 0;
+  if (i < H_COUNT) host_flag(g.hflags, (int)i, 0);
   if (i < S_COUNT) g.scal[i] = 0.0;
   if (i < 3 * kMaxLog) g.stat[i] = 0.0;
   if (i < 2 * (kMaxLog + 1)) g.step_state[i] = 0.0;
@@ -274,8 +280,7 @@ __global__ void k_mark(Gn g) {
   }
 }
 
-// cnt[i] = blocks of row i; cnt[N] = max over rows (zeroed by the caller); cnt[N + 1] is set later
-// to the longest PCG wave (k_wave_max)
+// cnt[i] = blocks of row i
 __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restrict__ map, int32_t* __restrict__ cnt) {
   __shared__ int s[256];
   int i = blockIdx.x;
@@ -287,7 +292,7 @@ __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restr
     if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) { cnt[i] = s[0]; atomicMax(&cnt[N], s[0]); }
+  if (threadIdx.x == 0) cnt[i] = s[0];
 }
 
 // Per PCG wave (kCS consecutive rows = one contiguous CSR range) the (col, slot) of its first kWL
@@ -307,16 +312,30 @@ __global__ __launch_bounds__(256) void k_wave_list(Gn g) {
 
 // exclusive scan of cnt[0..n) into off[0..n] (off[n] = total), single workgroup: contiguous chunk
 // per thread, one block scan of the chunk sums
-__global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restrict__ cnt, int32_t* __restrict__ off) {
+// (max_out, nullable: max of cnt)
+__global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restrict__ cnt, int32_t* __restrict__ off,
+                                               int32_t* __restrict__ max_out) {
   __shared__ int s_w[16];
+  __shared__ int s_mx[16];
   const int64_t per = (n + blockDim.x - 1) / blockDim.x;
   const int64_t s = threadIdx.x * per, e = min(n, s + per);
-  int c = 0;
-  for (int64_t i = s; i < e; ++i) c += cnt[i];
+  int c = 0, mx = 0;
+  for (int64_t i = s; i < e; ++i) { c += cnt[i]; mx = max(mx, cnt[i]); }
   int total;
   int o = block_exscan(c, s_w, total);
   for (int64_t i = s; i < e; ++i) { off[i] = o; o += cnt[i]; }
   if (threadIdx.x == 0) off[n] = total;
+  if (max_out) {
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) mx = max(mx, __shfl_xor(mx, k, 64));
+    if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int m = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = max(m, s_mx[w]);
+      *max_out = m;
+    }
+  }
 }
 
 // ordered slot assignment per block row (one WG per row, one pass): contiguous column chunk per
@@ -776,7 +795,10 @@ __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const dou
 __global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
                                                  const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
+    host_flag(g.hflags, H_DONE, 0);
+  }
   const int lane = threadIdx.x;
   const int base = blockIdx.x * kCS;
   const int ti = lane / kCS, tj = lane % kCS;
@@ -1199,6 +1221,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
       if (!conv && !isfinite(alpha)) g.flags[F_ILL] = 1;
+      host_flag(g.hflags, H_PCG_IT, cnt);
+      host_flag(g.hflags, H_DONE, 1);
     }
     return;
   }
@@ -1266,6 +1290,7 @@ __global__ __launch_bounds__(256) void k_step(Gn g, const double* __restrict__ r
       g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
       if (stop) {
         g.flags[F_STOPPED] = 1;
+        host_flag(g.hflags, H_STOPPED, 1);
       } else {
         if (acc < n_iter_log) {
           g.loss_log[4 * acc + 0] = loss;
@@ -1454,10 +1479,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block, 0, hs, *g, it & 1);
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
-    OFX_HIP(hipMemcpyAsync(g->host_flags, g->flags, F_COUNT * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-    OFX_HIP(hipStreamSynchronize(hs));
-    if (g->host_flags[F_DONE] || g->host_flags[F_STOPPED]) {
-      if (g->host_flags[F_DONE]) g->last_pcg[gn_iter & 63] = g->host_flags[F_PCG_IT];
+    OFX_HIP(hipStreamSynchronize(hs));   // the kernels mirror done / count / stopped into host memory
+    const volatile int32_t* hf = g->host_flags;
+    if (hf[H_DONE] || hf[H_STOPPED]) {
+      if (hf[H_DONE]) g->last_pcg[gn_iter & 63] = hf[H_PCG_IT];
       break;
     }
     chunk = 8;
@@ -1505,7 +1530,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess) {   // pattern entries are cleared per setup
     free_all(g); delete g; set_error("hipMemset failed"); return OFX_ERR_HIP;
   }
-  if (hipHostMalloc((void**)&g->host_flags, F_COUNT * sizeof(int32_t), 0) != hipSuccess) {
+  if (hipHostMalloc((void**)&g->host_flags, H_COUNT * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
 
@@ -1658,9 +1684,9 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   // terms -> block pattern
   unsigned gT = grid_for(g->T, 256, 1 << 30);
   hipLaunchKernelGGL(k_mark, dim3(gT), dim3(256), 0, hs, *g);
-  OFX_HIP(hipMemsetAsync(g->row_cnt + N, 0, 2 * sizeof(int32_t), hs));
+  OFX_HIP(hipMemsetAsync(g->row_cnt + N + 1, 0, sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_row_count, dim3(N), dim3(256), 0, hs, N, g->map, g->row_cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N);
   hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
   int32_t nnz = 0, lens[2] = {0, 0};
@@ -1689,8 +1715,8 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
   OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_pair_count, dim3(gT), dim3(256), 0, hs, *g);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->blk_off);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->node_cnt, g->node_off);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->blk_off, (int32_t*)nullptr);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->node_cnt, g->node_off, (int32_t*)nullptr);
   OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
   OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_pair_scatter, dim3(gT), dim3(256), 0, hs, *g);
@@ -1763,7 +1789,7 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     if (st) return st;
     // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
     // decision: a stop costs at most one extra (no-op) linearisation instead of a sync per step
-    if (g->host_flags[F_STOPPED]) break;
+    if (((const volatile int32_t*)g->host_flags)[H_STOPPED]) break;
   }
   return ofx_gn_finish(handle, res, s);
 }

@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must precede loading libofx)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libofx.so")
+LIB_PATH = os.environ.get("OFX_LIB") or os.path.join(_HERE, "libofx.so")   # OFX_LIB: tuning builds (tools/)
 
 c_int32, c_int64, c_double, c_float, c_void_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_float, ctypes.c_void_p
 P = ctypes.c_void_p  # device pointer

@@ -35,30 +35,33 @@ def up_to_date():
     return all(os.path.getmtime(p) <= t for p in _deps())
 
 
-def _compile(src):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+def _compile(src, obj_dir=OBJ, defines=()):
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj
 
 
-def build(force=False, verbose=False):
-    if not force and up_to_date():
+def build(force=False, verbose=False, out=None, defines=()):
+    """out/defines: tuning builds (e.g. tools/bin/libofx_stamps.so with OFX_STAMPS); default = the product."""
+    lib = out or LIB
+    if not force and out is None and up_to_date():
         return LIB
-    os.makedirs(OBJ, exist_ok=True)
+    obj_dir = OBJ if out is None else OBJ + "_" + os.path.splitext(os.path.basename(out))[0]
+    os.makedirs(obj_dir, exist_ok=True)
     srcs = _sources()
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+        objs = list(ex.map(lambda s: _compile(s, obj_dir, defines), srcs))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 if __name__ == "__main__":

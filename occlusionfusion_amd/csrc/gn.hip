@@ -76,6 +76,7 @@ struct Gn {
   int max_deg = 0;               // longest block row of the pattern
   int max_wave = 0;              // most blocks of one PCG wave (kCS rows)
   int32_t* stopw = nullptr;      // per PCG wave and lane: 1 once the current solve has converged
+  uint64_t* stamps = nullptr;    // tuning builds (-DOFX_STAMPS): per iteration < 64 and wave, 8 clock stamps
   int32_t* blk_row = nullptr;    // block -> row (clears the slot map's pattern at the next setup)
   int pat_N = 0;                 // N and block count of the pattern currently set in `map`
   int64_t pat_nnzb = 0;
@@ -86,7 +87,7 @@ struct Gn {
   // state
   double *R = nullptr, *t = nullptr;
   double *A_own = nullptr, *rhs_own = nullptr;
-  float* Mcl = nullptr;           // cluster inverse rows (6N x 6kCS, f32)
+  float* Mcl = nullptr;           // cluster inverses, f32, per cluster 48x48 in the lane-interleaved order of mcl_idx
   const double* Aop = nullptr;    // PCG operator (the damped A of the current step)
   double *st = nullptr;          // PCG recurrence state, 6N records of 8 (see the PCG layout note)
   double *m0 = nullptr, *m1 = nullptr;   // double-buffered m = M⁻¹w (gathered by the SpMV)
@@ -94,7 +95,8 @@ struct Gn {
   int64_t pcg_cap = 0;
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
-  int32_t nw_pad = 0;            // stride of the iteration partial streams (nwg_row rounded up to even)
+  int32_t nw_pad = 0;            // stride of the iteration partial streams: 128·pcg_ku, zero beyond nwg_row
+  int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (3: <= 384 waves, else 17)
   double* scal = nullptr;
   int32_t* flags = nullptr;
   double* loss_log = nullptr;
@@ -769,11 +771,17 @@ __device__ __forceinline__ void store_rec(double* __restrict__ st, int64_t o, co
 #pragma unroll
   for (int k = 0; k < V_N / 2; ++k) p[k] = make_double2(v[2 * k], v[2 * k + 1]);
 }
+// Cluster inverse storage: entry (i, j) of a cluster's 48x48 block at float (j/4 · 48 + i) · 4 + j%4,
+// so row i's k-th float4 sits at float4 index k·48 + i: the 48 rows' float4 k are contiguous (LDS
+// reads by 48 lanes are bank-conflict free; the block is staged to LDS as one linear image).
+__device__ __forceinline__ int64_t mcl_idx(int64_t cluster, int i, int j) {
+  return cluster * kCD * kCD + ((j >> 2) * kCD + i) * 4 + (j & 3);
+}
 // The row's (r, c) f32 row of the cluster inverse, 12 x 16-B loads.
 __device__ __forceinline__ void load_mrow(const Gn& g, int64_t o, float4 mr[kCD / 4]) {
-  const float4* p = reinterpret_cast<const float4*>(g.Mcl + o * kCD);
+  const float4* p = reinterpret_cast<const float4*>(g.Mcl + mcl_idx(o / kCD, (int)(o % kCD), 0));
 #pragma unroll
-  for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k];
+  for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k * kCD];
 }
 // (M⁻¹ v)_(r,c) with v the wave's cluster vector staged in LDS (s_v[6 r' + c'], f64)
 __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const double* s_v) {
@@ -856,11 +864,11 @@ __global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __rest
       m[r][c] = bad ? ((ti == tj && r == c) ? 1.f : 0.f) : (float)(0.5 * (a[r][c] + t));
     }
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    float2* row = reinterpret_cast<float2*>(g.Mcl + ((int64_t)(base + ti) * 6 + r) * kCD + 6 * tj);
+  for (int r = 0; r < 6; ++r)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) row[c] = make_float2(m[r][2 * c], m[r][2 * c + 1]);
-  }
+    for (int c = 0; c < 3; ++c)   // (j, j+1) with j even share a float4
+      *reinterpret_cast<float2*>(g.Mcl + mcl_idx(blockIdx.x, 6 * ti + r, 6 * tj + 2 * c)) =
+          make_float2(m[r][2 * c], m[r][2 * c + 1]);
   if (g.warm_now) return;
   // cold start: u = M⁻¹ b with the stored (f32) operator; the 8 lanes of a block row sum in fixed order
   double bj[6], u[6];
@@ -1064,13 +1072,17 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) d[k] = wave_sum(d[k]);
+  const int ns = g.nw_pad;
   if (lane == 0) {
-    const int ns = g.nw_pad;
     g.part_p[blockIdx.x] = d[0]; g.part_p[ns + blockIdx.x] = d[1]; g.part_p[2 * ns + blockIdx.x] = d[2];
     g.part_b[blockIdx.x] = d[3];
-    if (blockIdx.x == 0 && ns > g.nwg_row)   // pad slot of every iteration stream (part_p is also proj scratch)
-      for (int k = 0; k < 6; ++k) g.part_p[k * ns + g.nwg_row] = 0.0;
   }
+  if (blockIdx.x == 0)   // zero tails of both parities' streams (part_p is also proj scratch) and of part_b
+    for (int i = g.nwg_row + lane; i < ns; i += 64) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g.part_p[k * ns + i] = 0.0;
+      g.part_b[i] = 0.0;
+    }
 }
 
 // One PCG iteration; par = parity of the iteration (iteration i has par = i & 1), kFirst only for
@@ -1087,13 +1099,19 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
 // stop word: a converged (or broken-down) launch copies its wave's partials (rr = 0 on breakdown)
 // into the next parity and sets the stop words, so later launches of the chunk end after trip 1.
 // kWave = false: plain CSR rows (waves of more than kWL blocks or rows longer than kRowMax).
-constexpr int kRowMax = 24;
+constexpr int kRowMax = 20;
+#ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
+#define OFX_STAMP(k)                                                                                  \
+  if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OFX_STAMP(k)
+#endif
 template <bool kWave, bool kFirst, int kU>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(Gn g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   __shared__ double s_v[kCD];
   __shared__ float4 s_m[kCD * kCD / 4];
-  __shared__ double s_prod[kWave ? kWL * 6 : 1];
+  __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   const int lane = threadIdx.x;
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
@@ -1107,6 +1125,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int qc = own ? q : 5;
   const int64_t o = 6 * (int64_t)row + qc;
   // ---- trip 1 (block list first: trip 2 waits only for it)
+#ifdef OFX_STAMPS
+  const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
   int2 bl0 = make_int2(-1, 0), bl1 = make_int2(-1, 0);
   if (kWave) {
     bl0 = g.wl[(int64_t)wv * kWL + lane];
@@ -1122,85 +1143,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   double v[V_N];
   load_rec(g.st, o, v);
   const double m = mc[o];
-  double2 tp[3][kU];
+  double2 tp[3][kU];              // the streams are zero beyond nw up to ns = 128·kU: no masks
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int i = 2 * (lane + 64 * u);
-      tp[k][u] = *reinterpret_cast<const double2*>(Pc + (int64_t)k * ns + (i < ns ? i : ns - 2));
-    }
+    for (int u = 0; u < kU; ++u) tp[k][u] = *reinterpret_cast<const double2*>(Pc + (int64_t)k * ns + 2 * (lane + 64 * u));
   double tb[kFirst ? 2 * kU : 1];
   if (kFirst)
 #pragma unroll
-    for (int u = 0; u < 2 * kU; ++u) tb[u] = g.part_b[min(lane + 64 * u, nw - 1)];
+    for (int u = 0; u < 2 * kU; ++u) tb[u] = g.part_b[lane + 64 * u];
   double own_p[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * ns + wv];
   const int cnt = g.flags[F_PCG_CNT];
-  const double gam_prev = kFirst ? 1.0 : g.pcg_gamma[par ^ 1];
-  const double alpha_prev = kFirst ? 1.0 : g.pcg_alpha[par ^ 1];
+  const double rgam_prev = kFirst ? 1.0 : g.pcg_gamma[2 + (par ^ 1)];     // 1/γ, 1/α of the previous iteration
+  const double ralpha_prev = kFirst ? 1.0 : g.pcg_alpha[2 + (par ^ 1)];
   const double bb_stored = g.scal[S_BB];
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
   if (stop) return;
-  // ---- trip 2: n = A m
-  double n[6];
-  if (kWave) {
-    double pr[2][6];
+#ifdef OFX_STAMPS
+  if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
+#endif
+  OFX_STAMP(1)
+  // ---- trip 2: A blocks and gathered m (issued first; the scalar work below overlaps their flight)
+  double2 ab[kWave ? 2 : 1][18], xb[kWave ? 2 : 1][3];
+  if (kWave)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked)
+    for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked later)
       const int2 e = j ? bl1 : bl0;
-      const bool ok = e.x >= 0;
       const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e.y);
-      const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(ok ? e.x : 0));
-      double x[6];
+      const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { const double2 t = vc[k]; x[2 * k] = t.x; x[2 * k + 1] = t.y; }
+      for (int k = 0; k < 18; ++k) ab[j][k] = blk[k];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
-        const double t = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
-        pr[j][i] = ok ? t : 0.0;
-      }
+      for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 6; ++i) s_prod[(j * 64 + lane) * 6 + i] = pr[j][i];
-    __syncthreads();
-    // row sums in CSR order (rows of at most kRowMax blocks; unrolled, masked LDS reads)
-    const int lb = b0 - wb0, len = b1 - b0;
-    double a = 0.0;
-#pragma unroll
-    for (int k = 0; k < kRowMax; ++k) {
-      const double t = s_prod[(lb + (k < len ? k : 0)) * 6 + qc];
-      a += k < len ? t : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) n[i] = i == qc ? a : 0.0;
-  } else {
-    row_spmv(g, b0, b1, q, mc, n);
-  }
-  // ---- scalars
+  asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
+  // ---- scalars from the partials (trip-1 data)
   double pa[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double t = 0.0;
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int i = 2 * (lane + 64 * u);
-      t += i < nw ? tp[k][u].x + (i + 1 < nw ? tp[k][u].y : 0.0) : 0.0;
-    }
+    for (int u = 0; u < kU; ++u) t += tp[k][u].x + tp[k][u].y;
     pa[k] = wave_sum(t);
   }
   double bb = bb_stored;
   if (kFirst) {
     double t = 0.0;
 #pragma unroll
-    for (int u = 0; u < 2 * kU; ++u) t += lane + 64 * u < nw ? tb[u] : 0.0;
+    for (int u = 0; u < 2 * kU; ++u) t += tb[u];
     bb = wave_sum(t);
   }
   const double gam = pa[0], del = pa[1], rr = pa[2];
@@ -1211,8 +1206,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (kFirst) {
     alpha = gam / del;
   } else {
-    beta = gam / gam_prev;
-    alpha = gam / (del - beta * gam / alpha_prev);
+    beta = gam * rgam_prev;
+    alpha = gam / (del - beta * gam * ralpha_prev);
   }
   const bool conv = rr <= tol * tol * bb || gam == 0.0;
   if (conv || !isfinite(alpha) || !(alpha > 0.0)) {   // converged, or breakdown (A SPD => alpha > 0): keep x
@@ -1226,39 +1221,76 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
     return;
   }
-  if (lead) { g.pcg_alpha[par] = alpha; g.pcg_gamma[par] = gam; g.flags[F_PCG_CNT] = cnt + 1; }
+  if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
+  OFX_STAMP(2)
+  // ---- n = A m (own component)
+  double nc;
+  if (kWave) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = (j ? bl1 : bl0).x >= 0;
+      double x[6];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { x[2 * k] = xb[j][k].x; x[2 * k + 1] = xb[j][k].y; }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {   // (the PCG is not bit-pinned: fused multiply-adds)
+        const double2 b01 = ab[j][3 * i], b23 = ab[j][3 * i + 1], b45 = ab[j][3 * i + 2];
+        const double t = fma(b45.y, x[5], fma(b45.x, x[4], fma(b23.y, x[3], fma(b23.x, x[2], fma(b01.y, x[1], b01.x * x[0])))));
+        s_prod[(j * 64 + lane) * 6 + i] = ok ? t : 0.0;
+      }
+    }
+    OFX_STAMP(3)
+    __syncthreads();
+    // row sums in CSR order (rows of at most kRowMax blocks; unrolled reads at immediate offsets,
+    // masked; s_prod is padded so the reads past the wave's last block stay inside it)
+    const int len = b1 - b0;
+    const double* sp = s_prod + (b0 - wb0) * 6 + qc;
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRowMax; ++k) {
+      const double t = sp[6 * k];
+      a += k < len ? t : 0.0;
+    }
+    nc = a;
+  } else {
+    double n[6];
+    row_spmv(g, b0, b1, q, mc, n);
+    nc = pick6(n, qc);
+  }
+  OFX_STAMP(4)
   double d[3] = {0.0, 0.0, 0.0};
-  const double nc = pick6(n, qc);
   {
-    const double zz = nc + beta * v[V_Z];
-    const double qq = m + beta * v[V_Q];
-    const double sv = v[V_W] + beta * v[V_S];
-    const double p = v[V_U] + beta * v[V_P];
-    const double rn = v[V_R] - alpha * sv;
-    const double un = v[V_U] - alpha * qq;
-    const double w2 = v[V_W] - alpha * zz;
+    const double zz = fma(beta, v[V_Z], nc);
+    const double qq = fma(beta, v[V_Q], m);
+    const double sv = fma(beta, v[V_S], v[V_W]);
+    const double p = fma(beta, v[V_P], v[V_U]);
+    const double rn = fma(-alpha, sv, v[V_R]);
+    const double un = fma(-alpha, qq, v[V_U]);
+    const double w2 = fma(-alpha, zz, v[V_W]);
     if (own) {
-      const double nv[V_N] = {v[V_X] + alpha * p, rn, un, zz, qq, sv, p, w2};
+      const double nv[V_N] = {fma(alpha, p, v[V_X]), rn, un, zz, qq, sv, p, w2};
       store_rec(g.st, o, nv);
       s_v[6 * r + q] = w2;
       d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
     }
   }
+  OFX_STAMP(5)
   __syncthreads();
   if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (inverse rows staged in LDS)
-    const float4* mrow = s_m + (6 * r + q) * (kCD / 4);
+    const float4* mrow = s_m + (6 * r + q);
     double a = 0.0;
 #pragma unroll
     for (int k = 0; k < kCD / 4; ++k) {
-      const float4 t = mrow[k];
-      a += (((double)t.x * s_v[4 * k] + (double)t.y * s_v[4 * k + 1]) +
-            ((double)t.z * s_v[4 * k + 2] + (double)t.w * s_v[4 * k + 3]));
+      const float4 t = mrow[k * kCD];
+      a = fma((double)t.w, s_v[4 * k + 3], fma((double)t.z, s_v[4 * k + 2], fma((double)t.y, s_v[4 * k + 1], fma((double)t.x, s_v[4 * k], a))));
     }
     mn[o] = a;
   }
+  OFX_STAMP(6)
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
+  OFX_STAMP(7)
 }
 
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
@@ -1466,7 +1498,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const dim3 grid(g->nwg_row), block(64);
   // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width for up to 384 / 2176 waves
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
-  const bool small = g->nwg_row <= 2 * 64 * 3;
+  const bool small = g->pcg_ku == 3;
   auto iter0 = wave ? (small ? k_pcg_iter<true, true, 3> : k_pcg_iter<true, true, 17>)
                     : (small ? k_pcg_iter<false, true, 3> : k_pcg_iter<false, true, 17>);
   auto iter = wave ? (small ? k_pcg_iter<true, false, 3> : k_pcg_iter<true, false, 17>)
@@ -1523,7 +1555,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
   ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes); ALLOC(g->wl, N / kCS * kWL); ALLOC(g->stopw, N / kCS * 64);
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
-  ALLOC(g->part_p, (6 > kProjP ? 6 : kProjP) * max_row_wg); ALLOC(g->part_b, max_row_wg);
+  const int64_t max_ns = 128 * 17;   // nw_pad bound: 2·64·17 >= max_pad / kCS waves
+  static_assert(2 * 64 * 17 * kCS >= 2 * kMaxNodes + kCS, "partial stream width");
+  ALLOC(g->part_p, (6 * max_ns > kProjP * max_row_wg ? 6 * max_ns : kProjP * max_row_wg)); ALLOC(g->part_b, max_ns);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
@@ -1583,6 +1617,18 @@ int ofx_gn_row_order(void* handle, int32_t* perm, int32_t cap) {
   return OFX_OK;
 }
 
+#ifdef OFX_STAMPS
+// tuning build only (not part of include/ofx.h): arm (n > 0) / read back the PCG phase stamps
+int ofx_gn_stamps(void* handle, uint64_t* out, int64_t n) {
+  Gn* g = (Gn*)handle;
+  const int64_t cap = (int64_t)64 * (g->max_pad / kCS) * 8;
+  if (!g->stamps) OFX_HIP(hipMalloc((void**)&g->stamps, cap * sizeof(uint64_t)));
+  if (out) OFX_HIP(hipMemcpy(out, g->stamps, (n < cap ? n : cap) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  OFX_HIP(hipMemset(g->stamps, 0, cap * sizeof(uint64_t)));
+  return OFX_OK;
+}
+#endif
+
 int ofx_gn_destroy(void* handle) {
   if (!handle) return OFX_OK;
   Gn* g = (Gn*)handle;
@@ -1631,15 +1677,16 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   g->N = N; g->N_real = N0; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
   g->T = (int64_t)M + (int64_t)N * NB + N;
-  if (prm->pcg_max_iter + 1 > g->pcg_cap) {
+  if (4 > g->pcg_cap) {   // [alpha, gamma] of both parities + their reciprocals
     if (g->pcg_alpha) OFX_HIP(hipFree(g->pcg_alpha));
     if (g->pcg_gamma) OFX_HIP(hipFree(g->pcg_gamma));
-    g->pcg_cap = prm->pcg_max_iter + 1;
+    g->pcg_cap = 4;
     OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
   g->nwg_row = N / kRW;
-  g->nw_pad = (g->nwg_row + 1) & ~1;
+  g->pcg_ku = g->nwg_row <= 2 * 64 * 3 ? 3 : 17;
+  g->nw_pad = 128 * g->pcg_ku;
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T

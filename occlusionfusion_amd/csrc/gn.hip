@@ -647,6 +647,14 @@ constexpr int kSL = 64 / kRW;   // lanes (block slots) per row
 constexpr int kCD = 6 * kCS;    // cluster dimension
 static_assert(kCS * kCS == 64, "k_pcg_prep maps the cluster's kCS x kCS node blocks onto one wave");
 
+// LDS hand-off inside a single-wave workgroup: wait for this wave's LDS operations only. (A
+// __syncthreads() is a workgroup-scope release that also drains every outstanding global store —
+// a full memory round trip — and one wave needs no s_barrier.) gfx9 s_waitcnt: lgkmcnt(0), others max.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Sum over each aligned group of kSL (= 8) lanes; every lane of the group ends with identical bits.
 __device__ __forceinline__ double slot_sum(double x) {
   x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
@@ -1240,7 +1248,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     OFX_STAMP(3)
-    __syncthreads();
+    wave_lds_sync();
     // row sums in CSR order (rows of at most kRowMax blocks; unrolled reads at immediate offsets,
     // masked; s_prod is padded so the reads past the wave's last block stay inside it)
     const int len = b1 - b0;
@@ -1275,16 +1283,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   }
   OFX_STAMP(5)
-  __syncthreads();
+  wave_lds_sync();
   if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (inverse rows staged in LDS)
     const float4* mrow = s_m + (6 * r + q);
-    double a = 0.0;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};   // four independent FMA chains
 #pragma unroll
     for (int k = 0; k < kCD / 4; ++k) {
       const float4 t = mrow[k * kCD];
-      a = fma((double)t.w, s_v[4 * k + 3], fma((double)t.z, s_v[4 * k + 2], fma((double)t.y, s_v[4 * k + 1], fma((double)t.x, s_v[4 * k], a))));
+      a[0] = fma((double)t.x, s_v[4 * k], a[0]);
+      a[1] = fma((double)t.y, s_v[4 * k + 1], a[1]);
+      a[2] = fma((double)t.z, s_v[4 * k + 2], a[2]);
+      a[3] = fma((double)t.w, s_v[4 * k + 3], a[3]);
     }
-    mn[o] = a;
+    mn[o] = (a[0] + a[1]) + (a[2] + a[3]);
   }
   OFX_STAMP(6)
 #pragma unroll

@@ -36,6 +36,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <chrono>
 #include <utility>
 #include <vector>
 
@@ -110,6 +111,9 @@ struct Gn {
   int warm_now = 0;               // this step starts from the projected x0
   int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED] mirrored by the kernels
   int32_t* hflags = nullptr;      // its device address (system-scope stores: no copy kernel per poll)
+  hipEvent_t poll_ev = nullptr;   // recorded after each chunk of PCG launches
+  double host_enqueue_us = 0.0;   // tuning build: host time spent enqueuing PCG iterations
+  int64_t host_enqueued = 0;
   int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
   bool setup_done = false;
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
@@ -750,7 +754,8 @@ __device__ __forceinline__ double pick6(const double n[6], int c) {
 }
 // (A v)_row summed over the row's kSL lanes: every lane of the row gets all 6 components.
 // [b0, b1) = the row's block range (empty for padding rows).
-__device__ __forceinline__ void row_spmv(const Gn& g, int b0, int b1, int q, const double* __restrict__ v,
+template <typename G>
+__device__ __forceinline__ void row_spmv(const G& g, int b0, int b1, int q, const double* __restrict__ v,
                                          double n[6]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) n[i] = 0.0;
@@ -1108,6 +1113,28 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
 // into the next parity and sets the stop words, so later launches of the chunk end after trip 1.
 // kWave = false: plain CSR rows (waves of more than kWL blocks or rows longer than kRowMax).
 constexpr int kRowMax = 20;
+// The iteration kernel's arguments: only what it reads (a ~200-B kernarg instead of the whole Gn:
+// the host enqueues ~1000 of these per frame, so per-launch host work is on the critical path).
+struct PcgIt {
+  const double* Aop;
+  const float* Mcl;
+  const int32_t *row_ptr, *col;
+  const int2* wl;
+  double *m0, *m1, *st, *part_p, *part_b, *pcg_alpha, *pcg_gamma, *scal;
+  int32_t *flags, *hflags, *stopw;
+  uint64_t* stamps;
+  int32_t nwg_row, nw_pad;
+  struct { double pcg_tol; } prm;
+};
+static PcgIt pcg_args(const Gn* g) {
+  PcgIt a;
+  a.Aop = g->Aop; a.Mcl = g->Mcl; a.row_ptr = g->row_ptr; a.col = g->col; a.wl = g->wl;
+  a.m0 = g->m0; a.m1 = g->m1; a.st = g->st; a.part_p = g->part_p; a.part_b = g->part_b;
+  a.pcg_alpha = g->pcg_alpha; a.pcg_gamma = g->pcg_gamma; a.scal = g->scal;
+  a.flags = g->flags; a.hflags = g->hflags; a.stopw = g->stopw; a.stamps = g->stamps;
+  a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol;
+  return a;
+}
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
 #define OFX_STAMP(k)                                                                                  \
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8 + (k)] = __builtin_amdgcn_s_memtime();
@@ -1115,7 +1142,7 @@ constexpr int kRowMax = 20;
 #define OFX_STAMP(k)
 #endif
 template <bool kWave, bool kFirst, int kU>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(Gn g, int par) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   __shared__ double s_v[kCD];
   __shared__ float4 s_m[kCD * kCD / 4];
@@ -1225,7 +1252,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
       if (!conv && !isfinite(alpha)) g.flags[F_ILL] = 1;
       host_flag(g.hflags, H_PCG_IT, cnt);
-      host_flag(g.hflags, H_DONE, 1);
+      __hip_atomic_store(g.hflags + H_DONE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
     }
     return;
   }
@@ -1413,6 +1440,7 @@ static void free_all(Gn* g) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
+  if (g->poll_ev) (void)hipEventDestroy(g->poll_ev);
 }
 
 // Row order for the cluster preconditioner (host, from the ED graph). Clusters: the lowest
@@ -1514,20 +1542,42 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
                     : (small ? k_pcg_iter<false, true, 3> : k_pcg_iter<false, true, 17>);
   auto iter = wave ? (small ? k_pcg_iter<true, false, 3> : k_pcg_iter<true, false, 17>)
                    : (small ? k_pcg_iter<false, false, 3> : k_pcg_iter<false, false, 17>);
+  // No stream sync: the converging launch stores H_DONE straight into host memory and the host
+  // spins on it, so the next GN step is enqueued while the chunk's remaining (no-op) launches drain.
+  // The chunk event only tells "all launched iterations ran without converging" -> launch more.
+  volatile int32_t* hf = g->host_flags;
+  hf[H_DONE] = 0;   // the previous step's converged launch has run (we saw it); prep also clears it
+  const PcgIt pa = pcg_args(g);
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
+#ifdef OFX_STAMPS
+    const auto h0 = std::chrono::steady_clock::now();
+#endif
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block, 0, hs, *g, it & 1);
+      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block, 0, hs, pa, it & 1);
+#ifdef OFX_STAMPS
+    g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+    g->host_enqueued += n;
+#endif
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
-    OFX_HIP(hipStreamSynchronize(hs));   // the kernels mirror done / count / stopped into host memory
-    const volatile int32_t* hf = g->host_flags;
-    if (hf[H_DONE] || hf[H_STOPPED]) {
-      if (hf[H_DONE]) g->last_pcg[gn_iter & 63] = hf[H_PCG_IT];
+    OFX_HIP(hipEventRecord(g->poll_ev, hs));
+    bool ran = false;
+    for (int spin = 0; !hf[H_DONE] && !hf[H_STOPPED]; ++spin) {
+      if ((spin & 63) == 63) {
+        const hipError_t q = hipEventQuery(g->poll_ev);
+        if (q == hipSuccess) { ran = true; break; }
+        if (q != hipErrorNotReady) OFX_HIP(q);
+      }
+    }
+    if (hf[H_STOPPED]) break;
+    if (hf[H_DONE]) {
+      g->last_pcg[gn_iter & 63] = hf[H_PCG_IT];
       break;
     }
+    (void)ran;   // the chunk ran out without convergence: next chunk
     chunk = 8;
   }
   g->n_iter_launches += it;
@@ -1576,7 +1626,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     free_all(g); delete g; set_error("hipMemset failed"); return OFX_ERR_HIP;
   }
   if (hipHostMalloc((void**)&g->host_flags, H_COUNT * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess) {
+      hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess ||
+      hipEventCreateWithFlags(&g->poll_ev, hipEventDisableTiming) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
 
@@ -1630,6 +1681,12 @@ int ofx_gn_row_order(void* handle, int32_t* perm, int32_t cap) {
 
 #ifdef OFX_STAMPS
 // tuning build only (not part of include/ofx.h): arm (n > 0) / read back the PCG phase stamps
+int ofx_gn_host_enqueue(void* handle, double* us, int64_t* n) {
+  Gn* g = (Gn*)handle;
+  *us = g->host_enqueue_us; *n = g->host_enqueued;
+  g->host_enqueue_us = 0.0; g->host_enqueued = 0;
+  return OFX_OK;
+}
 int ofx_gn_stamps(void* handle, uint64_t* out, int64_t n) {
   Gn* g = (Gn*)handle;
   const int64_t cap = (int64_t)64 * (g->max_pad / kCS) * 8;

@@ -32,8 +32,18 @@ for t in range(1, 6):
 torch.cuda.synchronize()
 h = pipe.solver._h
 fn(h, None, 0)                      # allocate + clear
+he = _lib.lib.ofx_gn_host_enqueue
+he.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+us, ne = ctypes.c_double(), ctypes.c_int64()
+he(h, ctypes.byref(us), ctypes.byref(ne))
+import time
+t0 = time.perf_counter()
 pipe.step(frames[6], 6)
 torch.cuda.synchronize()
+t1 = time.perf_counter()
+he(h, ctypes.byref(us), ctypes.byref(ne))
+print(f"frame wall {1e3 * (t1 - t0):.2f} ms; host enqueue of {ne.value} PCG launches {us.value / 1e3:.2f} ms "
+      f"({us.value / max(1, ne.value):.2f} us each)")
 nw = pipe.solver.info()[4] // 8
 buf = np.zeros(64 * nw * 8, np.uint64)
 fn(h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)

@@ -149,10 +149,11 @@ def main():
     B = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
     t_int_avg = float(np.mean(t_int))
     achieved = B / t_kint
-    # k_pcg_iter algorithmic bytes per launch: A blocks (288 B) + column ids (4 B) per block; per row
-    # (nodes in cluster order, padded): row_ptr (4 B), gathered m (48 B), cluster-inverse rows (6 x 48
-    # f32 = 1152 B), 8-vector state read + written (2 x 384 B), new m written (48 B)
-    B_pcg = nnzb * 292 + rows * (4 + 48 + 1152 + 768 + 48)
+    # k_pcg_iter algorithmic (unique) bytes per launch: per JᵀJ block its 6x6 f64 values (288 B) + its
+    # (col, slot) wave-list entry (8 B); per PCG row (nodes in cluster order, padded) the cluster-inverse
+    # rows (6 x 48 f32 = 1152 B), the 8-vector state read + written (2 x 384 B), m read (48 B; the
+    # neighbour gathers re-read these) and the new m written (48 B). DESIGN.md §5.
+    B_pcg = nnzb * 296 + rows * (1152 + 768 + 48 + 48)
     t_pcg = pcg_ms * 1e-3 / max(1, pcg_launches)
     ach_pcg = B_pcg / t_pcg
     res = {
@@ -168,12 +169,12 @@ def main():
         "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * t_int_avg,
                          "pcg_iters_per_frame": float(np.mean(pcg)), "gn_iters": float(np.mean(gn_it)),
                          "valid_solves": int(np.sum(valid))},
-        "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: BSR SpMV + recurrences)", "bound": "hbm",
+        "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster block-Jacobi apply)", "bound": "hbm",
                      "achieved": ach_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": ach_pcg / PEAK_HBM,
                      "traffic": pmc_traffic("k_pcg_iter"), "traffic_source": os.path.relpath(PMC_FILE, ROOT),
                      "bytes_per_launch": B_pcg, "avg_launch_us": 1e6 * t_pcg,
                      "launches_per_frame": pcg_launches / a.steps, "nnz_blocks": nnzb,
-                     "note": "dominant kernel by time; latency-bound (one launch per iteration: launch + gather chain)"},
+                     "note": "dominant kernel by time; latency-bound (one launch per iteration: launch floor + two dependent memory trips + the wave's instruction stream)"},
         "roofline_integrate": {"kernel": "k_integrate<true,true> (fused warp+integrate, LDS node palette)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp"),

@@ -24,8 +24,10 @@
  *   ofx_integrate_palette   same, node records staged per brick in LDS      warpfield.py:369-380, tsdf.py:442-494
  *   ofx_deform_points       ED_warp / deform_ED / deform_mesh / normals     NonRigidICP/model/geometry.py:9-25,
  *                                                                          registration_fusion.py:157-184, warpfield.py:312-367
+ *   ofx_deform_points_lbs   WarpField.deform_lbs / deform_lbs_cuda (origin form) warpfield.py:208-266,270-305
  *   ofx_visibility          TSDFVolume.check_visibility                     tsdf.py:576-612
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
+ *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
  */
 #ifndef OFX_H
@@ -60,12 +62,21 @@ typedef struct ofx_volume_desc {
   int32_t dim[3];       /* Dx, Dy, Dz (TSDFVolume._vol_dim) */
   int32_t brick_x0;     /* first brick column along x owned by this shard */
   int32_t brick_x1;     /* one past the last (full volume: ceil(Dx/8)) */
-  int32_t _pad0;
+  int32_t semantics;    /* integrate arithmetic: OFX_SEM_CPU (0) or OFX_SEM_PYCUDA (1) */
   float origin[3];      /* TSDFVolume._vol_origin (f32) */
   float _pad1;
   double voxel_size;    /* TSDFVolume._voxel_size (f64) */
   double trunc_margin;  /* TSDFVolume._trunc_margin (0.04) */
 } ofx_volume_desc;
+
+/* Integrate semantics (ofx_volume_desc.semantics). The reference has two integrate paths that compute
+ * different numbers:
+ *   OFX_SEM_CPU    numba/numpy CPU branch, tsdf.py:442-494: f64 projection, round-half-even pixels,
+ *                  update iff depth > 0 and d - z >= -trunc, plain d - z.
+ *   OFX_SEM_PYCUDA pycuda kernel, tsdf.py:192-288 (used when fopt.gpu and pycuda import): f32 throughout,
+ *                  pixel = (int)roundf(f32(f·x/z + c) + 0.5) (half away from zero), skip iff depth == 0,
+ *                  (d - z) scaled by the ray factor sqrt(1 + mx² + my²) of the integer pixel, roundf colours. */
+enum { OFX_SEM_CPU = 0, OFX_SEM_PYCUDA = 1 };
 
 typedef struct ofx_camera {
   float fx, fy, cx, cy; /* cam_intr (cast to f32 as tsdf.py:357) */
@@ -143,6 +154,13 @@ int ofx_deform_points(const float* points, int64_t n_points, const int32_t* anch
                       const uint8_t* valid, int32_t k, const float* packed_nodes, int32_t n_nodes,
                       int32_t normals, float* out, ofx_stream_t s);
 
+/* WarpField.deform_lbs (origin-form LBS, the use_pytorch=False branch of WarpField.deform):
+ * out = Σ_{k: w_k != 0} w_k (R_k x + t_k) for valid points, x otherwise; rotations f32[N*9] row-major,
+ * translations f32[N*3] in origin form (t = -R g + g + T). Anchors must be in [0, n_nodes) where w != 0. */
+int ofx_deform_points_lbs(const float* points, int64_t n_points, const int32_t* anchors, const float* weights,
+                          const uint8_t* valid, int32_t k, const float* rotations, const float* translations,
+                          int32_t n_nodes, float* out, ofx_stream_t s);
+
 /* check_visibility: valid u8[P], depth_diff f64[P] */
 int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
                    double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s);
@@ -161,7 +179,18 @@ typedef struct ofx_gn_params {
   double lm_factor;          /* 1e-7 (model.py:111) */
   double stop_loss_diff;     /* 1   (model.py:114) */
   double pcg_tol;            /* relative residual target of the inner solve */
+  int32_t mode;              /* OFX_GN_OPTIMIZE (0): DeformNet.optimize; OFX_GN_ARAP (1): DeformNet.arap */
+  int32_t _pad;
 } ofx_gn_params;
+
+/* OFX_GN_ARAP restates DeformNet.arap (model/model.py:1639-1986), the graph-update solve for nodes
+ * that are invisible or new: no match rows (n_matches = 0); node_conf = valid-node mask (1/0) and
+ * target_node_pos = the valid nodes' targets; per valid node three "flow" rows
+ * r = sqrt(lambda_flow)·(g + t - target) whose Jacobian on t is r itself (model.py:1772-1784, as
+ * written); ARAP rows as in optimize; only nodes with node_conf == 0 are updated (:1940-1943). With
+ * lambda_flow = 0 (model.py:98) the system's exact null space (a common translation of each
+ * connected graph component) is projected out of every step, as the dense LU solution has none. */
+enum { OFX_GN_OPTIMIZE = 0, OFX_GN_ARAP = 1 };
 
 typedef struct ofx_gn_problem {
   int32_t n_nodes, n_matches, n_neighbors, _pad;

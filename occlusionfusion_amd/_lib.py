@@ -17,7 +17,7 @@ P = ctypes.c_void_p  # device pointer
 
 
 class VolumeDesc(ctypes.Structure):
-    _fields_ = [("dim", c_int32 * 3), ("brick_x0", c_int32), ("brick_x1", c_int32), ("_pad0", c_int32),
+    _fields_ = [("dim", c_int32 * 3), ("brick_x0", c_int32), ("brick_x1", c_int32), ("semantics", c_int32),
                 ("origin", c_float * 3), ("_pad1", c_float), ("voxel_size", c_double), ("trunc_margin", c_double)]
 
 
@@ -30,7 +30,7 @@ class GnParams(ctypes.Structure):
     _fields_ = [("num_iter", c_int32), ("use_edge_weighting", c_int32), ("pcg_max_iter", c_int32), ("pcg_warm", c_int32),
                 ("lambda_flow", c_double), ("lambda_depth", c_double), ("lambda_arap", c_double),
                 ("lambda_motion", c_double), ("lm_factor", c_double), ("stop_loss_diff", c_double),
-                ("pcg_tol", c_double)]
+                ("pcg_tol", c_double), ("mode", c_int32), ("_pad", c_int32)]
 
 
 class GnProblem(ctypes.Structure):
@@ -61,6 +61,7 @@ _SIGS = {
     "ofx_integrate": [P, P, P, P, c_int32, P, c_int32, c_int32, P, c_int32, P, P, c_double, P, P, P, P, P],
     "ofx_integrate_palette": [P, P, P, P, P, c_int32, c_int32, P, c_int32, P, P, P, P, P, c_double, P, P, P, P, P],
     "ofx_deform_points": [P, c_int64, P, P, P, c_int32, P, c_int32, c_int32, P, P],
+    "ofx_deform_points_lbs": [P, c_int64, P, P, P, c_int32, P, P, c_int32, P, P],
     "ofx_visibility": [P, c_int64, P, P, c_double, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],

@@ -100,6 +100,10 @@ struct Gn {
   int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (3: <= 384 waves, else 17)
   double* scal = nullptr;
   int32_t* flags = nullptr;
+  // DeformNet.arap mode with lambda_flow = 0: rows of each multi-node connected graph component
+  // (comp_off[c]..comp_off[c+1] in comp_rows), whose common translation is the exact null space
+  int32_t *comp_rows = nullptr, *comp_off = nullptr;
+  int n_comp = 0, comp_cap = 0;
   double* loss_log = nullptr;
   double* stat = nullptr;         // kMaxLog x [pcg iterations, |b|², loss] of the last solve
   double* step_state = nullptr;   // (kMaxLog+1) x [previous loss, accepted steps] before each GN step
@@ -530,7 +534,14 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
       const int i = (int)(t - g.M - (int64_t)g.N * g.NB);
 #pragma unroll
       for (int c = 0; c < 18; ++c) J[c] = 0.0;
-      if (add_reg) {
+      if (add_reg && g.prm.mode == OFX_GN_ARAP) {
+        // DeformNet.arap "flow" rows of the valid nodes (model.py:1766-1784): the Jacobian entry on
+        // t_c is the residual itself, as the reference writes it
+        const double c = dc.lf * g.conf[i];
+        for (int q = 0; q < 3; ++q) r[q] = c * (g.t[3 * i + q] + g.nodes[3 * i + q] - g.tpos[3 * i + q]);
+        J[3] = r[0]; J[10] = r[1]; J[17] = r[2];
+        l2[0] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+      } else if (add_reg) {
         double c = dc.lm * g.conf[i];
         for (int q = 0; q < 3; ++q) r[q] = c * (g.t[3 * i + q] + g.nodes[3 * i + q] - g.tpos[3 * i + q]);
         J[3] = c; J[10] = c; J[17] = c;
@@ -1382,6 +1393,7 @@ __global__ __launch_bounds__(256) void k_step(Gn g, const double* __restrict__ r
   if (xsave)
 #pragma unroll
     for (int c = 0; c < 6; ++c) xsave[6 * (int64_t)i + c] = x[c];
+  if (g.prm.mode == OFX_GN_ARAP && g.conf[i] != 0.0) return;   // arap: valid nodes keep R, t (model.py:1940-1943)
   double a0 = x[0], a1 = x[1], a2 = x[2];
   double th2 = a0 * a0 + a1 * a1 + a2 * a2;
   double Ri[9];
@@ -1401,6 +1413,28 @@ __global__ __launch_bounds__(256) void k_step(Gn g, const double* __restrict__ r
     for (int c = 0; c < 3; ++c) Rn[3 * r + c] = Ri[3 * r] * R[c] + Ri[3 * r + 1] * R[3 + c] + Ri[3 * r + 2] * R[6 + c];
   for (int c = 0; c < 9; ++c) R[c] = Rn[c];
   for (int c = 0; c < 3; ++c) g.t[3 * i + c] += x[3 + c];
+}
+
+// arap mode, lambda_flow = 0: remove each connected component's mean translation from the PCG
+// solution (one wave per component, fixed-order sums). A·n = λ_LM·n for that common translation n and
+// b ⊥ n, so the dense LU solution has no n component; CG barely resolves the λ_LM eigenvalue.
+__global__ __launch_bounds__(64) void k_null_project(Gn g) {
+  const int c = blockIdx.x;
+  const int b = g.comp_off[c], e = g.comp_off[c + 1];
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int k = b + (int)threadIdx.x; k < e; k += 64) {
+    const int64_t i = g.comp_rows[k];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) s[q] += g.st[V_N * (6 * i + 3 + q) + V_X];
+  }
+  double mean[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) mean[q] = wave_sum(s[q]) / (double)(e - b);
+  for (int k = b + (int)threadIdx.x; k < e; k += 64) {
+    const int64_t i = g.comp_rows[k];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) g.st[V_N * (6 * i + 3 + q) + V_X] -= mean[q];
+  }
 }
 
 __global__ void k_finish(Gn g, float* __restrict__ rot, float* __restrict__ trans, int32_t* __restrict__ status,
@@ -1436,7 +1470,7 @@ static void free_all(Gn* g) {
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->perm, g->iperm};
+                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->perm, g->iperm, g->comp_rows, g->comp_off};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -1741,7 +1775,51 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
       g->h_edges.swap(he);
     }
   }
+  OFX_CHECK_ARG(prm->mode == OFX_GN_OPTIMIZE || prm->mode == OFX_GN_ARAP, "bad gn mode %d", prm->mode);
+  OFX_CHECK_ARG(prm->mode != OFX_GN_ARAP || M == 0, "arap mode takes no match rows");
   const int N = (int)g->h_perm.size();
+  g->n_comp = 0;
+  if (prm->mode == OFX_GN_ARAP && prm->lambda_flow == 0.0) {
+    // connected components of the (undirected) ED graph, rows listed per component
+    std::vector<int32_t> lab(N0, -1), rows, off{0}, stack;
+    std::vector<std::vector<int32_t>> adj(N0);
+    for (int i = 0; i < N0; ++i)
+      for (int k = 0; k < NB; ++k) {
+        const int j = g->h_edges[(size_t)i * NB + k];
+        if (j >= 0 && j < N0 && j != i) { adj[i].push_back(j); adj[j].push_back(i); }
+      }
+    std::vector<int32_t> ip(N0, -1);
+    for (int r = 0; r < N; ++r)
+      if (g->h_perm[r] >= 0) ip[g->h_perm[r]] = r;
+    for (int s0 = 0; s0 < N0; ++s0) {
+      if (lab[s0] >= 0 || adj[s0].empty()) continue;
+      const size_t first = rows.size();
+      lab[s0] = 1;
+      stack.assign(1, s0);
+      while (!stack.empty()) {
+        const int v = stack.back();
+        stack.pop_back();
+        rows.push_back(ip[v]);
+        for (int j : adj[v])
+          if (lab[j] < 0) { lab[j] = 1; stack.push_back(j); }
+      }
+      std::sort(rows.begin() + first, rows.end());
+      off.push_back((int32_t)rows.size());
+    }
+    g->n_comp = (int)off.size() - 1;
+    if (g->n_comp > 0) {
+      if ((int)rows.size() + (int)off.size() > g->comp_cap) {
+        if (g->comp_rows) OFX_HIP(hipFree(g->comp_rows));
+        if (g->comp_off) OFX_HIP(hipFree(g->comp_off));
+        g->comp_cap = (int)(rows.size() + off.size());
+        OFX_HIP(hipMalloc((void**)&g->comp_rows, g->comp_cap * sizeof(int32_t)));
+        OFX_HIP(hipMalloc((void**)&g->comp_off, g->comp_cap * sizeof(int32_t)));
+      }
+      OFX_HIP(hipMemcpyAsync(g->comp_rows, rows.data(), rows.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+      OFX_HIP(hipMemcpyAsync(g->comp_off, off.data(), off.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+      OFX_HIP(hipStreamSynchronize(hs));   // pageable sources
+    }
+  }
   g->N = N; g->N_real = N0; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
   g->T = (int64_t)M + (int64_t)N * NB + N;
@@ -1873,6 +1951,7 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   hipStream_t hs = as_stream(s);
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
+  if (g->n_comp > 0) hipLaunchKernelGGL(k_null_project, dim3(g->n_comp), dim3(64), 0, hs, *g);
   double* xsave = g->prm.pcg_warm ? g->xh + (int64_t)(gn_iter % kProj) * 6 * g->N : nullptr;
   hipLaunchKernelGGL(k_step, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g, (const double*)rhs, 64,
                      g->prm.pcg_max_iter, gn_iter, xsave);

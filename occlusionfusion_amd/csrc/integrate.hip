@@ -153,6 +153,68 @@ __device__ __forceinline__ int update_voxel(const CamD& c, const float* __restri
   return 1;
 }
 
+// (int)f with the saturating conversion both CUDA (cvt.rzi.s32.f32) and CDNA (v_cvt_i32_f32) perform
+// for the pycuda kernel's casts: NaN -> 0, out of range -> INT_MIN / INT_MAX.
+__device__ __forceinline__ int cvt_sat_i32(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return 2147483647;
+  if (f <= -2147483648.0f) return (-2147483647 - 1);
+  return (int)f;
+}
+
+// One voxel update with the pycuda kernel's arithmetic (OFX_SEM_PYCUDA, tsdf.py:192-288): f32
+// throughout (correctly rounded divisions / sqrt via f64, exact by the double-rounding theorem), the
+// identity cam_pose applied literally (tsdf.py:236-241), pixel = (int)roundf(f32(f·(x/z) + c) + 0.5)
+// (the `+0.5` is a double literal: the sum is formed in f64 and narrowed to roundf's f32 argument),
+// skip iff outside the image, z < 0 or depth == 0; depth difference scaled by the ray factor of the
+// integer pixel; colours rounded half away from zero. Un-contracted (nvcc's default --fmad=true may
+// fuse some of these products: the reference's last bits are not reproducible without nvcc).
+__device__ __forceinline__ int update_voxel_pycuda(const CamD& c, const float* __restrict__ depth,
+                                                   const float* __restrict__ color_im, float trunc, float obs,
+                                                   float x, float y, float z, int64_t vi, float* __restrict__ tsdf,
+                                                   float* __restrict__ weight, float* __restrict__ color) {
+  const float one = 1.0f, zero = 0.0f;
+  const float tx = x - zero, ty = y - zero, tz = z - zero;
+  const float px_ = (one * tx + zero * ty) + zero * tz;
+  const float py_ = (zero * tx + one * ty) + zero * tz;
+  const float pz_ = (zero * tx + zero * ty) + one * tz;
+  const float fx = (float)c.fx, fy = (float)c.fy, cx = (float)c.cx, cy = (float)c.cy;
+  const float sx = fx * cdiv(px_, pz_) + cx;
+  const float sy = fy * cdiv(py_, pz_) + cy;
+  const int u = cvt_sat_i32(roundf((float)((double)sx + 0.5)));
+  const int v = cvt_sat_i32(roundf((float)((double)sy + 0.5)));
+  if (u < 0 || u >= c.W || v < 0 || v >= c.H || pz_ < 0.0f) return 0;
+  const int64_t pix = (int64_t)v * c.W + u;
+  const float d = depth[pix];
+  if (d == 0.0f) return 0;
+  float dd = d - pz_;
+  const float mx = cdiv((float)u - cx, fx);
+  const float my = cdiv((float)v - cy, fy);
+  const float ss = (1.0f + mx * mx) + my * my;
+  dd = dd * (float)sqrt((double)ss);
+  if (dd < -trunc) return 0;
+  const float dist = fminf(1.0f, cdiv(dd, trunc));
+  const float w_old = weight[vi];
+  const float w_new = w_old + obs;
+  weight[vi] = w_new;
+  tsdf[vi] = cdiv(tsdf[vi] * w_old + obs * dist, w_new);
+  if (color) {
+    const float C = 65536.0f;
+    const float oc = color[vi];
+    const float ob = floorf(cdiv(oc, C));
+    const float og = floorf(cdiv(oc - ob * 256.0f * 256.0f, 256.0f));
+    const float orr = (oc - ob * 256.0f * 256.0f) - og * 256.0f;
+    const float nc = color_im[pix];
+    const float nb = floorf(cdiv(nc, C));
+    const float ng = floorf(cdiv(nc - nb * 256.0f * 256.0f, 256.0f));
+    const float nr = (nc - nb * 256.0f * 256.0f) - ng * 256.0f;
+    const float b2 = fminf(roundf(cdiv(ob * w_old + obs * nb, w_new)), 255.0f);
+    const float g2 = fminf(roundf(cdiv(og * w_old + obs * ng, w_new)), 255.0f);
+    const float r2 = fminf(roundf(cdiv(orr * w_old + obs * nr, w_new)), 255.0f);
+    color[vi] = (b2 * 256.0f * 256.0f + g2 * 256.0f) + r2;
+  }
+  return 1;
+}
 
 // per-workgroup (= per-brick) update count, plain store: no contended atomics in the hot kernel
 __device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
@@ -170,7 +232,7 @@ __device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
 // register budget is capped at 64 VGPRs for full occupancy (87 -> 77 us at 512^3). Prefetching the
 // voxels' tsdf/weight/colour ahead of the palette barrier is slower: vmcnt retires in order, so the
 // barrier would wait on those HBM loads.
-template <bool WARP, bool PAL>
+template <bool WARP, bool PAL, bool PYC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_integrate(BrickGeom g, CamD c, const float* __restrict__ depth,
                                                     const float* __restrict__ color_im,
                                                     const float4* __restrict__ nodes, int K,
@@ -228,7 +290,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       if (PAL && use_pal) ed_warp(s_node, ids, w, K, x, y, z);
       else ed_warp(nodes, ids, w, K, x, y, z);
     }
-    n_upd += update_voxel(c, depth, color_im, trunc, 1.0 / trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
+    if (PYC) n_upd += update_voxel_pycuda(c, depth, color_im, (float)trunc, (float)obs, x, y, z, b * kBrickVox + l, tsdf,
+                                          weight, color);
+    else n_upd += update_voxel(c, depth, color_im, trunc, 1.0 / trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
   }
   count_updates(n_upd, counter);
 }
@@ -271,6 +335,37 @@ __global__ __launch_bounds__(256) void k_deform_points(const float* __restrict__
   out[3 * p] = x; out[3 * p + 1] = y; out[3 * p + 2] = z;
 }
 
+// WarpField.deform_lbs (warpfield.py:208-231, numba; CUDA twin deform_lbs_cuda :234-266 with
+// warp_point_with_nodes :607-630): origin-form transforms, y = Σ_k w_k (R_k x + t_k) over the anchors
+// with w_k != 0, accumulated from 0 in anchor order, f32; R_k x as ((R0·x + R1·y) + R2·z). Invalid
+// points keep x. R f32[N*9] row-major, t f32[N*3] (t = -R g + g + T, warpfield.py:407-408).
+__global__ __launch_bounds__(256) void k_deform_lbs(const float* __restrict__ pts, int64_t n,
+                                                     const int32_t* __restrict__ anchors,
+                                                     const float* __restrict__ weights,
+                                                     const uint8_t* __restrict__ valid, int K,
+                                                     const float* __restrict__ R, const float* __restrict__ t,
+                                                     float* __restrict__ out) {
+  int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const float x = pts[3 * p], y = pts[3 * p + 1], z = pts[3 * p + 2];
+  float ox = x, oy = y, oz = z;
+  if (valid ? valid[p] != 0 : true) {
+    ox = 0.f; oy = 0.f; oz = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float w = weights[p * K + k];
+      if (w == 0.f) continue;
+      const int64_t a = anchors[p * K + k];
+      const float* r = R + 9 * a;
+      const float* tt = t + 3 * a;
+      const float nx = ((r[0] * x + r[1] * y) + r[2] * z) + tt[0];
+      const float ny = ((r[3] * x + r[4] * y) + r[5] * z) + tt[1];
+      const float nz = ((r[6] * x + r[7] * y) + r[8] * z) + tt[2];
+      ox = ox + w * nx; oy = oy + w * ny; oz = oz + w * nz;
+    }
+  }
+  out[3 * p] = ox; out[3 * p + 1] = oy; out[3 * p + 2] = oz;
+}
+
 __global__ void k_visibility(const float* __restrict__ pts, int64_t n, CamD c, const float* __restrict__ depth,
                              double trunc, uint8_t* __restrict__ valid, double* __restrict__ ddiff) {
   int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -308,8 +403,11 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
   OFX_CHECK_ARG((color == nullptr) == (color_im == nullptr), "color and color_im must both be set or both NULL");
   CamD c = make_cam(cam);
   hipStream_t hs = as_stream(s);
+  OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
+  const bool pyc = desc->semantics == OFX_SEM_PYCUDA;
   if (!warp) {
-    hipLaunchKernelGGL((k_integrate<false, false>), dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth,
+    hipLaunchKernelGGL(pyc ? (k_integrate<false, false, true>) : (k_integrate<false, false, false>),
+                       dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth,
                        color_im, (const float4*)nullptr, 1, (const int32_t*)nullptr, (const ushort4*)nullptr,
                        (const float4*)nullptr, (const uint16_t*)nullptr, (const int32_t*)nullptr,
                        (const uchar4*)nullptr, desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
@@ -318,7 +416,8 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
     OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
     if (n_list == 0) return OFX_OK;
     OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights, "null warp buffer");
-    hipLaunchKernelGGL((k_integrate<true, false>), dim3((unsigned)n_list), dim3(256), 0, hs, g, c, depth, color_im,
+    hipLaunchKernelGGL(pyc ? (k_integrate<true, false, true>) : (k_integrate<true, false, false>), dim3((unsigned)n_list),
+                       dim3(256), 0, hs, g, c, depth, color_im,
                        (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors, (const float4*)weights,
                        (const uint16_t*)nullptr, (const int32_t*)nullptr, (const uchar4*)nullptr,
                        desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
@@ -344,7 +443,9 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
   if (n_list == 0) return OFX_OK;
   OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights && pal_ids && pal_n && local_anchors,
                 "null warp/palette buffer");
-  hipLaunchKernelGGL((k_integrate<true, true>), dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_cam(cam),
+  OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
+  hipLaunchKernelGGL(desc->semantics == OFX_SEM_PYCUDA ? (k_integrate<true, true, true>) : (k_integrate<true, true, false>),
+                     dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_cam(cam),
                      depth, color_im, (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors,
                      (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,
                      obs_weight, tsdf, weight, color, n_updated);
@@ -360,6 +461,18 @@ int ofx_deform_points(const float* points, int64_t n_points, const int32_t* anch
   OFX_CHECK_ARG(points && anchors && weights && packed_nodes && out, "null buffer");
   hipLaunchKernelGGL(k_deform_points, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
                      n_points, anchors, weights, valid, k, (const float4*)packed_nodes, normals, out);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_deform_points_lbs(const float* points, int64_t n_points, const int32_t* anchors, const float* weights,
+                          const uint8_t* valid, int32_t k, const float* rotations, const float* translations,
+                          int32_t n_nodes, float* out, ofx_stream_t s) {
+  OFX_CHECK_ARG(n_points >= 0 && k >= 1 && k <= 4 && n_nodes >= 1, "bad sizes");
+  if (n_points == 0) return OFX_OK;
+  OFX_CHECK_ARG(points && anchors && weights && rotations && translations && out, "null buffer");
+  hipLaunchKernelGGL(k_deform_lbs, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
+                     n_points, anchors, weights, valid, k, rotations, translations, out);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

@@ -7,6 +7,8 @@
 * Registration.optimize — NonRigidICP/model/registration_fusion.py:98-145 API (returns
   node_rotations, node_translations, deformed_nodes_to_target, warped_verts, convergence_info,
   source/target frame ids) with the GN solver in place of the Adam/lietorch loop.
+* GaussNewtonSolver.arap — DeformNet.arap (model/model.py:1639-1986): the graph-update solve that moves
+  only the invalid (invisible / new) nodes under ARAP with the valid nodes held at their transforms.
 * optimize_distributed — match-sharded multi-GPU solve: every rank assembles JᵀJ/Jᵀr over its own
   matches, one all-reduce (sum) of the block-sparse accumulators per GN iteration, identical solve
   on every rank.
@@ -92,6 +94,7 @@ class GaussNewtonSolver:
         p.lambda_flow, p.lambda_depth = float(q["lambda_flow"]), float(q["lambda_depth"])
         p.lambda_arap, p.lambda_motion = float(q["lambda_arap"]), float(q["lambda_motion"])
         p.lm_factor, p.stop_loss_diff, p.pcg_tol = float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"])
+        p.mode = 0
         return p
 
     def _problem(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
@@ -165,6 +168,50 @@ class GaussNewtonSolver:
         prm = self._params()
         call("ofx_gn_solve", self._h, byref(pb), byref(prm), byref(r), stream_ptr())
         return self._pack(out, sync)
+
+    def arap(self, graph_nodes, source_node_position, target_node_position, valid_nodes_mask, original_graph_nodes,
+             graph_edges, graph_edges_weights, graph_clusters, R_current, t_current, sync=True, pcg_tol=1e-10):
+        """model.py:1639-1986. graph_nodes (N,3) at the source; source/target_node_position (V,3) of the
+        V valid nodes (mask order); only invalid nodes are updated. The reference builds its ARAP rows on
+        original_graph_nodes and its data rows on graph_nodes; its only caller passes the same array for
+        both (run_model.py:604-619), which this solver requires. Returns node_rotations (N,3,3),
+        node_translations (N,3), deformed_nodes_to_target (V,3), valid_solve, convergence_info."""
+        d = self.device
+        nodes = _t(graph_nodes, d, torch.float32).reshape(-1, 3)
+        N = nodes.shape[0]
+        if original_graph_nodes is not None and not torch.equal(_t(original_graph_nodes, d, torch.float32).reshape(N, 3),
+                                                                nodes):
+            raise ValueError("arap: original_graph_nodes must equal graph_nodes (run_model.py:604-619)")
+        valid = _t(valid_nodes_mask, d, torch.bool).reshape(N)
+        vidx = torch.nonzero(valid).reshape(-1)
+        conv = {"total": [], "arap": [], "data": [], "condition_numbers": [], "valid": 0, "errors": []}
+        if vidx.numel() == 0:                          # model.py:1683-1687
+            conv["errors"].append("Solver failed: No valid correspondences after filtering")
+            return {"convergence_info": conv}
+        src = _t(source_node_position, d, torch.float32).reshape(-1, 3)
+        if not torch.equal(src, nodes[vidx]):
+            raise ValueError("arap: source_node_position must be graph_nodes[valid_nodes_mask] (tsdf.py:660-661)")
+        tpos = torch.zeros((N, 3), device=d)
+        tpos[vidx] = _t(target_node_position, d, torch.float32).reshape(-1, 3)
+        z3 = np.zeros((0, 3), np.float32)
+        pb, N, _ = self._problem(nodes, graph_edges, graph_edges_weights, tpos, valid.float(), z3,
+                                 np.zeros((0, 4), np.int32), np.zeros((0, 4), np.float32), z3, (1.0, 1.0, 0.0, 0.0),
+                                 None, None, R_current, t_current)
+        r, out = self._result(N)
+        prm = self._params()
+        prm.mode = 1
+        prm.pcg_tol = float(pcg_tol)
+        call("ofx_gn_solve", self._h, byref(pb), byref(prm), byref(r), stream_ptr())
+        res = self._pack(out, sync)
+        t_init = self._keep["prev_trans"]
+        t0 = t_init[vidx] if t_init is not None else torch.zeros_like(src)
+        res["deformed_nodes_to_target"] = src + t0          # valid nodes never move (model.py:1719,1961-1962)
+        if sync:
+            ci = res["convergence_info"]
+            res["convergence_info"] = {"total": ci["total"], "arap": ci["arap"], "data": ci["data"],
+                                       "condition_numbers": [], "valid": ci["valid"], "errors": ci["errors"],
+                                       "gn_iterations": ci["gn_iterations"], "pcg_iterations": ci["pcg_iterations"]}
+        return res
 
     def optimize_distributed(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position,
                              node_confidence, source_points, anchors, weights, target_points, intrinsics,

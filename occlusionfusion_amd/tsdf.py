@@ -4,8 +4,11 @@ Same constructor (bbox, max_depth, cam_intr, fopt, visualizer), same `integrate(
 obs_weight=1.)`, `update(im, frame_id)`, `get_volume() -> (tsdf, color, weight)`,
 `check_visibility(points) -> (valid, depth_diff)`, `get_visible_nodes()`, `save_volume/load_volume`,
 `clear()`. Volume state stays device-resident (8³ bricks); get_volume() copies D2H only on request.
-Only the CPU-mode semantics of the reference are implemented (round-half-even pixels, no ray factor:
-tsdf.py:442-494); its pycuda kernel (tsdf.py:192-288) computes different numbers and is not mirrored.
+Both of the reference's integrate arithmetics are available (`semantics`, include/ofx.h OFX_SEM_*):
+"cpu" (default; the numba/numpy branch, tsdf.py:442-494: f64 projection, round-half-even pixels, no
+ray factor) and "pycuda" (the GPU-mode kernel, tsdf.py:192-288: f32, roundf(.+0.5) pixels, ray-factor
+scaled depth difference). The reference picks pycuda iff `fopt.gpu` and pycuda imports (tsdf.py:143);
+here the choice is explicit: constructor argument, else `fopt.integrate_semantics`, else "cpu".
 """
 import logging
 import os
@@ -20,6 +23,7 @@ from .sharding import shard_bricks  # noqa: F401  (re-exported: reference-style 
 
 log = logging.getLogger(__name__)
 TRUNC_MARGIN = 0.04  # tsdf.py:127
+SEMANTICS = {"cpu": 0, "pycuda": 1}   # OFX_SEM_CPU / OFX_SEM_PYCUDA
 
 
 def _opt(fopt, name, default=None):
@@ -54,23 +58,24 @@ def volume_geometry(bbox, max_depth, cam_intr, voxel_dim=None, voxel_size=None):
 class TSDFVolume:
     """Volumetric TSDF fusion of RGB-D images (tsdf.py:37-876), MI355X-resident."""
 
-    def __init__(self, bbox, max_depth, cam_intr, fopt, visualizer=None, device=None, shard=None):
+    def __init__(self, bbox, max_depth, cam_intr, fopt, visualizer=None, device=None, shard=None, semantics=None):
         vd = _opt(fopt, "voxel_dim")
         vs = _opt(fopt, "voxel_size")
         vol_bnds, vol_dim, voxel_size, origin = volume_geometry(bbox, max_depth, cam_intr, vd, vs)
-        self._init(vol_bnds, vol_dim, voxel_size, origin, cam_intr, fopt, visualizer, device, shard)
+        self._init(vol_bnds, vol_dim, voxel_size, origin, cam_intr, fopt, visualizer, device, shard, semantics)
 
     @classmethod
-    def from_grid(cls, origin, voxel_size, vol_dim, cam_intr, fopt=None, visualizer=None, device=None, shard=None):
+    def from_grid(cls, origin, voxel_size, vol_dim, cam_intr, fopt=None, visualizer=None, device=None, shard=None,
+                  semantics=None):
         """Direct grid construction (benchmark configs): origin (3,), voxel size (m), dims (3,)."""
         self = cls.__new__(cls)
         origin = np.asarray(origin, np.float32)
         vol_dim = np.asarray(vol_dim, np.int64).reshape(3)
         vol_bnds = np.stack([origin.astype(np.float64), origin.astype(np.float64) + vol_dim * float(voxel_size)], 1)
-        self._init(vol_bnds, vol_dim, float(voxel_size), origin, cam_intr, fopt, visualizer, device, shard)
+        self._init(vol_bnds, vol_dim, float(voxel_size), origin, cam_intr, fopt, visualizer, device, shard, semantics)
         return self
 
-    def _init(self, vol_bnds, vol_dim, voxel_size, origin, cam_intr, fopt, visualizer, device, shard):
+    def _init(self, vol_bnds, vol_dim, voxel_size, origin, cam_intr, fopt, visualizer, device, shard, semantics=None):
         self.fopt = fopt if fopt is not None else SimpleNamespace(source_frame=0, skip_rate=1)
         self.vis = visualizer
         self.cam_intr = np.eye(3)
@@ -93,6 +98,11 @@ class TSDFVolume:
         self.desc.origin[:] = [float(o) for o in self._vol_origin]
         self.desc.voxel_size = float(self._voxel_size)
         self.desc.trunc_margin = float(self._trunc_margin)
+        sem = semantics if semantics is not None else _opt(self.fopt, "integrate_semantics", "cpu")
+        if sem not in SEMANTICS:
+            raise ValueError(f"integrate semantics must be one of {sorted(SEMANTICS)}, got {sem!r}")
+        self.semantics = sem
+        self.desc.semantics = SEMANTICS[sem]
         n = _lib.c_int64()
         call("ofx_volume_num_slots", byref(self.desc), byref(n))
         self.n_slots = int(n.value)

@@ -67,6 +67,7 @@ class WarpField:
         self.frame_id = src
         self.log = log
         self.updating_warpfield = False
+        self.use_pytorch = True      # warpfield.py:75: deform() -> deform_ED; False -> origin-form deform_lbs
         self._set_graph(graph)
         tsdf.warpfield = self
 
@@ -194,8 +195,30 @@ class WarpField:
              self.num_nodes, 1 if normals else 0, ptr(out), stream_ptr())
         return out
 
+    def deform_lbs_device(self, node_rotations, node_translations, points, anchors, weights, valid_pts=None):
+        """warpfield.py:208-231 deform_lbs (origin-form R x + t, weights == 0 skipped) on device."""
+        pts = _t(points, self.device, torch.float32).reshape(-1, 3)
+        R = _t(node_rotations, self.device, torch.float32).reshape(-1, 9)
+        tt = _t(node_translations, self.device, torch.float32).reshape(-1, 3)
+        a = _t(anchors, self.device, torch.int32)
+        w = _t(weights, self.device, torch.float32)
+        v = None if valid_pts is None else _t(valid_pts, self.device, torch.uint8)
+        out = torch.empty_like(pts)
+        call("ofx_deform_points_lbs", ptr(pts), pts.shape[0], ptr(a), ptr(w), ptr(v), a.shape[1], ptr(R), ptr(tt),
+             R.shape[0], ptr(out), stream_ptr())
+        return out
+
+    def deform_lbs(self, node_rotations, node_translations, world_pts, world_anchors, world_weights, valid_pts):
+        """warpfield.py:208-231 (numpy in, numpy out)."""
+        return self.deform_lbs_device(node_rotations, node_translations, world_pts, world_anchors, world_weights,
+                                      valid_pts).cpu().numpy()
+
     def deform(self, points, anchors, weights, reshape_gpu_vol=None, valid_pts=None):
-        """warpfield.py:270-305 (use_pytorch=True branch -> deform_ED semantics)."""
+        """warpfield.py:270-305: use_pytorch=True -> deform_ED semantics; False -> deform_lbs with the
+        origin-form (rotations, translations) (its CPU and numba-CUDA branches compute the same formula)."""
+        if not self.use_pytorch:
+            return self.deform_lbs(self.rotations.astype(np.float32), self.translations.astype(np.float32), points,
+                                   anchors, weights, valid_pts)
         return self.deform_device(points, anchors, weights, valid_pts).cpu().numpy()
 
     def deform_normals(self, normals, anchors, weights, reshape_gpu_vol=None, valid_pts=None):

@@ -182,6 +182,30 @@ def ed_warp(points, anchors, weights, valid, node_R, node_T, nodes):
     return out
 
 
+def deform_lbs(node_rotations, node_translations, world_pts, world_anchors, world_weights, valid_pts):
+    """warpfield.py:208-231 (numba): origin-form y = Σ_{k: w_k != 0} w_k (R_k x + t_k), accumulated from
+    zero in anchor order, f32; np.dot(R, x) taken as ((R0 x + R1 y) + R2 z) — numba's BLAS gemv order
+    is implementation-defined (last-bit parity with the reference unpinned). Invalid points keep x."""
+    x = np.asarray(world_pts, F32)
+    out = x.copy()
+    v = np.asarray(valid_pts, bool)
+    R = np.asarray(node_rotations, F32).reshape(-1, 3, 3)
+    T = np.asarray(node_translations, F32).reshape(-1, 3)
+    a = np.asarray(world_anchors)
+    w = np.asarray(world_weights, F32)
+    acc = np.zeros((int(v.sum()), 3), F32)
+    xv, av, wv = x[v], a[v], w[v]
+    for k in range(a.shape[1]):
+        use = wv[:, k] != 0
+        ak = np.where(use, av[:, k], 0)
+        Rk, tk = R[ak], T[ak]
+        y = np.stack([((Rk[:, i, 0] * xv[:, 0] + Rk[:, i, 1] * xv[:, 1]) + Rk[:, i, 2] * xv[:, 2]) + tk[:, i]
+                      for i in range(3)], 1)
+        acc = np.where(use[:, None], acc + wv[:, k:k + 1] * y, acc)
+    out[v] = acc
+    return out
+
+
 # ----------------------------------------------------------------------------
 # a7: CPU integrate (tsdf.py:378-494 with 329-376, 576-612)
 # ----------------------------------------------------------------------------
@@ -245,6 +269,81 @@ def integrate(tsdf, weight, color, pts, valid_points, depth_im, color_im, intr,
         nr = np.minimum(F32(255.), np.rint((w_old * old_r + owf * new_r) / w_new))
         color[idx] = nb * F32(COLOR_CONST) + ng * F32(256) + nr
     return int(idx.size)
+
+
+# ----------------------------------------------------------------------------
+# a8: pycuda integrate kernel (tsdf.py:192-288) — the reference's GPU-mode arithmetic
+# ----------------------------------------------------------------------------
+def _roundf(v):
+    """CUDA roundf (half away from zero) of f32 values, formed exactly in f64."""
+    a = np.floor(np.abs(v.astype(F64)) + 0.5)
+    return np.copysign(a, v).astype(F32)
+
+
+def _cvt_sat_i32(v):
+    """(int) of f32 with the saturating GPU conversion: NaN -> 0, clamp to the int32 range."""
+    v64 = v.astype(F64)
+    out = np.where(np.isnan(v64), 0.0, np.clip(np.trunc(np.nan_to_num(v64, nan=0.0)), -2147483648.0, 2147483647.0))
+    return out.astype(np.int64)
+
+
+def integrate_pycuda(tsdf, weight, color, pts, valid_points, depth_im, color_im, intr, obs_weight=1.0,
+                     trunc=TRUNC_MARGIN, with_color=True):
+    """In-place restatement of the pycuda `integrate` kernel (tsdf.py:192-288) over flat f32 volumes.
+
+    f32 arithmetic, identity cam_pose applied literally (tsdf.py:236-241); pixel =
+    (int)roundf(f32(f64(f·(x/z)+c) + 0.5)) (:243-244: the 0.5 literal is a double); skip if outside the
+    image or z < 0 (:248) or depth == 0 (:252); depth difference times sqrt(1+mx²+my²) of the integer
+    pixel (:261-264); dist = fminf(1, dd/trunc); roundf colours (:282-284). nvcc's default FMA
+    contraction is not modelled (each product is rounded): parity unpinned at the last-bit level.
+    Returns the number of updated voxels."""
+    one, zero = F32(1), F32(0)
+    P = np.asarray(pts, F32)
+    sel = np.nonzero(np.asarray(valid_points, bool))[0]
+    x, y, z = P[sel, 0] - zero, P[sel, 1] - zero, P[sel, 2] - zero
+    with np.errstate(all="ignore"):
+        cxp = (one * x + zero * y) + zero * z
+        cyp = (zero * x + one * y) + zero * z
+        czp = (zero * x + zero * y) + one * z
+        fx, fy, cx, cy = (F32(v) for v in intr)
+        sx = fx * (cxp / czp) + cx
+        sy = fy * (cyp / czp) + cy
+        u = _cvt_sat_i32(_roundf((sx.astype(F64) + 0.5).astype(F32)))
+        v = _cvt_sat_i32(_roundf((sy.astype(F64) + 0.5).astype(F32)))
+        H, W = depth_im.shape
+        ok = (u >= 0) & (u < W) & (v >= 0) & (v < H) & ~(czp < 0)
+        sel, u, v, czp = sel[ok], u[ok], v[ok], czp[ok]
+        d = np.asarray(depth_im, F32)[v, u]
+        ok = d != 0
+        sel, u, v, czp, d = sel[ok], u[ok], v[ok], czp[ok], d[ok]
+        dd = d - czp
+        mx = (u.astype(F32) - cx) / fx
+        my = (v.astype(F32) - cy) / fy
+        dd = dd * np.sqrt((one + mx * mx) + my * my)
+        tr = F32(trunc)
+        ok = ~(dd < -tr)
+        sel, u, v, dd = sel[ok], u[ok], v[ok], dd[ok]
+        dist = np.fmin(one, dd / tr)
+        ow = F32(obs_weight)
+        w_old = weight[sel]
+        w_new = w_old + ow
+        weight[sel] = w_new
+        tsdf[sel] = (tsdf[sel] * w_old + ow * dist) / w_new
+        if with_color:
+            C, c256 = F32(65536), F32(256)
+            oc = color[sel]
+            ob = np.floor(oc / C)
+            og = np.floor((oc - ob * c256 * c256) / c256)
+            orr = (oc - ob * c256 * c256) - og * c256
+            nc = np.asarray(color_im, F32)[v, u]
+            nb = np.floor(nc / C)
+            ng = np.floor((nc - nb * c256 * c256) / c256)
+            nr = (nc - nb * c256 * c256) - ng * c256
+            b2 = np.fmin(_roundf((ob * w_old + ow * nb) / w_new), F32(255))
+            g2 = np.fmin(_roundf((og * w_old + ow * ng) / w_new), F32(255))
+            r2 = np.fmin(_roundf((orr * w_old + ow * nr) / w_new), F32(255))
+            color[sel] = (b2 * c256 * c256 + g2 * c256) + r2
+    return int(sel.size)
 
 
 # ----------------------------------------------------------------------------
@@ -439,6 +538,97 @@ def gn_optimize(graph_nodes, graph_edges, graph_edges_weights, target_node_posit
         t = np.zeros((N, 3))
     conv['valid'] = int(valid)
     return dict(node_rotations=R, node_translations=t, valid_solve=int(valid), convergence_info=conv)
+
+
+def gn_arap(graph_nodes, source_node_position, target_node_position, valid_nodes_mask, original_graph_nodes,
+            graph_edges, graph_edges_weights, R_current, t_current, **params):
+    """DeformNet.arap (model/model.py:1639-1986), dense float64: data rows per valid node with the
+    residual as its own translation Jacobian (:1766-1784), ARAP rows on original_graph_nodes
+    (:1796-1840), A = JᵀJ + λI, b = -Jᵀr, LU, early stop (:1915-1926), update of the invalid nodes
+    only (:1935-1943). Returns dict(node_rotations, node_translations, deformed_nodes_to_target,
+    valid_solve, convergence_info)."""
+    p = dict(GN_DEFAULTS)
+    p.update(params)
+    from scipy.linalg import lu_factor, lu_solve
+    g = np.asarray(graph_nodes, F64)
+    go = np.asarray(original_graph_nodes, F64)
+    N = g.shape[0]
+    valid = np.asarray(valid_nodes_mask, bool).reshape(N)
+    vidx = np.nonzero(valid)[0]
+    M = vidx.size
+    src = np.asarray(source_node_position, F64).reshape(M, 3)
+    tgt = np.asarray(target_node_position, F64).reshape(M, 3)
+    R = np.asarray(R_current, F64).reshape(N, 3, 3).copy()
+    t = np.asarray(t_current, F64).reshape(N, 3).copy()
+    edges, (ei, ek) = gn_edges(graph_edges)
+    E = edges.shape[0]
+    n_nb = np.asarray(graph_edges).shape[1]
+    ew = np.ones(E)
+    if p['use_edge_weighting']:
+        ew = float(n_nb) * np.asarray(graph_edges_weights, F64)[ei, ek]
+    lf, la = math.sqrt(p['lambda_flow']), math.sqrt(p['lambda_arap'])
+    lm_factor = p['lm_factor']
+    conv = dict(total=[], arap=[], data=[], condition_numbers=[], valid=0, errors=[])
+    inv = ~valid
+    ill_posed = False
+    res = None
+    deformed = None
+    for gn_i in range(p['num_iter']):
+        if gn_i % 3 == 2:
+            lm_factor /= 2
+        deformed = src + t[vidx]
+        J = np.zeros((M * 3, N * 6))
+        rd = (lf * (deformed - tgt)).reshape(-1)
+        for c in range(3):
+            J[np.arange(M) * 3 + c, 3 * N + 3 * vidx + c] += rd[c::3]
+        blocks_J, blocks_r = [J], [rd]
+        ra = None
+        if E > 0:
+            Ja = np.zeros((E * 3, N * 6))
+            i0, i1 = edges[:, 0], edges[:, 1]
+            rowsE = np.arange(E) * 3
+            delta = np.einsum('eij,ej->ei', R[i0], go[i1] - go[i0])
+            ra = (la * ew[:, None] * (delta + go[i0] + t[i0] - (go[i1] + t[i1]))).reshape(-1)
+            for c in range(3):
+                Ja[rowsE + c, 3 * N + 3 * i0 + c] += la * ew
+                Ja[rowsE + c, 3 * N + 3 * i1 + c] += -la * ew
+            Sa = -la * ew[:, None, None] * skew(delta)
+            for i in range(3):
+                for j in range(3):
+                    Ja[rowsE + i, 3 * i0 + j] += Sa[:, i, j]
+            blocks_J.append(Ja)
+            blocks_r.append(ra)
+        Jall = np.concatenate(blocks_J, 0)
+        res = np.concatenate(blocks_r, 0)
+        A = Jall.T @ Jall + np.eye(6 * N) * lm_factor
+        b = -(Jall.T @ res)
+        try:
+            x = lu_solve(lu_factor(A), b)
+        except Exception:
+            ill_posed = True
+            conv['errors'].append("Solver failed: Ill-posed system!")
+            break
+        if not np.all(np.isfinite(x)):
+            ill_posed = True
+            conv['errors'].append("Solver failed: Non-finite solution x!")
+            break
+        loss_data, loss_total = float(np.linalg.norm(rd)), float(np.linalg.norm(res))
+        if len(conv['total']):
+            if loss_total - conv['total'][-1] > p['stop_loss_diff']:
+                break
+            if loss_total == conv['total'][-1]:
+                break
+        conv['data'].append(loss_data)
+        conv['total'].append(loss_total)
+        R_inc = angle_axis_to_rotation_matrix(x[:3 * N].reshape(N, 3))
+        R[inv] = R_inc[inv] @ R[inv]
+        t[inv] = t[inv] + x[3 * N:].reshape(N, 3)[inv]
+        if ra is not None:
+            conv['arap'].append(float(np.linalg.norm(ra)))
+    valid_solve = (not ill_posed) and res is not None and bool(np.all(np.isfinite(res)))
+    conv['valid'] = int(valid_solve)
+    return dict(node_rotations=R, node_translations=t, deformed_nodes_to_target=deformed,
+                valid_solve=int(valid_solve), convergence_info=conv)
 
 
 def gn_system(graph_nodes, graph_edges, target_node_position, node_confidence, source_points, anchors,

@@ -166,6 +166,27 @@ def test_deform_points_and_visibility(cuda, golden_dir):
     np.testing.assert_array_equal(dd, odd)
 
 
+def test_deform_lbs_origin_form_bitexact(cuda, golden_dir):
+    """WarpField.deform with use_pytorch=False -> deform_lbs on the origin-form transforms
+    (warpfield.py:208-231,270-305) vs the oracle; zero weights skipped; invalid points unchanged."""
+    from occlusionfusion_amd import WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    vol = _small_volume(g)
+    wf = WarpField(_graph(g), vol)
+    wf.set_node_transforms(g["R"], g["T"])
+    rng = np.random.default_rng(1)
+    pts = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))[rng.choice(240240, 5000)]
+    a, w, v = wf.skin(pts)
+    w[::7, 1] = 0.0
+    wf.use_pytorch = False
+    out = wf.deform(pts, a, w, None, v)
+    Rf, tf = wf.rotations.astype(np.float32), wf.translations.astype(np.float32)
+    np.testing.assert_array_equal(out, fo.deform_lbs(Rf, tf, pts, a, w, v))
+    np.testing.assert_array_equal(out[~v], pts[~v])
+    ed = fo.ed_warp(pts, a, w, v, g["R"], g["T"], g["nodes"])
+    assert np.abs(out - ed).max() < 2e-6     # same warp, different association order
+
+
 def test_volume_save_load_roundtrip(cuda, golden_dir, tmp_path):
     g = _g(golden_dir, "integrate_small.npz")
     vol = _small_volume(g)
@@ -274,3 +295,79 @@ def test_gn_repeatable(cuda, golden_dir):
     a = s.optimize(*_gn_inputs(g))
     b = s.optimize(*_gn_inputs(g))
     np.testing.assert_allclose(a["node_translations"].cpu().numpy(), b["node_translations"].cpu().numpy(), atol=1e-9)
+
+
+def _oracle_two_frames(g, integ):
+    """Source frame + one ED-warped frame through an oracle integrate function (flat f32 volumes)."""
+    world = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))
+    V = world.shape[0]
+    tsdf, weight, color = np.ones(V, np.float32), np.zeros(V, np.float32), np.zeros(V, np.float32)
+    intr = tuple(g["intr"])
+    integ(tsdf, weight, color, world, np.ones(V, bool), fo.depth_of(g["im0"]), fo.pack_color(g["im0"]), intr)
+    a, w, v = fo.skin(world, g["nodes"], float(g["node_coverage"]))
+    warped = fo.ed_warp(world, a, w, v, g["R"], g["T"], g["nodes"])
+    n = integ(tsdf, weight, color, warped, v, fo.depth_of(g["im1"]), fo.pack_color(g["im1"]), intr)
+    return tsdf, weight, color, n
+
+
+@pytest.mark.parametrize("path", ["palette", "global"])
+def test_integrate_pycuda_semantics_bitexact(cuda, golden_dir, path):
+    """semantics="pycuda" (tsdf.py:192-288 arithmetic) vs the oracle restatement, source + warped frame."""
+    from occlusionfusion_amd import TSDFVolume, WarpField
+    g = _g(golden_dir, "integrate_small.npz")
+    t_o, w_o, c_o, n_o = _oracle_two_frames(g, fo.integrate_pycuda)
+    vol = TSDFVolume.from_grid(g["origin"], float(g["voxel_size"]), g["dims"], tuple(g["intr"]), _Opt(),
+                               semantics="pycuda")
+    vol.use_palette = path == "palette"
+    vol.integrate({"im": g["im0"], "id": 0})
+    wf = WarpField(_graph(g), vol)
+    wf.frame_id = 1
+    wf.set_node_transforms(g["R"], g["T"])
+    vol.integrate({"im": g["im1"], "id": 1})
+    t, c, w = vol.get_volume()
+    D = tuple(g["dims"])
+    np.testing.assert_array_equal(t, t_o.reshape(D))
+    np.testing.assert_array_equal(w, w_o.reshape(D))
+    np.testing.assert_array_equal(c, c_o.reshape(D))
+    # the two reference arithmetics really differ on this input (ray factor, pixel rounding)
+    assert not np.array_equal(t, g["tsdf1"].reshape(D))
+
+
+@pytest.mark.parametrize("case", ["nonrigid", "two_components"])
+def test_gn_arap_matches_dense_oracle(cuda, case):
+    """GaussNewtonSolver.arap (DeformNet.arap, model.py:1639-1986) vs the dense f64 oracle: node
+    transforms within 1e-5; valid nodes untouched. Second case: two disconnected graph components
+    (two null-space translations projected out). lambda_flow = 0 as in the reference (model.py:98 and
+    its own arap tests, fusion_tests/motion_complete_model_test.py:606,781): with lambda_flow > 0 the
+    residual-as-Jacobian rows leave the common translation only weakly determined (eigenvalue ~ |r|²),
+    so an iterative solve and a dense LU differ along it — no parity is claimed there."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    from occlusionfusion_amd import synthetic as S
+    rng = np.random.default_rng(4)
+    pts = rng.normal(size=(3000, 3))
+    pts = 0.3 * pts / np.linalg.norm(pts, axis=1, keepdims=True) + np.array([0, 0, 1.4])
+    nodes = S.sample_nodes(pts.astype(np.float32), 0.08, 5)
+    params = {}
+    if case == "two_components":
+        nodes = np.concatenate([nodes, nodes + np.array([1.5, 0, 0], np.float32)], 0)
+    e, w = S.euclidean_edges(nodes, 8)
+    N = len(nodes)
+    valid = np.ones(N, bool)
+    valid[rng.choice(N, N // 3, replace=False)] = False
+    R = fo.angle_axis_to_rotation_matrix(rng.normal(0, 0.03, (N, 3))).astype(np.float32)
+    t = rng.normal(0, 0.01, (N, 3)).astype(np.float32)
+    tgt = (nodes[valid] + t[valid] + rng.normal(0, 0.002, (valid.sum(), 3))).astype(np.float32)
+    ref = fo.gn_arap(nodes, nodes[valid], tgt, valid, nodes, e, w, R, t, **params)
+    s = GaussNewtonSolver(N, 16, **params)
+    out = s.arap(nodes, nodes[valid], tgt, valid, nodes, e, w, None, R, t)
+    assert out["valid_solve"] == ref["valid_solve"] == 1
+    Rg, tg = out["node_rotations"].cpu().numpy(), out["node_translations"].cpu().numpy()
+    np.testing.assert_array_equal(Rg[valid], R[valid])
+    np.testing.assert_array_equal(tg[valid], t[valid])
+    assert np.abs(Rg - ref["node_rotations"]).max() < 1e-5
+    assert np.abs(tg - ref["node_translations"]).max() < 1e-5
+    ci = out["convergence_info"]
+    assert len(ci["total"]) == len(ref["convergence_info"]["total"])
+    np.testing.assert_allclose(ci["total"], ref["convergence_info"]["total"], rtol=1e-4)   # per-step states differ ~1e-5
+    np.testing.assert_allclose(out["deformed_nodes_to_target"].cpu().numpy(), ref["deformed_nodes_to_target"],
+                               atol=1e-7)

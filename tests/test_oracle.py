@@ -117,6 +117,68 @@ def test_color_running_average_kat():
     assert (r, g_, b) == (15, 30, 46)    # (30+61)/2 = 45.5 -> half-even 46
 
 
+def test_pycuda_semantics_kat():
+    """tsdf.py:192-288: pixel = (int)roundf(s + 0.5) (s = f·x/z + c), ray-factor scaled depth
+    difference, skip iff depth == 0 or z < 0, colours rounded half away from zero."""
+    intr = (100.0, 100.0, 10.0, 10.0)
+    depth = np.ones((21, 21), np.float32)
+    cim = np.zeros_like(depth)
+    # s = 10.0 -> pixel 11 (CPU: rint -> 10); s = -0.6 -> roundf(-0.1) = -0 -> 0, in bounds;
+    # s = -1.0 -> roundf(-0.5) = -1 -> out of the image
+    pts = np.array([[0.0, 0.0, 0.98], [-0.106, 0.0, 1.0], [-0.11, 0.0, 1.0]], np.float32)
+    t, w, c = np.ones(3, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    n = fo.integrate_pycuda(t, w, c, pts, np.ones(3, bool), depth, cim, intr)
+    assert n == 2 and w.tolist() == [1.0, 1.0, 0.0]
+    mx = (11 - 10) / 100.0
+    expect = min(1.0, (1.0 - 0.98) * np.sqrt(1 + 2 * mx * mx) / 0.04)     # pixel (11, 11)
+    assert abs(t[0] - expect) < 1e-6 and t[0] != np.float32(0.02 / 0.04)
+    # depth == 0 skips; negative z skips; valid mask respected
+    d0 = depth.copy()
+    d0[11, 11] = 0.0
+    t2, w2, c2 = np.ones(3, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    pts2 = np.array([[0.0, 0.0, 0.98], [0.0, 0.0, -0.5], [0.01, 0.0, 1.0]], np.float32)
+    fo.integrate_pycuda(t2, w2, c2, pts2, np.array([True, True, False]), d0, cim, intr)
+    assert w2.tolist() == [0.0, 0.0, 0.0]
+    # colour: (30 + 59) / 2 = 44.5 -> roundf 45 (the CPU branch's np.round gives 44)
+    depth2 = np.ones((4, 4), np.float32)
+    rgb = np.zeros((3, 4, 4), np.float32)
+    rgb[2] = 30 / 255
+    im = np.concatenate([rgb, np.zeros((2, 4, 4), np.float32), depth2[None]], 0)
+    p1 = np.array([[0, 0, 0.99]], np.float32)
+    res = []
+    for integ in (fo.integrate_pycuda, fo.integrate):
+        t3, w3, c3 = np.ones(1, np.float32), np.zeros(1, np.float32), np.zeros(1, np.float32)
+        integ(t3, w3, c3, p1, np.ones(1, bool), depth2, fo.pack_color(im), (1.0, 1.0, 1.0, 1.0))
+        rgb2 = rgb * 0
+        rgb2[2] = 59 / 255
+        im2 = np.concatenate([rgb2, np.zeros((2, 4, 4), np.float32), depth2[None]], 0)
+        integ(t3, w3, c3, p1, np.ones(1, bool), depth2, fo.pack_color(im2), (1.0, 1.0, 1.0, 1.0))
+        res.append(c3[0] // 65536)
+    assert res == [45, 44]
+
+
+def test_deform_lbs_equals_ed_warp_in_origin_form():
+    """warpfield.py:208-231 with t = -R g + g + T (warpfield.py:407-408) is the ED warp up to rounding;
+    zero-weight anchors are skipped (their node index is never read)."""
+    rng = np.random.default_rng(3)
+    N = 30
+    nodes = rng.uniform(-0.2, 0.2, (N, 3)).astype(np.float32)
+    R = fo.angle_axis_to_rotation_matrix(rng.normal(0, 0.1, (N, 3))).astype(np.float32)
+    T = rng.normal(0, 0.01, (N, 3)).astype(np.float32)
+    pts = rng.uniform(-0.2, 0.2, (500, 3)).astype(np.float32)
+    a, w, v = fo.skin(pts, nodes, 0.1)
+    t_org = fo.to_origin_form(R.astype(np.float64), T.astype(np.float64), nodes.astype(np.float64)).astype(np.float32)
+    lbs = fo.deform_lbs(R, t_org, pts, a, w, v)
+    ed = fo.ed_warp(pts, a, w, v, R, T, nodes)
+    assert v.any() and np.abs(lbs - ed).max() < 2e-6
+    np.testing.assert_array_equal(lbs[~v], pts[~v])
+    a2 = a.copy()
+    w2 = w.copy()
+    w2[:, 3] = 0
+    a2[:, 3] = 10 ** 6                      # never dereferenced
+    fo.deform_lbs(R, t_org, pts, a2, w2, v)
+
+
 def test_ed_warp_identity_shrinks_by_weight_sum():
     nodes = np.array([[0, 0, 0], [0.02, 0, 0], [0, 0.02, 0], [0, 0, 0.02]], np.float32)
     x = np.array([[0.01, 0.01, 0.01]], np.float32)
@@ -173,6 +235,36 @@ def test_kornia_angle_axis_matches_rodrigues():
     small = np.array([[1e-4, -2e-4, 3e-4]])
     Rs = fo.angle_axis_to_rotation_matrix(small)
     np.testing.assert_array_equal(Rs[0], [[1, -3e-4, -2e-4], [3e-4, 1, -1e-4], [2e-4, 1e-4, 1]])
+
+
+def _arap_graph(seed=0, n_pts=3000):
+    from occlusionfusion_amd import synthetic as S
+    rng = np.random.default_rng(seed)
+    pts = rng.normal(size=(n_pts, 3))
+    pts = 0.3 * pts / np.linalg.norm(pts, axis=1, keepdims=True) + np.array([0, 0, 1.4])
+    nodes = S.sample_nodes(pts.astype(np.float32), 0.08, seed + 1)
+    e, w = S.euclidean_edges(nodes, 8)
+    return rng, nodes, e, w
+
+
+def test_gn_arap_rigid_translation_propagates_to_invalid_nodes():
+    """DeformNet.arap: valid nodes translated by v (held fixed), invalid nodes start at 0 and are pulled
+    to v by the ARAP rows alone (lambda_flow = 0); valid nodes never move."""
+    rng, nodes, e, w = _arap_graph()
+    N = len(nodes)
+    valid = np.ones(N, bool)
+    valid[rng.choice(N, N // 4, replace=False)] = False
+    v = np.array([0.01, -0.02, 0.005])
+    R = np.tile(np.eye(3), (N, 1, 1))
+    t = np.zeros((N, 3))
+    t[valid] = v
+    out = fo.gn_arap(nodes, nodes[valid], nodes[valid] + v, valid, nodes, e, w, R, t)
+    assert out["valid_solve"] == 1
+    np.testing.assert_array_equal(out["node_translations"][valid], t[valid])
+    np.testing.assert_array_equal(out["node_rotations"][valid], R[valid])
+    assert np.abs(out["node_translations"][~valid] - v).max() < 1e-6
+    tot = out["convergence_info"]["total"]
+    assert tot[-1] < 1e-5 * tot[0] and out["convergence_info"]["data"] == [0.0] * len(tot)
 
 
 def test_gn_system_block_structure():

@@ -26,6 +26,8 @@
  *                                                                          registration_fusion.py:157-184, warpfield.py:312-367
  *   ofx_deform_points_lbs   WarpField.deform_lbs / deform_lbs_cuda (origin form) warpfield.py:208-266,270-305
  *   ofx_visibility          TSDFVolume.check_visibility                     tsdf.py:576-612
+ *   ofx_truncated_region    TSDFVolume.compute_truncated_region            tsdf.py:704-745
+ *   ofx_mesh_*              measure.marching_cubes in get_mesh / get_point_cloud, colours tsdf.py:748-809
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
  *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
@@ -164,6 +166,29 @@ int ofx_deform_points_lbs(const float* points, int64_t n_points, const int32_t* 
 /* check_visibility: valid u8[P], depth_diff f64[P] */
 int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
                    double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s);
+
+/* ---------------- Surface extraction ----------------
+ * Whole volume only (a shard needs a halo: OFX_ERR_ARG). Voxel-index coordinates as skimage returns. */
+/* TSDFVolume.compute_truncated_region (tsdf.py:704-745): mask u8 per voxel slot (bricked layout) */
+int ofx_truncated_region(const ofx_volume_desc* desc, const float* tsdf, double max_diff, uint8_t* mask,
+                         ofx_stream_t s);
+/* Marching cubes (measure.marching_cubes at tsdf.py:755,794), two phases on an opaque handle:
+ * ofx_mesh_count classifies cells and sizes the output (synchronises the stream), the caller allocates,
+ * ofx_mesh_emit writes verts f32[V*3] (voxel coordinates), faces i32[F*3] and optionally normals
+ * f32[V*3] (unit, towards increasing tsdf), values f32[V], keys i64[V] (= C-index(edge start)*3 + axis).
+ * use_mask = 0: every cell (get_point_cloud); use_mask = 1 with mask = NULL: the volume's truncated region
+ * with max_diff (get_mesh, tsdf.py:792); with a mask (bricked u8): that mask. A cell [c, c+1]^3 is
+ * processed iff the mask holds at its far corner c+1. */
+int ofx_mesh_create(void** handle);
+int ofx_mesh_destroy(void* handle);
+int ofx_mesh_count(void* handle, const ofx_volume_desc* desc, const float* tsdf, const uint8_t* mask, double max_diff,
+                   int32_t use_mask, float level, int64_t* n_verts, int64_t* n_faces, ofx_stream_t s);
+int ofx_mesh_emit(void* handle, float* verts, int32_t* faces, float* normals, float* values, int64_t* keys,
+                  ofx_stream_t s);
+/* get_mesh / get_point_cloud epilogue (tsdf.py:757-767,796-807): world = verts*f32(voxel_size) + origin
+ * (f32, may be NULL) and colours u8[V*3] = [r,g,b] of the voxel nearest each vertex (may be NULL). */
+int ofx_mesh_finish(const ofx_volume_desc* desc, const float* color, const float* verts, int64_t n_verts,
+                    float* world, uint8_t* colors, ofx_stream_t s);
 
 /* ---------------- Gauss-Newton (DeformNet.optimize) ---------------- */
 typedef struct ofx_gn_params {

@@ -63,6 +63,12 @@ _SIGS = {
     "ofx_deform_points": [P, c_int64, P, P, P, c_int32, P, c_int32, c_int32, P, P],
     "ofx_deform_points_lbs": [P, c_int64, P, P, P, c_int32, P, P, c_int32, P, P],
     "ofx_visibility": [P, c_int64, P, P, c_double, P, P, P],
+    "ofx_truncated_region": [P, P, c_double, P, P],
+    "ofx_mesh_create": [P],
+    "ofx_mesh_destroy": [P],
+    "ofx_mesh_count": [P, P, P, P, c_double, c_int32, c_float, P, P, P],
+    "ofx_mesh_emit": [P, P, P, P, P, P, P],
+    "ofx_mesh_finish": [P, P, P, c_int64, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],

@@ -254,6 +254,106 @@ class TSDFVolume:
         visible, _ = self.check_visibility(self.warpfield.get_deformed_nodes())
         return visible
 
+    # ------------------------------------------------------------------ surface extraction
+    @staticmethod
+    def compute_truncated_region(tsdf_vol, max_diff):
+        """tsdf.py:704-745 on a dense numpy (W,H,D) volume -> bool (W,H,D); computed by the HIP kernel."""
+        t = np.ascontiguousarray(tsdf_vol, np.float32)
+        desc = _lib.VolumeDesc()
+        desc.dim[:] = [int(x) for x in t.shape]
+        desc.brick_x0, desc.brick_x1 = 0, (t.shape[0] + 7) // 8
+        desc.voxel_size, desc.trunc_margin = 1.0, TRUNC_MARGIN
+        n = _lib.c_int64()
+        call("ofx_volume_num_slots", byref(desc), byref(n))
+        dev = torch.device("cuda", torch.cuda.current_device())
+        src = torch.from_numpy(t).to(dev)
+        br = torch.empty(int(n.value), dtype=torch.float32, device=dev)
+        call("ofx_volume_from_dense", byref(desc), ptr(src), ptr(br), stream_ptr())
+        m = torch.empty(int(n.value), dtype=torch.uint8, device=dev)
+        call("ofx_truncated_region", byref(desc), ptr(br), float(max_diff), ptr(m), stream_ptr())
+        mf = m.float()
+        dense = torch.empty(t.shape, dtype=torch.float32, device=dev)
+        call("ofx_volume_to_dense", byref(desc), ptr(mf), ptr(dense), stream_ptr())
+        return dense.cpu().numpy() != 0
+
+    def truncated_region_device(self, max_diff=1.2):
+        """Bricked u8 mask of this (whole) volume's truncated region."""
+        m = torch.empty(self.n_slots, dtype=torch.uint8, device=self.device)
+        call("ofx_truncated_region", byref(self.desc), ptr(self.tsdf_b), float(max_diff), ptr(m), stream_ptr())
+        return m
+
+    def extract_mesh_device(self, use_mask=True, mask=None, level=0.0, max_diff=1.2, with_normals=True,
+                            with_values=False, with_keys=False):
+        """Marching cubes on the resident volume -> dict of device tensors: verts (V,3) f32 voxel
+        coordinates, faces (F,3) int32 and optional normals / values / keys (include/ofx.h ofx_mesh_*)."""
+        if getattr(self, "_mesh_h", None) is None:
+            h = _lib.c_void_p()
+            call("ofx_mesh_create", byref(h))
+            self._mesh_h = h
+        nv, nf = _lib.c_int64(), _lib.c_int64()
+        call("ofx_mesh_count", self._mesh_h, byref(self.desc), ptr(self.tsdf_b), ptr(mask), float(max_diff),
+             1 if use_mask else 0, float(level), byref(nv), byref(nf), stream_ptr())
+        V, F = int(nv.value), int(nf.value)
+        kw = dict(device=self.device)
+        out = {"verts": torch.empty((V, 3), dtype=torch.float32, **kw),
+               "faces": torch.empty((F, 3), dtype=torch.int32, **kw),
+               "normals": torch.empty((V, 3), dtype=torch.float32, **kw) if with_normals else None,
+               "values": torch.empty(V, dtype=torch.float32, **kw) if with_values else None,
+               "keys": torch.empty(V, dtype=torch.int64, **kw) if with_keys else None}
+        call("ofx_mesh_emit", self._mesh_h, ptr(out["verts"]), ptr(out["faces"]), ptr(out["normals"]),
+             ptr(out["values"]), ptr(out["keys"]), stream_ptr())
+        return out
+
+    def _mesh_world_colors(self, verts):
+        V = verts.shape[0]
+        world = torch.empty((V, 3), dtype=torch.float32, device=self.device)
+        colors = torch.empty((V, 3), dtype=torch.uint8, device=self.device)
+        call("ofx_mesh_finish", byref(self.desc), ptr(self.color_b), ptr(verts), V, ptr(world), ptr(colors),
+             stream_ptr())
+        return world, colors
+
+    def get_mesh(self):
+        """tsdf.py:770-809: marching cubes of the truncated region (max_diff 1.2) -> (verts world f32 (V,3),
+        faces (F,3), norms f32 (V,3), colors uint8 (V,3) [r,g,b]), numpy."""
+        m = self.extract_mesh_device(use_mask=True, max_diff=1.2)
+        world, colors = self._mesh_world_colors(m["verts"])
+        return (world.cpu().numpy(), m["faces"].cpu().numpy().astype(np.int64), m["normals"].cpu().numpy(),
+                colors.cpu().numpy())
+
+    def get_point_cloud(self):
+        """tsdf.py:748-768: unmasked marching-cubes vertices in world coordinates + colours -> (V,6)."""
+        m = self.extract_mesh_device(use_mask=False, with_normals=False)
+        world, colors = self._mesh_world_colors(m["verts"])
+        return np.hstack([world.cpu().numpy(), colors.cpu().numpy()])
+
+    def get_canonical_model(self):
+        """tsdf.py:811-820 (cached until clear())."""
+        if not hasattr(self, "canonical_model"):
+            self.canonical_model = self.get_mesh()
+        return self.canonical_model
+
+    def get_deformed_model(self):
+        """tsdf.py:829-845: canonical mesh warped to the current frame (WarpField.deform_mesh)."""
+        if hasattr(self, "deformed_model"):
+            return self.deformed_model
+        src = _opt(self.fopt, "source_frame", 0)
+        if self.frame_id != src:
+            verts, faces, normals, colors = self.get_canonical_model()
+            dv, dn, _, _, _ = self.warpfield.deform_mesh(verts, normals)
+            self.deformed_model = (dv, faces, dn, colors)
+        else:
+            self.deformed_model = self.get_canonical_model()
+        return self.deformed_model
+
+    def __del__(self):
+        h = getattr(self, "_mesh_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.ofx_mesh_destroy(h)
+            except Exception:
+                pass
+            self._mesh_h = None
+
     def clear(self):
         """tsdf.py:857-876."""
         for a in ("reduced_graph_dict", "deformed_model", "canonical_model"):

@@ -716,3 +716,193 @@ def node_major_perm(N):
     """Permutation from the reference's [rot(3N) | trans(3N)] unknown order to [node: rot3, trans3]."""
     return np.concatenate([[3 * i, 3 * i + 1, 3 * i + 2, 3 * N + 3 * i, 3 * N + 3 * i + 1, 3 * N + 3 * i + 2]
                            for i in range(N)])
+
+
+# ----------------------------------------------------------------------------
+# f1: surface extraction — compute_truncated_region (tsdf.py:704-745) + marching cubes (skimage 0.22
+#     measure.marching_cubes as called at tsdf.py:755,794) + get_mesh colours (tsdf.py:770-809)
+# ----------------------------------------------------------------------------
+def compute_truncated_region(tsdf_vol, max_diff):
+    """tsdf.py:704-745 (numba prange): True where |t| <= 0.9, not on the volume boundary, and every one of
+    the 27 neighbours (itself included) differs from t by at most max_diff. The neighbour writes inside
+    the loop (`if abs(tsdf_vol[w,h,d]) > 0.9`, :738-739) are dead code (that case `continue`d at :727),
+    so the result is race-free. Comparisons: f32 |t| and f32 |t_n - t| against f64 literals."""
+    t = np.asarray(tsdf_vol, F32)
+    W, H, D = t.shape
+    out = ~(np.abs(t).astype(F64) > 0.9)
+    inner = np.zeros_like(out)
+    inner[1:-1, 1:-1, 1:-1] = True
+    out &= inner
+    if W < 3 or H < 3 or D < 3:
+        return out
+    c = t[1:-1, 1:-1, 1:-1]
+    ok = np.ones(c.shape, bool)
+    for dw in (-1, 0, 1):
+        for dh in (-1, 0, 1):
+            for dd in (-1, 0, 1):
+                n = t[1 + dw:W - 1 + dw, 1 + dh:H - 1 + dh, 1 + dd:D - 1 + dd]
+                ok &= ~(np.abs(n - c).astype(F64) > max_diff)
+    out[1:-1, 1:-1, 1:-1] &= ok
+    return out
+
+
+FLT_EPSILON = float(np.finfo(np.float32).eps)
+MC_EDGES = []          # 12 cube edges: (start corner, end corner); corner c = (c&1, c>>1&1, c>>2&1)
+for _a in range(3):
+    _b, _c = [x for x in range(3) if x != _a]
+    for _oc in range(2):
+        for _ob in range(2):
+            _s = [0, 0, 0]
+            _s[_b], _s[_c] = _ob, _oc
+            _e = list(_s)
+            _e[_a] = 1
+            MC_EDGES.append((_s[0] + 2 * _s[1] + 4 * _s[2], _e[0] + 2 * _e[1] + 4 * _e[2]))
+
+
+def mc_tables():
+    """Triangle table of the 256 cube configurations (corner inside iff value < level), generated by rule
+    rather than transcribed: on each cube face the cut edges pair up so that every run of inside corners
+    is cut off on its own (ambiguous faces separate the inside corners — a rule that depends on the
+    face's corner signs only, so neighbouring cells agree and the surface is closed); the face segments,
+    directed exit -> entry with the inside on the left seen from outside the cube, chain into loops;
+    each loop is fanned from its lowest edge id, wound so the right-hand normal points to the outside
+    (values >= level). Returns list of 256 lists of (e0, e1, e2). Same rule as csrc/mc.hip."""
+    edge_id = {}
+    for k, (p, q) in enumerate(MC_EDGES):
+        edge_id[(p, q)] = edge_id[(q, p)] = k
+    faces = []
+    for a in range(3):
+        b, c = [x for x in range(3) if x != a]
+        for s in range(2):
+            cs = []
+            for ub, uc in ((0, 0), (1, 0), (1, 1), (0, 1)):
+                v = [0, 0, 0]
+                v[a], v[b], v[c] = s, ub, uc
+                cs.append(v[0] + 2 * v[1] + 4 * v[2])
+            n = np.zeros(3)
+            n[a] = 2 * s - 1
+            if np.dot(np.cross(np.eye(3)[b], np.eye(3)[c]), n) < 0:
+                cs = cs[::-1]
+            faces.append(cs)
+    tables = []
+    for cfg in range(256):
+        inside = [(cfg >> c) & 1 for c in range(8)]
+        nxt = {}
+        for cs in faces:
+            ins = [inside[c] for c in cs]
+            for i in range(4):
+                if ins[i] and not ins[(i + 1) % 4]:
+                    j = i
+                    while ins[(j - 1) % 4]:
+                        j -= 1
+                    nxt[edge_id[(cs[i], cs[(i + 1) % 4])]] = edge_id[(cs[(j - 1) % 4], cs[j % 4])]
+        tris, used = [], set()
+        for s0 in sorted(nxt):
+            if s0 in used:
+                continue
+            loop = [s0]
+            used.add(s0)
+            while nxt[loop[-1]] != s0:
+                loop.append(nxt[loop[-1]])
+                used.add(loop[-1])
+            m = loop.index(min(loop))
+            loop = loop[m:] + loop[:m]
+            tris += [(loop[0], loop[i + 1], loop[i]) for i in range(1, len(loop) - 1)]
+        tables.append(tris)
+    return tables
+
+
+def _grad(v, p, axis):
+    """Central difference along axis at integer points p (n,3), one-sided on the volume boundary."""
+    D = v.shape[axis]
+    lo, hi = p.copy(), p.copy()
+    lo[:, axis] = np.maximum(p[:, axis] - 1, 0)
+    hi[:, axis] = np.minimum(p[:, axis] + 1, D - 1)
+    num = v[tuple(hi.T)].astype(F64) - v[tuple(lo.T)].astype(F64)
+    return num / (hi[:, axis] - lo[:, axis]).astype(F64)
+
+
+def marching_cubes(volume, level=0.0, mask=None):
+    """Marching cubes over a dense (X,Y,Z) f32 volume in voxel-index coordinates (the skimage convention,
+    tsdf.py:755,794). Cell c = [c, c+1]³ is processed iff mask[c+1] (the cell's far corner) when a mask
+    is given. One vertex per cut edge used by a processed cell: along the edge from p (value va) to
+    p+e_a (vb), w = 1/(FLT_EPSILON+|v-level|) per end, offset = wb/(wa+wb), coordinate f32(p_a + offset);
+    normal = normalised (wa·∇v(p) + wb·∇v(p+e_a))/(wa+wb) (central differences), pointing to increasing
+    values; value = (wa·va + wb·vb)/(wa+wb). Vertices ordered by edge key = C-index(p)·3 + a.
+    Returns (verts f32 (V,3), faces int64 (F,3), normals f32 (V,3), values f32 (V,), keys int64 (V,)).
+    skimage's Lewiner tables and its vertex order are not available here (skimage is not installed):
+    the triangulation is this module's rule (mc_tables), vertex positions follow the interpolation
+    above — parity with skimage unpinned."""
+    v = np.asarray(volume, F32)
+    X, Y, Z = v.shape
+    tabs = mc_tables()
+    if X < 2 or Y < 2 or Z < 2:
+        return (np.zeros((0, 3), F32), np.zeros((0, 3), np.int64), np.zeros((0, 3), F32), np.zeros(0, F32),
+                np.zeros(0, np.int64))
+    below = v < F32(level)
+    idx = np.zeros((X - 1, Y - 1, Z - 1), np.int64)
+    for c in range(8):
+        dx, dy, dz = c & 1, (c >> 1) & 1, (c >> 2) & 1
+        idx |= below[dx:X - 1 + dx, dy:Y - 1 + dy, dz:Z - 1 + dz].astype(np.int64) << c
+    emit = (idx != 0) & (idx != 255)
+    if mask is not None:
+        emit &= np.asarray(mask, bool)[1:, 1:, 1:]
+    cells = np.argwhere(emit)
+    cfg = idx[emit]
+    keys_t = []
+    corner_off = np.array([[c & 1, (c >> 1) & 1, (c >> 2) & 1] for c in range(8)])
+    edge_start = np.array([corner_off[p] for p, q in MC_EDGES])
+    edge_axis = np.array([k // 4 for k in range(12)])
+    tri_cell, tri_edges = [], []
+    for ci, cf in zip(range(len(cells)), cfg):
+        for tr in tabs[cf]:
+            tri_cell.append(ci)
+            tri_edges.append(tr)
+    if not tri_cell:
+        return (np.zeros((0, 3), F32), np.zeros((0, 3), np.int64), np.zeros((0, 3), F32), np.zeros(0, F32),
+                np.zeros(0, np.int64))
+    tri_cell = np.array(tri_cell)
+    tri_edges = np.array(tri_edges)
+    st = cells[tri_cell][:, None, :] + edge_start[tri_edges]                  # (F,3,3) start voxels
+    keys_t = ((st[..., 0] * Y + st[..., 1]) * Z + st[..., 2]) * 3 + edge_axis[tri_edges]
+    keys, faces = np.unique(keys_t.reshape(-1), return_inverse=True)
+    faces = faces.reshape(-1, 3).astype(np.int64)
+    a = keys % 3
+    flat = keys // 3
+    p = np.stack([flat // (Y * Z), (flat // Z) % Y, flat % Z], 1)
+    q = p.copy()
+    q[np.arange(len(q)), a] += 1
+    va, vb = v[tuple(p.T)].astype(F64), v[tuple(q.T)].astype(F64)
+    wa = 1.0 / (FLT_EPSILON + np.abs(va - level))
+    wb = 1.0 / (FLT_EPSILON + np.abs(vb - level))
+    off = wb / (wa + wb)
+    verts = p.astype(F64)
+    verts[np.arange(len(p)), a] += off
+    g = np.zeros((len(p), 3))
+    for ax in range(3):
+        g[:, ax] = (wa * _grad(v, p, ax) + wb * _grad(v, q, ax)) / (wa + wb)
+    nrm = np.sqrt((g[:, 0] * g[:, 0] + g[:, 1] * g[:, 1]) + g[:, 2] * g[:, 2])
+    normals = g / np.where(nrm > 0, nrm, 1.0)[:, None]
+    values = (wa * va + wb * vb) / (wa + wb)
+    return verts.astype(F32), faces, normals.astype(F32), values.astype(F32), keys
+
+
+def mesh_colors(verts, color_vol):
+    """tsdf.py:759-767 / 800-807: colour of the voxel nearest each vertex (np.round half-even), unpacked
+    from the b·65536 + g·256 + r float encoding in f32, as uint8 (N,3) [r, g, b]."""
+    vi = np.rint(np.asarray(verts, F32)).astype(np.int64)
+    rgb = np.asarray(color_vol, F32)[vi[:, 0], vi[:, 1], vi[:, 2]]
+    b = np.floor(rgb / F32(COLOR_CONST))
+    g = np.floor((rgb - b * F32(COLOR_CONST)) / F32(256))
+    r = rgb - b * F32(COLOR_CONST) - g * F32(256)
+    return np.floor(np.asarray([r, g, b])).T.astype(np.uint8)
+
+
+def get_mesh(tsdf_vol, color_vol, voxel_size, origin, max_diff=1.2):
+    """tsdf.py:770-809: masked marching cubes of the truncated region; voxel -> world as
+    verts·f32(voxel_size) + origin in f32 (numpy-1.26 value-based casting); (verts, faces, norms, colors)."""
+    mask = compute_truncated_region(tsdf_vol, max_diff)
+    verts, faces, norms, _, _ = marching_cubes(tsdf_vol, 0.0, mask)
+    colors = mesh_colors(verts, color_vol)
+    world = verts * F32(voxel_size) + np.asarray(origin, F32)
+    return world, faces, norms, colors

@@ -312,3 +312,32 @@ def test_oracle_reproduces_gn_fixture(golden_dir):
                          g["weights"], g["tgt"], g["intr"])
     np.testing.assert_allclose(out["node_rotations"], g["R"], atol=1e-9)
     np.testing.assert_allclose(out["node_translations"], g["t"], atol=1e-9)
+
+
+def test_mc_tables_and_truncated_region_kat():
+    """Rule-generated triangle table: <= 5 triangles per cell, empty for the trivial cubes, one triangle
+    for a single inside corner; the truncated region drops the boundary, |t| > 0.9 and steep voxels."""
+    tabs = fo.mc_tables()
+    assert max(len(t) for t in tabs) == 5 and tabs[0] == [] and tabs[255] == []
+    assert all(len(tabs[1 << c]) == 1 for c in range(8))
+    t = np.full((5, 5, 5), 0.5, np.float32)
+    t[2, 2, 2] = 0.95                      # |t| > 0.9
+    t[1, 1, 3] = -0.8                      # 1.3 away from its 0.5 neighbours
+    m = fo.compute_truncated_region(t, 1.2)
+    assert not m[0].any() and not m[:, :, 4].any()          # boundary
+    assert not m[2, 2, 2] and not m[1, 1, 3] and not m[1, 2, 2]
+    assert m[3, 3, 1] and m[3, 3, 3]
+    assert m.sum() == 27 - 8     # the 2x2x2 interior block around (1,1,3) holds (2,2,2) too
+
+
+def test_oracle_marching_cubes_sphere_closed():
+    X = np.arange(24)[:, None, None]
+    Y = np.arange(20)[None, :, None]
+    Z = np.arange(22)[None, None, :]
+    v = (np.sqrt((X - 11.3) ** 2 + (Y - 9.7) ** 2 + (Z - 10.2) ** 2) - 6.1).astype(np.float32)
+    verts, faces, normals, values, keys = fo.marching_cubes(v)
+    assert len(verts) - 3 * len(faces) // 2 + len(faces) == 2            # Euler characteristic of a sphere
+    r = np.linalg.norm(verts - np.array([11.3, 9.7, 10.2]), axis=1)
+    assert np.abs(r - 6.1).max() < 0.05 and np.abs(values).max() < 1e-6
+    fn = np.cross(verts[faces[:, 1]] - verts[faces[:, 0]], verts[faces[:, 2]] - verts[faces[:, 0]])
+    assert (np.einsum("ij,ij->i", fn, normals[faces[:, 0]]) > 0).all()

@@ -28,6 +28,13 @@
  *   ofx_visibility          TSDFVolume.check_visibility                     tsdf.py:576-612
  *   ofx_truncated_region    TSDFVolume.compute_truncated_region            tsdf.py:704-745
  *   ofx_mesh_*              measure.marching_cubes in get_mesh / get_point_cloud, colours tsdf.py:748-809
+ *   ofx_backproject_depth   image_proc.backproject_depth (csrc float/ushort) utils/image_proc.py:335-349,
+ *                                                                          csrc/cpu/image_proc.cpp:351-401
+ *   ofx_depth_mesh_*        compute_mesh_from_depth (pixel-grid mesh)       csrc/cpu/image_proc.cpp:405-545
+ *                           (EDGraph.create_mesh_from_depth, WarpField.skin of an image: embedded_deformation_graph.py:95-151,
+ *                           warpfield.py:160-175)
+ *   ofx_depth_to_pc         Registration.optimize target cloud: depth_2_pc, NonRigidICP/model/geometry.py:44-59,
+ *                           mask compaction, map_pixel_to_pcd              registration_fusion.py:104-109,388-395
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
  *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
@@ -189,6 +196,26 @@ int ofx_mesh_emit(void* handle, float* verts, int32_t* faces, float* normals, fl
  * (f32, may be NULL) and colours u8[V*3] = [r,g,b] of the voxel nearest each vertex (may be NULL). */
 int ofx_mesh_finish(const ofx_volume_desc* desc, const float* color, const float* verts, int64_t n_verts,
                     float* world, uint8_t* colors, ofx_stream_t s);
+
+/* ---------------- Correspondence front-end ---------------- */
+/* backproject_depth: point_image f32[3*H*W] (planar x, y, z); pixels with depth <= 0 are left untouched
+ * (the reference zero-fills before the call). depth is f32[H*W] metres (is_u16 = 0) or u16[H*W] scaled by
+ * 1/normalizer (is_u16 = 1). Arithmetic as the C++: f32 d*(x-cx)/fx, correctly rounded. */
+int ofx_backproject_depth(const void* depth, int32_t is_u16, int32_t height, int32_t width, float fx, float fy, float cx,
+                          float cy, float normalizer, float* point_image, ofx_stream_t s);
+/* compute_mesh_from_depth on a planar point image f32[3*H*W]; handle owns scratch (also used by
+ * ofx_depth_to_pc). count sizes the output (synchronises the stream); emit writes vertices f32[V*3],
+ * vertex_pixels i32[V*2] (x, y; may be NULL) and faces i32[F*3], numbered exactly as the sequential C++. */
+int ofx_depth_mesh_create(void** handle);
+int ofx_depth_mesh_destroy(void* handle);
+int ofx_depth_mesh_count(void* handle, const float* point_image, int32_t height, int32_t width,
+                         float max_triangle_distance, int64_t* n_verts, int64_t* n_faces, ofx_stream_t s);
+int ofx_depth_mesh_emit(void* handle, float* vertices, int32_t* vertex_pixels, int32_t* faces, ofx_stream_t s);
+/* depth_2_pc(depth, K) (f64 arithmetic, rounded to f32) of the pixels with depth > 0, row-major:
+ * points f32[capacity H*W*3], pix_map i64[H*W] (point index or -1; may be NULL), n_points: DEVICE int32.
+ * Asynchronous (no host sync). */
+int ofx_depth_to_pc(void* handle, const float* depth, int32_t height, int32_t width, double fx, double fy, double cx,
+                    double cy, float* points, int64_t* pix_map, int32_t* n_points, ofx_stream_t s);
 
 /* ---------------- Gauss-Newton (DeformNet.optimize) ---------------- */
 typedef struct ofx_gn_params {

@@ -10,6 +10,7 @@ _EXPORTS = {
     "WarpField": "warpfield", "EDGraph": "warpfield",
     "GaussNewtonSolver": "registration", "Registration": "registration",
     "FusionPipeline": "pipeline",
+    "backproject_depth": "image_proc", "compute_mesh_from_depth": "image_proc", "depth_2_pc": "image_proc",
 }
 
 __all__ = list(_EXPORTS)

@@ -69,6 +69,12 @@ _SIGS = {
     "ofx_mesh_count": [P, P, P, P, c_double, c_int32, c_float, P, P, P],
     "ofx_mesh_emit": [P, P, P, P, P, P, P],
     "ofx_mesh_finish": [P, P, P, c_int64, P, P, P],
+    "ofx_backproject_depth": [P, c_int32, c_int32, c_int32, c_float, c_float, c_float, c_float, c_float, P, P],
+    "ofx_depth_mesh_create": [P],
+    "ofx_depth_mesh_destroy": [P],
+    "ofx_depth_mesh_count": [P, P, c_int32, c_int32, c_float, P, P, P],
+    "ofx_depth_mesh_emit": [P, P, P, P, P],
+    "ofx_depth_to_pc": [P, P, c_int32, c_int32, c_double, c_double, c_double, c_double, P, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],

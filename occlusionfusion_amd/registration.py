@@ -241,6 +241,11 @@ class GaussNewtonSolver:
         return self._pack(out, sync)
 
 
+def depth_2_pc_device(depth, intrin):
+    from .image_proc import depth_2_pc_device as f
+    return f(depth, intrin)
+
+
 class Registration:
     """registration_fusion.py:37-397 API with the Gauss-Newton solver (DeformNet.optimize formulation)."""
 
@@ -273,6 +278,10 @@ class Registration:
 
     def optimize(self, optical_flow_data, scene_flow_data, complete_node_motion_data, target_frame_data,
                  landmarks=None):
+        im = target_frame_data.get("im") if isinstance(target_frame_data, dict) else None
+        if im is not None:   # registration_fusion.py:104-109: target cloud + pixel map (ofx_depth_to_pc)
+            depth = torch.as_tensor(np.ascontiguousarray(im[-1], np.float32), device=self.device)
+            self.tgt_pcd, self.pix_2_pcd = depth_2_pc_device(depth, self.intrinsics)
         tm = np.asarray(scene_flow_data["target_matches"], np.float32)[self.valid_source_verts]
         vv = np.asarray(scene_flow_data["valid_verts"], bool)
         sel = np.nonzero(vv[: self.source_pcd.shape[0]])[0]

@@ -906,3 +906,91 @@ def get_mesh(tsdf_vol, color_vol, voxel_size, origin, max_diff=1.2):
     colors = mesh_colors(verts, color_vol)
     world = verts * F32(voxel_size) + np.asarray(origin, F32)
     return world, faces, norms, colors
+
+
+# ----------------------------------------------------------------------------
+# f3: correspondence front-end — csrc image_proc.cpp:351-545 (backproject, pixel-grid mesh),
+#     depth_2_pc (NonRigidICP/model/geometry.py:44-59), target cloud + pixel map
+#     (registration_fusion.py:104-109, 388-395)
+# ----------------------------------------------------------------------------
+def backproject_depth(depth_image, fx, fy, cx, cy, normalizer=1000.0):
+    """image_proc.cpp:351-401 via utils/image_proc.py:335-349: f32 arithmetic d*(x-cx)/fx, zeros where d <= 0.
+    A float32 image is metres; any other dtype is read as uint16 and divided by f32(normalizer)."""
+    f32 = np.float32
+    if depth_image.dtype == np.float32:
+        d = depth_image
+    else:
+        d = depth_image.astype(np.uint16).astype(f32) / f32(normalizer)
+    H, W = d.shape
+    xs = np.arange(W, dtype=f32)[None, :]
+    ys = np.arange(H, dtype=f32)[:, None]
+    out = np.zeros((3, H, W), f32)
+    ok = d > 0
+    px = (d * (xs - f32(cx))) / f32(fx)
+    py = (d * (ys - f32(cy))) / f32(fy)
+    out[0][ok] = px[ok]
+    out[1][ok] = py[ok]
+    out[2][ok] = d[ok]
+    return out
+
+
+def _edge_len_f32(a, b):
+    """Eigen 3.3.7 (a-b).norm() for Vector3f: the unrolled redux sums x0 + (x1 + x2) (Redux.h:92-104)."""
+    f32 = np.float32
+    d = (a - b).astype(f32)
+    s = d * d
+    return np.sqrt(f32(s[0] + f32(s[1] + s[2])))
+
+
+def compute_mesh_from_depth(point_image, max_dist):
+    """image_proc.cpp:405-545, sequentially: quads row-major, triangle A (00, 01, 10) then B (11, 10, 01),
+    vertices numbered on first use. Returns (vertices f32 (V,3), vertex_pixels i32 (V,2) [x,y],
+    faces i32 (F,3)). Pure-Python loop: small images only."""
+    f32 = np.float32
+    P = np.asarray(point_image, f32)
+    _, H, W = P.shape
+    md = f32(max_dist)
+    vmap = -np.ones(H * W, np.int64)
+    verts, pix, faces = [], [], []
+
+    def vid(x, y):
+        i = y * W + x
+        if vmap[i] < 0:
+            vmap[i] = len(verts)
+            verts.append(P[:, y, x])
+            pix.append((x, y))
+        return int(vmap[i])
+
+    for y in range(H - 1):
+        for x in range(W - 1):
+            o00, o01, o10, o11 = P[:, y, x], P[:, y + 1, x], P[:, y, x + 1], P[:, y + 1, x + 1]
+            if o00[2] > 0 and o01[2] > 0 and o10[2] > 0:
+                if (_edge_len_f32(o00, o01) <= md and _edge_len_f32(o00, o10) <= md
+                        and _edge_len_f32(o01, o10) <= md):
+                    faces.append((vid(x, y), vid(x, y + 1), vid(x + 1, y)))
+            if o01[2] > 0 and o10[2] > 0 and o11[2] > 0:
+                if (_edge_len_f32(o10, o01) <= md and _edge_len_f32(o10, o11) <= md
+                        and _edge_len_f32(o01, o11) <= md):
+                    faces.append((vid(x + 1, y + 1), vid(x + 1, y), vid(x, y + 1)))
+    V = np.array(verts, f32).reshape(-1, 3)
+    return V, np.array(pix, np.int32).reshape(-1, 2), np.array(faces, np.int32).reshape(-1, 3)
+
+
+def depth_2_pc(depth, intrin):
+    """geometry.py:44-59: float64 (3,H,W) with X = ((u - cx)·d)/fx, Y = ((v - cy)·d)/fy, Z = d."""
+    K = np.asarray(intrin, np.float64)
+    H, W = depth.shape
+    u = np.broadcast_to(np.arange(W, dtype=np.float64)[None, :], (H, W))
+    v = np.broadcast_to(np.arange(H, dtype=np.float64)[:, None], (H, W))
+    d = depth.astype(np.float64)
+    return np.stack([(u - K[0, 2]) * d / K[0, 0], (v - K[1, 2]) * d / K[1, 1], d])
+
+
+def target_point_cloud(depth, intrin):
+    """registration_fusion.py:104-109 + map_pixel_to_pcd (:388-395): the f32 cloud of pixels with depth > 0
+    (row-major) and the pixel -> point index map (int64, -1 where invalid)."""
+    ok = depth > 0
+    pc = depth_2_pc(depth, intrin).transpose(1, 2, 0)[ok].astype(np.float32)
+    pmap = np.cumsum(ok.reshape(-1)).reshape(ok.shape).astype(np.int64) - 1
+    pmap[~ok] = -1
+    return pc, pmap

@@ -8,6 +8,10 @@
                         oracle restatement of tsdf.py/warpfield.py/geometry.py (inputs + expected
                         tsdf/weight/colour + skin valid mask).
   gn_small.npz        — one DeformNet.optimize solve (N≈100, M=600) by the dense f64 oracle.
+  frontend_csrc.npz   — backproject_depth_float / _ushort and compute_mesh_from_depth outputs of the
+                        REFERENCE's compiled C++ (csrc/cpu/image_proc.cpp:351-545) on a synthetic frame,
+                        incl. max-distance thresholds that tie exactly with triangle edge lengths; plus the
+                        oracle's depth_2_pc target cloud (geometry.py:44-59) of the same frame.
 
 Usage: python tests/golden/make_golden.py
 """
@@ -69,6 +73,43 @@ def make_skin_csrc():
     print("skin_csrc:", nodes.shape[0], "nodes,", q.shape[0], "points")
 
 
+def make_frontend_csrc():
+    from oracle.build_ref import build
+    m = build()
+    cam, scene, d0, d1, pts, nodes, edges, ew = small_setup()
+    rng = np.random.default_rng(3)
+    depth = d1.astype(np.float32)
+    depth_u16 = np.round(depth * 1000.0).astype(np.uint16)
+    intr = np.array([cam.fx, cam.fy, cam.cx, cam.cy], np.float32)
+    bf = np.zeros((3,) + depth.shape, np.float32)
+    m.backproject_depth_float(depth, bf, *[float(v) for v in intr])
+    bu = np.zeros((3,) + depth.shape, np.float32)
+    m.backproject_depth_ushort(depth_u16, bu, *[float(v) for v in intr], 1000.0)
+    # thresholds: the reference default (0.05), a tight one, and exact ties with realised edge lengths
+    xs = bf[:, :-1, :-1].reshape(3, -1).T
+    nb = bf[:, 1:, :-1].reshape(3, -1).T
+    ok = (xs[:, 2] > 0) & (nb[:, 2] > 0)
+    lens = np.array([fo._edge_len_f32(a, b) for a, b in zip(xs[ok][:4000], nb[ok][:4000])], np.float32)
+    ties = np.sort(rng.choice(lens, 2, replace=False))
+    thresholds = np.array([0.05, np.median(lens) * 1.01, ties[0], ties[1]], np.float32)
+    meshes = {}
+    for i, t in enumerate(thresholds):
+        v = np.zeros((0,), np.float32)
+        px = np.zeros((0,), np.int32)
+        f = np.zeros((0,), np.int32)
+        m.compute_mesh_from_depth(bf, float(t), v, px, f)
+        meshes[f"mesh{i}_vertices"] = v.reshape(-1, 3)
+        meshes[f"mesh{i}_pixels"] = px.reshape(-1, 2)
+        meshes[f"mesh{i}_faces"] = f.reshape(-1, 3)
+    K = np.eye(3)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = intr
+    pc, pmap = fo.target_point_cloud(depth, K)
+    np.savez_compressed(os.path.join(HERE, "frontend_csrc.npz"), depth=depth, depth_u16=depth_u16, intr=intr,
+                        backproject_float=bf, backproject_ushort=bu, thresholds=thresholds, K=K,
+                        target_pc=pc, target_pix_map=pmap, **meshes)
+    print("frontend_csrc:", depth.shape, [meshes[f"mesh{i}_faces"].shape[0] for i in range(4)], "faces")
+
+
 def make_integrate_small():
     cam, scene, d0, d1, pts, nodes, edges, ew = small_setup()
     origin = np.array([-0.40, -0.33, 0.95], np.float32)
@@ -116,9 +157,11 @@ def make_gn_small():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["skin", "integrate", "gn"]
+    which = sys.argv[1:] or ["skin", "frontend", "integrate", "gn"]
     if "skin" in which:
         make_skin_csrc()
+    if "frontend" in which:
+        make_frontend_csrc()
     if "integrate" in which:
         make_integrate_small()
     if "gn" in which:

@@ -341,3 +341,42 @@ def test_oracle_marching_cubes_sphere_closed():
     assert np.abs(r - 6.1).max() < 0.05 and np.abs(values).max() < 1e-6
     fn = np.cross(verts[faces[:, 1]] - verts[faces[:, 0]], verts[faces[:, 2]] - verts[faces[:, 0]])
     assert (np.einsum("ij,ij->i", fn, normals[faces[:, 0]]) > 0).all()
+
+
+# ---------------- f3: correspondence front-end (csrc image_proc.cpp, geometry.py depth_2_pc) ----------------
+def test_oracle_backproject_matches_csrc(golden_dir):
+    g = np.load(os.path.join(golden_dir, "frontend_csrc.npz"), allow_pickle=False)
+    fx, fy, cx, cy = [float(v) for v in g["intr"]]
+    assert np.array_equal(fo.backproject_depth(g["depth"], fx, fy, cx, cy), g["backproject_float"])
+    assert np.array_equal(fo.backproject_depth(g["depth_u16"], fx, fy, cx, cy, 1000.0), g["backproject_ushort"])
+
+
+def test_oracle_depth_mesh_matches_csrc(golden_dir):
+    g = np.load(os.path.join(golden_dir, "frontend_csrc.npz"), allow_pickle=False)
+    for i, t in enumerate(g["thresholds"]):
+        v, px, f = fo.compute_mesh_from_depth(g["backproject_float"], t)
+        assert np.array_equal(v, g[f"mesh{i}_vertices"]), i
+        assert np.array_equal(px, g[f"mesh{i}_pixels"]), i
+        assert np.array_equal(f, g[f"mesh{i}_faces"]), i
+
+
+def test_oracle_edge_length_uses_eigen_order():
+    # dx² + (dy² + dz²) differs from (dx² + dy²) + dz² in the last bit for these values
+    a = np.array([1.199515461921692, 1.9421131610870361, 1.365110158920288], np.float32)
+    b = np.array([1.1774803400039673, 1.9426335096359253, 1.3719470500946045], np.float32)
+    s = ((a - b) * (a - b)).astype(np.float32)
+    left = np.sqrt(np.float32(np.float32(s[0] + s[1]) + s[2]))
+    right = np.sqrt(np.float32(s[0] + np.float32(s[1] + s[2])))
+    assert left != right and fo._edge_len_f32(a, b) == right
+
+
+def test_oracle_target_point_cloud(golden_dir):
+    g = np.load(os.path.join(golden_dir, "frontend_csrc.npz"), allow_pickle=False)
+    pc, pmap = fo.target_point_cloud(g["depth"], g["K"])
+    assert np.array_equal(pc, g["target_pc"]) and np.array_equal(pmap, g["target_pix_map"])
+    ok = g["depth"] > 0
+    assert pc.shape[0] == ok.sum() and np.array_equal(pmap[ok], np.arange(ok.sum()))
+    assert np.array_equal(pc[:, 2], g["depth"][ok])
+    # the float64 cloud and the f32 csrc backprojection agree to f32 rounding
+    bp = g["backproject_float"].transpose(1, 2, 0)[ok]
+    assert np.allclose(pc, bp, rtol=0, atol=1e-6)

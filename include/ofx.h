@@ -35,6 +35,10 @@
  *                           warpfield.py:160-175)
  *   ofx_depth_to_pc         Registration.optimize target cloud: depth_2_pc, NonRigidICP/model/geometry.py:44-59,
  *                           mask compaction, map_pixel_to_pcd              registration_fusion.py:104-109,388-395
+ *   ofx_pixel_anchors_euclidean  csrc compute_pixel_anchors_euclidean     csrc/cpu/graph_proc.cpp:610-709
+ *   ofx_pixel_anchors_geodesic   csrc compute_pixel_anchors_geodesic      csrc/cpu/graph_proc.cpp:483-608
+ *   ofx_remap_anchors       csrc update_pixel_anchors                       csrc/cpu/graph_proc.cpp:934-961
+ *   ofx_knn_points          KDTree.query (pykdtree) in WarpField.find_unreachable_nodes  warpfield.py:462-485
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
  *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
@@ -216,6 +220,27 @@ int ofx_depth_mesh_emit(void* handle, float* vertices, int32_t* vertex_pixels, i
  * Asynchronous (no host sync). */
 int ofx_depth_to_pc(void* handle, const float* depth, int32_t height, int32_t width, double fx, double fy, double cx,
                     double cy, float* points, int64_t* pix_map, int32_t* n_points, ofx_stream_t s);
+
+/* ---------------- Standalone skinning / anchors ---------------- */
+/* csrc twins, exact (Eigen summation order, list tie order, f32 weights): outputs (H, W, 4) images,
+ * anchors i32 (-1 = none) and weights f32, fully (re)initialised by the call. point_image planar f32[3*H*W]. */
+int ofx_pixel_anchors_euclidean(const float* nodes, int32_t n_nodes, const float* point_image, int32_t height,
+                                int32_t width, float node_coverage, int32_t* pixel_anchors, float* pixel_weights,
+                                ofx_stream_t s);
+/* node_to_vertex_distance f32[N*V] (row per node, < 0 = unreachable), valid_nodes_mask i32[N],
+ * vertex_pixels i32[V*2] (x, y). */
+int ofx_pixel_anchors_geodesic(const float* node_to_vertex_distance, const int32_t* valid_nodes_mask, int32_t n_nodes,
+                               int64_t n_vertices, const int32_t* vertex_pixels, int32_t width, int32_t height,
+                               float node_coverage, int32_t* pixel_anchors, float* pixel_weights, ofx_stream_t s);
+/* anchors[i] = id_map[anchors[i]] for anchors[i] != -1 (in place). An anchor with no mapping (outside
+ * [0, n_map) or mapped to -1; std::map::at would throw) is left as is and counted into *n_missing (DEVICE
+ * int32, accumulated: zero it first). */
+int ofx_remap_anchors(int32_t* anchors, int64_t n, const int32_t* id_map, int32_t n_map, int32_t* n_missing,
+                      ofx_stream_t s);
+/* k nearest nodes (k <= 8) of each point: idx i32[P*k] ascending by (squared distance, node id), -1 past
+ * n_nodes; sq_dist f32[P*k] = (dx²+dy²)+dz² in f32. */
+int ofx_knn_points(const float* points, int64_t n_points, const float* nodes, int32_t n_nodes, int32_t k, int32_t* idx,
+                   float* sq_dist, ofx_stream_t s);
 
 /* ---------------- Gauss-Newton (DeformNet.optimize) ---------------- */
 typedef struct ofx_gn_params {

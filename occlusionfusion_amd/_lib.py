@@ -75,6 +75,10 @@ _SIGS = {
     "ofx_depth_mesh_count": [P, P, c_int32, c_int32, c_float, P, P, P],
     "ofx_depth_mesh_emit": [P, P, P, P, P],
     "ofx_depth_to_pc": [P, P, c_int32, c_int32, c_double, c_double, c_double, c_double, P, P, P, P],
+    "ofx_pixel_anchors_euclidean": [P, c_int32, P, c_int32, c_int32, c_float, P, P, P],
+    "ofx_pixel_anchors_geodesic": [P, P, c_int32, c_int64, P, c_int32, c_int32, c_float, P, P, P],
+    "ofx_remap_anchors": [P, c_int64, P, c_int32, P, P],
+    "ofx_knn_points": [P, c_int64, P, c_int32, c_int32, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],

@@ -149,6 +149,44 @@ class WarpField:
         a, w, v = self.skin_device(points, nodes)
         return a.cpu().numpy(), w.cpu().numpy(), v.cpu().numpy()
 
+    def skin_image(self, nodes, image_data):
+        """warpfield.py:143-199: mesh the (masked) point image (compute_mesh_from_depth), skin its vertices
+        against `nodes` and scatter anchors / weights to the vertex pixels -> {"pixel_anchors" (H,W,K) i32,
+        "pixel_weights" (H,W,K) f32}; pixels without a vertex hold 0 / 0 as in the reference."""
+        from .image_proc import compute_mesh_from_depth_device
+        self.source_im = image_data["im"]
+        im = _t(image_data["im"], self.device, torch.float32)
+        point_image = im[3:]
+        if image_data.get("mask") is not None:
+            m = _t(image_data["mask"], self.device, torch.float32)
+            point_image = point_image * (m > 0).float()[None]
+        mesh = compute_mesh_from_depth_device(point_image.contiguous(),
+                                              self.graph.graph_generation_parameters["max_triangle_distance"])
+        a, w, _ = self.skin_device(mesh["vertices"], nodes=nodes)
+        H, W = point_image.shape[1:3]
+        K = self.graph_neighbours
+        pa = torch.zeros((H, W, K), dtype=torch.int32, device=self.device)
+        pw = torch.zeros((H, W, K), dtype=torch.float32, device=self.device)
+        px = mesh["vertex_pixels"].long()
+        pa[px[:, 1], px[:, 0]] = a
+        pw[px[:, 1], px[:, 0]] = w
+        self.log.info(f"Skinned Source Image, valid pixels:{int((pa != -1).all(-1).sum())}")
+        return {"pixel_anchors": pa.cpu().numpy(), "pixel_weights": pw.cpu().numpy()}
+
+    def find_unreachable_nodes(self, points):
+        """warpfield.py:462-485: indices of points farther than 2·node_coverage from every node, sorted by that
+        distance descending (1-NN by ofx_knn_points; the reference's pykdtree distance rounding and argsort tie
+        order are unpinned)."""
+        from .graph_proc import knn_device
+        pts = _t(points, self.device, torch.float32).reshape(-1, 3)
+        _, d2 = knn_device(pts, self.nodes_t, 1)
+        dist = torch.sqrt(d2.reshape(-1).double()).float()
+        un = torch.nonzero(dist > np.float32(2 * self.node_coverage)).reshape(-1)
+        if un.numel() == 0:
+            return []
+        order = torch.argsort(dist[un], stable=True).flip(0)
+        return un[order].cpu().numpy()
+
     def skin_tsdf_cache(self):
         """Bricked skin cache of the TSDF voxel grid (warpfield.py:131-141 cache semantics)."""
         if self._cache is None or self.updating_warpfield:

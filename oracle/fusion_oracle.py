@@ -994,3 +994,102 @@ def target_point_cloud(depth, intrin):
     pmap = np.cumsum(ok.reshape(-1)).reshape(ok.shape).astype(np.int64) - 1
     pmap[~ok] = -1
     return pc, pmap
+
+
+# ----------------------------------------------------------------------------
+# f2: standalone skinning / anchors — csrc graph_proc.cpp:483-709,934-961; KDTree.query in
+#     WarpField.find_unreachable_nodes (warpfield.py:462-485); skin_image (warpfield.py:143-199)
+# ----------------------------------------------------------------------------
+GRAPH_K = 4   # csrc/cpu/graph_proc.h:8
+
+
+def _csrc_weights(d2, cov):
+    """graph_proc.cpp:147-153 + the normalisation at :672-696 / :583-597 for one anchor list (f32)."""
+    f32 = np.float32
+    two_c2 = f32(f32(2.0 * f32(cov)) * f32(cov))
+    w = np.array([exp_f32(np.array([f32(-d) / two_c2], f32))[0] for d in d2], f32)
+    s = f32(0)
+    for x in w:
+        s = f32(s + x)
+    if s > 0:
+        return (w / s).astype(f32)
+    if len(w):
+        return np.full(len(w), f32(1) / f32(len(w)), f32)
+    return w
+
+
+def pixel_anchors_euclidean(nodes, point_image, node_coverage):
+    """compute_pixel_anchors_euclidean (graph_proc.cpp:610-709): brute-force 4-NN per pixel with z > 0, no
+    cut-off; squared distance summed x0 + (x1 + x2) (Eigen); equal distances: the later node id first."""
+    f32 = np.float32
+    nodes = np.asarray(nodes, f32)
+    P = np.asarray(point_image, f32)
+    _, H, W = P.shape
+    A = -np.ones((H, W, GRAPH_K), np.int32)
+    Wt = np.zeros((H, W, GRAPH_K), f32)
+    ys, xs = np.nonzero(P[2] > 0)
+    pts = P[:, ys, xs].T
+    if pts.shape[0] == 0 or nodes.shape[0] == 0:
+        return A, Wt
+    d = (pts[:, None, :] - nodes[None, :, :]).astype(f32)
+    s = d * d
+    d2 = (s[..., 0] + (s[..., 1] + s[..., 2])).astype(f32)
+    ids = np.arange(nodes.shape[0])
+    for r in range(pts.shape[0]):
+        o = np.lexsort((-ids, d2[r]))[:GRAPH_K]
+        A[ys[r], xs[r], :len(o)] = o
+        Wt[ys[r], xs[r], :len(o)] = _csrc_weights(d2[r][o], node_coverage)
+    return A, Wt
+
+
+def pixel_anchors_geodesic(node_to_vertex_distance, valid_nodes_mask, vertex_pixels, width, height, node_coverage):
+    """compute_pixel_anchors_geodesic (graph_proc.cpp:483-608): per vertex the valid nodes with distance >= 0
+    in a set ordered by distance alone (the lowest node id of each distinct distance survives), first 4."""
+    f32 = np.float32
+    D = np.asarray(node_to_vertex_distance, f32)
+    valid = np.asarray(valid_nodes_mask).reshape(-1) != 0
+    A = -np.ones((height, width, GRAPH_K), np.int32)
+    Wt = np.zeros((height, width, GRAPH_K), f32)
+    for v in range(D.shape[1]):
+        col = D[:, v]
+        cand = np.nonzero(valid & (col >= 0))[0]
+        if cand.size == 0:
+            continue
+        uq, first = np.unique(col[cand], return_index=True)
+        sel = cand[first][:GRAPH_K]
+        u, y = vertex_pixels[v]
+        A[y, u, :len(sel)] = sel
+        dd = col[sel]
+        Wt[y, u, :len(sel)] = _csrc_weights((dd * dd).astype(f32), node_coverage)
+    return A, Wt
+
+
+def remap_anchors(anchors, node_id_mapping):
+    """update_pixel_anchors (graph_proc.cpp:934-961): every anchor != -1 through the (old -> new) map."""
+    out = np.array(anchors, np.int32, copy=True)
+    flat = out.reshape(-1)
+    for i, a in enumerate(flat):
+        if a != -1:
+            flat[i] = node_id_mapping[int(a)]
+    return out
+
+
+def knn(points, nodes, k):
+    """k nearest nodes ascending by (f32 squared distance (dx²+dy²)+dz², node id) -> (idx, sq_dist)."""
+    f32 = np.float32
+    d = (np.asarray(points, f32)[:, None, :] - np.asarray(nodes, f32)[None, :, :]).astype(f32)
+    s = d * d
+    d2 = ((s[..., 0] + s[..., 1]) + s[..., 2]).astype(f32)
+    o = np.argsort(d2, axis=1, kind="stable")[:, :k]
+    return o.astype(np.int32), np.take_along_axis(d2, o, 1)
+
+
+def find_unreachable_nodes(points, nodes, node_coverage):
+    """warpfield.py:462-485: indices of points whose nearest node is farther than 2·coverage, sorted by that
+    distance descending (argsort(...)[::-1]: among equal distances the later index first)."""
+    _, d2 = knn(points, nodes, 1)
+    dist = np.sqrt(d2.reshape(-1))
+    un = np.where(dist > np.float32(2 * node_coverage))[0]
+    if un.size == 0:
+        return []
+    return un[np.argsort(dist[un], kind="stable")[::-1]]

@@ -7,6 +7,9 @@
   integrate_small.npz — a 66x52x70 volume fused over a source frame and one ED-warped frame by the
                         oracle restatement of tsdf.py/warpfield.py/geometry.py (inputs + expected
                         tsdf/weight/colour + skin valid mask).
+  anchors_csrc.npz    — compute_pixel_anchors_euclidean / _geodesic and update_pixel_anchors outputs of the
+                        REFERENCE's compiled C++ (csrc/cpu/graph_proc.cpp:483-709,934-961): a point image with
+                        duplicated nodes (distance ties) and a node->vertex distance matrix with ties and -1s.
   gn_small.npz        — one DeformNet.optimize solve (N≈100, M=600) by the dense f64 oracle.
   frontend_csrc.npz   — backproject_depth_float / _ushort and compute_mesh_from_depth outputs of the
                         REFERENCE's compiled C++ (csrc/cpu/image_proc.cpp:351-545) on a synthetic frame,
@@ -110,6 +113,46 @@ def make_frontend_csrc():
     print("frontend_csrc:", depth.shape, [meshes[f"mesh{i}_faces"].shape[0] for i in range(4)], "faces")
 
 
+def make_anchors_csrc():
+    from oracle.build_ref import build
+    m = build()
+    cam, scene, d0, d1, pts, nodes, edges, ew = small_setup()
+    rng = np.random.default_rng(17)
+    bf = np.zeros((3,) + d0.shape, np.float32)
+    m.backproject_depth_float(d0.astype(np.float32), bf, float(cam.fx), float(cam.fy), float(cam.cx), float(cam.cy))
+    nd = np.concatenate([nodes, nodes[rng.choice(nodes.shape[0], 12, replace=False)]]).astype(np.float32)  # ties
+    cov = 0.07
+    pa = np.zeros((0,), np.int32)
+    pw = np.zeros((0,), np.float32)
+    m.compute_pixel_anchors_euclidean(nd, bf, cov, pa, pw)
+    # geodesic: V vertices on pixels, quantised distances (ties), unreachable (-1) entries, invalid nodes
+    V, N = 3000, 60
+    H, W = 40, 90
+    flat = rng.choice(H * W, V, replace=False)
+    vpix = np.stack([flat % W, flat // W], 1).astype(np.int32)
+    D = (np.round(rng.random((N, V)) * 40) / 100).astype(np.float32)
+    D[rng.random((N, V)) < 0.3] = -1.0
+    valid = (rng.random((N, 1)) > 0.15).astype(np.int32)
+    verts = rng.random((V, 3)).astype(np.float32)
+    ga = np.zeros((0,), np.int32)
+    gw = np.zeros((0,), np.float32)
+    m.compute_pixel_anchors_geodesic(D, valid, verts, vpix, ga, gw, W, H, cov)
+    # update_pixel_anchors: old ids -> new ids for the valid nodes
+    ids = np.nonzero(valid[:, 0])[0]
+    mapping = {int(o): int(n) for n, o in enumerate(ids)}
+    ra = np.where(np.isin(ga, ids), ga, -1).astype(np.int32)
+    rb = ra.copy()
+    m.update_pixel_anchors(mapping, rb)
+    np.savez_compressed(os.path.join(HERE, "anchors_csrc.npz"), nodes=nd, point_image=bf, node_coverage=cov,
+                        euclid_anchors=pa.reshape(bf.shape[1], bf.shape[2], 4),
+                        euclid_weights=pw.reshape(bf.shape[1], bf.shape[2], 4),
+                        geo_dist=D, geo_valid=valid, geo_vertex_pixels=vpix, geo_width=W, geo_height=H,
+                        geo_anchors=ga.reshape(H, W, 4), geo_weights=gw.reshape(H, W, 4),
+                        remap_in=ra, remap_ids=ids.astype(np.int32), remap_out=rb)
+    print("anchors_csrc:", nd.shape[0], "nodes;", int((pa.reshape(-1, 4)[:, 0] >= 0).sum()), "anchored pixels;",
+          int((ga.reshape(-1, 4)[:, 0] >= 0).sum()), "geodesic pixels")
+
+
 def make_integrate_small():
     cam, scene, d0, d1, pts, nodes, edges, ew = small_setup()
     origin = np.array([-0.40, -0.33, 0.95], np.float32)
@@ -157,11 +200,13 @@ def make_gn_small():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["skin", "frontend", "integrate", "gn"]
+    which = sys.argv[1:] or ["skin", "frontend", "anchors", "integrate", "gn"]
     if "skin" in which:
         make_skin_csrc()
     if "frontend" in which:
         make_frontend_csrc()
+    if "anchors" in which:
+        make_anchors_csrc()
     if "integrate" in which:
         make_integrate_small()
     if "gn" in which:

@@ -380,3 +380,44 @@ def test_oracle_target_point_cloud(golden_dir):
     # the float64 cloud and the f32 csrc backprojection agree to f32 rounding
     bp = g["backproject_float"].transpose(1, 2, 0)[ok]
     assert np.allclose(pc, bp, rtol=0, atol=1e-6)
+
+
+# ---------------- f2: standalone anchors (csrc graph_proc.cpp:483-709,934-961) ----------------
+def _ulp_close(a, b, ulps=1):
+    ai = a.view(np.int32).astype(np.int64)
+    bi = b.view(np.int32).astype(np.int64)
+    return np.abs(ai - bi).max(initial=0) <= ulps
+
+
+def test_oracle_pixel_anchors_euclidean_matches_csrc(golden_dir):
+    g = np.load(os.path.join(golden_dir, "anchors_csrc.npz"), allow_pickle=False)
+    a, w = fo.pixel_anchors_euclidean(g["nodes"], g["point_image"], float(g["node_coverage"]))
+    assert np.array_equal(a, g["euclid_anchors"])          # incl. the tie order of duplicated nodes
+    # weights: csrc's glibc expf (< 1 ulp, not correctly rounded) vs the oracle's correctly rounded exp; a 1-ulp
+    # raw difference moves the f32 sum and the normalised weights by at most a few ulps
+    assert _ulp_close(w, g["euclid_weights"], 4)
+    assert (w != g["euclid_weights"]).mean() < 0.01
+    dup = g["nodes"].shape[0] - 12
+    assert np.isin(g["euclid_anchors"], np.arange(dup, g["nodes"].shape[0])).any()   # ties were exercised
+
+
+def test_oracle_pixel_anchors_geodesic_matches_csrc(golden_dir):
+    g = np.load(os.path.join(golden_dir, "anchors_csrc.npz"), allow_pickle=False)
+    a, w = fo.pixel_anchors_geodesic(g["geo_dist"], g["geo_valid"], g["geo_vertex_pixels"], int(g["geo_width"]),
+                                     int(g["geo_height"]), float(g["node_coverage"]))
+    assert np.array_equal(a, g["geo_anchors"])
+    assert _ulp_close(w, g["geo_weights"], 4)
+
+
+def test_oracle_remap_anchors_matches_csrc(golden_dir):
+    g = np.load(os.path.join(golden_dir, "anchors_csrc.npz"), allow_pickle=False)
+    mapping = {int(o): n for n, o in enumerate(g["remap_ids"])}
+    assert np.array_equal(fo.remap_anchors(g["remap_in"], mapping), g["remap_out"])
+
+
+def test_oracle_find_unreachable_nodes():
+    nodes = np.array([[0, 0, 0], [1, 0, 0]], np.float32)
+    pts = np.array([[0.05, 0, 0], [0.5, 0, 0], [0.3, 0, 0], [2.0, 0, 0], [0.5, 0.0, 0.0]], np.float32)
+    un = fo.find_unreachable_nodes(pts, nodes, 0.1)       # 2·coverage = 0.2
+    assert list(un) == [3, 4, 1, 2]                       # descending distance; ties: later index first
+    assert fo.find_unreachable_nodes(pts[:1], nodes, 0.1) == []

@@ -39,6 +39,14 @@
  *   ofx_pixel_anchors_geodesic   csrc compute_pixel_anchors_geodesic      csrc/cpu/graph_proc.cpp:483-608
  *   ofx_remap_anchors       csrc update_pixel_anchors                       csrc/cpu/graph_proc.cpp:934-961
  *   ofx_knn_points          KDTree.query (pykdtree) in WarpField.find_unreachable_nodes  warpfield.py:462-485
+ *   ofx_graph_create/destroy/adjacency  mesh vertex adjacency (std::set per vertex)  csrc/cpu/graph_proc.cpp:174-186
+ *   ofx_erode_mesh          csrc erode_mesh                                 csrc/cpu/graph_proc.cpp:17-77
+ *   ofx_sample_nodes        csrc sample_nodes (randomShuffle = false)       csrc/cpu/graph_proc.cpp:79-136
+ *   ofx_edges_geodesic      csrc compute_edges_geodesic                     csrc/cpu/graph_proc.cpp:155-300
+ *   ofx_edges_euclidean     csrc compute_edges_euclidean                    csrc/cpu/graph_proc.cpp:302-356
+ *   ofx_node_edge_cleanup   csrc node_and_edge_clean_up                     csrc/cpu/graph_proc.cpp:388-438
+ *   ofx_compute_clusters    csrc compute_clusters                           csrc/cpu/graph_proc.cpp:440-481
+ *                           (callers: EDGraph, fusion_with_occlusion/embedded_deformation_graph.py:153-380,496-609)
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
  *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
@@ -241,6 +249,37 @@ int ofx_remap_anchors(int32_t* anchors, int64_t n, const int32_t* id_map, int32_
  * n_nodes; sq_dist f32[P*k] = (dx²+dy²)+dz² in f32. */
 int ofx_knn_points(const float* points, int64_t n_points, const float* nodes, int32_t n_nodes, int32_t k, int32_t* idx,
                    float* sq_dist, ofx_stream_t s);
+
+/* ---------------- ED-graph construction ----------------
+ * Bit-exact with the compiled reference C++ (tests/test_gpu_graph.py). Graph building runs at init and on
+ * graph updates; these entry points synchronise the stream where an output size or a convergence test is
+ * needed. A handle keeps the mesh's vertex adjacency; it references (does not copy) vertices f32[V*3] and
+ * faces i32[F*3], which must stay alive until ofx_graph_destroy. */
+int ofx_graph_create(const float* vertices, int64_t n_vertices, const int32_t* faces, int64_t n_faces, void** handle,
+                     ofx_stream_t s);
+int ofx_graph_destroy(void* handle);
+int ofx_graph_adjacency(void* handle, int32_t* rowptr, int32_t* col, int64_t* n_col, ofx_stream_t s);
+/* non_eroded u8[V] */
+int ofx_erode_mesh(void* handle, int32_t n_iterations, int32_t min_neighbors, uint8_t* non_eroded, ofx_stream_t s);
+/* node_positions f32[V*3] / node_indices i32[V] capacity; *n_nodes written (host); *n_rounds: parallel rounds */
+int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverage, int32_t use_only_non_eroded,
+                     float* node_positions, int32_t* node_indices, int64_t* n_nodes, int64_t* n_rounds,
+                     ofx_stream_t s);
+/* graph_edges i32[N*K] (-1 padded), weights / distances f32[N*K] (0 padded), node_to_vertex_distances f32[N*V]
+ * (-1 where unvisited; may be NULL). valid_vertices u8[V] may be NULL (all valid). K <= 16. Reaching an
+ * invalid vertex with allow_only_valid_vertices (the reference calls exit(0)) returns OFX_ERR_STATE. */
+int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_t* node_indices, int32_t n_nodes,
+                       int32_t n_max_neighbors, float node_coverage, int32_t allow_only_valid_vertices,
+                       int32_t enforce_total_num_neighbors, int32_t* graph_edges, float* graph_edges_weights,
+                       float* graph_edges_distances, float* node_to_vertex_distances, ofx_stream_t s);
+int ofx_edges_euclidean(const float* node_positions, int32_t n_nodes, int32_t n_max_neighbors, int32_t* graph_edges,
+                        ofx_stream_t s);
+/* valid_in / valid_out u8[N] (may alias) */
+int ofx_node_edge_cleanup(const int32_t* graph_edges, int32_t n_nodes, int32_t max_neighbors, const uint8_t* valid_in,
+                          uint8_t* valid_out, ofx_stream_t s);
+/* clusters i32[N]; cluster_sizes i32[N] capacity (may be NULL); *n_clusters (host) */
+int ofx_compute_clusters(const int32_t* graph_edges, int32_t n_nodes, int32_t max_neighbors, int32_t* clusters,
+                         int32_t* cluster_sizes, int32_t* n_clusters, ofx_stream_t s);
 
 /* ---------------- Gauss-Newton (DeformNet.optimize) ---------------- */
 typedef struct ofx_gn_params {

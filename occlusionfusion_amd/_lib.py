@@ -79,6 +79,15 @@ _SIGS = {
     "ofx_pixel_anchors_geodesic": [P, P, c_int32, c_int64, P, c_int32, c_int32, c_float, P, P, P],
     "ofx_remap_anchors": [P, c_int64, P, c_int32, P, P],
     "ofx_knn_points": [P, c_int64, P, c_int32, c_int32, P, P, P],
+    "ofx_graph_create": [P, c_int64, P, c_int64, P, P],
+    "ofx_graph_destroy": [P],
+    "ofx_graph_adjacency": [P, P, P, P, P],
+    "ofx_erode_mesh": [P, c_int32, c_int32, P, P],
+    "ofx_sample_nodes": [P, P, c_float, c_int32, P, P, P, P, P],
+    "ofx_edges_geodesic": [P, P, P, c_int32, c_int32, c_float, c_int32, c_int32, P, P, P, P, P],
+    "ofx_edges_euclidean": [P, c_int32, c_int32, P, P],
+    "ofx_node_edge_cleanup": [P, c_int32, c_int32, P, P, P],
+    "ofx_compute_clusters": [P, c_int32, c_int32, P, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],

@@ -1,0 +1,871 @@
+// ED-graph construction on the device, bit-exact twins of the reference C++:
+//
+//   ofx_graph_*            opaque handle: the mesh's vertex adjacency (sorted unique neighbour lists, the
+//                          std::set<int> per vertex of graph_proc.cpp:174-186) and scratch
+//   ofx_erode_mesh         graph_proc::erode_mesh              csrc/cpu/graph_proc.cpp:17-77
+//   ofx_sample_nodes       graph_proc::sample_nodes (no shuffle) csrc/cpu/graph_proc.cpp:79-136
+//   ofx_edges_geodesic     graph_proc::compute_edges_geodesic  csrc/cpu/graph_proc.cpp:155-300
+//   ofx_edges_euclidean    graph_proc::compute_edges_euclidean csrc/cpu/graph_proc.cpp:302-356
+//   ofx_node_edge_cleanup  graph_proc::node_and_edge_clean_up  csrc/cpu/graph_proc.cpp:388-438
+//   ofx_compute_clusters   graph_proc::compute_clusters        csrc/cpu/graph_proc.cpp:363-386,440-481
+//   (callers: EDGraph.create_graph_from_mesh / update, embedded_deformation_graph.py:153-380,496-609)
+//
+// How the sequential C++ is reproduced in parallel:
+//  * sample_nodes is the lexicographically-first maximal set of the conflict graph (squaredNorm <= c²):
+//    rounds over per-vertex lists of lower-id conflicting vertices; a vertex becomes a node when all of them
+//    are rejected, and is rejected as soon as one of them is a node (decisions are final, so the rounds
+//    converge to the sequential result).
+//  * compute_edges_geodesic runs one Dijkstra per thread (nodes in parallel) with libstdc++'s exact binary-heap
+//    push/pop (std::priority_queue<..., CustomCompare>), so equal distances pop in the C++ order.
+//  * node_and_edge_clean_up removes nodes with <= 1 surviving neighbour until none changes; removal is
+//    monotone, so the fixpoint (the least closed removed set) does not depend on the sweep order: parallel
+//    Jacobi sweeps give the sequential result.
+//  * compute_clusters numbers connected components by their lowest node id (= the C++ traversal order):
+//    min-label propagation + a rank of the roots.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "ofx_common.h"
+
+namespace ofx {
+
+#define OFX_CHECKS(call)           \
+  do {                             \
+    const int st_ = (call);        \
+    if (st_ != OFX_OK) return st_; \
+  } while (0)
+
+__device__ __forceinline__ float eig_sq(float dx, float dy, float dz) {
+  const float a = dx * dx, b = dy * dy, c = dz * dz;
+  return a + (b + c);   // Eigen 3.3.7 Vector3f redux order
+}
+__device__ __forceinline__ float sqrt_rn(float x) { return (float)sqrt((double)x); }
+__device__ __forceinline__ float fexp(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float fdivr(float a, float b) { return (float)((double)a / (double)b); }
+
+// ------------------------------------------------------------------ adjacency
+__global__ __launch_bounds__(256) void k_adj_pairs(const int32_t* __restrict__ faces, int64_t nf, int64_t nv,
+                                                   uint64_t* __restrict__ keys, int32_t* __restrict__ bad) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= nf) return;
+  const int32_t v[3] = {faces[3 * f], faces[3 * f + 1], faces[3 * f + 2]};
+  int o = 0;
+  for (int j = 0; j < 3; ++j)
+    for (int k = 0; k < 3; ++k) {
+      if (j == k) continue;
+      uint64_t key = ~0ull;   // sorts last; dropped
+      if (v[j] < 0 || v[j] >= nv || v[k] < 0 || v[k] >= nv) atomicOr(bad, 1);
+      else if (v[j] != v[k]) key = (uint64_t)v[j] * (uint64_t)nv + (uint64_t)v[k];
+      keys[6 * f + o++] = key;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_adj_unique(const uint64_t* __restrict__ keys, int64_t n, uint8_t* __restrict__ flag) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flag[i] = keys[i] != ~0ull && (i == 0 || keys[i] != keys[i - 1]);
+}
+
+__global__ __launch_bounds__(256) void k_adj_fill(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ flag,
+                                                  const int32_t* __restrict__ pos, int64_t n, int64_t nv,
+                                                  int32_t* __restrict__ col, int32_t* __restrict__ rowcnt) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n || !flag[i]) return;
+  const int64_t a = (int64_t)(keys[i] / (uint64_t)nv), b = (int64_t)(keys[i] % (uint64_t)nv);
+  col[pos[i]] = (int32_t)b;
+  atomicAdd(&rowcnt[a], 1);
+}
+
+// ------------------------------------------------------------------ erode
+__global__ __launch_bounds__(256) void k_erode_count(const int32_t* __restrict__ faces, const uint8_t* __restrict__ alive,
+                                                     int64_t nf, int32_t* __restrict__ cnt) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= nf || !alive[f]) return;
+  atomicAdd(&cnt[faces[3 * f]], 1);
+  atomicAdd(&cnt[faces[3 * f + 1]], 1);
+  atomicAdd(&cnt[faces[3 * f + 2]], 1);
+}
+
+__global__ __launch_bounds__(256) void k_erode_keep(const int32_t* __restrict__ faces, uint8_t* __restrict__ alive,
+                                                    int64_t nf, const int32_t* __restrict__ cnt, int min_nb) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= nf || !alive[f]) return;
+  alive[f] = cnt[faces[3 * f]] >= min_nb && cnt[faces[3 * f + 1]] >= min_nb && cnt[faces[3 * f + 2]] >= min_nb;
+}
+
+__global__ __launch_bounds__(256) void k_erode_mark(const int32_t* __restrict__ faces, const uint8_t* __restrict__ alive,
+                                                    int64_t nf, uint8_t* __restrict__ mask) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= nf || !alive[f]) return;
+  mask[faces[3 * f]] = 1;
+  mask[faces[3 * f + 1]] = 1;
+  mask[faces[3 * f + 2]] = 1;
+}
+
+// ------------------------------------------------------------------ sample_nodes
+struct Grid {
+  float inv_cell;
+  uint32_t mask;   // table size - 1 (power of two)
+};
+
+__device__ __forceinline__ uint32_t cell_hash(int cx, int cy, int cz, uint32_t mask) {
+  return ((uint32_t)cx * 73856093u ^ (uint32_t)cy * 19349663u ^ (uint32_t)cz * 83492791u) & mask;
+}
+__device__ __forceinline__ void cell_of(const float* p, float inv, int& cx, int& cy, int& cz) {
+  cx = (int)floorf(p[0] * inv); cy = (int)floorf(p[1] * inv); cz = (int)floorf(p[2] * inv);
+}
+
+// eligible vertices get their cell hash as key; others ~0 (sorted last)
+__global__ __launch_bounds__(256) void k_sn_keys(const float* __restrict__ P, const uint8_t* __restrict__ elig, int64_t nv,
+                                                 Grid g, uint32_t* __restrict__ key, int32_t* __restrict__ val) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v >= nv) return;
+  uint32_t k = 0xFFFFFFFFu;
+  if (elig[v]) {
+    int cx, cy, cz;
+    cell_of(P + 3 * v, g.inv_cell, cx, cy, cz);
+    k = cell_hash(cx, cy, cz, g.mask);
+  }
+  key[v] = k;
+  val[v] = (int32_t)v;
+}
+
+__global__ __launch_bounds__(256) void k_sn_bounds(const uint32_t* __restrict__ key, int64_t nv, int32_t* __restrict__ start,
+                                                   int32_t* __restrict__ end) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= nv || key[i] == 0xFFFFFFFFu) return;
+  if (i == 0 || key[i - 1] != key[i]) start[key[i]] = (int32_t)i;
+  if (i == nv - 1 || key[i + 1] != key[i]) end[key[i]] = (int32_t)(i + 1);
+}
+
+// pass 0: count, pass 1: fill the lower-id conflicting eligible vertices of every eligible vertex (ascending
+// id order is not needed: decisions only depend on the set)
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_sn_conflicts(const float* __restrict__ P, const uint8_t* __restrict__ elig, int64_t nv,
+                                                      Grid g, const int32_t* __restrict__ start,
+                                                      const int32_t* __restrict__ end, const int32_t* __restrict__ sorted,
+                                                      float cov2, int32_t* __restrict__ cnt,
+                                                      const int64_t* __restrict__ off, int32_t* __restrict__ list) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v >= nv || !elig[v]) return;
+  const float px = P[3 * v], py = P[3 * v + 1], pz = P[3 * v + 2];
+  int cx, cy, cz;
+  cell_of(P + 3 * v, g.inv_cell, cx, cy, cz);
+  uint32_t seen[27];
+  int ns = 0;
+  int64_t o = FILL ? off[v] : 0;
+  int c = 0;
+  for (int dx = -1; dx <= 1; ++dx)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dz = -1; dz <= 1; ++dz) {
+        const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz, g.mask);
+        bool dup = false;
+        for (int q = 0; q < ns; ++q) dup |= seen[q] == h;   // colliding cells share a bucket: scan it once
+        if (dup) continue;
+        seen[ns++] = h;
+        for (int i = start[h]; i < end[h]; ++i) {
+          const int32_t u = sorted[i];
+          if (u >= v) continue;
+          // (point - node).squaredNorm() <= c² with point = v, node = u (graph_proc.cpp:120)
+          if (eig_sq(px - P[3 * u], py - P[3 * u + 1], pz - P[3 * u + 2]) <= cov2) {
+            if (FILL) list[o + c] = u;
+            ++c;
+          }
+        }
+      }
+  if (!FILL) cnt[v] = c;
+}
+
+enum : uint8_t { kUndecided = 0, kNode = 1, kRejected = 2 };
+
+__global__ __launch_bounds__(256) void k_sn_round(const uint8_t* __restrict__ elig, int64_t nv,
+                                                  const int64_t* __restrict__ off, const int32_t* __restrict__ list,
+                                                  int64_t* __restrict__ cursor, uint8_t* __restrict__ state,
+                                                  int32_t* __restrict__ n_undecided) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v >= nv || !elig[v] || state[v] != kUndecided) return;
+  int64_t c = cursor[v];
+  const int64_t e = off[v + 1];
+  uint8_t s = kNode;
+  for (; c < e; ++c) {
+    const uint8_t su = ((volatile const uint8_t*)state)[list[c]];   // decisions are final: a stale read only delays
+    if (su == kRejected) continue;
+    s = su == kNode ? kRejected : kUndecided;
+    break;
+  }
+  cursor[v] = c;
+  if (s != kUndecided) ((volatile uint8_t*)state)[v] = s;
+  else atomicAdd(n_undecided, 1);
+}
+
+__global__ __launch_bounds__(256) void k_sn_flags(const uint8_t* __restrict__ state, const uint8_t* __restrict__ elig,
+                                                  int64_t nv, uint8_t* __restrict__ is_node) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v < nv) is_node[v] = elig[v] && state[v] == kNode;
+}
+
+__global__ __launch_bounds__(256) void k_sn_emit(const float* __restrict__ P, const uint8_t* __restrict__ is_node,
+                                                 const int32_t* __restrict__ rank, int64_t nv, float* __restrict__ pos,
+                                                 int32_t* __restrict__ idx) {
+  const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (v >= nv || !is_node[v]) return;
+  const int32_t r = rank[v];
+  pos[3 * (int64_t)r] = P[3 * v]; pos[3 * (int64_t)r + 1] = P[3 * v + 1]; pos[3 * (int64_t)r + 2] = P[3 * v + 2];
+  idx[r] = (int32_t)v;
+}
+
+// ------------------------------------------------------------------ geodesic edges
+struct HeapEnt {
+  int32_t v;
+  float d;
+};
+
+// libstdc++ std::__push_heap with comp(a, b) = a.d > b.d
+__device__ __forceinline__ void heap_sift_up(HeapEnt* h, int64_t hole, int64_t top, HeapEnt val) {
+  int64_t parent = (hole - 1) / 2;
+  while (hole > top && h[parent].d > val.d) {
+    h[hole] = h[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  h[hole] = val;
+}
+
+// std::pop_heap on [0, n) followed by pop_back: returns the top, leaves n-1 entries
+__device__ __forceinline__ HeapEnt heap_pop(HeapEnt* h, int64_t n) {
+  const HeapEnt top = h[0];
+  const int64_t len = n - 1;
+  if (len > 0) {
+    const HeapEnt val = h[len];
+    int64_t hole = 0, second = 0;
+    while (second < (len - 1) / 2) {
+      second = 2 * (second + 1);
+      if (h[second].d > h[second - 1].d) second--;
+      h[hole] = h[second];
+      hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+      second = 2 * (second + 1);
+      h[hole] = h[second - 1];
+      hole = second - 1;
+    }
+    heap_sift_up(h, hole, 0, val);
+  }
+  return top;
+}
+
+struct GeoArgs {
+  const float* P;
+  const uint8_t* valid;      // per vertex (may be null: all valid)
+  const int32_t* rowptr;     // adjacency CSR
+  const int32_t* col;
+  const int32_t* v2n;        // vertex -> node (last node id wins, graph_proc.cpp:190-196) or -1
+  const int32_t* node_idx;   // node -> vertex
+  int32_t n_nodes, K;
+  int64_t nv;
+  float cov, max_inf, two_c2;
+  int32_t only_valid, enforce;
+  int32_t *edges;
+  float *wts, *dists, *n2v;  // n2v may be null
+  uint32_t* visited;         // bitmap, batch rows of ceil(nv/32) words
+  HeapEnt* heap;             // batch rows of cap entries
+  int64_t cap;
+  int32_t* status;           // per node: 0 ok, 1 heap overflow, 2 invalid vertex reached
+};
+
+__global__ __launch_bounds__(64) void k_geodesic(GeoArgs a, const int32_t* __restrict__ todo, int32_t n_todo) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_todo) return;
+  const int32_t node = todo[t];
+  const int64_t words = (a.nv + 31) / 32;
+  uint32_t* vis = a.visited + (int64_t)t * words;
+  HeapEnt* h = a.heap + (int64_t)t * a.cap;
+  for (int i = 0; i < a.K; ++i) {
+    a.edges[(int64_t)node * a.K + i] = -1;
+    a.wts[(int64_t)node * a.K + i] = 0.f;
+    a.dists[(int64_t)node * a.K + i] = 0.f;
+  }
+  a.status[node] = 0;
+  const int32_t s = a.node_idx[node];
+  if (s < 0) return;
+  int64_t n = 0;
+  h[n++] = HeapEnt{s, 0.f};
+  int32_t ids[16];
+  float ds[16];
+  int cnt = 0;
+  while (n > 0) {
+    const HeapEnt top = heap_pop(h, n);
+    --n;
+    const int32_t v = top.v;
+    const float d = top.d;
+    if (vis[v >> 5] & (1u << (v & 31))) continue;
+    if (a.only_valid && a.valid && !a.valid[v]) { a.status[node] = 2; return; }   // the C++ calls exit(0)
+    const int32_t m = a.v2n[v];
+    if (m >= 0 && m != node) {
+      ids[cnt] = m;
+      ds[cnt] = d;
+      ++cnt;
+      if (cnt >= a.K) break;
+    }
+    if (a.n2v) a.n2v[(int64_t)node * a.nv + v] = d;
+    vis[v >> 5] |= 1u << (v & 31);
+    const float vx = a.P[3 * (int64_t)v], vy = a.P[3 * (int64_t)v + 1], vz = a.P[3 * (int64_t)v + 2];
+    for (int32_t q = a.rowptr[v]; q < a.rowptr[v + 1]; ++q) {
+      const int32_t u = a.col[q];
+      if (a.only_valid && a.valid && !a.valid[u]) continue;
+      const float dist = d + sqrt_rn(eig_sq(vx - a.P[3 * (int64_t)u], vy - a.P[3 * (int64_t)u + 1],
+                                            vz - a.P[3 * (int64_t)u + 2]));
+      if (a.enforce || dist <= a.max_inf) {
+        if (n >= a.cap) { a.status[node] = 1; return; }
+        heap_sift_up(h, n, 0, HeapEnt{u, dist});
+        ++n;
+      }
+    }
+  }
+  // weights (graph_proc.cpp:262-281): exp(-(d*d)/(2c²)) f32, f32 sum, w/sum or w/n
+  float w[16];
+  float sum = 0.f;
+  for (int i = 0; i < cnt; ++i) {
+    w[i] = fexp(fdivr(-(ds[i] * ds[i]), a.two_c2));
+    sum += w[i];
+  }
+  for (int i = 0; i < cnt; ++i) {
+    const int64_t o = (int64_t)node * a.K + i;
+    a.edges[o] = ids[i];
+    a.wts[o] = sum > 0.f ? fdivr(w[i], sum) : fdivr(w[i], (float)cnt);
+    a.dists[o] = ds[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_v2n(const int32_t* __restrict__ node_idx, int32_t n_nodes, int64_t nv,
+                                             int32_t* __restrict__ v2n) {
+  // the C++ loop assigns in node order, so the LAST node on a vertex wins: max over node ids
+  const int32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  const int32_t v = node_idx[n];
+  if (v >= 0 && v < nv) atomicMax(&v2n[v], n);
+}
+
+__global__ __launch_bounds__(256) void k_fill_f32(float* __restrict__ p, int64_t n, float val) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = val;
+}
+
+// ------------------------------------------------------------------ euclidean edges
+__global__ __launch_bounds__(256) void k_edges_euclid(const float* __restrict__ X, int n_nodes, int K,
+                                                      int32_t* __restrict__ edges) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  const float px = X[3 * n], py = X[3 * n + 1], pz = X[3 * n + 2];
+  float d[16];
+  int id[16];
+  int cnt = 0;
+  for (int j = 0; j < n_nodes; ++j) {
+    if (j == n) continue;
+    const float d2 = eig_sq(px - X[3 * j], py - X[3 * j + 1], pz - X[3 * j + 2]);
+    int pos = cnt;
+    for (int s = cnt - 1; s >= 0; --s)
+      if (d2 <= d[s]) pos = s;
+    if (pos < K) {
+      const int last = cnt < K ? cnt : K - 1;
+      for (int s = last; s > pos; --s) { d[s] = d[s - 1]; id[s] = id[s - 1]; }
+      d[pos] = d2;
+      id[pos] = j;
+      if (cnt < K) ++cnt;
+    }
+  }
+  for (int s = 0; s < K; ++s) edges[(int64_t)n * K + s] = s < cnt ? id[s] : -1;
+}
+
+// ------------------------------------------------------------------ clean-up and clusters
+__global__ __launch_bounds__(256) void k_cleanup_sweep(const int32_t* __restrict__ E, int n_nodes, int K,
+                                                       const uint8_t* __restrict__ valid_in, uint8_t* __restrict__ removed,
+                                                       int32_t* __restrict__ changed) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes || !valid_in[n] || removed[n]) return;
+  int c = 0;
+  for (int i = 0; i < K; ++i) {
+    const int32_t j = E[(int64_t)n * K + i];
+    if (j == -1) break;
+    if (j >= 0 && j < n_nodes && ((volatile const uint8_t*)removed)[j]) continue;
+    ++c;
+  }
+  if (c <= 1) {
+    ((volatile uint8_t*)removed)[n] = 1;
+    atomicAdd(changed, 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cleanup_out(const uint8_t* __restrict__ valid_in, const uint8_t* __restrict__ removed,
+                                                     int n_nodes, uint8_t* __restrict__ valid_out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < n_nodes) valid_out[n] = valid_in[n] && !removed[n];
+}
+
+__global__ __launch_bounds__(256) void k_cc_init(int32_t* __restrict__ lab, int n_nodes) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < n_nodes) lab[n] = n;
+}
+
+// hook: for every edge (n, j) before the row's first -1, both ends take the smaller root label
+__global__ __launch_bounds__(256) void k_cc_hook(const int32_t* __restrict__ E, int n_nodes, int K, int32_t* __restrict__ lab,
+                                                 int32_t* __restrict__ changed) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  for (int i = 0; i < K; ++i) {
+    const int32_t j = E[(int64_t)n * K + i];
+    if (j == -1) break;
+    if (j < 0 || j >= n_nodes) continue;
+    const int32_t a = lab[n], b = lab[j];
+    if (a == b) continue;
+    const int32_t lo = min(a, b), hi = max(a, b);
+    if (atomicMin(&lab[hi], lo) > lo) atomicAdd(changed, 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cc_jump(int32_t* __restrict__ lab, int n_nodes, int32_t* __restrict__ changed) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  const int32_t l = lab[n], ll = lab[l];
+  if (ll != l) { lab[n] = ll; atomicAdd(changed, 1); }
+}
+
+__global__ __launch_bounds__(256) void k_cc_roots(const int32_t* __restrict__ lab, int n_nodes, uint8_t* __restrict__ root) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < n_nodes) root[n] = lab[n] == n;
+}
+
+__global__ __launch_bounds__(256) void k_cc_out(const int32_t* __restrict__ lab, const int32_t* __restrict__ rank, int n_nodes,
+                                                int32_t* __restrict__ clusters, int32_t* __restrict__ sizes) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  const int32_t c = rank[lab[n]];
+  clusters[n] = c;
+  if (sizes) atomicAdd(&sizes[c], 1);
+}
+
+// ------------------------------------------------------------------ handle
+struct Graph {
+  int64_t nv = 0, nf = 0;
+  int32_t* rowptr = nullptr;   // nv + 1
+  int32_t* col = nullptr;
+  int64_t ncol = 0;
+  const float* P = nullptr;
+  const int32_t* faces = nullptr;
+};
+
+template <typename T>
+int dalloc(T** p, int64_t n, hipStream_t s) {
+  OFX_HIP(hipMallocAsync((void**)p, (size_t)std::max<int64_t>(n, 1) * sizeof(T), s));
+  return OFX_OK;
+}
+template <typename T>
+void dfree(T* p, hipStream_t s) {
+  if (p) (void)hipFreeAsync(p, s);
+}
+
+inline int exclusive_sum_i32(const int32_t* in, int32_t* out, int64_t n, hipStream_t s) {
+  size_t tmp = 0;
+  OFX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)n, s));
+  void* t = nullptr;
+  OFX_HIP(hipMallocAsync(&t, std::max<size_t>(tmp, 1), s));
+  OFX_HIP(hipcub::DeviceScan::ExclusiveSum(t, tmp, in, out, (int)n, s));
+  OFX_HIP(hipFreeAsync(t, s));
+  return OFX_OK;
+}
+inline int exclusive_sum_u8(const uint8_t* in, int32_t* out, int64_t n, hipStream_t s) {
+  size_t tmp = 0;
+  hipcub::TransformInputIterator<int32_t, hipcub::CastOp<int32_t>, const uint8_t*> it(in, hipcub::CastOp<int32_t>());
+  OFX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, out, (int)n, s));
+  void* t = nullptr;
+  OFX_HIP(hipMallocAsync(&t, std::max<size_t>(tmp, 1), s));
+  OFX_HIP(hipcub::DeviceScan::ExclusiveSum(t, tmp, it, out, (int)n, s));
+  OFX_HIP(hipFreeAsync(t, s));
+  return OFX_OK;
+}
+inline int exclusive_sum_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s) {
+  size_t tmp = 0;
+  hipcub::TransformInputIterator<int64_t, hipcub::CastOp<int64_t>, const int32_t*> it(in, hipcub::CastOp<int64_t>());
+  OFX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, out, (int)n, s));
+  void* t = nullptr;
+  OFX_HIP(hipMallocAsync(&t, std::max<size_t>(tmp, 1), s));
+  OFX_HIP(hipcub::DeviceScan::ExclusiveSum(t, tmp, it, out, (int)n, s));
+  OFX_HIP(hipFreeAsync(t, s));
+  return OFX_OK;
+}
+
+template <typename T>
+inline int read1(const T* dev, T* host, hipStream_t s) {
+  OFX_HIP(hipMemcpyAsync(host, dev, sizeof(T), hipMemcpyDeviceToHost, s));
+  OFX_HIP(hipStreamSynchronize(s));
+  return OFX_OK;
+}
+
+}  // namespace ofx
+
+using namespace ofx;
+
+extern "C" {
+
+int ofx_graph_create(const float* vertices, int64_t n_vertices, const int32_t* faces, int64_t n_faces, void** handle,
+                     ofx_stream_t s) {
+  OFX_CHECK_ARG(handle && n_vertices >= 0 && n_faces >= 0, "bad arguments");
+  OFX_CHECK_ARG(n_vertices < (1ll << 31) && 6 * n_faces < (1ll << 31), "mesh too large");
+  OFX_CHECK_ARG((n_vertices == 0 || vertices) && (n_faces == 0 || faces), "null mesh");
+  hipStream_t hs = as_stream(s);
+  Graph* g = new Graph();
+  g->nv = n_vertices;
+  g->nf = n_faces;
+  g->P = vertices;
+  g->faces = faces;
+  *handle = g;
+  const int64_t np = 6 * n_faces;
+  OFX_CHECKS(dalloc(&g->rowptr, n_vertices + 1, hs));
+  OFX_HIP(hipMemsetAsync(g->rowptr, 0, (n_vertices + 1) * sizeof(int32_t), hs));
+  if (np == 0) {
+    OFX_CHECKS(dalloc(&g->col, 1, hs));
+    return OFX_OK;
+  }
+  uint64_t *keys = nullptr, *keys2 = nullptr;
+  uint8_t* flag = nullptr;
+  int32_t *pos = nullptr, *cnt = nullptr, *bad = nullptr;
+  OFX_CHECKS(dalloc(&keys, np, hs));
+  OFX_CHECKS(dalloc(&keys2, np, hs));
+  OFX_CHECKS(dalloc(&flag, np, hs));
+  OFX_CHECKS(dalloc(&pos, np + 1, hs));
+  OFX_CHECKS(dalloc(&cnt, n_vertices + 1, hs));
+  OFX_CHECKS(dalloc(&bad, 1, hs));
+  OFX_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), hs));
+  OFX_HIP(hipMemsetAsync(cnt, 0, (n_vertices + 1) * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_adj_pairs, dim3(grid_for(n_faces, 256, 1 << 30)), dim3(256), 0, hs, faces, n_faces, n_vertices, keys, bad);
+  size_t tmp = 0;
+  OFX_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, keys, keys2, (int)np, 0, 64, hs));
+  void* t = nullptr;
+  OFX_HIP(hipMallocAsync(&t, std::max<size_t>(tmp, 1), hs));
+  OFX_HIP(hipcub::DeviceRadixSort::SortKeys(t, tmp, keys, keys2, (int)np, 0, 64, hs));
+  OFX_HIP(hipFreeAsync(t, hs));
+  hipLaunchKernelGGL(k_adj_unique, dim3(grid_for(np, 256, 1 << 30)), dim3(256), 0, hs, (const uint64_t*)keys2, np, flag);
+  OFX_CHECKS(exclusive_sum_u8(flag, pos, np, hs));
+  int32_t ncol = 0, hbad = 0;
+  // total = pos[np-1] + flag[np-1]
+  int32_t last_pos = 0;
+  uint8_t last_flag = 0;
+  OFX_HIP(hipMemcpyAsync(&last_pos, pos + np - 1, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipMemcpyAsync(&last_flag, flag + np - 1, 1, hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipStreamSynchronize(hs));
+  ncol = last_pos + last_flag;
+  if (hbad) {
+    dfree(keys, hs); dfree(keys2, hs); dfree(flag, hs); dfree(pos, hs); dfree(cnt, hs); dfree(bad, hs);
+    set_error("face index out of range [0, %lld)", (long long)n_vertices);
+    return OFX_ERR_ARG;
+  }
+  g->ncol = ncol;
+  OFX_CHECKS(dalloc(&g->col, ncol, hs));
+  hipLaunchKernelGGL(k_adj_fill, dim3(grid_for(np, 256, 1 << 30)), dim3(256), 0, hs, (const uint64_t*)keys2,
+                     (const uint8_t*)flag, (const int32_t*)pos, np, n_vertices, g->col, cnt);
+  OFX_CHECKS(exclusive_sum_i32(cnt, g->rowptr, n_vertices + 1, hs));
+  OFX_LAUNCH_CHECK();
+  dfree(keys, hs); dfree(keys2, hs); dfree(flag, hs); dfree(pos, hs); dfree(cnt, hs); dfree(bad, hs);
+  return OFX_OK;
+}
+
+int ofx_graph_destroy(void* handle) {
+  if (!handle) return OFX_OK;
+  Graph* g = (Graph*)handle;
+  (void)hipDeviceSynchronize();
+  if (g->rowptr) (void)hipFree(g->rowptr);
+  if (g->col) (void)hipFree(g->col);
+  delete g;
+  return OFX_OK;
+}
+
+/* vertex adjacency (CSR) of the handle's mesh, for inspection: rowptr i32[V+1], col i32[rowptr[V]] */
+int ofx_graph_adjacency(void* handle, int32_t* rowptr, int32_t* col, int64_t* n_col, ofx_stream_t s) {
+  Graph* g = (Graph*)handle;
+  OFX_CHECK_ARG(g && n_col, "null argument");
+  *n_col = g->ncol;
+  hipStream_t hs = as_stream(s);
+  if (rowptr) OFX_HIP(hipMemcpyAsync(rowptr, g->rowptr, (g->nv + 1) * sizeof(int32_t), hipMemcpyDeviceToDevice, hs));
+  if (col && g->ncol) OFX_HIP(hipMemcpyAsync(col, g->col, g->ncol * sizeof(int32_t), hipMemcpyDeviceToDevice, hs));
+  return OFX_OK;
+}
+
+int ofx_erode_mesh(void* handle, int32_t n_iterations, int32_t min_neighbors, uint8_t* non_eroded, ofx_stream_t s) {
+  Graph* g = (Graph*)handle;
+  OFX_CHECK_ARG(g && non_eroded && n_iterations >= 0, "bad arguments");
+  hipStream_t hs = as_stream(s);
+  if (g->nv == 0) return OFX_OK;
+  OFX_HIP(hipMemsetAsync(non_eroded, 0, g->nv, hs));
+  if (g->nf == 0) return OFX_OK;
+  uint8_t* alive = nullptr;
+  int32_t* cnt = nullptr;
+  OFX_CHECKS(dalloc(&alive, g->nf, hs));
+  OFX_CHECKS(dalloc(&cnt, g->nv, hs));
+  OFX_HIP(hipMemsetAsync(alive, 1, g->nf, hs));
+  const dim3 gf(grid_for(g->nf, 256, 1 << 30));
+  for (int it = 0; it < n_iterations; ++it) {
+    OFX_HIP(hipMemsetAsync(cnt, 0, g->nv * sizeof(int32_t), hs));
+    hipLaunchKernelGGL(k_erode_count, gf, dim3(256), 0, hs, g->faces, (const uint8_t*)alive, g->nf, cnt);
+    hipLaunchKernelGGL(k_erode_keep, gf, dim3(256), 0, hs, g->faces, alive, g->nf, (const int32_t*)cnt, min_neighbors);
+  }
+  hipLaunchKernelGGL(k_erode_mark, gf, dim3(256), 0, hs, g->faces, (const uint8_t*)alive, g->nf, non_eroded);
+  OFX_LAUNCH_CHECK();
+  dfree(alive, hs);
+  dfree(cnt, hs);
+  return OFX_OK;
+}
+
+int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverage, int32_t use_only_non_eroded,
+                     float* node_positions, int32_t* node_indices, int64_t* n_nodes, int64_t* n_rounds,
+                     ofx_stream_t s) {
+  Graph* g = (Graph*)handle;
+  OFX_CHECK_ARG(g && node_positions && node_indices && n_nodes, "null argument");
+  OFX_CHECK_ARG(node_coverage > 0.f, "node_coverage must be > 0");
+  OFX_CHECK_ARG(!use_only_non_eroded || non_eroded, "non_eroded mask required");
+  hipStream_t hs = as_stream(s);
+  const int64_t nv = g->nv;
+  *n_nodes = 0;
+  if (n_rounds) *n_rounds = 0;
+  if (nv == 0) return OFX_OK;
+  uint8_t *elig = nullptr, *state = nullptr, *is_node = nullptr;
+  uint32_t *key = nullptr, *key2 = nullptr;
+  int32_t *val = nullptr, *sorted = nullptr, *bstart = nullptr, *bend = nullptr, *cnt = nullptr, *list = nullptr;
+  int32_t *rank = nullptr, *und = nullptr;
+  int64_t *off = nullptr, *cursor = nullptr;
+  uint32_t tsize = 1;
+  while (tsize < 2 * nv) tsize <<= 1;
+  OFX_CHECKS(dalloc(&elig, nv, hs));
+  if (use_only_non_eroded) OFX_HIP(hipMemcpyAsync(elig, non_eroded, nv, hipMemcpyDeviceToDevice, hs));
+  else OFX_HIP(hipMemsetAsync(elig, 1, nv, hs));
+  OFX_CHECKS(dalloc(&key, nv, hs));
+  OFX_CHECKS(dalloc(&key2, nv, hs));
+  OFX_CHECKS(dalloc(&val, nv, hs));
+  OFX_CHECKS(dalloc(&sorted, nv, hs));
+  OFX_CHECKS(dalloc(&bstart, tsize, hs));
+  OFX_CHECKS(dalloc(&bend, tsize, hs));
+  OFX_HIP(hipMemsetAsync(bstart, 0, tsize * sizeof(int32_t), hs));
+  OFX_HIP(hipMemsetAsync(bend, 0, tsize * sizeof(int32_t), hs));
+  // cells a little larger than the coverage so every conflicting pair lies in adjacent cells despite rounding
+  Grid gr{1.f / (node_coverage * 1.01f), tsize - 1};
+  const float cov2 = node_coverage * node_coverage;
+  const dim3 gv(grid_for(nv, 256, 1 << 30));
+  hipLaunchKernelGGL(k_sn_keys, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr, key, val);
+  size_t tmp = 0;
+  OFX_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, key, key2, val, sorted, (int)nv, 0, 32, hs));
+  void* t = nullptr;
+  OFX_HIP(hipMallocAsync(&t, std::max<size_t>(tmp, 1), hs));
+  OFX_HIP(hipcub::DeviceRadixSort::SortPairs(t, tmp, key, key2, val, sorted, (int)nv, 0, 32, hs));
+  OFX_HIP(hipFreeAsync(t, hs));
+  hipLaunchKernelGGL(k_sn_bounds, gv, dim3(256), 0, hs, (const uint32_t*)key2, nv, bstart, bend);
+  OFX_CHECKS(dalloc(&cnt, nv + 1, hs));
+  OFX_HIP(hipMemsetAsync(cnt, 0, (nv + 1) * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_sn_conflicts<false>, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                     (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                     (const int64_t*)nullptr, (int32_t*)nullptr);
+  OFX_CHECKS(dalloc(&off, nv + 1, hs));
+  OFX_CHECKS(exclusive_sum_i32_to_i64(cnt, off, nv + 1, hs));
+  int64_t total = 0;
+  OFX_CHECKS(read1(off + nv, &total, hs));
+  OFX_CHECKS(dalloc(&list, total, hs));
+  hipLaunchKernelGGL(k_sn_conflicts<true>, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                     (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                     (const int64_t*)off, list);
+  OFX_CHECKS(dalloc(&cursor, nv, hs));
+  OFX_HIP(hipMemcpyAsync(cursor, off, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, hs));
+  OFX_CHECKS(dalloc(&state, nv, hs));
+  OFX_HIP(hipMemsetAsync(state, kUndecided, nv, hs));
+  constexpr int kChunk = 32;
+  OFX_CHECKS(dalloc(&und, kChunk, hs));
+  int64_t rounds = 0;
+  for (;;) {
+    OFX_HIP(hipMemsetAsync(und, 0, kChunk * sizeof(int32_t), hs));
+    for (int r = 0; r < kChunk; ++r)
+      hipLaunchKernelGGL(k_sn_round, gv, dim3(256), 0, hs, (const uint8_t*)elig, nv, (const int64_t*)off,
+                         (const int32_t*)list, cursor, state, und + r);
+    OFX_LAUNCH_CHECK();
+    int32_t h[kChunk];
+    OFX_HIP(hipMemcpyAsync(h, und, sizeof(h), hipMemcpyDeviceToHost, hs));
+    OFX_HIP(hipStreamSynchronize(hs));
+    int r = 0;
+    while (r < kChunk && h[r] != 0) ++r;
+    rounds += (r < kChunk) ? r + 1 : kChunk;
+    if (r < kChunk) break;
+    if (rounds > nv + kChunk) { set_error("sample_nodes did not converge"); return OFX_ERR_STATE; }
+  }
+  OFX_CHECKS(dalloc(&is_node, nv + 1, hs));
+  OFX_CHECKS(dalloc(&rank, nv + 1, hs));
+  OFX_HIP(hipMemsetAsync(is_node + nv, 0, 1, hs));
+  hipLaunchKernelGGL(k_sn_flags, gv, dim3(256), 0, hs, (const uint8_t*)state, (const uint8_t*)elig, nv, is_node);
+  OFX_CHECKS(exclusive_sum_u8(is_node, rank, nv + 1, hs));
+  hipLaunchKernelGGL(k_sn_emit, gv, dim3(256), 0, hs, g->P, (const uint8_t*)is_node, (const int32_t*)rank, nv,
+                     node_positions, node_indices);
+  OFX_LAUNCH_CHECK();
+  int32_t nn = 0;
+  OFX_CHECKS(read1(rank + nv, &nn, hs));
+  *n_nodes = nn;
+  if (n_rounds) *n_rounds = rounds;
+  for (void* p : {(void*)elig, (void*)state, (void*)is_node, (void*)key, (void*)key2, (void*)val, (void*)sorted,
+                  (void*)bstart, (void*)bend, (void*)cnt, (void*)list, (void*)rank, (void*)und, (void*)off,
+                  (void*)cursor})
+    dfree(p, hs);
+  return OFX_OK;
+}
+
+int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_t* node_indices, int32_t n_nodes,
+                       int32_t n_max_neighbors, float node_coverage, int32_t allow_only_valid_vertices,
+                       int32_t enforce_total_num_neighbors, int32_t* graph_edges, float* graph_edges_weights,
+                       float* graph_edges_distances, float* node_to_vertex_distances, ofx_stream_t s) {
+  Graph* g = (Graph*)handle;
+  OFX_CHECK_ARG(g && n_nodes >= 0, "bad arguments");
+  OFX_CHECK_ARG(n_max_neighbors >= 1 && n_max_neighbors <= 16, "n_max_neighbors must be in [1, 16]");
+  if (n_nodes == 0) return OFX_OK;
+  OFX_CHECK_ARG(node_indices && graph_edges && graph_edges_weights && graph_edges_distances, "null buffer");
+  hipStream_t hs = as_stream(s);
+  const int64_t nv = g->nv;
+  int32_t *v2n = nullptr, *status = nullptr, *todo = nullptr;
+  OFX_CHECKS(dalloc(&v2n, nv, hs));
+  OFX_HIP(hipMemsetAsync(v2n, 0xFF, std::max<int64_t>(nv, 1) * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_v2n, dim3(grid_for(n_nodes, 256)), dim3(256), 0, hs, node_indices, n_nodes, nv, v2n);
+  if (node_to_vertex_distances)
+    hipLaunchKernelGGL(k_fill_f32, dim3(grid_for((int64_t)n_nodes * nv, 256, 65536)), dim3(256), 0, hs,
+                       node_to_vertex_distances, (int64_t)n_nodes * nv, -1.f);
+  OFX_CHECKS(dalloc(&status, n_nodes, hs));
+  OFX_CHECKS(dalloc(&todo, n_nodes, hs));
+  std::vector<int32_t> h_todo(n_nodes);
+  for (int i = 0; i < n_nodes; ++i) h_todo[i] = i;
+  GeoArgs a{};
+  a.P = g->P; a.valid = valid_vertices; a.rowptr = g->rowptr; a.col = g->col; a.v2n = v2n; a.node_idx = node_indices;
+  a.n_nodes = n_nodes; a.K = n_max_neighbors; a.nv = nv; a.cov = node_coverage;
+  a.max_inf = 2.f * node_coverage;
+  a.two_c2 = (2.f * node_coverage) * node_coverage;
+  a.only_valid = allow_only_valid_vertices; a.enforce = enforce_total_num_neighbors;
+  a.edges = graph_edges; a.wts = graph_edges_weights; a.dists = graph_edges_distances; a.n2v = node_to_vertex_distances;
+  const int64_t words = (nv + 31) / 32;
+  int64_t cap = 8192;
+  while (!h_todo.empty()) {
+    // batch so that visited bitmaps + heaps stay within ~1 GiB
+    const int64_t per = words * 4 + cap * (int64_t)sizeof(HeapEnt);
+    const int64_t batch = std::max<int64_t>(1, std::min<int64_t>((int64_t)h_todo.size(), (1ll << 30) / per));
+    OFX_HIP(hipMemcpyAsync(todo, h_todo.data(), h_todo.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+    OFX_CHECKS(dalloc(&a.visited, batch * words, hs));
+    OFX_CHECKS(dalloc(&a.heap, batch * cap, hs));
+    a.cap = cap;
+    a.status = status;
+    for (int64_t b0 = 0; b0 < (int64_t)h_todo.size(); b0 += batch) {
+      const int64_t nb = std::min<int64_t>(batch, (int64_t)h_todo.size() - b0);
+      OFX_HIP(hipMemsetAsync(a.visited, 0, nb * words * sizeof(uint32_t), hs));
+      hipLaunchKernelGGL(k_geodesic, dim3((unsigned)((nb + 63) / 64)), dim3(64), 0, hs, a, (const int32_t*)(todo + b0),
+                         (int32_t)nb);
+      OFX_LAUNCH_CHECK();
+    }
+    std::vector<int32_t> st(n_nodes);
+    OFX_HIP(hipMemcpyAsync(st.data(), status, n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+    OFX_HIP(hipStreamSynchronize(hs));
+    dfree(a.visited, hs);
+    dfree(a.heap, hs);
+    std::vector<int32_t> again;
+    for (int32_t n : h_todo) {
+      if (st[n] == 2) {
+        dfree(v2n, hs); dfree(status, hs); dfree(todo, hs);
+        set_error("compute_edges_geodesic: node %d reached an invalid vertex (the reference exits)", n);
+        return OFX_ERR_STATE;
+      }
+      if (st[n] == 1) again.push_back(n);
+    }
+    h_todo.swap(again);
+    if (!h_todo.empty()) {
+      if (cap >= (int64_t)1 << 34) { set_error("geodesic heap capacity exhausted"); return OFX_ERR_RANGE; }
+      cap *= 16;
+      // a rerun node restarts from scratch: its n2v row may hold partial distances
+      if (node_to_vertex_distances)
+        for (int32_t n : h_todo)
+          hipLaunchKernelGGL(k_fill_f32, dim3(grid_for(nv, 256, 4096)), dim3(256), 0, hs,
+                             node_to_vertex_distances + (int64_t)n * nv, nv, -1.f);
+    }
+  }
+  dfree(v2n, hs);
+  dfree(status, hs);
+  dfree(todo, hs);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_edges_euclidean(const float* node_positions, int32_t n_nodes, int32_t n_max_neighbors, int32_t* graph_edges,
+                        ofx_stream_t s) {
+  OFX_CHECK_ARG(n_nodes >= 0 && n_max_neighbors >= 1 && n_max_neighbors <= 16, "bad arguments");
+  if (n_nodes == 0) return OFX_OK;
+  OFX_CHECK_ARG(node_positions && graph_edges, "null buffer");
+  hipLaunchKernelGGL(k_edges_euclid, dim3(grid_for(n_nodes, 256)), dim3(256), 0, as_stream(s), node_positions, n_nodes,
+                     n_max_neighbors, graph_edges);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_node_edge_cleanup(const int32_t* graph_edges, int32_t n_nodes, int32_t max_neighbors, const uint8_t* valid_in,
+                          uint8_t* valid_out, ofx_stream_t s) {
+  OFX_CHECK_ARG(n_nodes >= 0 && max_neighbors >= 0, "bad arguments");
+  if (n_nodes == 0) return OFX_OK;
+  OFX_CHECK_ARG(graph_edges && valid_in && valid_out, "null buffer");
+  hipStream_t hs = as_stream(s);
+  uint8_t* removed = nullptr;
+  int32_t* changed = nullptr;
+  OFX_CHECKS(dalloc(&removed, n_nodes, hs));
+  OFX_CHECKS(dalloc(&changed, 1, hs));
+  OFX_HIP(hipMemsetAsync(removed, 0, n_nodes, hs));
+  const dim3 gn(grid_for(n_nodes, 256));
+  for (int it = 0; it <= n_nodes; ++it) {
+    OFX_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), hs));
+    hipLaunchKernelGGL(k_cleanup_sweep, gn, dim3(256), 0, hs, graph_edges, n_nodes, max_neighbors, valid_in, removed, changed);
+    OFX_LAUNCH_CHECK();
+    int32_t c = 0;
+    OFX_CHECKS(read1(changed, &c, hs));
+    if (c == 0) break;
+  }
+  hipLaunchKernelGGL(k_cleanup_out, gn, dim3(256), 0, hs, valid_in, (const uint8_t*)removed, n_nodes, valid_out);
+  OFX_LAUNCH_CHECK();
+  dfree(removed, hs);
+  dfree(changed, hs);
+  return OFX_OK;
+}
+
+int ofx_compute_clusters(const int32_t* graph_edges, int32_t n_nodes, int32_t max_neighbors, int32_t* clusters,
+                         int32_t* cluster_sizes, int32_t* n_clusters, ofx_stream_t s) {
+  OFX_CHECK_ARG(n_nodes >= 0 && max_neighbors >= 0 && n_clusters, "bad arguments");
+  *n_clusters = 0;
+  if (n_nodes == 0) return OFX_OK;
+  OFX_CHECK_ARG(graph_edges && clusters, "null buffer");
+  hipStream_t hs = as_stream(s);
+  int32_t *lab = nullptr, *changed = nullptr, *rank = nullptr;
+  uint8_t* root = nullptr;
+  OFX_CHECKS(dalloc(&lab, n_nodes, hs));
+  OFX_CHECKS(dalloc(&changed, 1, hs));
+  OFX_CHECKS(dalloc(&rank, n_nodes + 1, hs));
+  OFX_CHECKS(dalloc(&root, n_nodes + 1, hs));
+  const dim3 gn(grid_for(n_nodes, 256));
+  hipLaunchKernelGGL(k_cc_init, gn, dim3(256), 0, hs, lab, n_nodes);
+  for (int it = 0; it <= 2 * n_nodes + 2; ++it) {
+    OFX_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), hs));
+    hipLaunchKernelGGL(k_cc_hook, gn, dim3(256), 0, hs, graph_edges, n_nodes, max_neighbors, lab, changed);
+    for (int j = 0; j < 4; ++j) hipLaunchKernelGGL(k_cc_jump, gn, dim3(256), 0, hs, lab, n_nodes, changed);
+    OFX_LAUNCH_CHECK();
+    int32_t c = 0;
+    OFX_CHECKS(read1(changed, &c, hs));
+    if (c == 0) break;
+  }
+  OFX_HIP(hipMemsetAsync(root + n_nodes, 0, 1, hs));
+  hipLaunchKernelGGL(k_cc_roots, gn, dim3(256), 0, hs, (const int32_t*)lab, n_nodes, root);
+  OFX_CHECKS(exclusive_sum_u8(root, rank, n_nodes + 1, hs));
+  if (cluster_sizes) OFX_HIP(hipMemsetAsync(cluster_sizes, 0, n_nodes * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_cc_out, gn, dim3(256), 0, hs, (const int32_t*)lab, (const int32_t*)rank, n_nodes, clusters,
+                     cluster_sizes);
+  OFX_LAUNCH_CHECK();
+  int32_t nc = 0;
+  OFX_CHECKS(read1(rank + n_nodes, &nc, hs));
+  *n_clusters = nc;
+  dfree(lab, hs); dfree(changed, hs); dfree(rank, hs); dfree(root, hs);
+  return OFX_OK;
+}
+
+}  // extern "C"

@@ -111,3 +111,166 @@ def knn_device(points, nodes, k):
     d2 = torch.empty((P, k), dtype=torch.float32, device=pts.device)
     call("ofx_knn_points", ptr(pts), P, ptr(nd), nd.shape[0], int(k), ptr(idx), ptr(d2), stream_ptr())
     return idx, d2
+
+
+# ------------------------------------------------------------------ ED-graph construction (§8(f) row 4)
+class MeshGraph:
+    """Device handle over a mesh (ofx_graph_create): vertex adjacency + the construction entry points.
+    vertices (V,3) f32 / faces (F,3) i32 device tensors stay referenced by the handle."""
+
+    def __init__(self, vertices, faces, device=None):
+        from . import _lib
+        d = _dev(device) if not isinstance(vertices, torch.Tensor) else vertices.device
+        self.vertices = _t(vertices, d, torch.float32).reshape(-1, 3)
+        self.faces = _t(faces, d, torch.int32).reshape(-1, 3)
+        self.device = d
+        self.nv, self.nf = self.vertices.shape[0], self.faces.shape[0]
+        self._h = _lib.c_void_p()
+        call("ofx_graph_create", ptr(self.vertices), self.nv, ptr(self.faces), self.nf, _lib.byref(self._h),
+             stream_ptr())
+
+    def __del__(self):
+        from . import _lib
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.ofx_graph_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def adjacency(self):
+        from . import _lib
+        n = _lib.c_int64()
+        call("ofx_graph_adjacency", self._h, None, None, _lib.byref(n), stream_ptr())
+        rp = torch.empty(self.nv + 1, dtype=torch.int32, device=self.device)
+        col = torch.empty(max(1, n.value), dtype=torch.int32, device=self.device)
+        call("ofx_graph_adjacency", self._h, ptr(rp), ptr(col), _lib.byref(n), stream_ptr())
+        return rp, col[: n.value]
+
+    def erode(self, n_iterations, min_neighbors):
+        m = torch.empty(self.nv, dtype=torch.uint8, device=self.device)
+        call("ofx_erode_mesh", self._h, int(n_iterations), int(min_neighbors), ptr(m), stream_ptr())
+        return m.bool()
+
+    def sample_nodes(self, non_eroded, node_coverage, use_only_non_eroded=True):
+        """-> (node positions (n,3) f32, node vertex indices (n,) i32), ascending vertex order."""
+        from . import _lib
+        ne = None if non_eroded is None else _t(non_eroded, self.device, torch.uint8).reshape(-1)
+        pos = torch.empty((max(1, self.nv), 3), dtype=torch.float32, device=self.device)
+        idx = torch.empty(max(1, self.nv), dtype=torch.int32, device=self.device)
+        n, rounds = _lib.c_int64(), _lib.c_int64()
+        call("ofx_sample_nodes", self._h, ptr(ne), float(node_coverage), 1 if use_only_non_eroded else 0, ptr(pos),
+             ptr(idx), _lib.byref(n), _lib.byref(rounds), stream_ptr())
+        self.sample_rounds = int(rounds.value)
+        return pos[: n.value], idx[: n.value]
+
+    def edges_geodesic(self, node_indices, n_max_neighbors, node_coverage, allow_only_valid_vertices=True,
+                       enforce_total_num_neighbors=True, valid_vertices=None, with_node_to_vertex=False):
+        """-> (edges (N,K) i32, weights (N,K) f32, distances (N,K) f32, node_to_vertex (N,V) f32 or None)."""
+        ni = _t(node_indices, self.device, torch.int32).reshape(-1)
+        N, K = ni.shape[0], int(n_max_neighbors)
+        kw = dict(device=self.device)
+        E = torch.empty((N, K), dtype=torch.int32, **kw)
+        W = torch.empty((N, K), dtype=torch.float32, **kw)
+        D = torch.empty((N, K), dtype=torch.float32, **kw)
+        n2v = torch.empty((N, self.nv), dtype=torch.float32, **kw) if with_node_to_vertex else None
+        vv = None if valid_vertices is None else _t(valid_vertices, self.device, torch.uint8).reshape(-1)
+        call("ofx_edges_geodesic", self._h, ptr(vv), ptr(ni), N, K, float(node_coverage),
+             1 if allow_only_valid_vertices else 0, 1 if enforce_total_num_neighbors else 0, ptr(E), ptr(W), ptr(D),
+             ptr(n2v), stream_ptr())
+        return E, W, D, n2v
+
+
+def edges_euclidean_device(nodes, n_max_neighbors):
+    X = nodes.contiguous().float().reshape(-1, 3)
+    E = torch.empty((X.shape[0], int(n_max_neighbors)), dtype=torch.int32, device=X.device)
+    call("ofx_edges_euclidean", ptr(X), X.shape[0], int(n_max_neighbors), ptr(E), stream_ptr())
+    return E
+
+
+def node_edge_cleanup_device(edges, valid):
+    E = edges.to(torch.int32).contiguous()
+    vin = valid.reshape(-1).to(torch.uint8).contiguous()
+    out = torch.empty_like(vin)
+    call("ofx_node_edge_cleanup", ptr(E), E.shape[0], E.shape[1], ptr(vin), ptr(out), stream_ptr())
+    return out.bool()
+
+
+def clusters_device(edges):
+    """-> (clusters (N,) i32, sizes list)."""
+    from . import _lib
+    E = edges.to(torch.int32).contiguous()
+    N = E.shape[0]
+    cl = torch.empty(max(1, N), dtype=torch.int32, device=E.device)
+    sz = torch.empty(max(1, N), dtype=torch.int32, device=E.device)
+    nc = _lib.c_int32()
+    call("ofx_compute_clusters", ptr(E), N, E.shape[1], ptr(cl), ptr(sz), _lib.byref(nc), stream_ptr())
+    return cl[:N], sz[: nc.value].cpu().tolist()
+
+
+# ---- csrc call shapes (numpy in / numpy out, outputs resized or written in place) ----
+def erode_mesh(vertexPositions, faceIndices, nIterations, minNeighbors, device=None):
+    """NeuralNRT._C.erode_mesh -> non-eroded mask (V,1) bool."""
+    g = MeshGraph(vertexPositions, faceIndices, device)
+    return g.erode(nIterations, minNeighbors).cpu().numpy().reshape(-1, 1)
+
+
+def sample_nodes(vertexPositions, nonErodedVertices, nodePositions, nodeIndices, nodeCoverage,
+                 useOnlyNonErodedIndices=True, randomShuffle=True, device=None):
+    """NeuralNRT._C.sample_nodes: outputs resized to (V,3) / (V,1) with the first n rows filled; returns n.
+    randomShuffle visits the vertices in a random permutation (numpy generator; the reference seeds
+    std::random_device, i.e. it is not reproducible either); EDGraph passes False."""
+    P = np.ascontiguousarray(vertexPositions, np.float32).reshape(-1, 3)
+    ne = np.asarray(nonErodedVertices).reshape(-1).astype(bool)
+    V = P.shape[0]
+    perm = np.random.default_rng().permutation(V) if randomShuffle else None
+    if perm is not None:
+        P, ne = P[perm], ne[perm]
+    g = MeshGraph(P, np.zeros((0, 3), np.int32), device)
+    pos, idx = g.sample_nodes(torch.from_numpy(ne.astype(np.uint8)), nodeCoverage, useOnlyNonErodedIndices)
+    n = pos.shape[0]
+    idx = idx.cpu().numpy()
+    if perm is not None:
+        idx = perm[idx].astype(np.int32)
+    nodePositions.resize((V, 3), refcheck=False)
+    nodeIndices.resize((V, 1), refcheck=False)
+    nodePositions[:n] = pos.cpu().numpy()
+    nodeIndices[:n, 0] = idx
+    return n
+
+
+def compute_edges_geodesic(vertexPositions, validVertices, faceIndices, nodeIndices, nMaxNeighbors, nodeCoverage,
+                           graphEdges, graphEdgesWeights, graphEdgesDistances, nodeToVertexDistances,
+                           allow_only_valid_vertices, enforce_total_num_neighbors, device=None):
+    """NeuralNRT._C.compute_edges_geodesic: writes the four output arrays in place. Rows are fully written
+    (-1 / 0 / 0 past the found neighbours, -1 for unvisited vertices): the values every reference call site
+    pre-fills. Reaching an invalid vertex raises (the C++ calls exit(0))."""
+    g = MeshGraph(vertexPositions, faceIndices, device)
+    vv = np.asarray(validVertices).reshape(g.nv, -1)[:, 0].astype(np.uint8)
+    E, W, D, n2v = g.edges_geodesic(np.asarray(nodeIndices).reshape(-1), nMaxNeighbors, nodeCoverage,
+                                    allow_only_valid_vertices, enforce_total_num_neighbors,
+                                    valid_vertices=torch.from_numpy(vv), with_node_to_vertex=True)
+    graphEdges[...] = E.cpu().numpy()
+    graphEdgesWeights[...] = W.cpu().numpy()
+    graphEdgesDistances[...] = D.cpu().numpy()
+    nodeToVertexDistances[...] = n2v.cpu().numpy()
+
+
+def compute_edges_euclidean(nodePositions, nMaxNeighbors, device=None):
+    """NeuralNRT._C.compute_edges_euclidean -> (N, K) int32."""
+    return edges_euclidean_device(_t(nodePositions, _dev(device), torch.float32), nMaxNeighbors).cpu().numpy()
+
+
+def node_and_edge_clean_up(graph_edges, valid_nodes_mask, device=None):
+    """NeuralNRT._C.node_and_edge_clean_up: valid_nodes_mask (N,1) bool updated in place."""
+    d = _dev(device)
+    out = node_edge_cleanup_device(_t(graph_edges, d, torch.int32), _t(valid_nodes_mask, d, torch.uint8))
+    valid_nodes_mask[...] = out.cpu().numpy().reshape(valid_nodes_mask.shape)
+
+
+def compute_clusters(graph_edges, graph_clusters, device=None):
+    """NeuralNRT._C.compute_clusters: graph_clusters (N,1) i32 written in place; returns the cluster sizes."""
+    cl, sizes = clusters_device(_t(graph_edges, _dev(device), torch.int32))
+    graph_clusters[...] = cl.cpu().numpy().reshape(graph_clusters.shape)
+    return sizes

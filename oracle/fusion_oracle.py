@@ -1093,3 +1093,271 @@ def find_unreachable_nodes(points, nodes, node_coverage):
     if un.size == 0:
         return []
     return un[np.argsort(dist[un], kind="stable")[::-1]]
+
+
+# ----------------------------------------------------------------------------
+# f4: graph construction — csrc graph_proc.cpp:17-481 (erode_mesh, sample_nodes, compute_edges_geodesic,
+#     compute_edges_euclidean, node_and_edge_clean_up, compute_clusters) as called by EDGraph
+#     (embedded_deformation_graph.py:153-380); get_reduced_graph (:382-477)
+# ----------------------------------------------------------------------------
+def _eigen_sqnorm(d):
+    """Eigen 3.3.7 squaredNorm of Vector3f rows: x0 + (x1 + x2) in f32."""
+    s = (d * d).astype(np.float32)
+    return (s[..., 0] + (s[..., 1] + s[..., 2])).astype(np.float32)
+
+
+def erode_mesh(vertices, faces, n_iterations, min_neighbors):
+    """graph_proc.cpp:17-77 -> non-eroded mask (V,1) bool."""
+    V = np.asarray(vertices).shape[0]
+    F = np.asarray(faces, np.int64).reshape(-1, 3)
+    for _ in range(n_iterations):
+        cnt = np.bincount(F.reshape(-1), minlength=V)
+        F = F[(cnt[F] >= min_neighbors).all(1)]
+    m = np.zeros(V, bool)
+    m[F.reshape(-1)] = True
+    return m.reshape(V, 1)
+
+
+def sample_nodes(vertices, non_eroded, node_coverage, use_only_non_eroded=True):
+    """graph_proc.cpp:79-136 with randomShuffle = False (EDGraph's SAMPLE_RANDOM_SHUFFLE,
+    embedded_deformation_graph.py:195): vertices in index order, a vertex becomes a node iff no earlier node
+    lies within squaredNorm <= coverage² (f32). -> (node positions (n,3) f32, node vertex indices (n,1) i32)."""
+    f32 = np.float32
+    P = np.asarray(vertices, f32)
+    valid = np.asarray(non_eroded).reshape(-1).astype(bool)
+    cov2 = f32(f32(node_coverage) * f32(node_coverage))
+    nodes = np.zeros((0, 3), f32)
+    idx = []
+    for v in range(P.shape[0]):
+        if use_only_non_eroded and not valid[v]:
+            continue
+        if nodes.shape[0] and (_eigen_sqnorm(P[v][None, :] - nodes) <= cov2).any():
+            continue
+        nodes = np.concatenate([nodes, P[v][None, :]])
+        idx.append(v)
+    return nodes, np.array(idx, np.int32).reshape(-1, 1)
+
+
+def _lt_push(h, hole, top, val):
+    """libstdc++ std::__push_heap with CustomCompare (a.dist > b.dist: a min-heap on distance)."""
+    parent = (hole - 1) // 2
+    while hole > top and h[parent][1] > val[1]:
+        h[hole] = h[parent]
+        hole = parent
+        parent = (hole - 1) // 2
+    h[hole] = val
+
+
+def _heap_push(h, val):
+    h.append(val)
+    _lt_push(h, len(h) - 1, 0, val)
+
+
+def _heap_pop(h):
+    """std::pop_heap + pop_back (libstdc++ __pop_heap / __adjust_heap)."""
+    top = h[0]
+    n = len(h) - 1
+    if n > 0:
+        val = h[n]
+        h[n] = h[0]
+        hole, second = 0, 0
+        while second < (n - 1) // 2:
+            second = 2 * (second + 1)
+            if h[second][1] > h[second - 1][1]:
+                second -= 1
+            h[hole] = h[second]
+            hole = second
+        if (n & 1) == 0 and second == (n - 2) // 2:
+            second = 2 * (second + 1)
+            h[hole] = h[second - 1]
+            hole = second - 1
+        _lt_push(h, hole, 0, val)
+    h.pop()
+    return top
+
+
+def vertex_neighbors(faces, V):
+    nb = [set() for _ in range(V)]
+    for f in np.asarray(faces).reshape(-1, 3):
+        a, b, c = (int(x) for x in f)
+        nb[a].update((b, c)); nb[b].update((a, c)); nb[c].update((a, b))
+    for i in range(V):
+        nb[i].discard(i)
+    return [sorted(s) for s in nb]
+
+
+def compute_edges_geodesic(vertices, valid_vertices, faces, node_indices, n_max_neighbors, node_coverage,
+                           allow_only_valid_vertices=True, enforce_total_num_neighbors=True):
+    """graph_proc.cpp:155-300: per node a Dijkstra over the mesh (std::priority_queue semantics restated
+    exactly, neighbours in ascending id) collecting the first n_max_neighbors other nodes reached.
+    -> (edges (N,K) i32 -1-padded, weights (N,K) f32, distances (N,K) f32, node_to_vertex (N,V) f32 -1)."""
+    f32 = np.float32
+    P = np.asarray(vertices, f32)
+    V = P.shape[0]
+    valid = np.asarray(valid_vertices).reshape(V, -1)[:, 0].astype(bool)
+    ni = np.asarray(node_indices).reshape(-1)
+    N = ni.shape[0]
+    K = n_max_neighbors
+    nb = vertex_neighbors(faces, V)
+    v2n = -np.ones(V, np.int64)
+    for n in range(N):
+        if ni[n] >= 0:
+            v2n[ni[n]] = n
+    max_inf = f32(2.0 * f32(node_coverage))
+    E = -np.ones((N, K), np.int32)
+    EW = np.zeros((N, K), f32)
+    ED = np.zeros((N, K), f32)
+    D = -np.ones((N, V), f32)
+    for n in range(N):
+        s = int(ni[n])
+        if s < 0:
+            continue
+        h = [(s, f32(0))]
+        visited = set()
+        ids, ds = [], []
+        while h:
+            v, d = _heap_pop(h)
+            if v in visited:
+                continue
+            if allow_only_valid_vertices and not valid[v]:
+                raise RuntimeError("compute_edges_geodesic: visited an invalid vertex (the C++ calls exit(0))")
+            m = v2n[v]
+            if m >= 0 and m != n:
+                ids.append(int(m)); ds.append(d)
+                if len(ids) >= K:
+                    break
+            D[n, v] = d
+            visited.add(v)
+            for u in nb[v]:
+                if allow_only_valid_vertices and not valid[u]:
+                    continue
+                dist = f32(d + np.sqrt(_eigen_sqnorm((P[v] - P[u])[None, :])[0]))
+                if enforce_total_num_neighbors or dist <= max_inf:
+                    _heap_push(h, (u, dist))
+        if ids:
+            dd = np.array(ds, f32)
+            two_c2 = f32(f32(2.0 * f32(node_coverage)) * f32(node_coverage))
+            w = exp_f32(-(dd * dd) / two_c2)
+            tot = f32(0)
+            for x in w:
+                tot = f32(tot + x)
+            w = w / tot if tot > 0 else w / f32(len(ids))      # graph_proc.cpp:270-281 (w / n, not 1 / n)
+            E[n, :len(ids)] = ids
+            EW[n, :len(ids)] = w
+            ED[n, :len(ids)] = ds
+    return E, EW, ED, D
+
+
+def compute_edges_euclidean(nodes, n_max_neighbors):
+    """graph_proc.cpp:302-356: K nearest other nodes, csrc list semantics (ties: later id first), -1 padded."""
+    f32 = np.float32
+    X = np.asarray(nodes, f32)
+    N = X.shape[0]
+    E = -np.ones((N, n_max_neighbors), np.int32)
+    ids = np.arange(N)
+    for n in range(N):
+        d2 = _eigen_sqnorm(X[n][None, :] - X)
+        o = [i for i in np.lexsort((-ids, d2)) if i != n][:n_max_neighbors]
+        E[n, :len(o)] = o
+    return E
+
+
+def node_and_edge_clean_up(graph_edges, valid_nodes_mask):
+    """graph_proc.cpp:388-438 (in place on a copy): sweeps in node order until no removal; a node with <= 1
+    neighbour not removed BY THIS CALL is removed (neighbours invalid on entry still count)."""
+    E = np.asarray(graph_edges)
+    valid = np.array(valid_nodes_mask, bool).reshape(-1, 1).copy()
+    removed = set()
+    while True:
+        k = 0
+        for n in range(E.shape[0]):
+            if not valid[n, 0]:
+                continue
+            c = 0
+            for j in E[n]:
+                if j == -1:
+                    break
+                if int(j) in removed:
+                    continue
+                c += 1
+            if c <= 1:
+                valid[n, 0] = False
+                removed.add(n)
+                k += 1
+        if k == 0:
+            return valid
+
+
+def compute_clusters(graph_edges):
+    """graph_proc.cpp:440-481: connected components of the symmetrised edge graph, numbered by their lowest
+    node id -> (clusters (N,1) i32, sizes list)."""
+    E = np.asarray(graph_edges)
+    N = E.shape[0]
+    nb = [set() for _ in range(N)]
+    for n in range(N):
+        for j in E[n]:
+            if j == -1:
+                break
+            nb[n].add(int(j)); nb[int(j)].add(n)
+    cl = -np.ones(N, np.int32)
+    sizes = []
+    for s in range(N):
+        if cl[s] != -1:
+            continue
+        stack, size = [s], 0
+        cl[s] = len(sizes)
+        while stack:
+            a = stack.pop()
+            size += 1
+            for b in nb[a]:
+                if cl[b] == -1:
+                    cl[b] = len(sizes)
+                    stack.append(b)
+        sizes.append(size)
+    return cl.reshape(N, 1), sizes
+
+
+def reduced_graph(nodes, edges, edges_weights, edges_distances, clusters, valid_nodes_mask):
+    """EDGraph.get_reduced_graph (embedded_deformation_graph.py:382-477): keep valid nodes, drop edges to
+    removed nodes (compacted left, ids remapped) and renormalise the weights by (sum + 1e-6) in f32."""
+    m = np.asarray(valid_nodes_mask).reshape(-1).astype(bool)
+    nodes_r, E = nodes[m].copy(), edges[m].copy()
+    W, Dd, C = edges_weights[m].copy(), edges_distances[m].copy(), clusters[m].copy()
+    black = np.nonzero(~m)[0]
+    if black.size:
+        new_id = np.cumsum(m) - 1
+        for r in range(E.shape[0]):
+            e, w, d = E[r].copy(), W[r].copy(), Dd[r].copy()
+            keep = ~np.isin(e, black)
+            E[r], W[r], Dd[r] = -1, 0, 0
+            c = 0
+            for j in np.nonzero(keep)[0]:
+                E[r, c] = -1 if e[j] == -1 else new_id[e[j]]
+                W[r, c], Dd[r, c] = w[j], d[j]
+                c += 1
+            s = _np_sum_f32(W[r])
+            if s > 0:        # numpy 1.26 (environment.yml:94): f32 scalar + 1e-6 is f64, cast back for the division
+                W[r] /= np.float32(np.float64(s) + 1e-6)
+    return nodes_r, E, W, Dd, C
+
+
+def _np_sum_f32(a):
+    """numpy's pairwise float32 sum of a short contiguous row (< 8: in order; 8..128: 8 partial sums)."""
+    a = np.asarray(a, np.float32)
+    f32 = np.float32
+    n = a.shape[0]
+    if n < 8:
+        s = f32(0)
+        for x in a:
+            s = f32(s + x)
+        return s
+    r = [f32(x) for x in a[:8]]
+    i = 8
+    while i + 8 <= n:
+        for j in range(8):
+            r[j] = f32(r[j] + a[i + j])
+        i += 8
+    s = f32(f32(f32(r[0] + r[1]) + f32(r[2] + r[3])) + f32(f32(r[4] + r[5]) + f32(r[6] + r[7])))
+    for x in a[i:]:
+        s = f32(s + x)
+    return s

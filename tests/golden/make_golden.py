@@ -10,6 +10,11 @@
   anchors_csrc.npz    — compute_pixel_anchors_euclidean / _geodesic and update_pixel_anchors outputs of the
                         REFERENCE's compiled C++ (csrc/cpu/graph_proc.cpp:483-709,934-961): a point image with
                         duplicated nodes (distance ties) and a node->vertex distance matrix with ties and -1s.
+  graph_csrc.npz      — ED-graph construction by the REFERENCE's compiled C++ (graph_proc.cpp:17-481) on two
+                        meshes (a depth mesh of the synthetic frame and an exact grid plane, whose equal edge
+                        lengths tie the Dijkstra priority queue): erode_mesh, sample_nodes (no shuffle),
+                        compute_edges_geodesic in the three modes EDGraph uses, node_and_edge_clean_up,
+                        compute_clusters, compute_edges_euclidean.
   gn_small.npz        — one DeformNet.optimize solve (N≈100, M=600) by the dense f64 oracle.
   frontend_csrc.npz   — backproject_depth_float / _ushort and compute_mesh_from_depth outputs of the
                         REFERENCE's compiled C++ (csrc/cpu/image_proc.cpp:351-545) on a synthetic frame,
@@ -153,6 +158,70 @@ def make_anchors_csrc():
           int((ga.reshape(-1, 4)[:, 0] >= 0).sum()), "geodesic pixels")
 
 
+def _graph_case(m, verts, faces, cov, K, out, tag):
+    V = verts.shape[0]
+    ne = m.erode_mesh(verts, faces, 1, 3)
+    npos, nidx = np.zeros((0,), np.float32), np.zeros((0,), np.int32)
+    n = m.sample_nodes(verts, ne, npos, nidx, cov, True, False)
+    npos, nidx = npos[:n], nidx[:n]
+    modes = {"valid_enforce": (True, True), "all_enforce": (False, True), "valid_prune": (True, False)}
+    for name, (only_valid, enforce) in modes.items():
+        E = -np.ones((n, K), np.int32)
+        W = np.zeros((n, K), np.float32)
+        Dd = np.zeros((n, K), np.float32)
+        D = -np.ones((n, V), np.float32)
+        vis = np.ones((V, 1), bool)
+        m.compute_edges_geodesic(verts, vis, faces, nidx, K, cov, E, W, Dd, D, only_valid, enforce)
+        out[f"{tag}_{name}_edges"], out[f"{tag}_{name}_weights"] = E, W
+        out[f"{tag}_{name}_dists"], out[f"{tag}_{name}_n2v"] = Dd, D
+    E = out[f"{tag}_valid_enforce_edges"]
+    valid = np.ones((n, 1), bool)
+    m.node_and_edge_clean_up(E, valid)
+    cl = -np.ones((n, 1), np.int32)
+    sizes = m.compute_clusters(E, cl)
+    out.update({f"{tag}_verts": verts, f"{tag}_faces": faces, f"{tag}_cov": cov, f"{tag}_K": K,
+                f"{tag}_non_eroded": ne, f"{tag}_nodes": npos, f"{tag}_node_indices": nidx,
+                f"{tag}_cleanup_valid": valid, f"{tag}_clusters": cl, f"{tag}_cluster_sizes": np.array(sizes, np.int32),
+                f"{tag}_euclid_edges": m.compute_edges_euclidean(npos, K)})
+    print(f"graph_csrc[{tag}]:", V, "verts,", faces.shape[0], "faces,", n, "nodes,", int(valid.sum()), "kept,",
+          len(sizes), "clusters")
+
+
+def make_graph_csrc():
+    from oracle.build_ref import build
+    m = build()
+    f = np.load(os.path.join(HERE, "frontend_csrc.npz"), allow_pickle=False)
+    out = {}
+    _graph_case(m, f["mesh0_vertices"], f["mesh0_faces"], 0.05, 8, out, "depth")
+    # exact grid plane (0.01 spacing) with a hole: massive distance ties in the priority queue
+    H, W = 36, 44
+    yy, xx = np.mgrid[0:H, 0:W]
+    P = np.stack([xx * np.float32(0.01), yy * np.float32(0.01), np.ones((H, W))]).astype(np.float32)
+    P[:, 10:16, 12:20] = 0
+    v = np.zeros((0,), np.float32)
+    px = np.zeros((0,), np.int32)
+    fc = np.zeros((0,), np.int32)
+    m.compute_mesh_from_depth(P, 0.05, v, px, fc)
+    _graph_case(m, v.reshape(-1, 3), fc.reshape(-1, 3), 0.045, 8, out, "grid")
+    # clean-up / clusters on a sparse random graph: chains of removals, nodes invalid on entry, islands
+    rng = np.random.default_rng(23)
+    n, K = 300, 8
+    E = -np.ones((n, K), np.int32)
+    for i in range(n):
+        deg = int(rng.choice([0, 1, 1, 2, 2, 3, 4, 8]))
+        nb = rng.choice(np.setdiff1d(np.arange(max(0, i - 6), min(n, i + 7)), [i]), min(deg, 12), replace=False)
+        E[i, :len(nb)] = nb
+    valid0 = (rng.random((n, 1)) > 0.1)
+    valid = valid0.copy()
+    m.node_and_edge_clean_up(E, valid)
+    cl = -np.ones((n, 1), np.int32)
+    sizes = m.compute_clusters(E, cl)
+    out.update(rand_edges=E, rand_valid_in=valid0, rand_valid_out=valid, rand_clusters=cl,
+               rand_cluster_sizes=np.array(sizes, np.int32))
+    print("graph_csrc[rand]:", int(valid0.sum()), "->", int(valid.sum()), "valid,", len(sizes), "clusters")
+    np.savez_compressed(os.path.join(HERE, "graph_csrc.npz"), **out)
+
+
 def make_integrate_small():
     cam, scene, d0, d1, pts, nodes, edges, ew = small_setup()
     origin = np.array([-0.40, -0.33, 0.95], np.float32)
@@ -200,13 +269,15 @@ def make_gn_small():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["skin", "frontend", "anchors", "integrate", "gn"]
+    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn"]
     if "skin" in which:
         make_skin_csrc()
     if "frontend" in which:
         make_frontend_csrc()
     if "anchors" in which:
         make_anchors_csrc()
+    if "graph" in which:
+        make_graph_csrc()
     if "integrate" in which:
         make_integrate_small()
     if "gn" in which:

@@ -421,3 +421,51 @@ def test_oracle_find_unreachable_nodes():
     un = fo.find_unreachable_nodes(pts, nodes, 0.1)       # 2·coverage = 0.2
     assert list(un) == [3, 4, 1, 2]                       # descending distance; ties: later index first
     assert fo.find_unreachable_nodes(pts[:1], nodes, 0.1) == []
+
+
+# ---------------- f4: graph construction (csrc graph_proc.cpp:17-481) ----------------
+@pytest.fixture(scope="module")
+def graph_golden(golden_dir):
+    return np.load(os.path.join(golden_dir, "graph_csrc.npz"), allow_pickle=False)
+
+
+@pytest.mark.parametrize("tag", ["depth", "grid"])
+def test_oracle_graph_construction_matches_csrc(graph_golden, tag):
+    g = graph_golden
+    V, F = g[f"{tag}_verts"], g[f"{tag}_faces"]
+    cov, K = float(g[f"{tag}_cov"]), int(g[f"{tag}_K"])
+    ne = fo.erode_mesh(V, F, 1, 3)
+    assert np.array_equal(ne, g[f"{tag}_non_eroded"])
+    nodes, idx = fo.sample_nodes(V, ne, cov)
+    assert np.array_equal(nodes, g[f"{tag}_nodes"]) and np.array_equal(idx, g[f"{tag}_node_indices"])
+    modes = {"valid_enforce": (True, True), "all_enforce": (False, True), "valid_prune": (True, False)}
+    if tag == "depth":
+        modes = {"valid_prune": modes["valid_prune"]}      # keep the CPU suite fast; all modes run on the grid
+    for name, (only_valid, enforce) in modes.items():
+        E, W, D, N2V = fo.compute_edges_geodesic(V, np.ones((V.shape[0], 1), bool), F, idx, K, cov, only_valid, enforce)
+        assert np.array_equal(E, g[f"{tag}_{name}_edges"]), name
+        assert np.array_equal(D, g[f"{tag}_{name}_dists"]), name
+        assert np.array_equal(N2V, g[f"{tag}_{name}_n2v"]), name
+        ref = g[f"{tag}_{name}_weights"]
+        assert np.abs(W.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64)).max() <= 4, name
+    assert np.array_equal(fo.compute_edges_euclidean(nodes, K), g[f"{tag}_euclid_edges"])
+    E = g[f"{tag}_valid_enforce_edges"]
+    assert np.array_equal(fo.node_and_edge_clean_up(E, np.ones((E.shape[0], 1), bool)), g[f"{tag}_cleanup_valid"])
+    cl, sizes = fo.compute_clusters(E)
+    assert np.array_equal(cl, g[f"{tag}_clusters"]) and list(sizes) == list(g[f"{tag}_cluster_sizes"])
+
+
+def test_oracle_cleanup_and_clusters_match_csrc(graph_golden):
+    g = graph_golden
+    assert np.array_equal(fo.node_and_edge_clean_up(g["rand_edges"], g["rand_valid_in"]), g["rand_valid_out"])
+    cl, sizes = fo.compute_clusters(g["rand_edges"])
+    assert np.array_equal(cl, g["rand_clusters"]) and list(sizes) == list(g["rand_cluster_sizes"])
+
+
+def test_oracle_libstdcxx_heap_order():
+    # equal priorities pop in the order libstdc++'s push_heap / __adjust_heap leave them (not FIFO)
+    h = []
+    for v, d in [(0, 1.0), (1, 1.0), (2, 0.5), (3, 1.0), (4, 1.0), (5, 0.5)]:
+        fo._heap_push(h, (v, np.float32(d)))
+    order = [fo._heap_pop(h)[0] for _ in range(6)]
+    assert order[:2] in ([2, 5], [5, 2]) and sorted(order[2:]) == [0, 1, 3, 4]

@@ -47,6 +47,7 @@
  *   ofx_node_edge_cleanup   csrc node_and_edge_clean_up                     csrc/cpu/graph_proc.cpp:388-438
  *   ofx_compute_clusters    csrc compute_clusters                           csrc/cpu/graph_proc.cpp:440-481
  *                           (callers: EDGraph, fusion_with_occlusion/embedded_deformation_graph.py:153-380,496-609)
+ *   ofx_reduce_graph        EDGraph.get_reduced_graph                       embedded_deformation_graph.py:382-477
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
  *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
@@ -280,6 +281,15 @@ int ofx_node_edge_cleanup(const int32_t* graph_edges, int32_t n_nodes, int32_t m
 /* clusters i32[N]; cluster_sizes i32[N] capacity (may be NULL); *n_clusters (host) */
 int ofx_compute_clusters(const int32_t* graph_edges, int32_t n_nodes, int32_t max_neighbors, int32_t* clusters,
                          int32_t* cluster_sizes, int32_t* n_clusters, ofx_stream_t s);
+
+/* get_reduced_graph: keep the nodes with valid_nodes_mask (u8[N]) in order; edges to removed nodes are
+ * dropped (compacted left, ids remapped) and the weights renormalised by f32(f64(np.sum) + 1e-6) as numpy 1.26
+ * evaluates it; if no node is removed the rows are copied unchanged. clusters / clusters_out may be NULL.
+ * Outputs sized for N rows; *n_kept (host). */
+int ofx_reduce_graph(const uint8_t* valid_nodes_mask, int32_t n_nodes, int32_t max_neighbors, const float* nodes,
+                     const int32_t* edges, const float* edges_weights, const float* edges_distances,
+                     const int32_t* clusters, float* nodes_out, int32_t* edges_out, float* weights_out,
+                     float* distances_out, int32_t* clusters_out, int32_t* n_kept, ofx_stream_t s);
 
 /* ---------------- Gauss-Newton (DeformNet.optimize) ---------------- */
 typedef struct ofx_gn_params {

@@ -88,6 +88,7 @@ _SIGS = {
     "ofx_edges_euclidean": [P, c_int32, c_int32, P, P],
     "ofx_node_edge_cleanup": [P, c_int32, c_int32, P, P, P],
     "ofx_compute_clusters": [P, c_int32, c_int32, P, P, P, P],
+    "ofx_reduce_graph": [P, c_int32, c_int32, P, P, P, P, P, P, P, P, P, P, P, P],
     "ofx_gn_create": [c_int32, c_int32, P],
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],

@@ -869,3 +869,96 @@ int ofx_compute_clusters(const int32_t* graph_edges, int32_t n_nodes, int32_t ma
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ get_reduced_graph
+namespace ofx {
+
+// numpy's float32 np.sum of a contiguous row of n <= 16 (pairwise_sum: < 8 in order, else 8 partials)
+__device__ __forceinline__ float np_sum_f32(const float* a, int n) {
+  if (n < 8) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += a[i];
+    return s;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i + 8 <= n; i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) s += a[i];
+  return s;
+}
+
+// one thread per kept node (embedded_deformation_graph.py:382-477)
+__global__ __launch_bounds__(256) void k_reduce_graph(const uint8_t* __restrict__ valid, const int32_t* __restrict__ new_id,
+                                                      int n_nodes, int K, const float* __restrict__ nodes,
+                                                      const int32_t* __restrict__ E, const float* __restrict__ W,
+                                                      const float* __restrict__ D, const int32_t* __restrict__ C,
+                                                      int any_removed, float* __restrict__ nodes_o, int32_t* __restrict__ E_o,
+                                                      float* __restrict__ W_o, float* __restrict__ D_o,
+                                                      int32_t* __restrict__ C_o) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes || !valid[n]) return;
+  const int r = new_id[n];
+  for (int c = 0; c < 3; ++c) nodes_o[3 * (int64_t)r + c] = nodes[3 * (int64_t)n + c];
+  if (C_o) C_o[r] = C ? C[n] : -1;
+  float w[16];
+  int c = 0;
+  for (int i = 0; i < K; ++i) { E_o[(int64_t)r * K + i] = -1; w[i] = 0.f; D_o[(int64_t)r * K + i] = 0.f; }
+  for (int i = 0; i < K; ++i) {
+    const int32_t j = E[(int64_t)n * K + i];
+    if (!any_removed) {
+      E_o[(int64_t)r * K + i] = j;
+      w[i] = W[(int64_t)n * K + i];
+      D_o[(int64_t)r * K + i] = D[(int64_t)n * K + i];
+      continue;
+    }
+    if (j >= 0 && j < n_nodes && !valid[j]) continue;          // neighbour on the black list: dropped
+    E_o[(int64_t)r * K + c] = (j == -1) ? -1 : new_id[j];
+    w[c] = W[(int64_t)n * K + i];
+    D_o[(int64_t)r * K + c] = D[(int64_t)n * K + i];
+    ++c;
+  }
+  if (any_removed) {
+    const float s = np_sum_f32(w, K);
+    // numpy 1.26 (environment.yml:94): f32 scalar + 1e-6 promotes to f64, the in-place f32 division casts back
+    if (s > 0.f) {
+      const float den = (float)((double)s + 1e-6);
+      for (int i = 0; i < K; ++i) w[i] = (float)((double)w[i] / (double)den);
+    }
+  }
+  for (int i = 0; i < K; ++i) W_o[(int64_t)r * K + i] = w[i];
+}
+
+}  // namespace ofx
+
+extern "C" int ofx_reduce_graph(const uint8_t* valid_nodes_mask, int32_t n_nodes, int32_t max_neighbors,
+                                const float* nodes, const int32_t* edges, const float* edges_weights,
+                                const float* edges_distances, const int32_t* clusters, float* nodes_out,
+                                int32_t* edges_out, float* weights_out, float* distances_out, int32_t* clusters_out,
+                                int32_t* n_kept, ofx_stream_t s) {
+  using namespace ofx;
+  OFX_CHECK_ARG(n_nodes >= 0 && max_neighbors >= 1 && max_neighbors <= 16 && n_kept, "bad arguments");
+  *n_kept = 0;
+  if (n_nodes == 0) return OFX_OK;
+  OFX_CHECK_ARG(valid_nodes_mask && nodes && edges && edges_weights && edges_distances && nodes_out && edges_out &&
+                    weights_out && distances_out, "null buffer");
+  hipStream_t hs = as_stream(s);
+  int32_t* new_id = nullptr;
+  OFX_CHECKS(dalloc(&new_id, n_nodes + 1, hs));
+  OFX_CHECKS(exclusive_sum_u8(valid_nodes_mask, new_id, n_nodes, hs));
+  int32_t last = 0;
+  uint8_t lastv = 0;
+  OFX_HIP(hipMemcpyAsync(&last, new_id + n_nodes - 1, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipMemcpyAsync(&lastv, valid_nodes_mask + n_nodes - 1, 1, hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipStreamSynchronize(hs));
+  const int32_t kept = last + (lastv ? 1 : 0);
+  *n_kept = kept;
+  hipLaunchKernelGGL(k_reduce_graph, dim3(grid_for(n_nodes, 256)), dim3(256), 0, hs, valid_nodes_mask,
+                     (const int32_t*)new_id, n_nodes, max_neighbors, nodes, edges, edges_weights, edges_distances,
+                     clusters, kept < n_nodes ? 1 : 0, nodes_out, edges_out, weights_out, distances_out, clusters_out);
+  OFX_LAUNCH_CHECK();
+  dfree(new_id, hs);
+  return OFX_OK;
+}

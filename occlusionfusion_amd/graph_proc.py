@@ -12,6 +12,7 @@ rounded exp; tests/test_gpu_anchors.py). There is no CPU fallback.
 import numpy as np
 import torch
 
+from . import _lib
 from ._lib import call, ptr, stream_ptr
 
 GRAPH_K = 4   # csrc/cpu/graph_proc.h:8
@@ -130,7 +131,6 @@ class MeshGraph:
              stream_ptr())
 
     def __del__(self):
-        from . import _lib
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             try:

@@ -302,3 +302,49 @@ class Registration:
                "valid_solve": out["valid_solve"],
                "source_frame_id": optical_flow_data["source_id"], "target_frame_id": optical_flow_data["target_id"]}
         return res
+
+
+def run_arap(solver, reduced_graph_dict, model_data, graph, log=None):
+    """run_model.py:448-627 (Model.run_arap): initialise every invalid node from its highest-weight already-
+    updated graph neighbour (queue ordered by the number of valid neighbours, descending), then the device
+    DeformNet.arap GN (GaussNewtonSolver.arap) on all nodes. Returns node_rotations (N,3,3), node_translations
+    (N,3), deformed_nodes_to_target (N,3), source/target frame ids, convergence_info, valid_solve.
+    np.argsort's tie order in the reference is unspecified (quicksort); here it is stable."""
+    for k in ("node_rotations", "node_translations", "deformed_nodes_to_target"):
+        assert np.asarray(model_data[k]).dtype == np.float32, f"model_data[{k}] not np.float32"
+    valid = np.asarray(reduced_graph_dict["valid_nodes_mask"]).reshape(-1).astype(bool)
+    N = len(graph.nodes)
+    assert len(valid) == N, f"Valid nodes not from current graph. Expected:{N} got:{len(valid)}"
+    R = np.tile(np.eye(3, dtype=np.float32)[None], (N, 1, 1))
+    T = np.zeros((N, 3), np.float32)
+    R[valid] = model_data["node_rotations"]
+    T[valid] = model_data["node_translations"]
+    invalid = np.where(~valid)[0]
+    n_edges = np.sum(graph.edges != -1, axis=1)
+    vis = [np.sum(valid[graph.edges[n, :n_edges[n]]]) for n in invalid]
+    queue = list(invalid[np.argsort(vis, kind="stable")[::-1]])
+    g = np.asarray(reduced_graph_dict["all_nodes_at_source"], np.float32)
+    updated = valid.copy()
+    while updated.sum() < N:
+        L = len(queue)
+        for i in range(L):
+            ind = queue[i]
+            nb = graph.edges[ind, :n_edges[ind]]
+            cand = np.where(updated[nb])[0]
+            if len(cand) == 0:
+                queue.append(ind)
+                continue
+            c = graph.edges[ind, cand[np.argmax(graph.edges_weights[ind, cand])]]
+            R[ind] = R[c]
+            T[ind] = R[ind] @ (g[ind] - g[c]) + T[c] + g[c] - g[ind]
+            updated[ind] = True
+        del queue[:L]
+        if len(queue) == 0 or len(queue) == L:
+            break
+    res = solver.arap(g, reduced_graph_dict["valid_nodes_at_source"], model_data["deformed_nodes_to_target"], valid, g,
+                      graph.edges, graph.edges_weights, graph.clusters, R, T)
+    out = {k: (v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in res.items()}
+    out["deformed_nodes_to_target"] = g + out["node_translations"]
+    out["source_frame_id"] = model_data.get("source_frame_id")
+    out["target_frame_id"] = model_data.get("target_frame_id")
+    return out

@@ -17,24 +17,220 @@ from ._lib import call, ptr, stream_ptr, byref
 log = logging.getLogger(__name__)
 
 
+DEFAULT_GRAPH_PARAMETERS = {   # embedded_deformation_graph.py:60-69 (graph_config.json defaults)
+    "max_triangle_distance": 0.05, "erosion_num_iterations": 1, "erosion_min_neighbours": 3,
+    "node_coverage": 0.05, "min_neighbours": 2, "num_neighbours": 8, "require_mask": True}
+
+
 class EDGraph:
-    """Embedded-deformation graph state (embedded_deformation_graph.py:26-52,241-256): nodes (N,3) f32,
-    edges (N,8) i32 (-1 padded), edges_weights (N,8) f32, clusters (N,1) i32, generation parameters.
-    Construction from a mesh (csrc erode/sample/geodesic edges) is outside this hot path."""
+    """Embedded-deformation graph (embedded_deformation_graph.py:26-741): nodes (N,3) f32, edges (N,K) i32
+    (-1 padded), edges_weights / edges_distances (N,K) f32, clusters (N,1) i32, node_indices (N,1) and the
+    graph_generation_parameters dict. Built either from given arrays (the hot-path state) or from a mesh /
+    a TSDFVolume (EDGraph.from_mesh / from_tsdf) with the device graph-construction kernels (graph_proc)."""
 
     def __init__(self, nodes, edges, edges_weights=None, clusters=None, node_coverage=0.05, graph_neighbours=8):
+        self.log = log
         self.nodes = np.ascontiguousarray(nodes, np.float32)
         self.edges = np.ascontiguousarray(edges, np.int32)
         N = self.nodes.shape[0]
         self.edges_weights = (np.ascontiguousarray(edges_weights, np.float32) if edges_weights is not None
                               else np.where(self.edges >= 0, 1.0 / max(1, self.edges.shape[1]), 0).astype(np.float32))
+        self.edges_distances = np.zeros(self.edges.shape, np.float32)
         self.clusters = (np.asarray(clusters, np.int32).reshape(N, 1) if clusters is not None
                          else np.zeros((N, 1), np.int32))
+        self.node_indices = -np.ones((N, 1), np.int32)
         self.num_nodes = N
-        self.graph_generation_parameters = {"node_coverage": float(node_coverage),
-                                            "graph_neighbours": int(graph_neighbours),
-                                            "max_triangle_distance": 0.05, "erosion_num_iterations": 10,
-                                            "erosion_min_neighbours": 4}
+        self.graph_generation_parameters = dict(DEFAULT_GRAPH_PARAMETERS, node_coverage=float(node_coverage),
+                                                num_neighbours=int(graph_neighbours), graph_neighbours=int(graph_neighbours),
+                                                erosion_num_iterations=10, erosion_min_neighbours=4)
+
+    # ---------------------------------------------------------------- construction (SURVEY §8(f) row 4)
+    @classmethod
+    def from_mesh(cls, vertices, faces, graph_generation_parameters=None, device=None, with_pyramid=False):
+        """create_graph_from_mesh (embedded_deformation_graph.py:174-256) on the device."""
+        g = cls.__new__(cls)
+        g.log = log
+        g.graph_generation_parameters = dict(DEFAULT_GRAPH_PARAMETERS, **(graph_generation_parameters or {}))
+        g.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        g.create_graph_from_mesh(vertices, faces, with_pyramid=with_pyramid)
+        return g
+
+    @classmethod
+    def from_tsdf(cls, tsdf, graph_generation_parameters=None, with_pyramid=False):
+        """create_graph_from_tsdf (embedded_deformation_graph.py:80-86): graph of the TSDF's marching-cubes mesh."""
+        g = cls.from_mesh(*tsdf.get_mesh()[:2], graph_generation_parameters, tsdf.device, with_pyramid)
+        g.tsdf = tsdf
+        tsdf.graph = g
+        return g
+
+    def erode_mesh(self, vertices, faces, num_iterations=-1):
+        """embedded_deformation_graph.py:153-172 — any non-zero num_iterations is replaced by the configured
+        erosion_num_iterations (the reference's `if num_iterations:`). -> non-eroded mask (V,1) bool."""
+        from .graph_proc import MeshGraph
+        if num_iterations:
+            num_iterations = self.graph_generation_parameters["erosion_num_iterations"]
+        mg = MeshGraph(vertices, faces, getattr(self, "device", None))
+        return mg.erode(num_iterations, self.graph_generation_parameters["erosion_min_neighbours"]).cpu().numpy()[:, None]
+
+    def create_graph_from_mesh(self, vertices, faces, with_pyramid=False):
+        from .graph_proc import MeshGraph
+        p = self.graph_generation_parameters
+        cov, K = float(p["node_coverage"]), int(p["num_neighbours"])
+        mg = MeshGraph(vertices, faces, getattr(self, "device", None))
+        assert mg.nv > 0 and mg.nf > 0
+        ne = mg.erode(p["erosion_num_iterations"], p["erosion_min_neighbours"])   # erode_mesh(num_iterations=-1)
+        pos, idx = mg.sample_nodes(ne, cov, True)
+        E, W, D, _ = mg.edges_geodesic(idx, K, cov, True, True)                      # visible_vertices = all ones
+        self._mesh = mg
+        self.vertices = mg.vertices.cpu().numpy()
+        self.faces = mg.faces.cpu().numpy()
+        self.nodes = pos.cpu().numpy()
+        self.node_indices = idx.cpu().numpy().reshape(-1, 1)
+        self.edges, self.edges_weights, self.edges_distances = E.cpu().numpy(), W.cpu().numpy(), D.cpu().numpy()
+        self.clusters = -np.ones((self.edges.shape[0], 1), np.int32)
+        self.remove_nodes_with_not_enough_neighbours()
+        self.compute_clusters()
+        if with_pyramid:
+            self.create_graph_pyramid()
+
+    def remove_nodes_with_not_enough_neighbours(self):
+        """embedded_deformation_graph.py:330-369 (node_and_edge_clean_up + get_reduced_graph)."""
+        from .graph_proc import node_edge_cleanup_device
+        dev = self._dev()
+        E = torch.from_numpy(self.edges).to(dev)
+        valid = node_edge_cleanup_device(E, torch.ones(E.shape[0], dtype=torch.bool, device=dev))
+        r = self.get_reduced_graph(valid.cpu().numpy().reshape(-1, 1))
+        self.nodes, self.edges = r["valid_nodes_at_source"], r["graph_edges"]
+        self.edges_weights, self.edges_distances = r["graph_edges_weights"], r["graph_edges_distances"]
+        self.clusters, self.num_nodes = r["graph_clusters"], int(r["num_nodes"])
+        self.node_indices = self.node_indices[r["valid_nodes_mask"].reshape(-1)]
+
+    def _dev(self):
+        return getattr(self, "device", None) or torch.device("cuda", torch.cuda.current_device())
+
+    def get_reduced_graph(self, valid_nodes_mask):
+        """embedded_deformation_graph.py:382-477 on the device (ofx_reduce_graph)."""
+        dev = self._dev()
+        m = np.asarray(valid_nodes_mask).reshape(-1).astype(bool)
+        N, K = self.edges.shape
+        kw = dict(device=dev)
+        vm = torch.from_numpy(m.astype(np.uint8)).to(dev)
+        src = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
+               (self.nodes, self.edges, self.edges_weights, self.edges_distances, self.clusters.reshape(-1))]
+        out = [torch.empty((N, 3), dtype=torch.float32, **kw), torch.empty((N, K), dtype=torch.int32, **kw),
+               torch.empty((N, K), dtype=torch.float32, **kw), torch.empty((N, K), dtype=torch.float32, **kw),
+               torch.empty(N, dtype=torch.int32, **kw)]
+        n = _lib.c_int32()
+        call("ofx_reduce_graph", ptr(vm), N, K, *[ptr(t) for t in src], *[ptr(t) for t in out], byref(n), stream_ptr())
+        k = int(n.value)
+        if k == 0:
+            raise RuntimeError("No nodes! (embedded_deformation_graph.py:399-401)")
+        nodes, E, W, D, C = (t[:k].cpu().numpy() for t in out)
+        self.log.info(f"Node filtering: initial num nodes: {k} | invalid nodes: {N - k}")
+        return {"all_nodes_at_source": self.nodes.copy(), "valid_nodes_at_source": nodes, "graph_edges": E,
+                "graph_edges_weights": W, "graph_edges_distances": D, "graph_clusters": C.reshape(-1, 1),
+                "num_nodes": np.array(k, dtype=np.int64), "valid_nodes_mask": m.reshape(-1, 1)}
+
+    def compute_clusters(self):
+        """embedded_deformation_graph.py:371-380."""
+        from .graph_proc import clusters_device
+        cl, sizes = clusters_device(torch.from_numpy(self.edges).to(self._dev()))
+        self.clusters = cl.cpu().numpy().reshape(-1, 1)
+        for i, sz in enumerate(sizes):
+            if sz <= 2:
+                self.log.error(f"Cluster is too small {sizes}")
+                self.log.error(f"It only has nodes:{np.where(self.clusters == i)[0]}")
+        return sizes
+
+    def create_graph_pyramid(self):
+        """embedded_deformation_graph.py:261-328 (input of the OcclusionFusion motion-completion network):
+        greedy down-sampling at doubled coverage per level (numpy norms as the reference), geodesic edges of
+        the kept nodes over the mesh on the device."""
+        from .graph_proc import MeshGraph
+        cov = float(self.graph_generation_parameters["node_coverage"])
+        mg = getattr(self, "_mesh", None) or MeshGraph(self.vertices, self.faces, self._dev())
+        pyd = {"nn_index_l0": self.edges}
+        old_nodes, idx = self.nodes, self.node_indices
+        for level, k in zip(range(1, 4), (6, 4, 3)):
+            cov *= 2
+            down, up = [], []
+            for i in range(old_nodes.shape[0]):
+                if not down:
+                    up.append(i)
+                    down.append(i)
+                    continue
+                d = np.linalg.norm(old_nodes[down] - old_nodes[i], axis=1)
+                j = int(np.argmin(d))
+                up.append(j)
+                if float(d[j]) < cov:
+                    continue
+                down.append(i)
+            idx = idx[down]
+            E, _, _, _ = mg.edges_geodesic(idx.reshape(-1), k, cov, False, True)
+            pyd[f"down_sample_idx{level}"] = down
+            pyd[f"up_sample_idx{level}"] = up
+            pyd[f"nn_index_l{level}"] = E.cpu().numpy()
+            old_nodes = old_nodes[down]
+        self.pyd = pyd
+        return pyd
+
+    def get_graph_pyramid(self):
+        return self.pyd
+
+    def update(self, canonical_model_vertices, canonical_model_faces, new_verts_indices, plot_update=False):
+        """embedded_deformation_graph.py:496-609: add nodes at uncovered vertices (greedy, coverage apart,
+        numpy f32 norms as the reference), re-anchor every node to its nearest canonical vertex, rebuild the
+        geodesic edges on the device, clean up, cluster. Returns whether nodes were added."""
+        from .graph_proc import MeshGraph, knn_device
+        if len(new_verts_indices) == 0:
+            return False
+        cov = float(self.graph_generation_parameters["node_coverage"])
+        V = np.ascontiguousarray(canonical_model_vertices, np.float32)
+        new = []
+        for x in new_verts_indices:
+            if np.min(np.linalg.norm(self.nodes - V[x], axis=1)) < cov:
+                continue
+            if new and np.min(np.linalg.norm(V[new] - V[x], axis=1)) < cov:
+                continue
+            new.append(x)
+        if not new:
+            return False
+        self.nodes = np.concatenate([self.nodes, V[new]], axis=0)
+        dev = self._dev()
+        # node_indices = argmin over vertices of |node - vertex| (calculate_distance_matrix, :491-501)
+        idx, _ = knn_device(torch.from_numpy(self.nodes).to(dev), torch.from_numpy(V).to(dev), 1)
+        self.node_indices = idx.cpu().numpy().reshape(-1, 1)
+        K = int(self.graph_generation_parameters["num_neighbours"])
+        mg = MeshGraph(V, canonical_model_faces, dev)
+        E, W, D, _ = mg.edges_geodesic(self.node_indices.reshape(-1), K, cov, True, True)
+        self._mesh = mg
+        self.vertices, self.faces = V, np.asarray(canonical_model_faces)
+        self.edges, self.edges_weights, self.edges_distances = E.cpu().numpy(), W.cpu().numpy(), D.cpu().numpy()
+        self.clusters = -np.ones((self.edges.shape[0], 1), np.int32)
+        self.remove_nodes_with_not_enough_neighbours()
+        self.compute_clusters()
+        return True
+
+    # ---------------------------------------------------------------- on-disk formats (utils/utils.py:205-383)
+    def save(self, directory, name="graph"):
+        """Graph arrays in the reference's .bin formats (utils/utils.py save_graph_*)."""
+        from . import formats
+        import os
+        os.makedirs(directory, exist_ok=True)
+        formats.save_graph_nodes(os.path.join(directory, f"{name}_nodes.bin"), self.nodes)
+        formats.save_graph_edges(os.path.join(directory, f"{name}_edges.bin"), self.edges)
+        formats.save_graph_edges_weights(os.path.join(directory, f"{name}_edges_weights.bin"), self.edges_weights)
+        formats.save_graph_clusters(os.path.join(directory, f"{name}_clusters.bin"), self.clusters)
+
+    @classmethod
+    def load(cls, directory, name="graph", node_coverage=0.05):
+        from . import formats
+        import os
+        nodes = formats.load_graph_nodes(os.path.join(directory, f"{name}_nodes.bin"))
+        edges = formats.load_graph_edges(os.path.join(directory, f"{name}_edges.bin"))
+        w = formats.load_graph_edges_weights(os.path.join(directory, f"{name}_edges_weights.bin"))
+        cl = formats.load_graph_clusters(os.path.join(directory, f"{name}_clusters.bin"))
+        return cls(nodes, edges, w, cl, node_coverage=node_coverage, graph_neighbours=edges.shape[1])
 
 
 @dataclass
@@ -186,6 +382,40 @@ class WarpField:
             return []
         order = torch.argsort(dist[un], stable=True).flip(0)
         return un[order].cpu().numpy()
+
+    def update_graph(self, solver=None):
+        """warpfield.py:487-582 (the reference's drivers keep this call commented out): add nodes where the eroded
+        canonical model leaves the graph's coverage, re-skin the TSDF and estimate the new nodes' transforms by
+        ARAP from the existing ones (run_model.py:448-627 -> DeformNet.arap on the device). The vertex subset /
+        index quirk of the reference (indices into the non-eroded subset used on the full vertex array) is kept."""
+        from .registration import GaussNewtonSolver, run_arap
+        self.updating_warpfield = True
+        verts, faces = self.tsdf.get_canonical_model()[:2]
+        keep = self.graph.erode_mesh(verts, faces, num_iterations=3).reshape(-1)
+        new_idx = self.find_unreachable_nodes(verts[keep])
+        if len(new_idx) == 0:
+            self.updating_warpfield = False
+            return False
+        old_n = self.graph.nodes.shape[0]
+        R_old, T_old = self.R_t.cpu().numpy(), self.T_t.cpu().numpy()
+        update = self.graph.update(verts, faces, new_idx)
+        if update:
+            N = self.graph.nodes.shape[0]
+            self._set_graph(self.graph)
+            self.skin_tsdf_cache()
+            mask = np.zeros(N, bool)
+            mask[:old_n] = True
+            red = self.graph.get_reduced_graph(mask)
+            td = {"source_frame_id": getattr(self.tsdf.fopt, "source_frame", 0), "target_frame_id": self.frame_id,
+                  "node_rotations": R_old.astype(np.float32), "node_translations": T_old.astype(np.float32)}
+            td["deformed_nodes_to_target"] = (self.graph.nodes[mask] + td["node_translations"]).astype(np.float32)
+            solver = solver or GaussNewtonSolver(N, 1, self.device)
+            est = run_arap(solver, red, td, self.graph, self.log)
+            self.set_node_transforms(est["node_rotations"], est["node_translations"])
+            self.deformed_nodes = est["deformed_nodes_to_target"]
+        self.frame_id = self.tsdf.frame_id
+        self.updating_warpfield = False
+        return update
 
     def skin_tsdf_cache(self):
         """Bricked skin cache of the TSDF voxel grid (warpfield.py:131-141 cache semantics)."""

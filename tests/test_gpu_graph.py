@@ -114,3 +114,72 @@ def test_sample_nodes_and_geodesic_large_mesh(cuda):
     assert (E != np.arange(E.shape[0])[:, None]).all()
     assert np.allclose(W1.sum(1).cpu().numpy(), 1, atol=1e-5)
     assert (np.diff(D1.cpu().numpy(), axis=1) >= 0).all()     # neighbours in non-decreasing geodesic distance
+
+
+def test_edgraph_from_mesh_matches_oracle_pipeline(golden_dir, cuda):
+    """EDGraph.create_graph_from_mesh (embedded_deformation_graph.py:174-256) == the oracle composition
+    erode -> sample -> geodesic edges -> clean-up -> reduced graph -> clusters, on the depth mesh."""
+    from occlusionfusion_amd import EDGraph
+    f = np.load(os.path.join(golden_dir, "frontend_csrc.npz"), allow_pickle=False)
+    V, F = f["mesh0_vertices"], f["mesh0_faces"]
+    prm = {"node_coverage": 0.04, "num_neighbours": 8, "erosion_num_iterations": 2, "erosion_min_neighbours": 4}
+    gr = EDGraph.from_mesh(V, F, prm, device=cuda, with_pyramid=True)
+    ne = fo.erode_mesh(V, F, 2, 4)
+    nodes, idx = fo.sample_nodes(V, ne, 0.04)
+    E, W, D, _ = fo.compute_edges_geodesic(V, np.ones((V.shape[0], 1), bool), F, idx, 8, 0.04)
+    valid = fo.node_and_edge_clean_up(E, np.ones((E.shape[0], 1), bool))
+    nr, Er, Wr, Dr, _ = fo.reduced_graph(nodes, E, W, D, -np.ones((E.shape[0], 1), np.int32), valid)
+    cl, _ = fo.compute_clusters(Er)
+    assert np.array_equal(gr.nodes, nr) and np.array_equal(gr.edges, Er)
+    assert np.array_equal(gr.edges_weights, Wr) and np.array_equal(gr.edges_distances, Dr)
+    assert np.array_equal(gr.clusters, cl) and np.array_equal(gr.node_indices, idx[valid.reshape(-1)])
+    assert set(gr.pyd) >= {"nn_index_l0", "nn_index_l1", "nn_index_l2", "nn_index_l3"}
+    assert gr.pyd["nn_index_l3"].shape[1] == 3 and len(gr.pyd["up_sample_idx1"]) == gr.nodes.shape[0]
+
+
+def test_reduced_graph_with_removals(g, cuda):
+    from occlusionfusion_amd import EDGraph
+    E = g["rand_edges"]
+    n = E.shape[0]
+    rng = np.random.default_rng(1)
+    W = np.where(E >= 0, rng.random(E.shape), 0).astype(np.float32)
+    D = np.where(E >= 0, rng.random(E.shape), 0).astype(np.float32)
+    nodes = rng.random((n, 3)).astype(np.float32)
+    C = rng.integers(0, 4, (n, 1)).astype(np.int32)
+    gr = EDGraph(nodes, E, W, C)
+    gr.edges_distances = D
+    valid = g["rand_valid_out"]
+    r = gr.get_reduced_graph(valid)
+    on, oE, oW, oD, oC = fo.reduced_graph(nodes, E, W, D, C, valid)
+    assert int(r["num_nodes"]) == int(valid.sum())
+    for a, b in ((r["valid_nodes_at_source"], on), (r["graph_edges"], oE), (r["graph_edges_weights"], oW),
+                 (r["graph_edges_distances"], oD), (r["graph_clusters"], oC)):
+        assert np.array_equal(a, b)
+
+
+def test_update_graph_adds_nodes_and_arap_keeps_rest_pose(cuda):
+    """WarpField.update_graph (warpfield.py:487-582): a graph covering only part of the canonical surface gets
+    new nodes; with identity transforms the ARAP estimate of the new nodes is the rest pose."""
+    from types import SimpleNamespace
+    from occlusionfusion_amd import EDGraph, TSDFVolume, WarpField
+    from occlusionfusion_amd import synthetic as S
+    cam = S.Intrinsics(525.0 / 4, 525.0 / 4, 319.5 / 4, (239.5 - 16) / 4, 160, 112)
+    d = S.SphereScene().render(cam, 0, np.random.default_rng(3))
+    vol = TSDFVolume.from_grid(np.array([-0.40, -0.33, 0.95], np.float32), 0.012, (66, 52, 70),
+                               (cam.fx, cam.fy, cam.cx, cam.cy), SimpleNamespace(source_frame=0, skip_rate=1))
+    vol.integrate({"im": S.make_image(d), "id": 0})
+    full = EDGraph.from_mesh(*vol.get_mesh()[:2], {"node_coverage": 0.05}, device=cuda)
+    part = full.nodes[:, 0] < 0.0                        # keep the left half of the nodes only
+    e = np.where(np.isin(full.edges, np.nonzero(~part)[0]), -1, full.edges)
+    gr = EDGraph(full.nodes[part], np.sort(e[part], axis=1)[:, ::-1] * 0 - 1, None, None, node_coverage=0.05)
+    gr.graph_generation_parameters.update(full.graph_generation_parameters)
+    wf = WarpField(gr, vol)
+    n0 = gr.nodes.shape[0]
+    assert wf.update_graph() is True
+    assert gr.nodes.shape[0] > n0
+    assert np.allclose(wf.rotations, np.eye(3), atol=1e-5)
+    assert np.abs(wf.T_t.cpu().numpy()).max() < 1e-5
+    # the reference's subset-index quirk (warpfield.py:502-507) can leave regions uncovered: a second call may
+    # add more nodes; the rest pose is kept either way
+    wf.update_graph()
+    assert np.allclose(wf.rotations, np.eye(3), atol=1e-5) and np.abs(wf.T_t.cpu().numpy()).max() < 1e-5

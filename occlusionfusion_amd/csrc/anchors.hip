@@ -61,9 +61,11 @@ __global__ __launch_bounds__(256) void k_pixel_anchors_euclid(const float* __res
   float x = 0.f, y = 0.f, z = 0.f;
   if (act) { x = img[p]; y = img[hw + p]; z = img[2 * hw + p]; }
   act = act && z > 0.f;
+  // sorted list with +inf sentinels (registers); csrc inserts before the first entry >= d2 and drops the 5th
   float d[kGraphK];
   int id[kGraphK];
-  int cnt = 0;
+#pragma unroll
+  for (int s = 0; s < kGraphK; ++s) { d[s] = __builtin_inff(); id[s] = -1; }
   for (int t0 = 0; t0 < n_nodes; t0 += kNodeTile) {
     const int nt = min(kNodeTile, n_nodes - t0);
     __syncthreads();
@@ -76,19 +78,23 @@ __global__ __launch_bounds__(256) void k_pixel_anchors_euclid(const float* __res
       for (int i = 0; i < nt; ++i) {
         const float4 nd = sn[i];
         const float d2 = eigen_sqnorm(x - nd.x, y - nd.y, z - nd.z);
-        // first position whose distance is >= d2 (ties: the new node goes first)
-        int pos = cnt;
-        for (int s = cnt - 1; s >= 0; --s)
-          if (d2 <= d[s]) pos = s;
-        if (pos < kGraphK) {
-          const int last = cnt < kGraphK ? cnt : kGraphK - 1;
-          for (int s = last; s > pos; --s) { d[s] = d[s - 1]; id[s] = id[s - 1]; }
-          d[pos] = d2;
-          id[pos] = t0 + i;
-          if (cnt < kGraphK) ++cnt;
-        }
+        if (!(d2 <= d[kGraphK - 1])) continue;
+        d[kGraphK - 1] = d2;
+        id[kGraphK - 1] = t0 + i;
+        bool mv = true;                     // the new node moves before equal distances (ties: later id first)
+#pragma unroll
+        for (int s = kGraphK - 1; s > 0; --s)
+          if (mv && d[s] <= d[s - 1]) {
+            const float td = d[s]; d[s] = d[s - 1]; d[s - 1] = td;
+            const int ti = id[s]; id[s] = id[s - 1]; id[s - 1] = ti;
+          } else {
+            mv = false;
+          }
       }
   }
+  int cnt = 0;
+#pragma unroll
+  for (int s = 0; s < kGraphK; ++s) cnt += id[s] >= 0 ? 1 : 0;
   if (!act) return;
   // weights use (node - pixel).squaredNorm(): the same squares, the same order
   float w[kGraphK];
@@ -149,19 +155,21 @@ __global__ __launch_bounds__(256) void k_remap_anchors(int32_t* __restrict__ a, 
   a[i] = m;
 }
 
-// general k-NN (k <= 8): ascending (squared distance, node id); squared distances as (dx²+dy²)+dz² in f32
+// general k-NN (k <= 8): ascending (squared distance, node id); squared distances as (dx²+dy²)+dz² in f32.
+// K is a template parameter so the top-K lists stay in registers.
 constexpr int kMaxK = 8;
+template <int K>
 __global__ __launch_bounds__(256) void k_knn(const float* __restrict__ pts, int64_t n_pts, const float* __restrict__ nodes,
-                                             int n_nodes, int K, int32_t* __restrict__ idx, float* __restrict__ sqd) {
+                                             int n_nodes, int32_t* __restrict__ idx, float* __restrict__ sqd) {
   __shared__ float4 sn[kNodeTile];
   const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const bool act = p < n_pts;
   float x = 0.f, y = 0.f, z = 0.f;
   if (act) { x = pts[3 * p]; y = pts[3 * p + 1]; z = pts[3 * p + 2]; }
-  float d[kMaxK];
-  int id[kMaxK];
+  float d[K];
+  int id[K];
 #pragma unroll
-  for (int s = 0; s < kMaxK; ++s) { d[s] = __builtin_inff(); id[s] = 0x7fffffff; }
+  for (int s = 0; s < K; ++s) { d[s] = __builtin_inff(); id[s] = 0x7fffffff; }
   for (int t0 = 0; t0 < n_nodes; t0 += kNodeTile) {
     const int nt = min(kNodeTile, n_nodes - t0);
     __syncthreads();
@@ -177,14 +185,19 @@ __global__ __launch_bounds__(256) void k_knn(const float* __restrict__ pts, int6
         const float a = dx * dx, b = dy * dy, c = dz * dz;
         const float dn = (a + b) + c;
         const int in = t0 + i;
-        if (!(dn < d[K - 1] || (dn == d[K - 1] && in < id[K - 1]))) continue;
-        int s = K - 1;
-        while (s > 0 && (dn < d[s - 1] || (dn == d[s - 1] && in < id[s - 1]))) { d[s] = d[s - 1]; id[s] = id[s - 1]; --s; }
-        d[s] = dn;
-        id[s] = in;
+        if (!(dn < d[K - 1])) continue;          // ids ascend: an equal distance never displaces an earlier id
+        d[K - 1] = dn;
+        id[K - 1] = in;
+#pragma unroll
+        for (int s = K - 1; s > 0; --s)
+          if (d[s] < d[s - 1]) {
+            const float td = d[s]; d[s] = d[s - 1]; d[s - 1] = td;
+            const int ti = id[s]; id[s] = id[s - 1]; id[s - 1] = ti;
+          }
       }
   }
   if (!act) return;
+#pragma unroll
   for (int s = 0; s < K; ++s) {
     const bool ok = id[s] != 0x7fffffff;
     idx[p * K + s] = ok ? id[s] : -1;
@@ -252,8 +265,15 @@ int ofx_knn_points(const float* points, int64_t n_points, const float* nodes, in
   OFX_CHECK_ARG(n_points >= 0 && n_nodes >= 0, "bad sizes");
   if (n_points == 0) return OFX_OK;
   OFX_CHECK_ARG(points && idx && sq_dist && (n_nodes == 0 || nodes), "null buffer");
-  hipLaunchKernelGGL(k_knn, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points, n_points, nodes,
-                     n_nodes, k, idx, sq_dist);
+  const dim3 gr(grid_for(n_points, 256, 1 << 30));
+  hipStream_t hs = as_stream(s);
+  switch (k) {
+#define OFX_KNN_CASE(KK) \
+    case KK: hipLaunchKernelGGL(k_knn<KK>, gr, dim3(256), 0, hs, points, n_points, nodes, n_nodes, idx, sq_dist); break;
+    OFX_KNN_CASE(1) OFX_KNN_CASE(2) OFX_KNN_CASE(3) OFX_KNN_CASE(4)
+    OFX_KNN_CASE(5) OFX_KNN_CASE(6) OFX_KNN_CASE(7) OFX_KNN_CASE(8)
+#undef OFX_KNN_CASE
+  }
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

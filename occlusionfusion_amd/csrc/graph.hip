@@ -178,29 +178,81 @@ __global__ __launch_bounds__(256) void k_sn_conflicts(const float* __restrict__ 
   if (!FILL) cnt[v] = c;
 }
 
-enum : uint8_t { kUndecided = 0, kNode = 1, kRejected = 2 };
+enum : int32_t { kUndecided = 0, kNode = 1, kRejected = 2 };
 
+__device__ __forceinline__ int32_t ld_state(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: L1 bypass, other CUs' stores
+}
+__device__ __forceinline__ void st_state(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// round form (fallback): one launch per round, every undecided vertex advances its cursor
 __global__ __launch_bounds__(256) void k_sn_round(const uint8_t* __restrict__ elig, int64_t nv,
                                                   const int64_t* __restrict__ off, const int32_t* __restrict__ list,
-                                                  int64_t* __restrict__ cursor, uint8_t* __restrict__ state,
+                                                  int64_t* __restrict__ cursor, int32_t* __restrict__ state,
                                                   int32_t* __restrict__ n_undecided) {
   const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (v >= nv || !elig[v] || state[v] != kUndecided) return;
+  if (v >= nv || !elig[v] || ld_state(state + v) != kUndecided) return;
   int64_t c = cursor[v];
   const int64_t e = off[v + 1];
-  uint8_t s = kNode;
+  int32_t s = kNode;
   for (; c < e; ++c) {
-    const uint8_t su = ((volatile const uint8_t*)state)[list[c]];   // decisions are final: a stale read only delays
+    const int32_t su = ld_state(state + list[c]);   // decisions are final: a stale read only delays
     if (su == kRejected) continue;
     s = su == kNode ? kRejected : kUndecided;
     break;
   }
   cursor[v] = c;
-  if (s != kUndecided) ((volatile uint8_t*)state)[v] = s;
+  if (s != kUndecided) st_state(state + v, s);
   else atomicAdd(n_undecided, 1);
 }
 
-__global__ __launch_bounds__(256) void k_sn_flags(const uint8_t* __restrict__ state, const uint8_t* __restrict__ elig,
+// persistent form: a fully resident grid (<= 2 workgroups of 256 per CU); thread t owns vertices t, t+T, ...
+// in increasing order and advances them as a per-lane state machine inside ONE uniform loop (lanes of a
+// wave never wait on each other inside divergent code). The lowest undecided vertex always has all its
+// lower neighbours decided and its owner is at it, so the grid makes progress; every spin is bounded
+// (timeout -> *err, the host finishes with the round form: decisions already stored are final).
+__global__ __launch_bounds__(256) void k_sn_persistent(const uint8_t* __restrict__ elig, int64_t nv,
+                                                       const int64_t* __restrict__ off, const int32_t* __restrict__ list,
+                                                       int64_t* __restrict__ cursor, int32_t* __restrict__ state,
+                                                       int64_t max_iter, int32_t* __restrict__ err) {
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t c = 0, e = 0;
+  bool fresh = true;
+  for (int64_t it = 0; it < max_iter; ++it) {
+    if (__all(v >= nv)) return;
+    if (v < nv) {
+      if (fresh) {
+        if (!elig[v]) { v += T; continue; }
+        c = off[v];
+        e = off[v + 1];
+        fresh = false;
+      }
+      int32_t decided = kUndecided;
+      // advance over decided neighbours (at most 16 per step, so lanes stay in step)
+      for (int q = 0; q < 16; ++q) {
+        if (c >= e) { decided = kNode; break; }
+        const int32_t su = ld_state(state + list[c]);
+        if (su == kRejected) { ++c; continue; }
+        if (su == kNode) decided = kRejected;
+        break;
+      }
+      if (decided != kUndecided) {
+        st_state(state + v, decided);
+        v += T;
+        fresh = true;
+      } else {
+        cursor[v] = c;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (v < nv) atomicOr(err, 1);
+}
+
+__global__ __launch_bounds__(256) void k_sn_flags(const int32_t* __restrict__ state, const uint8_t* __restrict__ elig,
                                                   int64_t nv, uint8_t* __restrict__ is_node) {
   const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (v < nv) is_node[v] = elig[v] && state[v] == kNode;
@@ -629,7 +681,8 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   *n_nodes = 0;
   if (n_rounds) *n_rounds = 0;
   if (nv == 0) return OFX_OK;
-  uint8_t *elig = nullptr, *state = nullptr, *is_node = nullptr;
+  uint8_t *elig = nullptr, *is_node = nullptr;
+  int32_t* state = nullptr;
   uint32_t *key = nullptr, *key2 = nullptr;
   int32_t *val = nullptr, *sorted = nullptr, *bstart = nullptr, *bend = nullptr, *cnt = nullptr, *list = nullptr;
   int32_t *rank = nullptr, *und = nullptr;
@@ -675,10 +728,24 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   OFX_CHECKS(dalloc(&cursor, nv, hs));
   OFX_HIP(hipMemcpyAsync(cursor, off, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, hs));
   OFX_CHECKS(dalloc(&state, nv, hs));
-  OFX_HIP(hipMemsetAsync(state, kUndecided, nv, hs));
+  OFX_HIP(hipMemsetAsync(state, 0, nv * sizeof(int32_t), hs));
   constexpr int kChunk = 32;
   OFX_CHECKS(dalloc(&und, kChunk, hs));
   int64_t rounds = 0;
+  {
+    int32_t* err = und;   // reused: zeroed below before the rounds
+    OFX_HIP(hipMemsetAsync(err, 0, sizeof(int32_t), hs));
+    int dev = 0, ncu = 256;
+    OFX_HIP(hipGetDevice(&dev));
+    OFX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    hipLaunchKernelGGL(k_sn_persistent, dim3(2 * ncu), dim3(256), 0, hs, (const uint8_t*)elig, nv, (const int64_t*)off,
+                       (const int32_t*)list, cursor, state, (int64_t)1 << 22, err);
+    OFX_LAUNCH_CHECK();
+    int32_t herr = 0;
+    OFX_CHECKS(read1(err, &herr, hs));
+    rounds = herr ? -1 : 0;      // -1: the persistent pass timed out; the round form finishes
+  }
+  int64_t nr = 0;
   for (;;) {
     OFX_HIP(hipMemsetAsync(und, 0, kChunk * sizeof(int32_t), hs));
     for (int r = 0; r < kChunk; ++r)
@@ -690,14 +757,14 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
     OFX_HIP(hipStreamSynchronize(hs));
     int r = 0;
     while (r < kChunk && h[r] != 0) ++r;
-    rounds += (r < kChunk) ? r + 1 : kChunk;
+    nr += (r < kChunk) ? r + 1 : kChunk;
     if (r < kChunk) break;
-    if (rounds > nv + kChunk) { set_error("sample_nodes did not converge"); return OFX_ERR_STATE; }
+    if (nr > nv + kChunk) { set_error("sample_nodes did not converge"); return OFX_ERR_STATE; }
   }
   OFX_CHECKS(dalloc(&is_node, nv + 1, hs));
   OFX_CHECKS(dalloc(&rank, nv + 1, hs));
   OFX_HIP(hipMemsetAsync(is_node + nv, 0, 1, hs));
-  hipLaunchKernelGGL(k_sn_flags, gv, dim3(256), 0, hs, (const uint8_t*)state, (const uint8_t*)elig, nv, is_node);
+  hipLaunchKernelGGL(k_sn_flags, gv, dim3(256), 0, hs, (const int32_t*)state, (const uint8_t*)elig, nv, is_node);
   OFX_CHECKS(exclusive_sum_u8(is_node, rank, nv + 1, hs));
   hipLaunchKernelGGL(k_sn_emit, gv, dim3(256), 0, hs, g->P, (const uint8_t*)is_node, (const int32_t*)rank, nv,
                      node_positions, node_indices);
@@ -705,7 +772,7 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   int32_t nn = 0;
   OFX_CHECKS(read1(rank + nv, &nn, hs));
   *n_nodes = nn;
-  if (n_rounds) *n_rounds = rounds;
+  if (n_rounds) *n_rounds = rounds < 0 ? -nr : nr;   // > 0: launches of the round form after the persistent pass
   for (void* p : {(void*)elig, (void*)state, (void*)is_node, (void*)key, (void*)key2, (void*)val, (void*)sorted,
                   (void*)bstart, (void*)bend, (void*)cnt, (void*)list, (void*)rank, (void*)und, (void*)off,
                   (void*)cursor})

@@ -12,7 +12,7 @@ dev = torch.device("cuda", 0)
 seq = S.SyntheticSequence.build(2000, seed=3)
 pipe = FusionPipeline(seq, (-1.024, -1.024, 0.5), 0.004, (64, 64, 64), device=dev)
 N = len(seq.nodes)
-variants = [("cold1e-7", 0, 1e-7), ("warm1e-7", 1, 1e-7), ("warm1e-6", 1, 1e-6)]
+variants = [("warm1e-7", 1, 1e-7), ("warm3e-7", 1, 3e-7), ("warm1e-6", 1, 1e-6)]
 solvers = {}
 for name, wm, tol in variants:
     solvers[name] = GaussNewtonSolver(N, 10000, pcg_tol=tol, pcg_warm=bool(wm))

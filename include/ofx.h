@@ -306,7 +306,9 @@ typedef struct ofx_gn_params {
   double stop_loss_diff;     /* 1   (model.py:114) */
   double pcg_tol;            /* relative residual target of the inner solve */
   int32_t mode;              /* OFX_GN_OPTIMIZE (0): DeformNet.optimize; OFX_GN_ARAP (1): DeformNet.arap */
-  int32_t _pad;
+  int32_t precond_every;     /* the cluster preconditioner is rebuilt on GN steps gn_iter % precond_every == 0
+                                (0 or 1: every step) and reused by the warm-started steps in between; it only
+                                shapes convergence, the stop test is unchanged */
 } ofx_gn_params;
 
 /* OFX_GN_ARAP restates DeformNet.arap (model/model.py:1639-1986), the graph-update solve for nodes

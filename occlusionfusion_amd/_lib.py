@@ -30,7 +30,7 @@ class GnParams(ctypes.Structure):
     _fields_ = [("num_iter", c_int32), ("use_edge_weighting", c_int32), ("pcg_max_iter", c_int32), ("pcg_warm", c_int32),
                 ("lambda_flow", c_double), ("lambda_depth", c_double), ("lambda_arap", c_double),
                 ("lambda_motion", c_double), ("lm_factor", c_double), ("stop_loss_diff", c_double),
-                ("pcg_tol", c_double), ("mode", c_int32), ("_pad", c_int32)]
+                ("pcg_tol", c_double), ("mode", c_int32), ("precond_every", c_int32)]
 
 
 class GnProblem(ctypes.Structure):

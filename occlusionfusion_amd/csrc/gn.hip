@@ -825,7 +825,7 @@ __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const dou
 // from their owner lanes by cross-lane permutes and the pivot by a lane read — no LDS, no barrier.
 // Cold start also: x = 0, r = b, u = M⁻¹ b, z = q = s = p = w = 0, u -> m1.
 __global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
-                                                 const double* __restrict__ rhs) {
+                                                 const double* __restrict__ rhs, int invert) {
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
@@ -852,6 +852,7 @@ __global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __rest
       A[36 * (int64_t)slot + 7 * r] = a[r][r];
     }
   }
+  if (!invert) return;   // warm-started step reusing the stored cluster inverse (precond_every)
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < kCD; ++k) {
@@ -1549,7 +1550,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     g->warm_now = 1;
   }
   g->Aop = A;
-  hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs);
+  // the cluster inverse is rebuilt every precond_every GN steps; steps in between (always warm started,
+  // proj2 applies the stored M⁻¹) only damp A's diagonal
+  const int every = g->prm.precond_every > 1 ? g->prm.precond_every : 1;
+  const int invert = (!g->warm_now || gn_iter % every == 0) ? 1 : 0;
+  hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
   if (g->warm_now) {
     hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
     hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);

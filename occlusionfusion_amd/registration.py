@@ -25,7 +25,7 @@ from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
                    lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=1000, pcg_tol=1e-6,
-                   pcg_warm=True)
+                   pcg_warm=True, precond_every=10)
 MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
 
 
@@ -95,6 +95,7 @@ class GaussNewtonSolver:
         p.lambda_arap, p.lambda_motion = float(q["lambda_arap"]), float(q["lambda_motion"])
         p.lm_factor, p.stop_loss_diff, p.pcg_tol = float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"])
         p.mode = 0
+        p.precond_every = int(q.get("precond_every", 1))
         return p
 
     def _problem(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,

@@ -14,7 +14,7 @@ import sys
 
 import numpy as np
 
-KERNELS = {"k_pcg_iter": "ofx::k_pcg_iter<true, false", "k_integrate_warp": "ofx::k_integrate<true, true>"}
+KERNELS = {"k_pcg_iter": "ofx::k_pcg_iter<true, false", "k_integrate_warp": "ofx::k_integrate<true, true"}
 
 
 def main(d, out):

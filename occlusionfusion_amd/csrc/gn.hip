@@ -160,6 +160,24 @@ __device__ __forceinline__ double wave_sum(double x) {
   x = row16_sum(x);
   return (read_lane(x, 0) + read_lane(x, 16)) + (read_lane(x, 32) + read_lane(x, 48));
 }
+// four block sums at once: fixed-order wave sums, then the kBlk/64 wave results combined in wave order
+__device__ __forceinline__ void block_sum4(double v[4]) {
+  __shared__ double s4[kBlk / 64][4];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = wave_sum(v[k]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s4[w][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double a = 0.0;
+#pragma unroll
+    for (int q = 0; q < kBlk / 64; ++q) a += s4[q][k];
+    v[k] = a;
+  }
+}
 __device__ __forceinline__ double block_sum(double v) {
   __shared__ double s[kBlk];
   s[threadIdx.x] = v;
@@ -553,10 +571,11 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
       bad = (isfinite(l2[0]) && isfinite(l2[1]) && isfinite(l2[2])) ? 0.0 : 1.0;
     }
   }
-  double s0 = block_sum(l2[0]), s1 = block_sum(l2[1]), s2 = block_sum(l2[2]), s3 = block_sum(bad);
+  double sv[4] = {l2[0], l2[1], l2[2], bad};
+  block_sum4(sv);
   if (threadIdx.x == 0) {
     double* P = g.part_loss + 4 * (int64_t)blockIdx.x;
-    P[0] = s0; P[1] = s1; P[2] = s2; P[3] = s3;
+    P[0] = sv[0]; P[1] = sv[1]; P[2] = sv[2]; P[3] = sv[3];
   }
 }
 
@@ -603,14 +622,18 @@ __device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A,
 // rhs tail.
 constexpr int kRhsSlots = 10;
 __device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, int wg) {
-  if (wg == 0) {
-    double d0 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 0);
-    double d1 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 1);
-    double d2 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 2);
-    double d3 = wg_sum_fixed(g.part_loss, g.nwg_terms, 4, 3);
+  if (wg == 0 && threadIdx.x < 64) {   // the loss partials of k_terms, 4 streams in one pass, fixed order
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < g.nwg_terms; i += 64) {
+      const double4 t = *reinterpret_cast<const double4*>(g.part_loss + 4 * (int64_t)i);
+      a[0] += t.x; a[1] += t.y; a[2] += t.z; a[3] += t.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
     if (threadIdx.x == 0) {
       double* tail = rhs + 6 * (int64_t)g.N;
-      tail[0] = d0; tail[1] = d1; tail[2] = d2; tail[3] = d3;
+      tail[0] = a[0]; tail[1] = a[1]; tail[2] = a[2]; tail[3] = a[3];
     }
   }
   const int n = wg * (kBlk / 64) + (threadIdx.x >> 6);
@@ -635,10 +658,12 @@ __device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, 
   if (lane < 6) rhs[6 * (int64_t)n + c] = -tot;
 }
 
-// JᵀJ blocks and -Jᵀr in one launch: workgroups [0, nwb) assemble blocks, the rest the rhs.
+// JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
+// chains), then nwb workgroups of blocks.
 __global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A, double* __restrict__ rhs, int nwb) {
-  if ((int)blockIdx.x < nwb) blocks_body(g, A, blockIdx.x);
-  else rhs_body(g, rhs, blockIdx.x - nwb);
+  const int nrw = (int)gridDim.x - nwb;
+  if ((int)blockIdx.x < nrw) rhs_body(g, rhs, blockIdx.x);
+  else blocks_body(g, A, blockIdx.x - nrw);
 }
 
 // ---------------------------------------------------------------------------- PCG

@@ -591,8 +591,11 @@ __device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A,
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
   if (s < g.nnzb) {
     const int b = g.blk_off[s], e = g.blk_off[s + 1];
+    // the next entry's code is loaded one iteration ahead: one dependent memory trip per entry
+    int code_next = b + q < e ? g.blk_list[b + q] : 0;
     for (int k = b + q; k < e; k += 16) {
-      const int code = g.blk_list[k];
+      const int code = code_next;
+      code_next = k + 16 < e ? g.blk_list[k + 16] : 0;
       const int64_t t = code >> 4;
       const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * ((code >> 2) & 3));
       const double2* Jq = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code & 3));
@@ -665,6 +668,10 @@ __global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A,
   if ((int)blockIdx.x < nrw) rhs_body(g, rhs, blockIdx.x);
   else blocks_body(g, A, blockIdx.x - nrw);
 }
+#ifdef OFX_SPLIT_ASSEMBLE
+__global__ __launch_bounds__(kBlk) void k_assemble_blocks(Gn g, double* __restrict__ A) { blocks_body(g, A, blockIdx.x); }
+__global__ __launch_bounds__(kBlk) void k_assemble_rhs(Gn g, double* __restrict__ rhs) { rhs_body(g, rhs, blockIdx.x); }
+#endif
 
 // ---------------------------------------------------------------------------- PCG
 // Pipelined preconditioned CG (Ghysels & Vanroose 2014): one global reduction per iteration, ONE
@@ -1969,7 +1976,12 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   dc.fx = g->fx; dc.fy = g->fy; dc.cx = g->cx; dc.cy = g->cy;
   hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
   const int nwb = g->nnzb > 0 ? (int)grid_for(g->nnzb, kBlk / 16, 1 << 30) : 0;
+#ifdef OFX_SPLIT_ASSEMBLE   // tuning build: the two halves as separate kernels (rocprof times each)
+  if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, A);
+  hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, rhs);
+#else
   hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, A, rhs, nwb);
+#endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

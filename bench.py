@@ -41,7 +41,7 @@ def pmc_traffic(kernel):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
     p.add_argument("--dims", type=int, default=512)

@@ -369,12 +369,13 @@ int ofx_gn_destroy(void* handle);
 int ofx_gn_setup(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params, int64_t* nnz_blocks,
                  ofx_stream_t s);
 /* Assemble A (f64[nnz_blocks*36]) and rhs (f64[6·rows+4]: b = -Jᵀr then [loss² total,data,arap,motion])
- * from matches [m0,m1); regularizers (ARAP, motion) added iff add_reg. Zeroes both first.
+ * from matches [m0,m1); regularizers (ARAP, motion) and the LM damping λ_k·I of the diagonal blocks
+ * (model.py:418-419,641-662) added iff add_reg. Zeroes both first.
  * In a multi-GPU solve every rank calls this on its match shard, the caller all-reduces
  * (sum) A and rhs, then every rank calls ofx_gn_step with identical buffers. */
 int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int32_t add_reg, double* A,
                      double* rhs, ofx_stream_t s);
-/* LM damping, cluster block-Jacobi PCG solve, early-stop bookkeeping, R <- exp(x_rot) R, t += x_t. */
+/* Cluster block-Jacobi PCG solve of A x = b, early-stop bookkeeping, R <- exp(x_rot) R, t += x_t. */
 int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_stream_t s);
 int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s);
 /* setup + num_iter x (linearize + step) + finish, single device */

@@ -583,7 +583,7 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
 // block, loads both 3x6 Jacobian blocks of the entry whole (16-B accesses) and accumulates the full
 // 6x6 product; 16-lane DPP sums (fixed pairing) finish the block and lane 0 of the group stores it.
 // Deterministic; forward declared helpers live in the PCG section.
-__device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A, int64_t wg) {
+__device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A, int64_t wg, double lm) {
   const int64_t s = wg * (kBlk / 16) + (threadIdx.x >> 4);
   const int q = threadIdx.x & 15;
   double acc[36];
@@ -614,6 +614,9 @@ __device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A,
 #pragma unroll
   for (int k = 0; k < 36; ++k) acc[k] = row16_sum(acc[k]);
   if (s < g.nnzb && q == 0) {
+    if (lm != 0.0 && g.blk_row[s] == g.col[s])   // LM damping of the diagonal blocks (model.py:641-662)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) acc[7 * r] += lm;
     double2* out = reinterpret_cast<double2*>(A + 36 * s);
 #pragma unroll
     for (int k = 0; k < 18; ++k) out[k] = make_double2(acc[2 * k], acc[2 * k + 1]);
@@ -663,13 +666,16 @@ __device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, 
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
-__global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A, double* __restrict__ rhs, int nwb) {
+__global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A, double* __restrict__ rhs, int nwb,
+                                                  double lm) {
   const int nrw = (int)gridDim.x - nwb;
   if ((int)blockIdx.x < nrw) rhs_body(g, rhs, blockIdx.x);
-  else blocks_body(g, A, blockIdx.x - nrw);
+  else blocks_body(g, A, blockIdx.x - nrw, lm);
 }
 #ifdef OFX_SPLIT_ASSEMBLE
-__global__ __launch_bounds__(kBlk) void k_assemble_blocks(Gn g, double* __restrict__ A) { blocks_body(g, A, blockIdx.x); }
+__global__ __launch_bounds__(kBlk) void k_assemble_blocks(Gn g, double* __restrict__ A, double lm) {
+  blocks_body(g, A, blockIdx.x, lm);
+}
 __global__ __launch_bounds__(kBlk) void k_assemble_rhs(Gn g, double* __restrict__ rhs) { rhs_body(g, rhs, blockIdx.x); }
 #endif
 
@@ -877,14 +883,7 @@ __global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __rest
       a[(2 * e + 1) / 6][(2 * e + 1) % 6] = v.y;
     }
   }
-  if (ti == tj) {   // diagonal blocks are always in the pattern
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      a[r][r] += lm;
-      A[36 * (int64_t)slot + 7 * r] = a[r][r];
-    }
-  }
-  if (!invert) return;   // warm-started step reusing the stored cluster inverse (precond_every)
+  (void)lm; (void)invert;   // A arrives damped (k_assemble)
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < kCD; ++k) {
@@ -955,6 +954,10 @@ __device__ __forceinline__ constexpr int tri(int i, int j) { return j * (j + 1) 
 
 __global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {   // PCG bookkeeping of this GN step (also in k_pcg_prep)
+    g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
+    host_flag(g.hflags, H_DONE, 0);
+  }
   const int lane = threadIdx.x;
   const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int np = g.n_prev;
@@ -1586,7 +1589,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // proj2 applies the stored M⁻¹) only damp A's diagonal
   const int every = g->prm.precond_every > 1 ? g->prm.precond_every : 1;
   const int invert = (!g->warm_now || gn_iter % every == 0) ? 1 : 0;
-  hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
+  if (invert) hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
   if (g->warm_now) {
     hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
     hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
@@ -1975,12 +1978,15 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   dc.la = sqrt(g->prm.lambda_arap); dc.lm = sqrt(g->prm.lambda_motion);
   dc.fx = g->fx; dc.fy = g->fy; dc.cx = g->cx; dc.cy = g->cy;
   hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
+  // the LM damping λ_k I (model.py:418-419,641-662) is added by the rank that adds the regularisers, so a
+  // sum over ranks carries it once
+  const double lm = add_reg ? lm_for_iter(g->prm.lm_factor, gn_iter) : 0.0;
   const int nwb = g->nnzb > 0 ? (int)grid_for(g->nnzb, kBlk / 16, 1 << 30) : 0;
 #ifdef OFX_SPLIT_ASSEMBLE   // tuning build: the two halves as separate kernels (rocprof times each)
-  if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, A);
+  if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, A, lm);
   hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, rhs);
 #else
-  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, A, rhs, nwb);
+  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, A, rhs, nwb, lm);
 #endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;

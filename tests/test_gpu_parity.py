@@ -269,18 +269,23 @@ def test_gn_assembly_matches_dense_system(cuda, golden_dir):
     rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=cuda)
     call("ofx_gn_linearize", s._h, 0, 0, M, 1, ptr(A), ptr(rhs), stream_ptr())
     torch.cuda.synchronize()
+    lm = 1e-7   # linearize adds the LM damping λ_0·I to the diagonal blocks (model.py:418-419,641-662)
     sysd = fo.gn_system(g["nodes"], g["edges"], g["tpos"], g["conf"], g["src"], g["anchors"], g["weights"], g["tgt"],
-                        g["intr"], np.tile(np.eye(3), (N, 1, 1)), np.zeros((N, 3)), lm_factor=0.0)
+                        g["intr"], np.tile(np.eye(3), (N, 1, 1)), np.zeros((N, 3)), lm_factor=lm)
     p = fo.node_major_perm(N)
     Ad = sysd["A"][np.ix_(p, p)]
     bd = sysd["b"][p]
-    # the BSR pattern is internal: compare the multiset of block values (+ zero padding blocks)
+    # the BSR pattern is internal: compare the multiset of block values (+ the padding rows' λ·I diagonal
+    # blocks + zero padding blocks)
     Ab = A.cpu().numpy().reshape(-1, 6, 6)
     blocks_dense = Ad.reshape(N, 6, N, 6).transpose(0, 2, 1, 3)
     nzmask = np.abs(blocks_dense).sum((2, 3)) > 0
-    assert Ab.shape[0] >= nzmask.sum()
+    n_pad = int((perm < 0).sum())
+    assert Ab.shape[0] >= nzmask.sum() + n_pad
+    pad_diag = np.tile((lm * np.eye(6)).reshape(-1), n_pad)
     np.testing.assert_allclose(np.sort(Ab.reshape(-1)), np.sort(np.concatenate(
-        [blocks_dense[nzmask].reshape(-1), np.zeros((Ab.shape[0] - nzmask.sum()) * 36)])), rtol=1e-9, atol=1e-12)
+        [blocks_dense[nzmask].reshape(-1), pad_diag, np.zeros((Ab.shape[0] - nzmask.sum() - n_pad) * 36)])),
+        rtol=1e-9, atol=1e-12)
     rb = rhs.cpu().numpy()
     real = perm >= 0
     np.testing.assert_allclose(rb[:6 * rows].reshape(rows, 6)[real], bd.reshape(N, 6)[perm[real]], rtol=1e-9, atol=1e-12)

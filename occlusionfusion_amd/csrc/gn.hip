@@ -111,6 +111,8 @@ struct Gn {
   // the previous frame's solutions were measured not to help its first steps):
   // xh = previous solutions, th = A·xh
   double *xh = nullptr, *th = nullptr;
+  struct StepArgs* step_args = nullptr;   // device copy (fused GN step in the converging PCG launch)
+  bool step_fused = false;                // this step's k_step work was done by the PCG
   int n_prev = 0;                 // valid entries of the ring for the current step
   int warm_now = 0;               // this step starts from the projected x0
   int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED] mirrored by the kernels
@@ -1162,6 +1164,12 @@ __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ 
 constexpr int kRowMax = 20;
 // The iteration kernel's arguments: only what it reads (a ~200-B kernarg instead of the whole Gn:
 // the host enqueues ~1000 of these per frame, so per-launch host work is on the critical path).
+// What the converging PCG launch needs to also take the GN step (k_step's work, fused): fixed pointers in
+// device memory (written once at create), per-step values in the kernel arguments.
+struct StepArgs {
+  double *R, *t, *xh, *stat, *loss_log, *step_state;
+  const double* conf;
+};
 struct PcgIt {
   const double* Aop;
   const float* Mcl;
@@ -1172,6 +1180,11 @@ struct PcgIt {
   uint64_t* stamps;
   int32_t nwg_row, nw_pad;
   struct { double pcg_tol; } prm;
+  // fused GN step (fuse = 0: k_step runs as its own launch)
+  const StepArgs* sa;
+  const double* tail;           // rhs + 6N: [loss² total, data, arap, motion, nonfinite]
+  double stop_loss_diff;
+  int32_t fuse, gn_iter, N, mode, n_iter_log, warm;
 };
 static PcgIt pcg_args(const Gn* g) {
   PcgIt a;
@@ -1180,6 +1193,8 @@ static PcgIt pcg_args(const Gn* g) {
   a.pcg_alpha = g->pcg_alpha; a.pcg_gamma = g->pcg_gamma; a.scal = g->scal;
   a.flags = g->flags; a.hflags = g->hflags; a.stopw = g->stopw; a.stamps = g->stamps;
   a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol;
+  a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff;
+  a.fuse = 0; a.gn_iter = 0; a.N = g->N; a.mode = g->prm.mode; a.n_iter_log = 64; a.warm = g->prm.pcg_warm;
   return a;
 }
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
@@ -1188,6 +1203,76 @@ static PcgIt pcg_args(const Gn* g) {
 #else
 #define OFX_STAMP(k)
 #endif
+// k_step's work done by the converging PCG launch (every wave for its own rows; wave 0 lane 0 the
+// bookkeeping). Every wave derives the same decision from read-only inputs, as k_step's workgroups do.
+__device__ __forceinline__ void kornia_exp(const double x[3], double Ri[9]) {
+  const double a0 = x[0], a1 = x[1], a2 = x[2];
+  const double th2 = a0 * a0 + a1 * a1 + a2 * a2;
+  if (th2 > 1e-6) {
+    const double th = sqrt(th2);
+    const double wx = a0 / (th + 1e-6), wy = a1 / (th + 1e-6), wz = a2 / (th + 1e-6);
+    const double c = cos(th), s = sin(th), oc = 1.0 - c;
+    Ri[0] = c + wx * wx * oc; Ri[1] = wx * wy * oc - wz * s; Ri[2] = wy * s + wx * wz * oc;
+    Ri[3] = wz * s + wx * wy * oc; Ri[4] = c + wy * wy * oc; Ri[5] = -wx * s + wy * wz * oc;
+    Ri[6] = -wy * s + wx * wz * oc; Ri[7] = wx * s + wy * wz * oc; Ri[8] = c + wz * wz * oc;
+  } else {
+    Ri[0] = 1; Ri[1] = -a2; Ri[2] = a1; Ri[3] = a2; Ri[4] = 1; Ri[5] = -a0; Ri[6] = -a1; Ri[7] = a0; Ri[8] = 1;
+  }
+}
+__device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int r, int q, bool own, int64_t o,
+                                           int row, double xv, bool ill, int cnt, double bb) {
+  const StepArgs& sa = *g.sa;
+  const int gi = g.gn_iter;
+  const double* tail = g.tail;
+  const double loss = sqrt(tail[0] + tail[1] + tail[2]);
+  const double prev = sa.step_state[2 * gi];
+  const int acc = (int)sa.step_state[2 * gi + 1];
+  const bool stop = ill || (acc > 0 && (loss - prev > g.stop_loss_diff || loss == prev));
+  if (wv == 0 && lane == 0) {
+    if (gi < kMaxLog) {
+      sa.stat[3 * gi + 0] = (double)cnt;
+      sa.stat[3 * gi + 1] = bb;
+      sa.stat[3 * gi + 2] = loss;
+    }
+    g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
+    if (stop) {
+      g.flags[F_STOPPED] = 1;
+      host_flag(g.hflags, H_STOPPED, 1);
+    } else {
+      if (acc < g.n_iter_log) {
+        sa.loss_log[4 * acc + 0] = loss;
+        sa.loss_log[4 * acc + 1] = sqrt(tail[0]);
+        sa.loss_log[4 * acc + 2] = sqrt(tail[1]);
+        sa.loss_log[4 * acc + 3] = sqrt(tail[2]);
+      }
+      sa.step_state[2 * gi + 2] = loss;
+      sa.step_state[2 * gi + 3] = (double)(acc + 1);
+      g.flags[F_ACCEPTED] = acc + 1;
+    }
+  }
+  if (stop) return;
+  if (own && g.warm) sa.xh[(int64_t)(gi % kProj) * 6 * g.N + o] = xv;
+  double x[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) x[c] = __shfl(xv, r * kSL + c, 64);   // the row's 6 components (lanes q < 6)
+  if (q != 0) return;
+  if (g.mode == OFX_GN_ARAP && sa.conf[row] != 0.0) return;   // arap: valid nodes keep R, t (model.py:1940-1943)
+  double Ri[9];
+  kornia_exp(x, Ri);
+  double* R = sa.R + 9 * (int64_t)row;
+  double Rc[9], Rn[9];
+#pragma unroll
+  for (int c = 0; c < 9; ++c) Rc[c] = R[c];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Rn[3 * a + c] = Ri[3 * a] * Rc[c] + Ri[3 * a + 1] * Rc[3 + c] + Ri[3 * a + 2] * Rc[6 + c];
+#pragma unroll
+  for (int c = 0; c < 9; ++c) R[c] = Rn[c];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) sa.t[3 * (int64_t)row + c] += x[3 + c];
+}
+
 template <bool kWave, bool kFirst, int kU>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
@@ -1295,9 +1380,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (conv || !isfinite(alpha) || !(alpha > 0.0)) {   // converged, or breakdown (A SPD => alpha > 0): keep x
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
     g.stopw[(int64_t)wv * 64 + lane] = 1;
+    const bool ill = !conv && !isfinite(alpha);
+    if (g.fuse) fused_step(g, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
     if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
-      if (!conv && !isfinite(alpha)) g.flags[F_ILL] = 1;
+      if (ill) g.flags[F_ILL] = 1;
       host_flag(g.hflags, H_PCG_IT, cnt);
       __hip_atomic_store(g.hflags + H_DONE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
     }
@@ -1506,7 +1593,7 @@ static void free_all(Gn* g) {
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->perm, g->iperm, g->comp_rows, g->comp_off};
+                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->perm, g->iperm, g->comp_rows, g->comp_off};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -1621,7 +1708,12 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // The chunk event only tells "all launched iterations ran without converging" -> launch more.
   volatile int32_t* hf = g->host_flags;
   hf[H_DONE] = 0;   // the previous step's converged launch has run (we saw it); prep also clears it
-  const PcgIt pa = pcg_args(g);
+  PcgIt pa = pcg_args(g);
+  // the converging launch also takes the GN step (not when arap's null-space projection must run first)
+  pa.fuse = g->n_comp == 0 ? 1 : 0;
+  pa.gn_iter = gn_iter;
+  pa.tail = rhs + 6 * (int64_t)g->N;
+  g->step_fused = false;
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
@@ -1649,6 +1741,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (hf[H_STOPPED]) break;
     if (hf[H_DONE]) {
       g->last_pcg[gn_iter & 63] = hf[H_PCG_IT];
+      g->step_fused = pa.fuse != 0;
       break;
     }
     (void)ran;   // the chunk ran out without convergence: next chunk
@@ -1687,7 +1780,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
   ALLOC(g->Mcl, 6 * N * kCD); ALLOC(g->st, V_N * 6 * N); ALLOC(g->m0, 6 * N); ALLOC(g->m1, 6 * N);
-  ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N);
+  ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N); ALLOC(g->step_args, 1);
   ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes); ALLOC(g->wl, N / kCS * kWL); ALLOC(g->stopw, N / kCS * 64);
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   const int64_t max_ns = 128 * 17;   // nw_pad bound: 2·64·17 >= max_pad / kCS waves
@@ -1703,6 +1796,12 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
       hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess ||
       hipEventCreateWithFlags(&g->poll_ev, hipEventDisableTiming) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
+  }
+  {   // the fused GN step's fixed pointers (fused_step), in device memory
+    const StepArgs h{g->R, g->t, g->xh, g->stat, g->loss_log, g->step_state, g->conf};
+    if (hipMemcpy(g->step_args, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
+      free_all(g); delete g; set_error("hipMemcpy failed"); return OFX_ERR_HIP;
+    }
   }
 
   *handle = g;
@@ -1999,6 +2098,7 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   hipStream_t hs = as_stream(s);
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
+  if (g->step_fused) return OFX_OK;   // the converging PCG launch took the step (fused_step)
   if (g->n_comp > 0) hipLaunchKernelGGL(k_null_project, dim3(g->n_comp), dim3(64), 0, hs, *g);
   double* xsave = g->prm.pcg_warm ? g->xh + (int64_t)(gn_iter % kProj) * 6 * g->N : nullptr;
   hipLaunchKernelGGL(k_step, dim3(grid_for(g->N, 256)), dim3(256), 0, hs, *g, (const double*)rhs, 64,

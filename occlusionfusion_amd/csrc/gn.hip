@@ -79,6 +79,10 @@ struct Gn {
   int32_t* stopw = nullptr;      // per PCG wave and lane: 1 once the current solve has converged
   uint64_t* stamps = nullptr;    // tuning builds (-DOFX_STAMPS): per iteration < 64 and wave, 8 clock stamps
   int32_t* blk_row = nullptr;    // block -> row (clears the slot map's pattern at the next setup)
+  float* d_gnodes = nullptr;      // device copy of the graph the row order was built for (optimistic check)
+  int32_t* d_gedges = nullptr;
+  int32_t* d_gdiff = nullptr;
+  int64_t gcap_n = 0, gcap_e = 0;
   int pat_N = 0;                 // N and block count of the pattern currently set in `map`
   int64_t pat_nnzb = 0;
   int64_t ne_cap = 0;            // capacity of edges / ew
@@ -209,6 +213,17 @@ __device__ __forceinline__ double wg_sum_fixed(const double* __restrict__ p, int
 }
 
 // ---------------------------------------------------------------------------- setup kernels
+// graph unchanged since the row order was built? (bitwise compare; any difference sets *diff)
+__global__ __launch_bounds__(256) void k_graph_cmp(const float* __restrict__ a, const float* __restrict__ b, int64_t na,
+                                                   const int32_t* __restrict__ c, const int32_t* __restrict__ d,
+                                                   int64_t nc, int32_t* __restrict__ diff) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  bool x = false;
+  if (i < na) x = __float_as_uint(a[i]) != __float_as_uint(b[i]);
+  if (i < nc) x = x || c[i] != d[i];
+  if (x) *diff = 1;
+}
+
 // Per-solve upload in one launch: f32 problem -> f64 device copies, anchors/edges, edge weights,
 // initial R/t, term -> nodes table, flags/stats reset, and the previous pattern's entries of the
 // N x N slot map cleared (so the map never needs an N² memset).
@@ -345,16 +360,33 @@ __global__ __launch_bounds__(256) void k_wave_list(Gn g) {
 // (max_out, nullable: max of cnt)
 __global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restrict__ cnt, int32_t* __restrict__ off,
                                                int32_t* __restrict__ max_out) {
+  // tiles of 1024 x 8 counts: thread t scans its 8 contiguous entries (two coalesced 16-B loads), the
+  // block scan combines the threads, a carry runs across tiles (fixed order)
   __shared__ int s_w[16];
   __shared__ int s_mx[16];
-  const int64_t per = (n + blockDim.x - 1) / blockDim.x;
-  const int64_t s = threadIdx.x * per, e = min(n, s + per);
-  int c = 0, mx = 0;
-  for (int64_t i = s; i < e; ++i) { c += cnt[i]; mx = max(mx, cnt[i]); }
-  int total;
-  int o = block_exscan(c, s_w, total);
-  for (int64_t i = s; i < e; ++i) { off[i] = o; o += cnt[i]; }
-  if (threadIdx.x == 0) off[n] = total;
+  constexpr int kPer = 8;
+  int carry = 0, mx = 0;
+  for (int64_t base = 0; base < n; base += (int64_t)blockDim.x * kPer) {
+    const int64_t s0 = base + (int64_t)threadIdx.x * kPer;
+    int v[kPer];
+    if (s0 + kPer <= n && ((reinterpret_cast<uintptr_t>(cnt + s0) & 15) == 0)) {
+      const int4 a = *reinterpret_cast<const int4*>(cnt + s0), b = *reinterpret_cast<const int4*>(cnt + s0 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) v[k] = s0 + k < n ? cnt[s0 + k] : 0;
+    }
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) { c += v[k]; mx = max(mx, v[k]); }
+    int total;
+    int o = block_exscan(c, s_w, total) + carry;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (s0 + k < n) { off[s0 + k] = o; o += v[k]; }
+    carry += total;
+  }
+  if (threadIdx.x == 0) off[n] = carry;
   if (max_out) {
 #pragma unroll
     for (int k = 32; k > 0; k >>= 1) mx = max(mx, __shfl_xor(mx, k, 64));
@@ -1593,7 +1625,7 @@ static void free_all(Gn* g) {
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->perm, g->iperm, g->comp_rows, g->comp_off};
+                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -1893,8 +1925,18 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   hipStream_t hs = as_stream(s);
   int N0 = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
   if ((int64_t)N0 * NB > 0) OFX_CHECK_ARG(pb->edges, "null edges");
-  // row order (cluster preconditioner): rebuilt when the graph differs from the previous solve's
-  {
+  // row order (cluster preconditioner): rebuilt when the graph differs from the previous solve's. If a
+  // row order exists for a graph of the same size, assume it still holds and compare on the device; the
+  // result is read with the pattern size below (no extra sync) and a changed graph restarts the setup.
+  const bool optimistic = !g->h_perm.empty() && g->h_nodes.size() == 3 * (size_t)N0 &&
+                          g->h_edges.size() == (size_t)N0 * NB && g->gcap_n >= 3 * (int64_t)N0 &&
+                          g->gcap_e >= (int64_t)N0 * NB && g->d_gdiff;
+  if (optimistic) {
+    OFX_HIP(hipMemsetAsync(g->d_gdiff, 0, sizeof(int32_t), hs));
+    const int64_t na = 3 * (int64_t)N0, nc = (int64_t)N0 * NB;
+    hipLaunchKernelGGL(k_graph_cmp, dim3(grid_for(na > nc ? na : nc, 256, 1 << 30)), dim3(256), 0, hs, pb->nodes,
+                       (const float*)g->d_gnodes, na, pb->edges, (const int32_t*)g->d_gedges, nc, g->d_gdiff);
+  } else {
     std::vector<float> hn(3 * (size_t)N0);
     std::vector<int32_t> he((size_t)N0 * NB);
     OFX_HIP(hipMemcpyAsync(hn.data(), pb->nodes, hn.size() * sizeof(float), hipMemcpyDeviceToHost, hs));
@@ -1913,6 +1955,21 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
       g->h_nodes.swap(hn);
       g->h_edges.swap(he);
     }
+    // device copy of this graph for the next solves' optimistic check
+    if (3 * (int64_t)N0 > g->gcap_n) {
+      if (g->d_gnodes) OFX_HIP(hipFree(g->d_gnodes));
+      g->gcap_n = 3 * (int64_t)N0;
+      OFX_HIP(hipMalloc((void**)&g->d_gnodes, g->gcap_n * sizeof(float)));
+    }
+    if ((int64_t)N0 * NB > g->gcap_e || !g->d_gedges) {
+      if (g->d_gedges) OFX_HIP(hipFree(g->d_gedges));
+      g->gcap_e = (int64_t)N0 * NB > 1 ? (int64_t)N0 * NB : 1;
+      OFX_HIP(hipMalloc((void**)&g->d_gedges, g->gcap_e * sizeof(int32_t)));
+    }
+    if (!g->d_gdiff) OFX_HIP(hipMalloc((void**)&g->d_gdiff, sizeof(int32_t)));
+    OFX_HIP(hipMemcpyAsync(g->d_gnodes, pb->nodes, 3 * (size_t)N0 * sizeof(float), hipMemcpyDeviceToDevice, hs));
+    if ((int64_t)N0 * NB > 0)
+      OFX_HIP(hipMemcpyAsync(g->d_gedges, pb->edges, (size_t)N0 * NB * sizeof(int32_t), hipMemcpyDeviceToDevice, hs));
   }
   OFX_CHECK_ARG(prm->mode == OFX_GN_OPTIMIZE || prm->mode == OFX_GN_ARAP, "bad gn mode %d", prm->mode);
   OFX_CHECK_ARG(prm->mode != OFX_GN_ARAP || M == 0, "arap mode takes no match rows");
@@ -2021,10 +2078,18 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N);
   hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
-  int32_t nnz = 0, lens[2] = {0, 0};
+  int32_t nnz = 0, lens[2] = {0, 0}, gdiff = 0;
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipMemcpyAsync(lens, g->row_cnt + N, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  if (optimistic) OFX_HIP(hipMemcpyAsync(&gdiff, g->d_gdiff, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
+  if (gdiff) {   // the graph changed: clear the slot map marked with the stale order and start over
+    OFX_HIP(hipMemsetAsync(g->map, 0, (size_t)g->max_pad * g->max_pad * sizeof(int32_t), hs));
+    g->pat_N = 0;
+    g->pat_nnzb = 0;
+    g->h_perm.clear();
+    return ofx_gn_setup(handle, pb, prm, nnz_blocks, s);
+  }
   g->max_deg = lens[0];
   g->max_wave = lens[1];
   if ((int64_t)nnz + 1 > g->nnzb_cap) {

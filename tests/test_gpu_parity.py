@@ -302,6 +302,27 @@ def test_gn_repeatable(cuda, golden_dir):
     np.testing.assert_allclose(a["node_translations"].cpu().numpy(), b["node_translations"].cpu().numpy(), atol=1e-9)
 
 
+def test_gn_solver_reuse_across_graph_change(cuda, golden_dir):
+    """A solver handle reused on a different graph of the same size (the row order is kept optimistically
+    and checked on the device) gives exactly what a fresh handle gives."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    e2 = g["edges"].copy()
+    e2[:, -2:] = -1                                   # drop the last two neighbours of every node
+    inp2 = list(_gn_inputs(g))
+    inp2[1] = e2
+    s = GaussNewtonSolver(len(g["nodes"]), 1000)
+    s.optimize(*_gn_inputs(g))
+    s.optimize(*_gn_inputs(g))                        # optimistic path, unchanged graph
+    reused = s.optimize(*inp2)                        # optimistic path detects the change, restarts
+    fresh = GaussNewtonSolver(len(g["nodes"]), 1000).optimize(*inp2)
+    assert torch.equal(reused["node_translations"], fresh["node_translations"])
+    assert torch.equal(reused["node_rotations"], fresh["node_rotations"])
+    again = s.optimize(*_gn_inputs(g))                # and back
+    first = GaussNewtonSolver(len(g["nodes"]), 1000).optimize(*_gn_inputs(g))
+    assert torch.equal(again["node_translations"], first["node_translations"])
+
+
 def _oracle_two_frames(g, integ):
     """Source frame + one ED-warped frame through an oracle integrate function (flat f32 volumes)."""
     world = fo.world_points(g["origin"], g["dims"], float(g["voxel_size"]))

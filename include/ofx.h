@@ -273,6 +273,10 @@ int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_
                        int32_t n_max_neighbors, float node_coverage, int32_t allow_only_valid_vertices,
                        int32_t enforce_total_num_neighbors, int32_t* graph_edges, float* graph_edges_weights,
                        float* graph_edges_distances, float* node_to_vertex_distances, ofx_stream_t s);
+/* nodes the last ofx_edges_geodesic on this handle settled with the sequential heap kernel (distance ties
+ * the parallel relaxation cannot order, or a neighbourhood larger than its LDS table); the rest were settled
+ * by the parallel form. OFX_GEO_SEQ=1 in the environment forces the sequential kernel for every node. */
+int ofx_graph_geodesic_sequential(void* handle, int64_t* n_nodes);
 int ofx_edges_euclidean(const float* node_positions, int32_t n_nodes, int32_t n_max_neighbors, int32_t* graph_edges,
                         ofx_stream_t s);
 /* valid_in / valid_out u8[N] (may alias) */

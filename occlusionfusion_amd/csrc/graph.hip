@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "ofx_common.h"
@@ -140,9 +141,10 @@ __global__ __launch_bounds__(256) void k_sn_bounds(const uint32_t* __restrict__ 
   if (i == nv - 1 || key[i + 1] != key[i]) end[key[i]] = (int32_t)(i + 1);
 }
 
-// pass 0: count, pass 1: fill the lower-id conflicting eligible vertices of every eligible vertex (ascending
-// id order is not needed: decisions only depend on the set)
-template <bool FILL>
+// pass 0: count, pass 1: fill the conflicting eligible vertices of every eligible vertex — lower ids for the
+// round/persistent forms (FWD = false), higher ids for the greedy form (FWD = true). Ascending id order is not
+// needed: decisions only depend on the set.
+template <bool FILL, bool FWD>
 __global__ __launch_bounds__(256) void k_sn_conflicts(const float* __restrict__ P, const uint8_t* __restrict__ elig, int64_t nv,
                                                       Grid g, const int32_t* __restrict__ start,
                                                       const int32_t* __restrict__ end, const int32_t* __restrict__ sorted,
@@ -167,8 +169,9 @@ __global__ __launch_bounds__(256) void k_sn_conflicts(const float* __restrict__ 
         seen[ns++] = h;
         for (int i = start[h]; i < end[h]; ++i) {
           const int32_t u = sorted[i];
-          if (u >= v) continue;
-          // (point - node).squaredNorm() <= c² with point = v, node = u (graph_proc.cpp:120)
+          if (FWD ? u <= v : u >= v) continue;
+          // (point - node).squaredNorm() <= c² with point = v, node = u (graph_proc.cpp:120); the f32
+          // differences only change sign when the roles swap, so the test is symmetric bit for bit
           if (eig_sq(px - P[3 * u], py - P[3 * u + 1], pz - P[3 * u + 2]) <= cov2) {
             if (FILL) list[o + c] = u;
             ++c;
@@ -250,6 +253,64 @@ __global__ __launch_bounds__(256) void k_sn_persistent(const uint8_t* __restrict
     __builtin_amdgcn_s_sleep(1);
   }
   if (v < nv) atomicOr(err, 1);
+}
+
+// greedy form (the C++ loop itself, graph_proc.cpp:100-131): ONE workgroup holds the undecided-vertex bitmap
+// in LDS (1 bit per vertex, <= 160 KiB). Each step wave 0 finds the lowest undecided vertex — it is the
+// sequential loop's next node: every lower vertex is a node or within c of one — and the workgroup clears the
+// bits of its higher-id conflicts. Steps = nodes (a few µs each: one barrier pair + the conflict list load);
+// the loop ends when the bitmap is empty (<= nv steps, no inter-workgroup waiting).
+constexpr int kGreedyThreads = 1024;
+constexpr int64_t kGreedyMaxWords = 40 * 1024 - 64;   // 160 KiB of LDS minus a little
+
+__global__ __launch_bounds__(kGreedyThreads) void k_sn_greedy(const uint8_t* __restrict__ elig, int64_t nv,
+                                                               const int64_t* __restrict__ off,
+                                                               const int32_t* __restrict__ list,
+                                                               int32_t* __restrict__ state) {
+  extern __shared__ uint32_t bits[];
+  __shared__ int64_t s_v, s_w;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t nw = (nv + 31) >> 5;
+  for (int64_t w = tid; w < nw; w += kGreedyThreads) {
+    uint32_t x = 0;
+    const int64_t v0 = w << 5;
+    for (int b = 0; b < 32; ++b)
+      if (v0 + b < nv && elig[v0 + b]) x |= 1u << b;
+    bits[w] = x;
+  }
+  __syncthreads();
+  int64_t cw = 0;   // every word below cw is empty
+  for (int64_t step = 0; step < nv; ++step) {
+    if (tid < 64) {
+      int64_t v = -1;
+      for (; cw < nw; cw += 64) {
+        const uint32_t x = cw + lane < nw ? bits[cw + lane] : 0u;
+        const uint64_t nz = __ballot(x != 0u);
+        if (nz) {
+          const int first = __builtin_ctzll(nz);
+          const uint32_t xw = __shfl(x, first);
+          cw += first;
+          v = (cw << 5) + __builtin_ctz(xw);
+          break;
+        }
+      }
+      if (tid == 0) { s_v = v; s_w = cw; }
+    }
+    __syncthreads();
+    const int64_t v = s_v;
+    cw = s_w;
+    if (v < 0) break;
+    const int64_t b = off[v], e = off[v + 1];
+    if (tid == 0) {
+      state[v] = kNode;
+      atomicAnd(&bits[v >> 5], ~(1u << (v & 31)));
+    }
+    for (int64_t i = b + tid; i < e; i += kGreedyThreads) {
+      const int32_t u = list[i];
+      atomicAnd(&bits[u >> 5], ~(1u << (u & 31)));
+    }
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(256) void k_sn_flags(const int32_t* __restrict__ state, const uint8_t* __restrict__ elig,
@@ -391,6 +452,228 @@ __global__ __launch_bounds__(64) void k_geodesic(GeoArgs a, const int32_t* __res
   }
 }
 
+// Parallel form: ONE workgroup per node computes the f32 geodesic distances of its neighbourhood by
+// label-correcting relaxation in rounds (frontier queues + an open-addressing vertex table in LDS). With
+// positive edge lengths fl(d + len) >= d, so the least fixpoint d(v) = min_u fl(d(u) + len(u, v)) is exactly
+// the distance the C++ Dijkstra pops each vertex at (its predecessor pops first). Relaxation is bounded by a
+// radius R that grows ×1.25 from the coverage (capped at the 2·coverage pruning unless
+// enforce_total_num_neighbors) until K candidate nodes lie within R: below R every distance is final, and
+// vertices whose edges were cut by R are re-queued when it grows. Pop order then only matters among EQUAL
+// distances: ties among the first K+1 candidate nodes, or (with n2v) another vertex at the K-th node's
+// distance, send the node to the sequential heap kernel above (status 3); a full table or queue retries with
+// the larger table (status 4). Outputs are written only for a settled node.
+namespace geo {
+constexpr int kThreads = 256;
+constexpr int kQueue = 1280;     // frontier slots per queue
+constexpr int kCand = 256;       // candidate nodes
+constexpr int kMaxRounds = 8192;
+enum : int32_t { kOk = 0, kInvalid = 2, kTie = 3, kFull = 4 };
+}  // namespace geo
+
+template <int TBL>
+__device__ __forceinline__ uint32_t geo_hash(int32_t v) {
+  return ((uint32_t)v * 2654435761u) >> (32 - __builtin_ctz(TBL));
+}
+
+// TBL vertex slots (keys + f32 distances: 8 B each); 8192 -> ≈ 78 KiB of LDS (2 workgroups per CU),
+// 16384 -> ≈ 143 KiB (the retry tier for nodes whose neighbourhood did not fit)
+template <int TBL>
+__global__ __launch_bounds__(geo::kThreads) void k_geo_relax(GeoArgs a, const int32_t* __restrict__ todo, int32_t n_todo) {
+  using namespace geo;
+  __shared__ int32_t keys[TBL];
+  __shared__ uint32_t dist[TBL];
+  __shared__ int32_t queue[2][kQueue];
+  __shared__ uint32_t qflag[TBL / 32], bnd[TBL / 32];
+  __shared__ float cand_d[kCand];
+  __shared__ int32_t cand_m[kCand], cand_v[kCand];
+  __shared__ int32_t s_n[2], s_fail, s_nbnd, s_used, s_ncand, s_amb;
+  __shared__ float sel_d[17];
+  __shared__ int32_t sel_m[17], sel_v[17];
+  const int tid = threadIdx.x, lane = tid & 63;
+  if ((int)blockIdx.x >= n_todo) return;
+  const int32_t node = todo ? todo[blockIdx.x] : (int32_t)blockIdx.x;
+  const int32_t s0 = a.node_idx[node];
+  if (s0 < 0) {
+    if (tid < a.K) {
+      a.edges[(int64_t)node * a.K + tid] = -1;
+      a.wts[(int64_t)node * a.K + tid] = 0.f;
+      a.dists[(int64_t)node * a.K + tid] = 0.f;
+    }
+    if (tid == 0) a.status[node] = kOk;
+    return;
+  }
+  if (a.only_valid && a.valid && !a.valid[s0]) {   // popped first: the C++ exits
+    if (tid == 0) a.status[node] = kInvalid;
+    return;
+  }
+  for (int i = tid; i < TBL; i += kThreads) { keys[i] = -1; dist[i] = 0x7F800000u; }
+  for (int i = tid; i < TBL / 32; i += kThreads) { qflag[i] = 0u; bnd[i] = 0u; }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t h = geo_hash<TBL>(s0);
+    keys[h] = s0; dist[h] = 0u;
+    queue[0][0] = (int32_t)h;
+    s_n[0] = 1; s_n[1] = 0; s_fail = 0; s_nbnd = 0; s_used = 1; s_amb = 0;
+  }
+  float R = a.enforce ? a.cov : fminf(a.cov, a.max_inf);
+  int cur = 0, rounds = 0;
+  for (;;) {
+    __syncthreads();
+    // ---- relax to the fixpoint under R
+    for (;; ++rounds) {
+      const int nf = s_n[cur];
+      if (nf == 0 || s_fail) break;
+      if (rounds >= kMaxRounds) { s_fail = kFull; break; }   // uniform: every thread sees the same counts
+      for (int i = tid; i < nf; i += kThreads) {
+        const int32_t sl = queue[cur][i];
+        atomicAnd(&qflag[sl >> 5], ~(1u << (sl & 31)));
+      }
+      if (tid == 0) s_n[cur ^ 1] = 0;
+      __syncthreads();
+      for (int i = tid; i < nf; i += kThreads) {
+        const int32_t sl = queue[cur][i];
+        const int32_t v = keys[sl];
+        const float d = __uint_as_float(dist[sl]);
+        const float vx = a.P[3 * (int64_t)v], vy = a.P[3 * (int64_t)v + 1], vz = a.P[3 * (int64_t)v + 2];
+        const int32_t q1 = a.rowptr[v + 1];
+        bool cut = false;
+        for (int32_t q = a.rowptr[v]; q < q1; ++q) {
+          const int32_t u = a.col[q];
+          if (a.only_valid && a.valid && !a.valid[u]) continue;
+          const float nd = d + sqrt_rn(eig_sq(vx - a.P[3 * (int64_t)u], vy - a.P[3 * (int64_t)u + 1],
+                                              vz - a.P[3 * (int64_t)u + 2]));
+          if (!(nd <= R)) { cut = true; continue; }
+          uint32_t h = geo_hash<TBL>(u);
+          int32_t probe = 0;
+          for (; probe < TBL; ++probe, h = (h + 1) & (TBL - 1)) {
+            const int32_t k = keys[h];
+            if (k == u) break;
+            if (k == -1) {
+              const int32_t o = atomicCAS(&keys[h], -1, u);
+              if (o == -1) { if (atomicAdd(&s_used, 1) >= TBL * 7 / 8) s_fail = kFull; break; }
+              if (o == u) break;
+            }
+          }
+          if (probe == TBL) { s_fail = kFull; break; }
+          const uint32_t nb = __float_as_uint(nd);
+          if (nb < atomicMin(&dist[h], nb)) {
+            if (!(atomicOr(&qflag[h >> 5], 1u << (h & 31)) & (1u << (h & 31)))) {
+              const int32_t p = atomicAdd(&s_n[cur ^ 1], 1);
+              if (p < kQueue) queue[cur ^ 1][p] = (int32_t)h;
+              else s_fail = kFull;
+            }
+          }
+        }
+        if (cut && !(atomicOr(&bnd[sl >> 5], 1u << (sl & 31)) & (1u << (sl & 31)))) atomicAdd(&s_nbnd, 1);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    __syncthreads();
+    if (s_fail) break;
+    // ---- candidate nodes within R
+    if (tid == 0) s_ncand = 0;
+    __syncthreads();
+    for (int i = tid; i < TBL; i += kThreads) {
+      const int32_t v = keys[i];
+      if (v < 0) continue;
+      const int32_t m = a.v2n[v];
+      if (m >= 0 && m != node) {
+        const int32_t p = atomicAdd(&s_ncand, 1);
+        if (p < kCand) { cand_d[p] = __uint_as_float(dist[i]); cand_m[p] = m; cand_v[p] = v; }
+        else s_fail = kFull;
+      }
+    }
+    __syncthreads();
+    if (s_fail) break;
+    const bool at_cap = !a.enforce && R >= a.max_inf;
+    if (s_ncand >= a.K || at_cap || s_nbnd == 0) break;   // K found, pruning radius reached, or all reached
+    // ---- grow R; re-queue the vertices whose edges it cut
+    R = a.enforce ? R * 1.25f : fminf(R * 1.25f, a.max_inf);
+    if (tid == 0) { s_n[cur] = 0; s_nbnd = 0; }
+    __syncthreads();
+    for (int w = tid; w < TBL / 32; w += kThreads) {
+      uint32_t x = bnd[w];
+      if (!x) continue;
+      bnd[w] = 0u;
+      for (; x; x &= x - 1) {
+        const int32_t sl = w * 32 + __builtin_ctz(x);
+        if (!(atomicOr(&qflag[sl >> 5], 1u << (sl & 31)) & (1u << (sl & 31)))) {
+          const int32_t p = atomicAdd(&s_n[cur], 1);
+          if (p < kQueue) queue[cur][p] = sl;
+          else s_fail = kFull;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (s_fail) {
+    if (tid == 0) a.status[node] = s_fail;
+    return;
+  }
+  const int nc = s_ncand;
+  const int nsel = min(nc, a.K + 1);
+  if (tid < 64) {   // wave 0: the nsel smallest candidates in ascending distance
+    float ld[kCand / 64];
+#pragma unroll
+    for (int j = 0; j < kCand / 64; ++j) {
+      const int c = lane + 64 * j;
+      ld[j] = c < nc ? cand_d[c] : __builtin_inff();
+    }
+    for (int k = 0; k < nsel; ++k) {
+      uint64_t best = ~0ull;
+#pragma unroll
+      for (int j = 0; j < kCand / 64; ++j) {
+        const int c = lane + 64 * j;
+        if (c < nc) best = min(best, ((uint64_t)__float_as_uint(ld[j]) << 32) | (uint32_t)c);
+      }
+      for (int o = 32; o >= 1; o >>= 1) best = min(best, (uint64_t)__shfl_xor((unsigned long long)best, o));
+      const int c = (int)(uint32_t)best;
+#pragma unroll
+      for (int j = 0; j < kCand / 64; ++j)
+        if (lane + 64 * j == c) ld[j] = __uint_as_float(0x7F800001u);   // taken (sorts above +inf)
+      if (lane == 0) { sel_d[k] = cand_d[c]; sel_m[k] = cand_m[c]; sel_v[k] = cand_v[c]; }
+    }
+  }
+  __syncthreads();
+  bool tie = false;
+  for (int k = 1; k < nsel; ++k) tie |= sel_d[k] == sel_d[k - 1];
+  const int nn = min(nc, a.K);
+  const bool brk = nc >= a.K;                       // the C++ breaks at the K-th node
+  const float dK = brk ? sel_d[a.K - 1] : __builtin_inff();
+  const int32_t vK = brk ? sel_v[a.K - 1] : -1;
+  if (!tie && a.n2v && brk) {
+    for (int i = tid; i < TBL; i += kThreads)
+      if (keys[i] >= 0 && keys[i] != vK && __uint_as_float(dist[i]) == dK) s_amb = 1;
+    __syncthreads();
+  }
+  if (tie || s_amb) {
+    if (tid == 0) a.status[node] = kTie;
+    return;
+  }
+  if (a.n2v)
+    for (int i = tid; i < TBL; i += kThreads) {
+      const int32_t v = keys[i];
+      const float d = __uint_as_float(dist[i]);
+      if (v >= 0 && (!brk || d < dK)) a.n2v[(int64_t)node * a.nv + v] = d;
+    }
+  if (tid == 0) {
+    float w[16];
+    float sum = 0.f;
+    for (int i = 0; i < nn; ++i) {
+      w[i] = fexp(fdivr(-(sel_d[i] * sel_d[i]), a.two_c2));
+      sum += w[i];
+    }
+    for (int i = 0; i < a.K; ++i) {
+      const int64_t o = (int64_t)node * a.K + i;
+      a.edges[o] = i < nn ? sel_m[i] : -1;
+      a.wts[o] = i < nn ? (sum > 0.f ? fdivr(w[i], sum) : fdivr(w[i], (float)nn)) : 0.f;
+      a.dists[o] = i < nn ? sel_d[i] : 0.f;
+    }
+    a.status[node] = kOk;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_v2n(const int32_t* __restrict__ node_idx, int32_t n_nodes, int64_t nv,
                                              int32_t* __restrict__ v2n) {
   // the C++ loop assigns in node order, so the LAST node on a vertex wins: max over node ids
@@ -505,6 +788,7 @@ struct Graph {
   int64_t ncol = 0;
   const float* P = nullptr;
   const int32_t* faces = nullptr;
+  int64_t geo_sequential = 0;   // nodes the last ofx_edges_geodesic ran through the sequential heap kernel
 };
 
 template <typename T>
@@ -633,6 +917,13 @@ int ofx_graph_destroy(void* handle) {
   return OFX_OK;
 }
 
+int ofx_graph_geodesic_sequential(void* handle, int64_t* n_nodes) {
+  Graph* g = (Graph*)handle;
+  OFX_CHECK_ARG(g && n_nodes, "null argument");
+  *n_nodes = g->geo_sequential;
+  return OFX_OK;
+}
+
 /* vertex adjacency (CSR) of the handle's mesh, for inspection: rowptr i32[V+1], col i32[rowptr[V]] */
 int ofx_graph_adjacency(void* handle, int32_t* rowptr, int32_t* col, int64_t* n_col, ofx_stream_t s) {
   Graph* g = (Graph*)handle;
@@ -712,26 +1003,46 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   OFX_HIP(hipcub::DeviceRadixSort::SortPairs(t, tmp, key, key2, val, sorted, (int)nv, 0, 32, hs));
   OFX_HIP(hipFreeAsync(t, hs));
   hipLaunchKernelGGL(k_sn_bounds, gv, dim3(256), 0, hs, (const uint32_t*)key2, nv, bstart, bend);
+  // the greedy form when the bitmap fits one workgroup's LDS (1.28M vertices), else the parallel rounds
+  const int64_t nwords = (nv + 31) >> 5;
+  const bool greedy = nwords <= kGreedyMaxWords && !getenv("OFX_SN_ROUNDS");
   OFX_CHECKS(dalloc(&cnt, nv + 1, hs));
   OFX_HIP(hipMemsetAsync(cnt, 0, (nv + 1) * sizeof(int32_t), hs));
-  hipLaunchKernelGGL(k_sn_conflicts<false>, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
-                     (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
-                     (const int64_t*)nullptr, (int32_t*)nullptr);
+  if (greedy)
+    hipLaunchKernelGGL((k_sn_conflicts<false, true>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                       (const int64_t*)nullptr, (int32_t*)nullptr);
+  else
+    hipLaunchKernelGGL((k_sn_conflicts<false, false>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                       (const int64_t*)nullptr, (int32_t*)nullptr);
   OFX_CHECKS(dalloc(&off, nv + 1, hs));
   OFX_CHECKS(exclusive_sum_i32_to_i64(cnt, off, nv + 1, hs));
   int64_t total = 0;
   OFX_CHECKS(read1(off + nv, &total, hs));
-  OFX_CHECKS(dalloc(&list, total, hs));
-  hipLaunchKernelGGL(k_sn_conflicts<true>, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
-                     (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
-                     (const int64_t*)off, list);
-  OFX_CHECKS(dalloc(&cursor, nv, hs));
-  OFX_HIP(hipMemcpyAsync(cursor, off, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, hs));
+  OFX_CHECKS(dalloc(&list, std::max<int64_t>(total, 1), hs));
+  if (greedy)
+    hipLaunchKernelGGL((k_sn_conflicts<true, true>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                       (const int64_t*)off, list);
+  else
+    hipLaunchKernelGGL((k_sn_conflicts<true, false>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                       (const int64_t*)off, list);
   OFX_CHECKS(dalloc(&state, nv, hs));
   OFX_HIP(hipMemsetAsync(state, 0, nv * sizeof(int32_t), hs));
   constexpr int kChunk = 32;
+  int64_t rounds = 0, nr = 0;
+  if (greedy) {
+    const size_t lds = (size_t)nwords * sizeof(uint32_t);
+    OFX_HIP(hipFuncSetAttribute((const void*)k_sn_greedy, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_sn_greedy, dim3(1), dim3(kGreedyThreads), lds, hs, (const uint8_t*)elig, nv,
+                       (const int64_t*)off, (const int32_t*)list, state);
+    OFX_LAUNCH_CHECK();
+  } else {
+  OFX_CHECKS(dalloc(&cursor, nv, hs));
+  OFX_HIP(hipMemcpyAsync(cursor, off, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, hs));
   OFX_CHECKS(dalloc(&und, kChunk, hs));
-  int64_t rounds = 0;
   {
     int32_t* err = und;   // reused: zeroed below before the rounds
     OFX_HIP(hipMemsetAsync(err, 0, sizeof(int32_t), hs));
@@ -745,7 +1056,6 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
     OFX_CHECKS(read1(err, &herr, hs));
     rounds = herr ? -1 : 0;      // -1: the persistent pass timed out; the round form finishes
   }
-  int64_t nr = 0;
   for (;;) {
     OFX_HIP(hipMemsetAsync(und, 0, kChunk * sizeof(int32_t), hs));
     for (int r = 0; r < kChunk; ++r)
@@ -761,6 +1071,7 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
     if (r < kChunk) break;
     if (nr > nv + kChunk) { set_error("sample_nodes did not converge"); return OFX_ERR_STATE; }
   }
+  }
   OFX_CHECKS(dalloc(&is_node, nv + 1, hs));
   OFX_CHECKS(dalloc(&rank, nv + 1, hs));
   OFX_HIP(hipMemsetAsync(is_node + nv, 0, 1, hs));
@@ -772,7 +1083,9 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   int32_t nn = 0;
   OFX_CHECKS(read1(rank + nv, &nn, hs));
   *n_nodes = nn;
-  if (n_rounds) *n_rounds = rounds < 0 ? -nr : nr;   // > 0: launches of the round form after the persistent pass
+  // 0: greedy pass (or persistent pass + one round); > 0: round-form launches after the persistent pass;
+  // < 0: the persistent pass timed out
+  if (n_rounds) *n_rounds = rounds < 0 ? -nr : nr;
   for (void* p : {(void*)elig, (void*)state, (void*)is_node, (void*)key, (void*)key2, (void*)val, (void*)sorted,
                   (void*)bstart, (void*)bend, (void*)cnt, (void*)list, (void*)rank, (void*)und, (void*)off,
                   (void*)cursor})
@@ -809,6 +1122,44 @@ int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_
   a.two_c2 = (2.f * node_coverage) * node_coverage;
   a.only_valid = allow_only_valid_vertices; a.enforce = enforce_total_num_neighbors;
   a.edges = graph_edges; a.wts = graph_edges_weights; a.dists = graph_edges_distances; a.n2v = node_to_vertex_distances;
+  a.status = status;
+  if (!getenv("OFX_GEO_SEQ")) {   // parallel form; ties go sequential, overfull neighbourhoods to the big table
+    std::vector<int32_t> rest, big;
+    for (int tier = 0; tier < 2; ++tier) {
+      int32_t n_run = tier == 0 ? n_nodes : (int32_t)big.size();
+      if (n_run == 0) break;
+      if (tier == 0) {
+        hipLaunchKernelGGL(k_geo_relax<8192>, dim3((unsigned)n_run), dim3(geo::kThreads), 0, hs, a,
+                           (const int32_t*)nullptr, n_run);
+      } else {
+        OFX_HIP(hipMemcpyAsync(todo, big.data(), big.size() * sizeof(int32_t), hipMemcpyHostToDevice, hs));
+        hipLaunchKernelGGL(k_geo_relax<16384>, dim3((unsigned)n_run), dim3(geo::kThreads), 0, hs, a,
+                           (const int32_t*)todo, n_run);
+      }
+      OFX_LAUNCH_CHECK();
+      std::vector<int32_t> st(n_nodes);
+      OFX_HIP(hipMemcpyAsync(st.data(), status, n_nodes * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+      OFX_HIP(hipStreamSynchronize(hs));
+      std::vector<int32_t> ran;
+      if (tier == 0) { ran.resize(n_nodes); for (int32_t n = 0; n < n_nodes; ++n) ran[n] = n; }
+      else ran = big;
+      big.clear();
+      for (int32_t n : ran) {
+        if (st[n] == geo::kInvalid) {
+          dfree(v2n, hs); dfree(status, hs); dfree(todo, hs);
+          set_error("compute_edges_geodesic: node %d reached an invalid vertex (the reference exits)", n);
+          return OFX_ERR_STATE;
+        }
+        if (st[n] == geo::kTie || (st[n] == geo::kFull && tier == 1)) rest.push_back(n);
+        else if (st[n] == geo::kFull) big.push_back(n);
+      }
+    }
+    std::sort(rest.begin(), rest.end());
+    g->geo_sequential = (int64_t)rest.size();
+    h_todo.swap(rest);
+  } else {
+    g->geo_sequential = n_nodes;
+  }
   const int64_t words = (nv + 31) / 32;
   int64_t cap = 8192;
   while (!h_todo.empty()) {

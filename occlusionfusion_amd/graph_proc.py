@@ -179,6 +179,10 @@ class MeshGraph:
         call("ofx_edges_geodesic", self._h, ptr(vv), ptr(ni), N, K, float(node_coverage),
              1 if allow_only_valid_vertices else 0, 1 if enforce_total_num_neighbors else 0, ptr(E), ptr(W), ptr(D),
              ptr(n2v), stream_ptr())
+        from . import _lib
+        nseq = _lib.c_int64()
+        call("ofx_graph_geodesic_sequential", self._h, _lib.byref(nseq))
+        self.geodesic_sequential = int(nseq.value)   # nodes settled by the sequential heap kernel
         return E, W, D, n2v
 
 

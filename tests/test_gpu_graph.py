@@ -89,18 +89,38 @@ def test_csrc_call_shapes(g, cuda):
     assert (d2[~np.eye(n2, dtype=bool)] > c2).all()
 
 
-def test_sample_nodes_and_geodesic_large_mesh(cuda):
-    """A 512x512 grid-like noisy depth mesh (~250k vertices): sample_nodes equals the oracle's sequential
-    sampling; geodesic edges are deterministic and well formed (the Python Dijkstra is too slow here)."""
+def _noisy_depth_mesh(cuda, H=512, W=512):
     from occlusionfusion_amd.graph_proc import MeshGraph
     from occlusionfusion_amd.image_proc import compute_mesh_from_depth_device
     rng = np.random.default_rng(4)
-    H, W = 512, 512
     yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
     z = (1.2 + 0.1 * np.sin(xx / 40) * np.cos(yy / 55) + rng.normal(0, 0.0005, (H, W))).astype(np.float32)
     P = np.stack([(xx - 256) * z / 500, (yy - 256) * z / 500, z]).astype(np.float32)
     m = compute_mesh_from_depth_device(torch.from_numpy(P).to(cuda), 0.05)
-    mg = MeshGraph(m["vertices"], m["faces"], cuda)
+    return m, MeshGraph(m["vertices"], m["faces"], cuda)
+
+
+@pytest.mark.parametrize("form", ["greedy", "rounds"])
+@pytest.mark.parametrize("cov,size", [(0.05, 512), (0.008, 160)])
+def test_sample_nodes_forms_large_mesh(cuda, monkeypatch, form, cov, size):
+    """Both device forms of sample_nodes — the single-workgroup greedy loop (bitmap in LDS) and the parallel
+    lexicographically-first rounds (OFX_SN_ROUNDS) — equal the oracle's sequential loop: ~250k vertices with
+    few nodes (cov 0.05), ~25k vertices with many (cov 0.008)."""
+    if form == "rounds":
+        monkeypatch.setenv("OFX_SN_ROUNDS", "1")
+    m, mg = _noisy_depth_mesh(cuda, size, size)
+    ne = mg.erode(1, 3)
+    pos, idx = mg.sample_nodes(ne, cov)
+    if form == "greedy":
+        assert mg.sample_rounds == 0
+    opos, oidx = fo.sample_nodes(m["vertices"].cpu().numpy(), ne.cpu().numpy(), cov)
+    assert np.array_equal(idx.cpu().numpy(), oidx.reshape(-1)) and np.array_equal(pos.cpu().numpy(), opos)
+
+
+def test_sample_nodes_and_geodesic_large_mesh(cuda):
+    """A 512x512 grid-like noisy depth mesh (~250k vertices): sample_nodes equals the oracle's sequential
+    sampling; geodesic edges are deterministic and well formed (the Python Dijkstra is too slow here)."""
+    m, mg = _noisy_depth_mesh(cuda)
     ne = mg.erode(1, 3)
     pos, idx = mg.sample_nodes(ne, 0.05)
     vn = m["vertices"].cpu().numpy()
@@ -109,6 +129,7 @@ def test_sample_nodes_and_geodesic_large_mesh(cuda):
     E1, W1, D1, _ = mg.edges_geodesic(idx, 8, 0.05)
     E2, W2, D2, _ = mg.edges_geodesic(idx, 8, 0.05)
     assert torch.equal(E1, E2) and torch.equal(W1, W2) and torch.equal(D1, D2)
+    assert mg.geodesic_sequential < idx.shape[0] // 10      # the parallel form settles (almost) every node
     E = E1.cpu().numpy()
     assert (E >= 0).all() and (E < idx.shape[0]).all()
     assert (E != np.arange(E.shape[0])[:, None]).all()
@@ -183,3 +204,23 @@ def test_update_graph_adds_nodes_and_arap_keeps_rest_pose(cuda):
     # add more nodes; the rest pose is kept either way
     wf.update_graph()
     assert np.allclose(wf.rotations, np.eye(3), atol=1e-5) and np.abs(wf.T_t.cpu().numpy()).max() < 1e-5
+
+
+@pytest.mark.parametrize("ov,en", [(True, True), (False, True), (True, False)])
+def test_geodesic_parallel_equals_sequential(cuda, monkeypatch, ov, en):
+    """The parallel relaxation form (one workgroup per node) and the sequential libstdc++-heap kernel give
+    identical edges, weights, distances and node->vertex distances on a ~66k-vertex noisy mesh (the
+    sequential kernel is pinned to the reference's C++ by the golden tests above)."""
+    m, mg = _noisy_depth_mesh(cuda, 256, 256)
+    ne = mg.erode(1, 3)
+    _, idx = mg.sample_nodes(ne, 0.03)
+    valid = ne if ov else None
+    par = mg.edges_geodesic(idx, 8, 0.03, ov, en, valid_vertices=valid, with_node_to_vertex=True)
+    n_seq = mg.geodesic_sequential
+    monkeypatch.setenv("OFX_GEO_SEQ", "1")
+    seq = mg.edges_geodesic(idx, 8, 0.03, ov, en, valid_vertices=valid, with_node_to_vertex=True)
+    assert mg.geodesic_sequential == idx.shape[0]
+    for a, b in zip(par, seq):
+        assert torch.equal(a, b)
+    assert n_seq < idx.shape[0] // 10
+

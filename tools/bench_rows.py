@@ -126,7 +126,7 @@ def main():
     rows["f4_graph"] = {"mesh_verts": int(verts.shape[0]), "mesh_faces": int(faces.shape[0]),
                         "nodes": int(idx.shape[0]), "sample_rounds": int(mg.sample_rounds),
                         "ms_adjacency": 1e3 * t_gc, "ms_erode": 1e3 * t_er, "ms_sample_nodes": 1e3 * t_sn,
-                        "ms_edges_geodesic": 1e3 * t_geo, "ms_cleanup": 1e3 * t_cu, "ms_clusters": 1e3 * t_cl,
+                        "ms_edges_geodesic": 1e3 * t_geo, "geodesic_sequential_nodes": int(mg.geodesic_sequential), "ms_cleanup": 1e3 * t_cu, "ms_clusters": 1e3 * t_cl,
                         "ms_from_mesh_total": 1e3 * t_all, "nodes_after_cleanup": int(gr.nodes.shape[0])}
 
     # ---- CPU: the reference's compiled C++ on the same inputs (this host)

@@ -262,7 +262,9 @@ int ofx_graph_destroy(void* handle);
 int ofx_graph_adjacency(void* handle, int32_t* rowptr, int32_t* col, int64_t* n_col, ofx_stream_t s);
 /* non_eroded u8[V] */
 int ofx_erode_mesh(void* handle, int32_t n_iterations, int32_t min_neighbors, uint8_t* non_eroded, ofx_stream_t s);
-/* node_positions f32[V*3] / node_indices i32[V] capacity; *n_nodes written (host); *n_rounds: parallel rounds */
+/* node_positions f32[V*3] / node_indices i32[V] capacity; *n_nodes written (host); *n_rounds: batches of the
+ * single-workgroup greedy form (meshes up to ~1.29M vertices), else launches of the parallel round form
+ * (OFX_SN_ROUNDS=1 forces it) */
 int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverage, int32_t use_only_non_eroded,
                      float* node_positions, int32_t* node_indices, int64_t* n_nodes, int64_t* n_rounds,
                      ofx_stream_t s);

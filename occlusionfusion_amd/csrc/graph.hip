@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -141,10 +142,9 @@ __global__ __launch_bounds__(256) void k_sn_bounds(const uint32_t* __restrict__ 
   if (i == nv - 1 || key[i + 1] != key[i]) end[key[i]] = (int32_t)(i + 1);
 }
 
-// pass 0: count, pass 1: fill the conflicting eligible vertices of every eligible vertex — lower ids for the
-// round/persistent forms (FWD = false), higher ids for the greedy form (FWD = true). Ascending id order is not
-// needed: decisions only depend on the set.
-template <bool FILL, bool FWD>
+// pass 0: count, pass 1: fill the lower-id conflicting eligible vertices of every eligible vertex (ascending
+// id order is not needed: decisions only depend on the set)
+template <bool FILL>
 __global__ __launch_bounds__(256) void k_sn_conflicts(const float* __restrict__ P, const uint8_t* __restrict__ elig, int64_t nv,
                                                       Grid g, const int32_t* __restrict__ start,
                                                       const int32_t* __restrict__ end, const int32_t* __restrict__ sorted,
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_sn_conflicts(const float* __restrict__ 
         seen[ns++] = h;
         for (int i = start[h]; i < end[h]; ++i) {
           const int32_t u = sorted[i];
-          if (FWD ? u <= v : u >= v) continue;
+          if (u >= v) continue;
           // (point - node).squaredNorm() <= c² with point = v, node = u (graph_proc.cpp:120); the f32
           // differences only change sign when the roles swap, so the test is symmetric bit for bit
           if (eig_sq(px - P[3 * u], py - P[3 * u + 1], pz - P[3 * u + 2]) <= cov2) {
@@ -256,20 +256,37 @@ __global__ __launch_bounds__(256) void k_sn_persistent(const uint8_t* __restrict
 }
 
 // greedy form (the C++ loop itself, graph_proc.cpp:100-131): ONE workgroup holds the undecided-vertex bitmap
-// in LDS (1 bit per vertex, <= 160 KiB). Each step wave 0 finds the lowest undecided vertex — it is the
-// sequential loop's next node: every lower vertex is a node or within c of one — and the workgroup clears the
-// bits of its higher-id conflicts. Steps = nodes (a few µs each: one barrier pair + the conflict list load);
-// the loop ends when the bitmap is empty (<= nv steps, no inter-workgroup waiting).
+// in LDS (1 bit per vertex, <= 160 KiB). A step takes the 64 lowest undecided vertices: the first is the
+// sequential loop's next node (every lower vertex is a node or within c of one); each later one is a node
+// iff no node chosen before it in the batch lies within c (a 64x64 conflict mask resolved in order by one
+// wave). The workgroup then clears, for every chosen node, the bits of all vertices within c, found in the
+// 27 hashed cells around it (positions in cell order, float4 + id). Steps <= nodes; the loop ends when the
+// bitmap is empty (<= nv steps, no inter-workgroup waiting).
 constexpr int kGreedyThreads = 1024;
-constexpr int64_t kGreedyMaxWords = 40 * 1024 - 64;   // 160 KiB of LDS minus a little
+constexpr int64_t kGreedyMaxWords = 40 * 1024 - 4096;   // 160 KiB of LDS minus the batch buffers (static LDS)
 
-__global__ __launch_bounds__(kGreedyThreads) void k_sn_greedy(const uint8_t* __restrict__ elig, int64_t nv,
-                                                               const int64_t* __restrict__ off,
-                                                               const int32_t* __restrict__ list,
-                                                               int32_t* __restrict__ state) {
+__global__ __launch_bounds__(256) void k_sn_spos(const float* __restrict__ P, const int32_t* __restrict__ sorted,
+                                                 int64_t nv, float4* __restrict__ spos) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  const int32_t u = sorted[i];
+  spos[i] = make_float4(P[3 * (int64_t)u], P[3 * (int64_t)u + 1], P[3 * (int64_t)u + 2], __int_as_float(u));
+}
+
+__global__ __launch_bounds__(kGreedyThreads) void k_sn_greedy(const float* __restrict__ P,
+                                                               const uint8_t* __restrict__ elig, int64_t nv, Grid gr,
+                                                               const int32_t* __restrict__ bstart,
+                                                               const int32_t* __restrict__ bend,
+                                                               const float4* __restrict__ spos, float cov2,
+                                                               int32_t* __restrict__ state,
+                                                               int64_t* __restrict__ n_steps, int64_t* __restrict__ stamps) {
   extern __shared__ uint32_t bits[];
-  __shared__ int64_t s_v, s_w;
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ int32_t s_cand[64];
+  __shared__ float4 s_sel[64];   // chosen nodes: position + id
+  __shared__ int32_t s_nsel;
+  __shared__ int64_t s_w;
+  __shared__ int32_t s_off[64 * 27], s_rs[64 * 27], s_wsum[kGreedyThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t nw = (nv + 31) >> 5;
   for (int64_t w = tid; w < nw; w += kGreedyThreads) {
     uint32_t x = 0;
@@ -280,36 +297,149 @@ __global__ __launch_bounds__(kGreedyThreads) void k_sn_greedy(const uint8_t* __r
   }
   __syncthreads();
   int64_t cw = 0;   // every word below cw is empty
-  for (int64_t step = 0; step < nv; ++step) {
-    if (tid < 64) {
-      int64_t v = -1;
-      for (; cw < nw; cw += 64) {
-        const uint32_t x = cw + lane < nw ? bits[cw + lane] : 0u;
+  int64_t step = 0;
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0}, t0 = wall_clock64();   // tuning: phase times (stamps != null)
+  for (; step < nv; ++step) {
+    if (wave == 0) {
+      // ---- the (up to) 64 lowest undecided vertices, in order
+      int got = 0;
+      int64_t first_w = -1;
+      for (int64_t w0 = cw; w0 < nw && got < 64 && (got == 0 || w0 < cw + 128); w0 += 64) {   // window: 4096 ids
+        const uint32_t x = w0 + lane < nw ? bits[w0 + lane] : 0u;
+        const int c = __popc(x);
+        int pre = c;   // inclusive prefix over lanes
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(pre, o);
+          if (lane >= o) pre += y;
+        }
         const uint64_t nz = __ballot(x != 0u);
-        if (nz) {
-          const int first = __builtin_ctzll(nz);
-          const uint32_t xw = __shfl(x, first);
-          cw += first;
-          v = (cw << 5) + __builtin_ctz(xw);
-          break;
+        if (first_w < 0 && nz) first_w = w0 + __builtin_ctzll(nz);
+        int slot = got + pre - c;
+        for (uint32_t y = x; y && slot < 64; y &= y - 1, ++slot)
+          s_cand[slot] = (int32_t)(((w0 + lane) << 5) + __builtin_ctz(y));
+        got += __shfl(pre, 63);
+      }
+      got = min(got, 64);
+      if (first_w >= 0) cw = first_w;
+      uint64_t ta = stamps ? wall_clock64() : 0;
+      // ---- in-batch resolution: lane i holds candidate i
+      const bool have = lane < got;
+      const int32_t v = have ? s_cand[lane] : 0;
+      const float px = have ? P[3 * (int64_t)v] : 0.f, py = have ? P[3 * (int64_t)v + 1] : 0.f,
+                  pz = have ? P[3 * (int64_t)v + 2] : 0.f;
+      const int ngot = __builtin_amdgcn_readfirstlane(got);   // uniform (SGPR) bound
+      uint64_t conf = 0;   // bit j: an earlier candidate j lies within c (point = this, node = j)
+#pragma unroll
+      for (int j = 0; j < 63; ++j) {   // constant lane indices: v_readlane into scalars
+        if (j + 1 >= ngot) break;
+        const float rx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), j));
+        const float ry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), j));
+        const float rz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz), j));
+        if (j < lane && eig_sq(px - rx, py - ry, pz - rz) <= cov2) conf |= 1ull << j;
+      }
+      uint64_t tb = stamps ? wall_clock64() : 0;
+      const uint32_t conf_lo = (uint32_t)conf, conf_hi = (uint32_t)(conf >> 32);
+      uint64_t sel = 0;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        if (i >= ngot) break;
+        const uint64_t row = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_lo, i) |
+                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_hi, i) << 32);
+        if (!(row & sel)) sel |= 1ull << i;
+      }
+      if (have && ((sel >> lane) & 1ull)) {
+        const int r = __popcll(sel & ((1ull << lane) - 1ull));
+        s_sel[r] = make_float4(px, py, pz, __int_as_float(v));
+        state[v] = kNode;
+      }
+      if (stamps) { const uint64_t tc = wall_clock64(); ph[4] += ta - t0; ph[5] += tb - ta; ph[6] += tc - tb; }
+      if (lane == 0) { s_nsel = __popcll(sel); s_w = got ? cw : -1; }
+    }
+    __syncthreads();
+    if (stamps) { const uint64_t t = wall_clock64(); ph[0] += t - t0; t0 = t; }
+    if (s_w < 0) break;
+    cw = s_w;
+    // ---- clear everything within c of the chosen nodes. Items = (node, cell): their bucket ranges load in
+    // one trip, a workgroup scan flattens them, and every thread tests 8 positions per trip.
+    const int nsel = s_nsel, items = nsel * 27;
+    int len2[2], rs2[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int it = 2 * tid + k;
+      len2[k] = 0; rs2[k] = 0;
+      if (it < items) {
+        const float4 q = s_sel[it / 27];
+        const int c = it % 27;
+        int cx, cy, cz;
+        const float qp[3] = {q.x, q.y, q.z};
+        cell_of(qp, gr.inv_cell, cx, cy, cz);
+        const int dx = c / 9 - 1, dy = (c / 3) % 3 - 1, dz = c % 3 - 1;
+        // skip a neighbour cell whose box lies farther than c (0.5 % margin; cells are 1.01·c wide)
+        const float cs = 1.f / gr.inv_cell;
+        const float gx = dx > 0 ? (cx + 1) * cs - q.x : dx < 0 ? q.x - cx * cs : 0.f;
+        const float gy = dy > 0 ? (cy + 1) * cs - q.y : dy < 0 ? q.y - cy * cs : 0.f;
+        const float gz = dz > 0 ? (cz + 1) * cs - q.z : dz < 0 ? q.z - cz * cs : 0.f;
+        if (fmaxf(gx, 0.f) * fmaxf(gx, 0.f) + fmaxf(gy, 0.f) * fmaxf(gy, 0.f) + fmaxf(gz, 0.f) * fmaxf(gz, 0.f) <=
+            cov2 * 1.01f) {
+          const uint32_t h = cell_hash(cx + dx, cy + dy, cz + dz, gr.mask);
+          rs2[k] = bstart[h];
+          len2[k] = bend[h] - rs2[k];
         }
       }
-      if (tid == 0) { s_v = v; s_w = cw; }
+    }
+    int x = len2[0] + len2[1];
+    const int own = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wsum[wave] = x;
+    __syncthreads();
+    int base = 0, total = 0;
+    for (int q = 0; q < kGreedyThreads / 64; ++q) {
+      const int wsum = s_wsum[q];
+      base += q < wave ? wsum : 0;
+      total += wsum;
+    }
+    {
+      const int ex = base + x - own;
+      if (2 * tid < items) { s_off[2 * tid] = ex; s_rs[2 * tid] = rs2[0]; }
+      if (2 * tid + 1 < items) { s_off[2 * tid + 1] = ex + len2[0]; s_rs[2 * tid + 1] = rs2[1]; }
     }
     __syncthreads();
-    const int64_t v = s_v;
-    cw = s_w;
-    if (v < 0) break;
-    const int64_t b = off[v], e = off[v + 1];
-    if (tid == 0) {
-      state[v] = kNode;
-      atomicAnd(&bits[v >> 5], ~(1u << (v & 31)));
-    }
-    for (int64_t i = b + tid; i < e; i += kGreedyThreads) {
-      const int32_t u = list[i];
-      atomicAnd(&bits[u >> 5], ~(1u << (u & 31)));
+    if (stamps) { const uint64_t t = wall_clock64(); ph[1] += t - t0; t0 = t; ph[3] += total; }
+    for (int e0 = 8 * tid; e0 < total; e0 += 8 * kGreedyThreads) {   // 8 consecutive positions per thread
+      int lo = 0, hi = items - 1;   // last item with s_off <= e0 (one search, then walk)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= e0) lo = mid; else hi = mid - 1;
+      }
+      float4 u[8];
+      int itm[8];
+      int it = lo, nxt = it + 1 < items ? s_off[it + 1] : total;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e0 + k;
+        while (e >= nxt && it + 1 < items) { ++it; nxt = it + 1 < items ? s_off[it + 1] : total; }
+        itm[k] = e < total ? it : -1;
+        u[k] = spos[e < total ? s_rs[it] + (e - s_off[it]) : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (itm[k] < 0) continue;
+        const float4 q = s_sel[itm[k] / 27];
+        if (eig_sq(u[k].x - q.x, u[k].y - q.y, u[k].z - q.z) <= cov2) {
+          const int32_t uid = __float_as_int(u[k].w);
+          atomicAnd(&bits[uid >> 5], ~(1u << (uid & 31)));
+        }
+      }
     }
     __syncthreads();
+    if (stamps) { const uint64_t t = wall_clock64(); ph[2] += t - t0; t0 = t; }
+  }
+  if (tid == 0) {
+    *n_steps = step;
+    if (stamps) for (int q = 0; q < 7; ++q) stamps[q] = (int64_t)ph[q];
   }
 }
 
@@ -789,6 +919,7 @@ struct Graph {
   const float* P = nullptr;
   const int32_t* faces = nullptr;
   int64_t geo_sequential = 0;   // nodes the last ofx_edges_geodesic ran through the sequential heap kernel
+  int64_t sn_steps = 0;         // batches of the last greedy sample_nodes
 };
 
 template <typename T>
@@ -1006,40 +1137,48 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   // the greedy form when the bitmap fits one workgroup's LDS (1.28M vertices), else the parallel rounds
   const int64_t nwords = (nv + 31) >> 5;
   const bool greedy = nwords <= kGreedyMaxWords && !getenv("OFX_SN_ROUNDS");
-  OFX_CHECKS(dalloc(&cnt, nv + 1, hs));
-  OFX_HIP(hipMemsetAsync(cnt, 0, (nv + 1) * sizeof(int32_t), hs));
-  if (greedy)
-    hipLaunchKernelGGL((k_sn_conflicts<false, true>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
-                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
-                       (const int64_t*)nullptr, (int32_t*)nullptr);
-  else
-    hipLaunchKernelGGL((k_sn_conflicts<false, false>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
-                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
-                       (const int64_t*)nullptr, (int32_t*)nullptr);
-  OFX_CHECKS(dalloc(&off, nv + 1, hs));
-  OFX_CHECKS(exclusive_sum_i32_to_i64(cnt, off, nv + 1, hs));
-  int64_t total = 0;
-  OFX_CHECKS(read1(off + nv, &total, hs));
-  OFX_CHECKS(dalloc(&list, std::max<int64_t>(total, 1), hs));
-  if (greedy)
-    hipLaunchKernelGGL((k_sn_conflicts<true, true>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
-                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
-                       (const int64_t*)off, list);
-  else
-    hipLaunchKernelGGL((k_sn_conflicts<true, false>), gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
-                       (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
-                       (const int64_t*)off, list);
   OFX_CHECKS(dalloc(&state, nv, hs));
   OFX_HIP(hipMemsetAsync(state, 0, nv * sizeof(int32_t), hs));
   constexpr int kChunk = 32;
   int64_t rounds = 0, nr = 0;
   if (greedy) {
+    float4* spos = nullptr;
+    int64_t* steps = nullptr;
+    const bool stamp = getenv("OFX_SN_STAMPS") != nullptr;   // tuning: per-phase times to stderr
+    OFX_CHECKS(dalloc(&spos, nv, hs));
+    OFX_CHECKS(dalloc(&steps, 8, hs));
+    hipLaunchKernelGGL(k_sn_spos, gv, dim3(256), 0, hs, g->P, (const int32_t*)sorted, nv, spos);
     const size_t lds = (size_t)nwords * sizeof(uint32_t);
     OFX_HIP(hipFuncSetAttribute((const void*)k_sn_greedy, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_sn_greedy, dim3(1), dim3(kGreedyThreads), lds, hs, (const uint8_t*)elig, nv,
-                       (const int64_t*)off, (const int32_t*)list, state);
+    hipLaunchKernelGGL(k_sn_greedy, dim3(1), dim3(kGreedyThreads), lds, hs, g->P, (const uint8_t*)elig, nv, gr,
+                       (const int32_t*)bstart, (const int32_t*)bend, (const float4*)spos, cov2, state, steps,
+                       stamp ? steps + 1 : nullptr);
     OFX_LAUNCH_CHECK();
+    OFX_CHECKS(read1(steps, &g->sn_steps, hs));
+    if (stamp) {
+      int64_t st[7];
+      OFX_HIP(hipMemcpy(st, steps + 1, sizeof(st), hipMemcpyDeviceToHost));
+      fprintf(stderr, "k_sn_greedy: %lld steps; find+resolve %.1f us (find %.1f, positions+conflicts %.1f, "
+              "resolve %.1f), ranges+scan %.1f us, clear %.1f us (100 MHz clock); %lld positions tested\n",
+              (long long)g->sn_steps, st[0] * 1e-2, st[4] * 1e-2, st[5] * 1e-2, st[6] * 1e-2, st[1] * 1e-2,
+              st[2] * 1e-2, (long long)st[3]);
+    }
+    dfree(spos, hs);
+    dfree(steps, hs);
   } else {
+  OFX_CHECKS(dalloc(&cnt, nv + 1, hs));
+  OFX_HIP(hipMemsetAsync(cnt, 0, (nv + 1) * sizeof(int32_t), hs));
+  hipLaunchKernelGGL(k_sn_conflicts<false>, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                     (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                     (const int64_t*)nullptr, (int32_t*)nullptr);
+  OFX_CHECKS(dalloc(&off, nv + 1, hs));
+  OFX_CHECKS(exclusive_sum_i32_to_i64(cnt, off, nv + 1, hs));
+  int64_t total = 0;
+  OFX_CHECKS(read1(off + nv, &total, hs));
+  OFX_CHECKS(dalloc(&list, std::max<int64_t>(total, 1), hs));
+  hipLaunchKernelGGL(k_sn_conflicts<true>, gv, dim3(256), 0, hs, g->P, (const uint8_t*)elig, nv, gr,
+                     (const int32_t*)bstart, (const int32_t*)bend, (const int32_t*)sorted, cov2, cnt,
+                     (const int64_t*)off, list);
   OFX_CHECKS(dalloc(&cursor, nv, hs));
   OFX_HIP(hipMemcpyAsync(cursor, off, nv * sizeof(int64_t), hipMemcpyDeviceToDevice, hs));
   OFX_CHECKS(dalloc(&und, kChunk, hs));
@@ -1083,9 +1222,9 @@ int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverag
   int32_t nn = 0;
   OFX_CHECKS(read1(rank + nv, &nn, hs));
   *n_nodes = nn;
-  // 0: greedy pass (or persistent pass + one round); > 0: round-form launches after the persistent pass;
-  // < 0: the persistent pass timed out
-  if (n_rounds) *n_rounds = rounds < 0 ? -nr : nr;
+  // greedy form: its batches (<= nodes); rounds form: launches of the round kernel after the persistent pass
+  // (negative: the persistent pass timed out)
+  if (n_rounds) *n_rounds = greedy ? g->sn_steps : (rounds < 0 ? -nr : nr);
   for (void* p : {(void*)elig, (void*)state, (void*)is_node, (void*)key, (void*)key2, (void*)val, (void*)sorted,
                   (void*)bstart, (void*)bend, (void*)cnt, (void*)list, (void*)rank, (void*)und, (void*)off,
                   (void*)cursor})

@@ -111,8 +111,8 @@ def test_sample_nodes_forms_large_mesh(cuda, monkeypatch, form, cov, size):
     m, mg = _noisy_depth_mesh(cuda, size, size)
     ne = mg.erode(1, 3)
     pos, idx = mg.sample_nodes(ne, cov)
-    if form == "greedy":
-        assert mg.sample_rounds == 0
+    if form == "greedy":   # batches of 64 candidates: at most one per node
+        assert 0 < mg.sample_rounds <= idx.shape[0]
     opos, oidx = fo.sample_nodes(m["vertices"].cpu().numpy(), ne.cpu().numpy(), cov)
     assert np.array_equal(idx.cpu().numpy(), oidx.reshape(-1)) and np.array_equal(pos.cpu().numpy(), opos)
 

@@ -188,7 +188,8 @@ int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam,
                    double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s);
 
 /* ---------------- Surface extraction ----------------
- * Whole volume only (a shard needs a halo: OFX_ERR_ARG). Voxel-index coordinates as skimage returns. */
+ * Voxel-index coordinates as skimage returns. ofx_truncated_region / ofx_mesh_count take the whole volume;
+ * ofx_mesh_count_range takes a shard whose stored bricks include a halo (see there). */
 /* TSDFVolume.compute_truncated_region (tsdf.py:704-745): mask u8 per voxel slot (bricked layout) */
 int ofx_truncated_region(const ofx_volume_desc* desc, const float* tsdf, double max_diff, uint8_t* mask,
                          ofx_stream_t s);
@@ -205,6 +206,15 @@ int ofx_mesh_count(void* handle, const ofx_volume_desc* desc, const float* tsdf,
                    int32_t use_mask, float level, int64_t* n_verts, int64_t* n_faces, ofx_stream_t s);
 int ofx_mesh_emit(void* handle, float* verts, int32_t* faces, float* normals, float* values, int64_t* keys,
                   ofx_stream_t s);
+/* Sharded marching cubes: like ofx_mesh_count on a shard desc (bricks [brick_x0, brick_x1), holding the
+ * shard's own bricks plus halo bricks copied from its neighbours), processing only the cells whose far corner
+ * x lies in [px0, px1) — the shard's own planes. px0 >= 8*brick_x0 + 2 unless brick_x0 = 0, px1 <= 8*brick_x1 - 2
+ * unless the shard reaches the volume's end (the truncated-region test and the vertex normals read ±2 planes).
+ * The emitted vertices are those the shard's cells use, in global order (keys identify them across shards);
+ * the full volume's mesh is the key-merge of the shards' meshes (occlusionfusion_amd.sharding). */
+int ofx_mesh_count_range(void* handle, const ofx_volume_desc* desc, const float* tsdf, const uint8_t* mask,
+                         double max_diff, int32_t use_mask, float level, int32_t px0, int32_t px1, int64_t* n_verts,
+                         int64_t* n_faces, ofx_stream_t s);
 /* get_mesh / get_point_cloud epilogue (tsdf.py:757-767,796-807): world = verts*f32(voxel_size) + origin
  * (f32, may be NULL) and colours u8[V*3] = [r,g,b] of the voxel nearest each vertex (may be NULL). */
 int ofx_mesh_finish(const ofx_volume_desc* desc, const float* color, const float* verts, int64_t n_verts,

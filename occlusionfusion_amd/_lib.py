@@ -67,6 +67,7 @@ _SIGS = {
     "ofx_mesh_create": [P],
     "ofx_mesh_destroy": [P],
     "ofx_mesh_count": [P, P, P, P, c_double, c_int32, c_float, P, P, P],
+    "ofx_mesh_count_range": [P, P, P, P, c_double, c_int32, c_float, c_int32, c_int32, P, P, P],
     "ofx_mesh_emit": [P, P, P, P, P, P, P],
     "ofx_mesh_finish": [P, P, P, c_int64, P, P, P],
     "ofx_backproject_depth": [P, c_int32, c_int32, c_int32, c_float, c_float, c_float, c_float, c_float, P, P],

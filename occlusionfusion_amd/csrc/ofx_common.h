@@ -45,6 +45,7 @@ struct BrickGeom {
   int32_t Dx, Dy, Dz;
   int32_t nbx, nby, nbz;   // full-volume brick counts
   int32_t bx0, bx1;        // shard range along x
+  int32_t px0, px1;        // marching cubes: far corners processed along x (whole volume: [0, Dx))
   int64_t n_bricks;        // bricks in shard
   float ox, oy, oz;
   double vs;
@@ -60,6 +61,7 @@ inline int make_geom(const ofx_volume_desc* d, BrickGeom* g) {
   g->bx0 = d->brick_x0; g->bx1 = d->brick_x1;
   if (g->bx0 < 0 || g->bx1 > g->nbx || g->bx0 >= g->bx1) { set_error("bad brick shard range [%d,%d) of %d", g->bx0, g->bx1, g->nbx); return OFX_ERR_ARG; }
   g->n_bricks = (int64_t)(g->bx1 - g->bx0) * g->nby * g->nbz;
+  g->px0 = 0; g->px1 = g->Dx;
   g->ox = d->origin[0]; g->oy = d->origin[1]; g->oz = d->origin[2];
   g->vs = d->voxel_size;
   return OFX_OK;

@@ -9,6 +9,9 @@
 """
 
 
+import torch
+
+
 def shard_bricks(n_bricks_x, rank, world):
     """Contiguous x-slab of bricks for `rank` of `world`: returns (x0, x1)."""
     if world < 1 or not 0 <= rank < world:
@@ -23,3 +26,100 @@ def match_range(n_matches, rank, world):
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad rank/world {rank}/{world}")
     return (n_matches * rank) // world, (n_matches * (rank + 1)) // world
+
+
+def _order_keys(keys, dims):
+    """Marching-cubes vertex key (C-index of the edge start · 3 + axis) -> its position in the whole volume's
+    vertex order (brick-major, then voxel within the 8³ brick, then axis: mesh.hip k_mc_vemit)."""
+    Dy, Dz = int(dims[1]), int(dims[2])
+    nby, nbz = (Dy + 7) // 8, (Dz + 7) // 8
+    a = keys % 3
+    lin = keys // 3
+    z = lin % Dz
+    y = (lin // Dz) % Dy
+    x = lin // (Dz * Dy)
+    brick = ((x // 8) * nby + (y // 8)) * nbz + (z // 8)
+    local = (x % 8) * 64 + (y % 8) * 8 + (z % 8)
+    return (brick * 512 + local) * 3 + a
+
+
+def merge_shard_meshes(parts, dims):
+    """Whole-volume mesh from per-shard parts (TSDFVolume.extract_mesh_shard, in rank order): vertices are the
+    union by key in the whole volume's order (a vertex on a slab boundary appears in both neighbours' parts,
+    bit-identical), faces the concatenation with indices remapped. -> dict with the parts' keys."""
+    okeys = torch.cat([_order_keys(p["keys"], dims) for p in parts])
+    uniq, inv = torch.unique(okeys, sorted=True, return_inverse=True)
+    V = int(uniq.shape[0])
+    out = {}
+    for name in ("verts", "normals", "values", "keys", "world", "colors"):
+        if any(p.get(name) is None for p in parts):
+            continue
+        src = torch.cat([p[name] for p in parts])
+        dst = torch.empty((V,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        dst[inv] = src   # duplicates carry identical values
+        out[name] = dst
+    faces, base = [], 0
+    for p in parts:
+        n = int(p["keys"].shape[0])
+        faces.append(inv[base:base + n][p["faces"].long()].to(torch.int32))
+        base += n
+    out["faces"] = torch.cat(faces) if faces else torch.empty((0, 3), dtype=torch.int32)
+    return out
+
+
+def exchange_boundary(first, last, group=None):
+    """Halo exchange along the slab chain: send `first` to rank-1 and `last` to rank+1; returns (lo, hi) =
+    (rank-1's last, rank+1's first), None at the chain's ends. One send/recv pair per neighbour
+    (RCCL point-to-point over xGMI on GPUs; gloo on CPU tensors)."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    lo = torch.empty_like(last) if rank > 0 else None
+    hi = torch.empty_like(first) if rank < world - 1 else None
+    ops = []
+    if rank > 0:
+        ops += [dist.P2POp(dist.isend, first.contiguous(), _global(rank - 1, group), group),
+                dist.P2POp(dist.irecv, lo, _global(rank - 1, group), group)]
+    if rank < world - 1:
+        ops += [dist.P2POp(dist.isend, last.contiguous(), _global(rank + 1, group), group),
+                dist.P2POp(dist.irecv, hi, _global(rank + 1, group), group)]
+    if ops:
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    return lo, hi
+
+
+def _global(r, group):
+    import torch.distributed as dist
+    return r if group is None else dist.get_global_rank(group, r)
+
+
+def _all_gather_var(t, group=None):
+    """all_gather of tensors whose first dimension differs per rank (padded to the largest)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    m = max(ns)
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return [o[:k] for o, k in zip(outs, ns)]
+
+
+def gather_mesh_parts(part, group=None):
+    """Every rank's extract_mesh_shard part, in rank order, on every rank."""
+    names = [k for k, v in part.items() if v is not None]
+    cols = {k: _all_gather_var(part[k], group) for k in names}
+    world = len(next(iter(cols.values())))
+    return [{k: cols[k][r] for k in names} for r in range(world)]
+
+
+def extract_mesh_distributed(vol, group=None, **kw):
+    """Marching cubes of a slab-sharded volume across ranks: halo exchange, per-rank mesh of its own cells,
+    all-gather, key merge -> the whole volume's mesh on every rank (device dict as merge_shard_meshes)."""
+    lo, hi = exchange_boundary(*vol.boundary_columns(), group=group)
+    part = vol.extract_mesh_shard(lo, hi, **kw)
+    return merge_shard_meshes(gather_mesh_parts(part, group), vol._vol_dim)

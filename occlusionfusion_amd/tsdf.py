@@ -304,6 +304,61 @@ class TSDFVolume:
              ptr(out["values"]), ptr(out["keys"]), stream_ptr())
         return out
 
+    def brick_column_slots(self):
+        """Voxel slots of one brick column (one x-brick of the bricked layout: ny·nz bricks of 512)."""
+        return int((self._vol_dim[1] + 7) // 8) * int((self._vol_dim[2] + 7) // 8) * 512
+
+    def boundary_columns(self):
+        """(first, last) brick columns of this shard as (2, slots) device tensors [tsdf; colour] — what the
+        neighbouring shards need as marching-cubes halo (sharding.exchange_boundary)."""
+        c = self.brick_column_slots()
+        first = torch.stack([self.tsdf_b[:c], self.color_b[:c]])
+        last = torch.stack([self.tsdf_b[-c:], self.color_b[-c:]])
+        return first, last
+
+    def extract_mesh_shard(self, lo=None, hi=None, use_mask=True, level=0.0, max_diff=1.2, with_normals=True,
+                           with_values=False):
+        """Marching cubes of this shard's own cells (far corners in its x-slab) -> device dict: verts (V,3)
+        voxel coordinates, faces (F,3) int32 into this part's vertices, keys (V,) int64, normals, values, world
+        (V,3) f32 and colors (V,3) u8. lo / hi: the neighbours' last / first brick columns as (2, slots)
+        [tsdf; colour] tensors (None at the volume's ends). sharding.merge_shard_meshes of the parts in rank
+        order is the whole volume's extract_mesh_device + get_mesh colours, bit for bit (include/ofx.h
+        ofx_mesh_count_range)."""
+        nbx = int((self._vol_dim[0] + 7) // 8)
+        x0, x1 = self.brick_x0, self.brick_x1
+        if (x0 > 0) != (lo is not None) or (x1 < nbx) != (hi is not None):
+            raise ValueError(f"shard bricks [{x0},{x1}) of {nbx}: halo columns needed below: {x0 > 0}, above: {x1 < nbx}")
+        c = self.brick_column_slots()
+        for h in (lo, hi):
+            if h is not None and tuple(h.shape) != (2, c):
+                raise ValueError(f"halo column must be (2, {c}), got {tuple(h.shape)}")
+        tsdf = torch.cat(([lo[0]] if lo is not None else []) + [self.tsdf_b] + ([hi[0]] if hi is not None else []))
+        color = torch.cat(([lo[1]] if lo is not None else []) + [self.color_b] + ([hi[1]] if hi is not None else []))
+        desc = _lib.VolumeDesc.from_buffer_copy(self.desc)
+        desc.brick_x0 = x0 - (1 if lo is not None else 0)
+        desc.brick_x1 = x1 + (1 if hi is not None else 0)
+        if getattr(self, "_mesh_h", None) is None:
+            h = _lib.c_void_p()
+            call("ofx_mesh_create", byref(h))
+            self._mesh_h = h
+        nv, nf = _lib.c_int64(), _lib.c_int64()
+        call("ofx_mesh_count_range", self._mesh_h, byref(desc), ptr(tsdf), None, float(max_diff), 1 if use_mask else 0,
+             float(level), 8 * x0, min(8 * x1, int(self._vol_dim[0])), byref(nv), byref(nf), stream_ptr())
+        V, F = int(nv.value), int(nf.value)
+        kw = dict(device=self.device)
+        out = {"verts": torch.empty((V, 3), dtype=torch.float32, **kw),
+               "faces": torch.empty((F, 3), dtype=torch.int32, **kw),
+               "normals": torch.empty((V, 3), dtype=torch.float32, **kw) if with_normals else None,
+               "values": torch.empty(V, dtype=torch.float32, **kw) if with_values else None,
+               "keys": torch.empty(V, dtype=torch.int64, **kw)}
+        call("ofx_mesh_emit", self._mesh_h, ptr(out["verts"]), ptr(out["faces"]), ptr(out["normals"]),
+             ptr(out["values"]), ptr(out["keys"]), stream_ptr())
+        out["world"] = torch.empty((V, 3), dtype=torch.float32, **kw)
+        out["colors"] = torch.empty((V, 3), dtype=torch.uint8, **kw)
+        call("ofx_mesh_finish", byref(desc), ptr(color), ptr(out["verts"]), V, ptr(out["world"]), ptr(out["colors"]),
+             stream_ptr())
+        return out
+
     def _mesh_world_colors(self, verts):
         V = verts.shape[0]
         world = torch.empty((V, 3), dtype=torch.float32, device=self.device)

@@ -4,6 +4,9 @@
    slabs equals the single-process volume bit for bit (voxels are independent, no halo).
 2. Match-sharded GN: each rank linearises its match range (sharding.match_range), rank 0 adds the
    ARAP + motion rows; all_reduce(sum) of (A, b, loss²) equals the full system.
+3. Sharded surface extraction plumbing (world 3): the halo exchange along the slab chain delivers each
+   neighbour's boundary column, and gathering + key-merging per-rank mesh parts rebuilds the whole mesh (the
+   per-shard marching cubes itself runs on the GPU: tests/test_gpu_mesh.py).
 """
 import os
 import socket
@@ -107,6 +110,43 @@ def gn_shard_job(rank, world):
     return bool(np.allclose(A.numpy(), full["A"], rtol=1e-12, atol=1e-12)
                 and np.allclose(b.numpy(), full["b"], rtol=1e-12, atol=1e-14)
                 and abs(l2.item() - full["loss2"]) <= 1e-12 * max(1.0, full["loss2"]))
+
+
+def mesh_plumbing_job(rank, world):
+    from occlusionfusion_amd.sharding import (_order_keys, exchange_boundary, gather_mesh_parts,
+                                              merge_shard_meshes)
+    # halo exchange: rank r's first / last columns are filled with 10r + 1 / 10r + 2
+    first, last = torch.full((2, 5), 10.0 * rank + 1), torch.full((2, 5), 10.0 * rank + 2)
+    lo, hi = exchange_boundary(first, last)
+    ok = (lo is None) == (rank == 0) and (hi is None) == (rank == world - 1)
+    ok &= lo is None or bool((lo == 10.0 * (rank - 1) + 2).all())
+    ok &= hi is None or bool((hi == 10.0 * (rank + 1) + 1).all())
+    # a whole mesh in the volume's vertex order; rank r holds a contiguous range of its faces and the
+    # vertices those faces use (boundary vertices appear in two parts)
+    dims = np.array([24, 9, 10])
+    rng = np.random.default_rng(7)
+    keys = torch.from_numpy(rng.choice(24 * 9 * 10 * 3, 300, replace=False).astype(np.int64))
+    keys = keys[torch.argsort(_order_keys(keys, dims))]
+    faces = torch.from_numpy(rng.integers(0, 300, (400, 3)).astype(np.int32))
+    used = torch.unique(faces.long())
+    remap = torch.full((300,), -1, dtype=torch.int64)
+    remap[used] = torch.arange(used.numel())
+    whole = {"keys": keys[used], "verts": keys[used].float()[:, None].repeat(1, 3), "faces": remap[faces.long()].int()}
+    f0, f1 = (400 * rank) // world, (400 * (rank + 1)) // world
+    pf = whole["faces"][f0:f1].long()
+    pv = torch.unique(pf)
+    loc = torch.full((whole["keys"].numel(),), -1, dtype=torch.int64)
+    loc[pv] = torch.arange(pv.numel())
+    part = {"keys": whole["keys"][pv], "verts": whole["verts"][pv], "faces": loc[pf].int()}
+    merged = merge_shard_meshes(gather_mesh_parts(part), dims)
+    ok &= torch.equal(merged["keys"], whole["keys"]) and torch.equal(merged["verts"], whole["verts"])
+    ok &= torch.equal(merged["faces"], whole["faces"])
+    return bool(ok)
+
+
+def test_mesh_halo_exchange_and_merge_world3():
+    out = _run(mesh_plumbing_job, world=3)
+    assert out == {0: True, 1: True, 2: True}, out
 
 
 @pytest.mark.slow

@@ -113,6 +113,77 @@ def test_unmasked_sphere_point_cloud_closed_surface(cuda):
     np.testing.assert_array_equal(pc[order, 3:].astype(np.uint8), fo.mesh_colors(ref[0], col))
 
 
+def _shards_of(full, world):
+    """Slab shards holding the full volume's bricks (the bricked layout is x-column-major: a slice)."""
+    from occlusionfusion_amd import TSDFVolume
+    out = []
+    c = full.brick_column_slots()
+    for r in range(world):
+        sh = TSDFVolume.from_grid(full._vol_origin, full._voxel_size, full._vol_dim,
+                                  (full.cam_intr[0, 0], full.cam_intr[1, 1], full.cam_intr[0, 2], full.cam_intr[1, 2]),
+                                  _Opt(), shard=(r, world))
+        sh.tsdf_b.copy_(full.tsdf_b[c * sh.brick_x0: c * sh.brick_x1])
+        sh.color_b.copy_(full.color_b[c * sh.brick_x0: c * sh.brick_x1])
+        out.append(sh)
+    return out
+
+
+def _sharded_mesh(shards, **kw):
+    from occlusionfusion_amd.sharding import merge_shard_meshes
+    parts = []
+    for r, sh in enumerate(shards):
+        lo = shards[r - 1].boundary_columns()[1] if r > 0 else None
+        hi = shards[r + 1].boundary_columns()[0] if r < len(shards) - 1 else None
+        parts.append(sh.extract_mesh_shard(lo, hi, with_values=True, **kw))
+    return merge_shard_meshes(parts, shards[0]._vol_dim), parts
+
+
+def _assert_same_mesh(merged, full, use_mask):
+    m = full.extract_mesh_device(use_mask=use_mask, with_values=True, with_keys=True)
+    world, colors = full._mesh_world_colors(m["verts"])
+    for name, ref in (("verts", m["verts"]), ("faces", m["faces"]), ("normals", m["normals"]),
+                      ("values", m["values"]), ("keys", m["keys"]), ("world", world), ("colors", colors)):
+        assert torch.equal(merged[name], ref), name
+    return m
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_marching_cubes_equals_whole_volume(cuda, golden_dir, world):
+    """Slab-sharded get_mesh (halo of one brick column per neighbour, each shard meshing
+    the cells whose far corner lies in its slab, key merge) == the whole volume's, bit for bit: vertices,
+    vertex order, faces, normals, values, world coordinates and colours."""
+    vol, g = _fused_small(golden_dir)
+    merged, parts = _sharded_mesh(_shards_of(vol, world), use_mask=True, max_diff=1.2)
+    m = _assert_same_mesh(merged, vol, True)
+    assert m["faces"].shape[0] > 500
+    if world > 1:   # vertices on the slab boundaries are shared by two parts
+        assert sum(p["keys"].shape[0] for p in parts) > m["keys"].shape[0]
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_sharded_point_cloud_sphere_across_slabs(cuda, world):
+    """Unmasked marching cubes of a sphere cut by every slab boundary (5 shards of 40 voxels: one brick
+    column each) == the whole volume's."""
+    X = np.arange(40)[:, None, None]
+    Y = np.arange(36)[None, :, None]
+    Z = np.arange(45)[None, None, :]
+    sdf = (np.sqrt((X - 19.3) ** 2 + (Y - 17.6) ** 2 + (Z - 22.1) ** 2) - 15.4).astype(np.float32)
+    col = ((X * 3 % 256) * 65536 + (Y * 5 % 256) * 256 + (Z * 7 % 256) + 0 * sdf).astype(np.float32)
+    vol = _volume_from(sdf, col)
+    merged, _ = _sharded_mesh(_shards_of(vol, world), use_mask=False)
+    _assert_same_mesh(merged, vol, False)
+
+
+def test_mesh_shard_halo_arguments(cuda):
+    from occlusionfusion_amd import TSDFVolume
+    sh = TSDFVolume.from_grid(np.zeros(3, np.float32), 0.01, (32, 8, 8), (1.0, 1.0, 0.0, 0.0), _Opt(), shard=(1, 3))
+    with pytest.raises(ValueError):
+        sh.extract_mesh_shard()                      # a middle shard needs both halo columns
+    c = sh.brick_column_slots()
+    with pytest.raises(ValueError):
+        sh.extract_mesh_shard(torch.zeros((2, c - 1), device=sh.device), torch.zeros((2, c), device=sh.device))
+
+
 def test_mesh_empty_and_sharded_refused(cuda):
     from occlusionfusion_amd import TSDFVolume, _lib
     vol = _volume_from(np.ones((10, 12, 9), np.float32))

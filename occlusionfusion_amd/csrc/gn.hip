@@ -679,23 +679,116 @@ __device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, 
   const int n = wg * (kBlk / 64) + (threadIdx.x >> 6);
   if (n >= g.N) return;
   const int lane = threadIdx.x & 63;
-  const int slot = lane / 6, c = lane % 6;
-  double v = 0.0;
-  if (slot < kRhsSlots) {
-    const int b = g.node_off[n], e = g.node_off[n + 1];
-#pragma unroll 2
-    for (int k = b + slot; k < e; k += kRhsSlots) {
-      const int code = g.node_list[k];
-      const int64_t t = code >> 2;
-      const double* Jp = g.J + t * 72 + 18 * (code & 3);
+  // one wave per node, one list entry per lane (two per lane per pass: a busy node's ~90 terms in one
+  // pass of two dependent trips — code, then J + r — where 10 slots took ~10 serial passes); every load
+  // unconditional (clamped index, masked value) so no branch splits a trip; fixed-order wave sums
+  const int b = g.node_off[n], e = g.node_off[n + 1];
+  double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int k0 = b; k0 < e; k0 += 128) {
+    int code[2];
+    bool ok[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = k0 + lane + 64 * j;
+      ok[j] = k < e;
+      code[j] = g.node_list[ok[j] ? k : e - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t t = code[j] >> 2;
+      const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code[j] & 3));
       const double* rr = g.res + 3 * t;
-      v += Jp[c] * rr[0] + Jp[6 + c] * rr[1] + Jp[12 + c] * rr[2];
+      double P[18];
+#pragma unroll
+      for (int u = 0; u < 9; ++u) { const double2 x = Jp[u]; P[2 * u] = x.x; P[2 * u + 1] = x.y; }
+      const double r0 = rr[0], r1 = rr[1], r2 = rr[2];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double t3 = P[c] * r0 + P[6 + c] * r1 + P[12 + c] * r2;
+        v[c] += ok[j] ? t3 : 0.0;
+      }
     }
   }
-  double tot = 0.0;
 #pragma unroll
-  for (int q = 0; q < kRhsSlots; ++q) tot += __shfl(v, q * 6 + c);
-  if (lane < 6) rhs[6 * (int64_t)n + c] = -tot;
+  for (int c = 0; c < 6; ++c) v[c] = wave_sum(v[c]);
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) rhs[6 * (int64_t)n + c] = -v[c];
+}
+
+// JᵀJ blocks, workgroup-cooperative: the workgroup's 16 blocks own one contiguous range of the sorted
+// contribution list. Chunks of kCoop entries: one thread per entry loads its two Jacobian blocks (the next
+// chunk's codes one chunk ahead) and writes the full 6×6 product to LDS ([output][entry], padded: conflict-
+// free writes); then each (block, output) pair — 576 per workgroup, up to 3 per thread — adds its entries of
+// the chunk in list order. A block's cost is its share of the workgroup's entries, not its own list length
+// (the 16-lane form took ceil(len/16) dependent trips: ~6 for a busy node's diagonal block).
+constexpr int kCoop = 128;
+__device__ __forceinline__ void blocks_coop(const Gn& g, double* __restrict__ A, int64_t wg, double lm) {
+  __shared__ double s_prod[36 * (kCoop + 1)];
+  __shared__ int s_off[17];
+  const int tid = threadIdx.x;
+  const int64_t sb = wg * (kBlk / 16);
+  const int nb = (int)min<int64_t>(kBlk / 16, g.nnzb - sb);
+  if (tid <= kBlk / 16) s_off[tid] = g.blk_off[sb + min(tid, nb)];
+  __syncthreads();
+  const int E0 = s_off[0], E1 = s_off[nb];
+  constexpr int kPairs = (kBlk / 16) * 36;
+  constexpr int kU = (kPairs + kBlk - 1) / kBlk;
+  double acc[kU];
+  int pb[kU], po[kU], lo[kU], hi[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int p = tid + kBlk * u;
+    pb[u] = p / 36; po[u] = p % 36;
+    const bool ok = p < kPairs && pb[u] < nb;
+    lo[u] = ok ? s_off[pb[u]] : 0;
+    hi[u] = ok ? s_off[pb[u] + 1] : 0;
+    acc[u] = 0.0;
+  }
+  int code_next = tid < kCoop && E0 + tid < E1 ? g.blk_list[E0 + tid] : 0;
+  for (int c0 = E0; c0 < E1; c0 += kCoop) {
+    if (tid < kCoop) {
+      const int k = c0 + tid;
+      const int code = code_next;
+      code_next = k + kCoop < E1 ? g.blk_list[k + kCoop] : 0;
+      if (k < E1) {
+        const int64_t t = code >> 4;
+        const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * ((code >> 2) & 3));
+        const double2* Jq = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code & 3));
+        double P[18], Q[18];
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {
+          const double2 x = Jp[u], y = Jq[u];
+          P[2 * u] = x.x; P[2 * u + 1] = x.y; Q[2 * u] = y.x; Q[2 * u + 1] = y.y;
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+#pragma unroll
+          for (int j = 0; j < 6; ++j)
+            s_prod[(6 * c + j) * (kCoop + 1) + tid] = P[c] * Q[j] + P[6 + c] * Q[6 + j] + P[12 + c] * Q[12 + j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int a = max(lo[u], c0), b = min(hi[u], c0 + kCoop);
+      const double* sp = s_prod + po[u] * (kCoop + 1) - c0;
+      double x = acc[u];
+      for (int e = a; e < b; ++e) x += sp[e];
+      acc[u] = x;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int p = tid + kBlk * u;
+    if (p >= kPairs || pb[u] >= nb) continue;
+    const int64_t s = sb + pb[u];
+    double v = acc[u];
+    // LM damping of the diagonal blocks (model.py:641-662)
+    if (lm != 0.0 && po[u] % 7 == 0 && g.blk_row[s] == g.col[s]) v += lm;
+    A[36 * s + po[u]] = v;
+  }
 }
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
@@ -704,11 +797,19 @@ __global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A,
                                                   double lm) {
   const int nrw = (int)gridDim.x - nwb;
   if ((int)blockIdx.x < nrw) rhs_body(g, rhs, blockIdx.x);
+#ifdef OFX_ASSEMBLE_LANES   // tuning: the 16-lanes-per-block form
   else blocks_body(g, A, blockIdx.x - nrw, lm);
+#else
+  else blocks_coop(g, A, blockIdx.x - nrw, lm);
+#endif
 }
 #ifdef OFX_SPLIT_ASSEMBLE
 __global__ __launch_bounds__(kBlk) void k_assemble_blocks(Gn g, double* __restrict__ A, double lm) {
+#ifdef OFX_ASSEMBLE_LANES
   blocks_body(g, A, blockIdx.x, lm);
+#else
+  blocks_coop(g, A, blockIdx.x, lm);
+#endif
 }
 __global__ __launch_bounds__(kBlk) void k_assemble_rhs(Gn g, double* __restrict__ rhs) { rhs_body(g, rhs, blockIdx.x); }
 #endif

@@ -48,6 +48,7 @@
  *   ofx_compute_clusters    csrc compute_clusters                           csrc/cpu/graph_proc.cpp:440-481
  *                           (callers: EDGraph, fusion_with_occlusion/embedded_deformation_graph.py:153-380,496-609)
  *   ofx_reduce_graph        EDGraph.get_reduced_graph                       embedded_deformation_graph.py:382-477
+ *   ofx_graph_downsample    EDGraph.create_graph_pyramid down-sampling      embedded_deformation_graph.py:278-299
  *   ofx_gn_*                DeformNet.optimize Gauss-Newton (JᵀJ, Jᵀr, LU)   model/model.py:222-859 (+ LinearSolverLU :59-86)
  *                           DeformNet.arap (params.mode = OFX_GN_ARAP)       model/model.py:1639-1986
  *                           (LU replaced by warm-started block-Jacobi PCG; ofx_gn_stats: per-step diagnostics)
@@ -289,6 +290,11 @@ int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_
  * the parallel relaxation cannot order, or a neighbourhood larger than its LDS table); the rest were settled
  * by the parallel form. OFX_GEO_SEQ=1 in the environment forces the sequential kernel for every node. */
 int ofx_graph_geodesic_sequential(void* handle, int64_t* n_nodes);
+/* one level of EDGraph.create_graph_pyramid's down-sampling (embedded_deformation_graph.py:278-299):
+ * down_idx i32[n] (first *n_down valid: kept node indices, ascending), up_idx i32[n] (per node: argmin index
+ * INTO the kept list, as the reference). At most 8192 kept nodes (else OFX_ERR_RANGE). Synchronises. */
+int ofx_graph_downsample(const float* node_positions, int32_t n_nodes, double node_coverage, int32_t* down_idx,
+                         int32_t* up_idx, int32_t* n_down, ofx_stream_t s);
 int ofx_edges_euclidean(const float* node_positions, int32_t n_nodes, int32_t n_max_neighbors, int32_t* graph_edges,
                         ofx_stream_t s);
 /* valid_in / valid_out u8[N] (may alias) */

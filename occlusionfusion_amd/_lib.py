@@ -84,6 +84,7 @@ _SIGS = {
     "ofx_graph_destroy": [P],
     "ofx_graph_adjacency": [P, P, P, P, P],
     "ofx_graph_geodesic_sequential": [P, P],
+    "ofx_graph_downsample": [P, c_int32, c_double, P, P, P, P],
     "ofx_erode_mesh": [P, c_int32, c_int32, P, P],
     "ofx_sample_nodes": [P, P, c_float, c_int32, P, P, P, P, P],
     "ofx_edges_geodesic": [P, P, P, c_int32, c_int32, c_float, c_int32, c_int32, P, P, P, P, P],

@@ -459,6 +459,62 @@ __global__ __launch_bounds__(256) void k_sn_emit(const float* __restrict__ P, co
   idx[r] = (int32_t)v;
 }
 
+// ------------------------------------------------------------------ graph pyramid down-sampling
+// embedded_deformation_graph.py:278-299, sequential by nature (node i's test depends on every kept node
+// before it): ONE workgroup keeps the kept nodes' positions in LDS; per node all threads compute the f32
+// np.linalg.norm distances ((dx² + dy²) + dz², correctly rounded sqrt) to the kept list in parallel and a
+// (distance, index) minimum gives numpy's argmin (first minimum). Two barriers per node.
+constexpr int kDsThreads = 1024;
+constexpr int kDsMax = 8192;   // kept nodes held in LDS (128 KiB)
+
+__global__ __launch_bounds__(kDsThreads) void k_downsample(const float* __restrict__ P, int n, double cov,
+                                                           int32_t* __restrict__ down, int32_t* __restrict__ up,
+                                                           int32_t* __restrict__ n_down) {
+  __shared__ float4 s_kp[kDsMax];
+  __shared__ uint64_t s_best[kDsThreads / 64];
+  __shared__ int s_nd;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_nd = 0;
+  __syncthreads();
+  for (int i = 0; i < n; ++i) {
+    const float px = P[3 * (int64_t)i], py = P[3 * (int64_t)i + 1], pz = P[3 * (int64_t)i + 2];
+    const int nd = s_nd;
+    uint64_t best = ~0ull;
+    for (int t = tid; t < nd; t += kDsThreads) {
+      const float4 q = s_kp[t];
+      const float dx = q.x - px, dy = q.y - py, dz = q.z - pz;   // old_nodes[down] - old_nodes[i]
+      const float d = sqrt_rn((dx * dx + dy * dy) + dz * dz);
+      best = min(best, ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)t);
+    }
+    for (int o = 32; o >= 1; o >>= 1) best = min(best, (uint64_t)__shfl_xor((unsigned long long)best, o));
+    if (lane == 0) s_best[wave] = best;
+    __syncthreads();
+    if (tid == 0) {
+      if (nd == 0) {
+        up[i] = i;
+        down[0] = i;
+        s_kp[0] = make_float4(px, py, pz, 0.f);
+        s_nd = 1;
+      } else {
+        uint64_t b = s_best[0];
+        for (int w = 1; w < kDsThreads / 64; ++w) b = min(b, s_best[w]);
+        const int j = (int)(uint32_t)b;
+        up[i] = j;
+        if (!((double)__uint_as_float((uint32_t)(b >> 32)) < cov) && nd < kDsMax) {
+          down[nd] = i;
+          s_kp[nd] = make_float4(px, py, pz, 0.f);
+          s_nd = nd + 1;
+        } else if (!((double)__uint_as_float((uint32_t)(b >> 32)) < cov)) {
+          s_nd = kDsMax + 1;   // overflow: reported, the host falls back
+        }
+      }
+    }
+    __syncthreads();
+    if (s_nd > kDsMax) break;
+  }
+  if (tid == 0) *n_down = s_nd;
+}
+
 // ------------------------------------------------------------------ geodesic edges
 struct HeapEnt {
   int32_t v;
@@ -1346,6 +1402,29 @@ int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_
   dfree(status, hs);
   dfree(todo, hs);
   OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_graph_downsample(const float* node_positions, int32_t n_nodes, double node_coverage, int32_t* down_idx,
+                         int32_t* up_idx, int32_t* n_down, ofx_stream_t s) {
+  OFX_CHECK_ARG(n_nodes >= 0 && n_down, "bad arguments");
+  *n_down = 0;
+  if (n_nodes == 0) return OFX_OK;
+  OFX_CHECK_ARG(node_positions && down_idx && up_idx, "null buffer");
+  hipStream_t hs = as_stream(s);
+  int32_t* nd = nullptr;
+  OFX_CHECKS(dalloc(&nd, 1, hs));
+  hipLaunchKernelGGL(k_downsample, dim3(1), dim3(kDsThreads), 0, hs, node_positions, n_nodes, node_coverage, down_idx,
+                     up_idx, nd);
+  OFX_LAUNCH_CHECK();
+  int32_t h = 0;
+  OFX_CHECKS(read1(nd, &h, hs));
+  dfree(nd, hs);
+  if (h > kDsMax) {
+    set_error("graph_downsample: more than %d kept nodes", kDsMax);
+    return OFX_ERR_RANGE;
+  }
+  *n_down = h;
   return OFX_OK;
 }
 

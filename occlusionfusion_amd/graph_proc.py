@@ -186,6 +186,20 @@ class MeshGraph:
         return E, W, D, n2v
 
 
+def downsample_device(nodes, node_coverage, device=None):
+    """One level of EDGraph.create_graph_pyramid's down-sampling (embedded_deformation_graph.py:278-299) on the
+    device -> (down_sample_idx, up_sample_idx) int lists, as the reference builds them."""
+    from . import _lib
+    dev = nodes.device if device is None and isinstance(nodes, torch.Tensor) else _dev(device)
+    P = _t(nodes, dev, torch.float32).reshape(-1, 3).contiguous()
+    n = P.shape[0]
+    down = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+    up = torch.empty(max(1, n), dtype=torch.int32, device=dev)
+    nd = _lib.c_int32()
+    call("ofx_graph_downsample", ptr(P), n, float(node_coverage), ptr(down), ptr(up), _lib.byref(nd), stream_ptr())
+    return down[: nd.value].cpu().tolist(), up[:n].cpu().tolist()
+
+
 def edges_euclidean_device(nodes, n_max_neighbors):
     X = nodes.contiguous().float().reshape(-1, 3)
     E = torch.empty((X.shape[0], int(n_max_neighbors)), dtype=torch.int32, device=X.device)

@@ -144,27 +144,16 @@ class EDGraph:
 
     def create_graph_pyramid(self):
         """embedded_deformation_graph.py:261-328 (input of the OcclusionFusion motion-completion network):
-        greedy down-sampling at doubled coverage per level (numpy norms as the reference), geodesic edges of
-        the kept nodes over the mesh on the device."""
-        from .graph_proc import MeshGraph
+        greedy down-sampling at doubled coverage per level (ofx_graph_downsample: numpy's f32 norms and argmin
+        order), geodesic edges of the kept nodes over the mesh, all on the device."""
+        from .graph_proc import MeshGraph, downsample_device
         cov = float(self.graph_generation_parameters["node_coverage"])
         mg = getattr(self, "_mesh", None) or MeshGraph(self.vertices, self.faces, self._dev())
         pyd = {"nn_index_l0": self.edges}
         old_nodes, idx = self.nodes, self.node_indices
         for level, k in zip(range(1, 4), (6, 4, 3)):
             cov *= 2
-            down, up = [], []
-            for i in range(old_nodes.shape[0]):
-                if not down:
-                    up.append(i)
-                    down.append(i)
-                    continue
-                d = np.linalg.norm(old_nodes[down] - old_nodes[i], axis=1)
-                j = int(np.argmin(d))
-                up.append(j)
-                if float(d[j]) < cov:
-                    continue
-                down.append(i)
+            down, up = downsample_device(old_nodes, cov, self._dev())   # the reference's greedy loop, on device
             idx = idx[down]
             E, _, _, _ = mg.edges_geodesic(idx.reshape(-1), k, cov, False, True)
             pyd[f"down_sample_idx{level}"] = down
@@ -187,10 +176,10 @@ class EDGraph:
         cov = float(self.graph_generation_parameters["node_coverage"])
         V = np.ascontiguousarray(canonical_model_vertices, np.float32)
         new = []
-        for x in new_verts_indices:
-            if np.min(np.linalg.norm(self.nodes - V[x], axis=1)) < cov:
+        for x in new_verts_indices:   # float(): numpy 1.26 (environment.yml:94) compares f32 scalar vs float in f64
+            if float(np.min(np.linalg.norm(self.nodes - V[x], axis=1))) < cov:
                 continue
-            if new and np.min(np.linalg.norm(V[new] - V[x], axis=1)) < cov:
+            if new and float(np.min(np.linalg.norm(V[new] - V[x], axis=1))) < cov:
                 continue
             new.append(x)
         if not new:

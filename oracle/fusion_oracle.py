@@ -1138,6 +1138,27 @@ def sample_nodes(vertices, non_eroded, node_coverage, use_only_non_eroded=True):
     return nodes, np.array(idx, np.int32).reshape(-1, 1)
 
 
+def graph_downsample(old_nodes, node_coverage):
+    """embedded_deformation_graph.py:278-299 (one level of create_graph_pyramid): nodes in order; the first is
+    kept; every later node appends argmin (first minimum) of its f32 np.linalg.norm distances to the kept
+    nodes (an index INTO the kept list, as the reference) to up_sample_idx, and is kept iff that minimum is
+    not < node_coverage (f32 distance vs Python float: compared in f64 under the reference's numpy 1.26). -> (down_sample_idx, up_sample_idx) int lists."""
+    P = np.asarray(old_nodes, np.float32)
+    down, up = [], []
+    for i in range(P.shape[0]):
+        if not down:
+            up.append(i)
+            down.append(i)
+            continue
+        d = np.linalg.norm(P[down] - P[i], axis=1)
+        j = int(np.argmin(d))
+        up.append(j)
+        if float(d[j]) < node_coverage:   # numpy 1.26 (environment.yml:94): f32 scalar vs Python float in f64
+            continue
+        down.append(i)
+    return down, up
+
+
 def _lt_push(h, hole, top, val):
     """libstdc++ std::__push_heap with CustomCompare (a.dist > b.dist: a min-heap on distance)."""
     parent = (hole - 1) // 2

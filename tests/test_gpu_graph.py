@@ -224,3 +224,23 @@ def test_geodesic_parallel_equals_sequential(cuda, monkeypatch, ov, en):
         assert torch.equal(a, b)
     assert n_seq < idx.shape[0] // 10
 
+
+def test_graph_downsample_matches_reference_loop(golden_dir, cuda):
+    """ofx_graph_downsample == the reference's pyramid loop (embedded_deformation_graph.py:278-299, restated in
+    oracle.graph_downsample with numpy's f32 norm and argmin): node sets from a real ED graph at the pyramid's
+    doubled coverages, a random cloud, and exact duplicates / equal distances (argmin takes the first)."""
+    from occlusionfusion_amd import EDGraph
+    from occlusionfusion_amd.graph_proc import downsample_device
+    f = np.load(os.path.join(golden_dir, "frontend_csrc.npz"), allow_pickle=False)
+    gr = EDGraph.from_mesh(f["mesh0_vertices"], f["mesh0_faces"], {"node_coverage": 0.04}, device=cuda)
+    rng = np.random.default_rng(5)
+    grid = np.stack(np.meshgrid(np.arange(6), np.arange(5), np.arange(4), indexing="ij"), -1).reshape(-1, 3)
+    cases = [(gr.nodes, 0.08), (gr.nodes, 0.16), (gr.nodes, 0.32),
+             (rng.random((3000, 3)).astype(np.float32), 0.05),
+             ((grid * 0.1).astype(np.float32), 0.1),                                   # ties and exact hits
+             (np.repeat(rng.random((40, 3)).astype(np.float32), 3, axis=0), 0.2)]     # duplicates
+    for nodes, cov in cases:
+        down, up = downsample_device(nodes, cov, cuda)
+        od, ou = fo.graph_downsample(nodes, cov)
+        assert down == od and up == ou, (len(nodes), cov)
+

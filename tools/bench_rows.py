@@ -91,6 +91,35 @@ def main():
     rows["f1_marching_cubes"] = {"ms": 1e3 * t_mc, "verts": int(m["verts"].shape[0]), "faces": int(m["faces"].shape[0]),
                                  "note": "masked MC incl. truncated region, count (1 sync) + emit + normals"}
     rows["f1_get_mesh"] = {"ms": 1e3 * t_mesh, "note": "get_mesh incl. world coordinates, colours, D2H copies"}
+    # sharded marching cubes: 4 slab shards of the same volume in one process (halo columns sliced from the
+    # neighbours, as exchange_boundary delivers them), per-shard meshing + key merge
+    from occlusionfusion_amd import TSDFVolume
+    from occlusionfusion_amd.sharding import merge_shard_meshes
+    W4 = 4
+    col = vol.brick_column_slots()
+    shards = []
+    for r in range(W4):
+        sh = TSDFVolume.from_grid(vol._vol_origin, vol._voxel_size, vol._vol_dim, (cam.fx, cam.fy, cam.cx, cam.cy),
+                                  device=dev, shard=(r, W4))
+        sh.tsdf_b.copy_(vol.tsdf_b[col * sh.brick_x0: col * sh.brick_x1])
+        sh.color_b.copy_(vol.color_b[col * sh.brick_x0: col * sh.brick_x1])
+        shards.append(sh)
+    bnd = [sh.boundary_columns() for sh in shards]
+    t_part = []
+
+    def sharded():
+        parts = []
+        for r, sh in enumerate(shards):
+            parts.append(sh.extract_mesh_shard(bnd[r - 1][1] if r > 0 else None, bnd[r + 1][0] if r < W4 - 1 else None))
+        return merge_shard_meshes(parts, vol._vol_dim)
+    t_sh, msh = timed(sharded, a.reps)
+    t_one, _ = timed(lambda: shards[1].extract_mesh_shard(bnd[0][1], bnd[2][0]), a.reps)
+    rows["f1_marching_cubes_sharded"] = {"shards": W4, "ms_all_shards_sequential_plus_merge": 1e3 * t_sh,
+                                         "ms_one_shard": 1e3 * t_one, "verts": int(msh["verts"].shape[0]),
+                                         "equal_to_whole": bool(msh["verts"].shape[0] == m["verts"].shape[0]),
+                                         "note": "one process; per rank a shard costs ms_one_shard + the halo "
+                                                 "exchange + gather"}
+    del shards, bnd
 
     # ---- f3: correspondence front-end
     depth = frames[-1].im[5].contiguous()
@@ -123,6 +152,9 @@ def main():
     t_cu, _ = timed(lambda: node_edge_cleanup_device(E, torch.ones(E.shape[0], dtype=torch.bool, device=dev)), a.reps)
     t_cl, _ = timed(lambda: clusters_device(E), a.reps)
     t_all, gr = timed(lambda: EDGraph.from_mesh(mesh[0], mesh[1], {"node_coverage": 0.05}, device=dev), a.reps)
+    from occlusionfusion_amd.graph_proc import downsample_device
+    t_ds, (dsd, _) = timed(lambda: downsample_device(pos, 0.1, dev), a.reps)
+    rows["f4_pyramid_downsample"] = {"ms": 1e3 * t_ds, "nodes_in": int(pos.shape[0]), "kept": len(dsd)}
     rows["f4_graph"] = {"mesh_verts": int(verts.shape[0]), "mesh_faces": int(faces.shape[0]),
                         "nodes": int(idx.shape[0]), "sample_rounds": int(mg.sample_rounds),
                         "ms_adjacency": 1e3 * t_gc, "ms_erode": 1e3 * t_er, "ms_sample_nodes": 1e3 * t_sn,

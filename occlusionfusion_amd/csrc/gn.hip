@@ -657,10 +657,8 @@ __device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A,
   }
 }
 
-// b = -Jᵀr: one wave per node, lane = slot*6 + c (10 slots); slot s sums list entries s, s+10, ...
-// and lane c combines the 10 slots in fixed order. WG 0 also reduces the loss partials into the
+// b = -Jᵀr: one wave per node, entry-parallel (below). WG 0 also reduces the loss partials into the
 // rhs tail.
-constexpr int kRhsSlots = 10;
 __device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, int wg) {
   if (wg == 0 && threadIdx.x < 64) {   // the loss partials of k_terms, 4 streams in one pass, fixed order
     double a[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1416,6 +1414,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
   const int nw = g.nwg_row;
+  (void)nw;   // read by the OFX_STAMPS tuning build
   const double* __restrict__ mc = par ? g.m1 : g.m0;
   double* __restrict__ mn = par ? g.m0 : g.m1;
   const int ns = g.nw_pad;

@@ -331,21 +331,19 @@ __global__ __launch_bounds__(kGreedyThreads) void k_sn_greedy(const float* __res
       uint64_t conf = 0;   // bit j: an earlier candidate j lies within c (point = this, node = j)
 #pragma unroll
       for (int j = 0; j < 63; ++j) {   // constant lane indices: v_readlane into scalars
-        if (j + 1 >= ngot) break;
         const float rx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), j));
         const float ry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), j));
         const float rz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz), j));
-        if (j < lane && eig_sq(px - rx, py - ry, pz - rz) <= cov2) conf |= 1ull << j;
+        if (j + 1 < ngot && j < lane && eig_sq(px - rx, py - ry, pz - rz) <= cov2) conf |= 1ull << j;
       }
       uint64_t tb = stamps ? wall_clock64() : 0;
       const uint32_t conf_lo = (uint32_t)conf, conf_hi = (uint32_t)(conf >> 32);
       uint64_t sel = 0;
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        if (i >= ngot) break;
         const uint64_t row = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_lo, i) |
                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)conf_hi, i) << 32);
-        if (!(row & sel)) sel |= 1ull << i;
+        if (i < ngot && !(row & sel)) sel |= 1ull << i;
       }
       if (have && ((sel >> lane) & 1ull)) {
         const int r = __popcll(sel & ((1ull << lane) - 1ull));
@@ -1320,7 +1318,10 @@ int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_
   a.status = status;
   if (!getenv("OFX_GEO_SEQ")) {   // parallel form; ties go sequential, overfull neighbourhoods to the big table
     std::vector<int32_t> rest, big;
-    for (int tier = 0; tier < 2; ++tier) {
+    const bool big_only = getenv("OFX_GEO_BIG") != nullptr;   // tuning/test: every node on the 16384-slot form
+    if (big_only)
+      for (int32_t n = 0; n < n_nodes; ++n) big.push_back(n);
+    for (int tier = big_only ? 1 : 0; tier < 2; ++tier) {
       int32_t n_run = tier == 0 ? n_nodes : (int32_t)big.size();
       if (n_run == 0) break;
       if (tier == 0) {

@@ -142,7 +142,6 @@ __global__ __launch_bounds__(256) void k_skin_volume(BrickGeom g, const float* _
                                                       float cull_r2, float cutoff, float denom, int K,
                                                       const int32_t* __restrict__ list, ushort4* __restrict__ anchors,
                                                       float4* __restrict__ weights) {
-  __shared__ float4 sn[kTile];
   __shared__ float4 sc[kTile];
   __shared__ int s_nc;
   const int64_t slot = blockIdx.x;

@@ -771,7 +771,9 @@ __global__ __launch_bounds__(geo::kThreads) void k_geo_relax(GeoArgs a, const in
     __syncthreads();
     if (s_fail) break;
     const bool at_cap = !a.enforce && R >= a.max_inf;
-    if (s_ncand >= a.K || at_cap || s_nbnd == 0) break;   // K found, pruning radius reached, or all reached
+    const bool done = s_ncand >= a.K || at_cap || s_nbnd == 0;   // K found, pruning radius reached, or all reached
+    __syncthreads();   // every wave has read s_ncand / s_nbnd before thread 0 resets them (else waves diverge)
+    if (done) break;
     // ---- grow R; re-queue the vertices whose edges it cut
     R = a.enforce ? R * 1.25f : fminf(R * 1.25f, a.max_inf);
     if (tid == 0) { s_n[cur] = 0; s_nbnd = 0; }

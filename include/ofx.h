@@ -275,7 +275,7 @@ int ofx_graph_adjacency(void* handle, int32_t* rowptr, int32_t* col, int64_t* n_
 int ofx_erode_mesh(void* handle, int32_t n_iterations, int32_t min_neighbors, uint8_t* non_eroded, ofx_stream_t s);
 /* node_positions f32[V*3] / node_indices i32[V] capacity; *n_nodes written (host); *n_rounds: batches of the
  * single-workgroup greedy form (meshes up to ~1.29M vertices), else launches of the parallel round form
- * (OFX_SN_ROUNDS=1 forces it) */
+ * (OFX_SN_ROUNDS=1 forces it; OFX_SN_STAMPS=1 prints the greedy form's phase times to stderr) */
 int ofx_sample_nodes(void* handle, const uint8_t* non_eroded, float node_coverage, int32_t use_only_non_eroded,
                      float* node_positions, int32_t* node_indices, int64_t* n_nodes, int64_t* n_rounds,
                      ofx_stream_t s);
@@ -288,7 +288,8 @@ int ofx_edges_geodesic(void* handle, const uint8_t* valid_vertices, const int32_
                        float* graph_edges_distances, float* node_to_vertex_distances, ofx_stream_t s);
 /* nodes the last ofx_edges_geodesic on this handle settled with the sequential heap kernel (distance ties
  * the parallel relaxation cannot order, or a neighbourhood larger than its LDS table); the rest were settled
- * by the parallel form. OFX_GEO_SEQ=1 in the environment forces the sequential kernel for every node. */
+ * by the parallel form. OFX_GEO_SEQ=1 in the environment forces the sequential kernel for every node,
+ * OFX_GEO_BIG=1 the 16384-slot parallel form (tests / tuning; results are identical either way). */
 int ofx_graph_geodesic_sequential(void* handle, int64_t* n_nodes);
 /* one level of EDGraph.create_graph_pyramid's down-sampling (embedded_deformation_graph.py:278-299):
  * down_idx i32[n] (first *n_down valid: kept node indices, ascending), up_idx i32[n] (per node: argmin index

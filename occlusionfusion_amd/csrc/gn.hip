@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <chrono>
 #include <utility>
+#include <cstdlib>
 #include <vector>
 
 #include "ofx_common.h"
@@ -101,6 +102,7 @@ struct Gn {
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
   int32_t nw_pad = 0;            // stride of the iteration partial streams: 128·pcg_ku, zero beyond nwg_row
+  int32_t pcg_w2 = 1;            // two waves per cluster in k_pcg_iter (OFX_PCG_W1=1: one)
   int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (3: <= 384 waves, else 17)
   double* scal = nullptr;
   int32_t* flags = nullptr;
@@ -1404,13 +1406,20 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
   for (int c = 0; c < 3; ++c) sa.t[3 * (int64_t)row + c] += x[3 + c];
 }
 
-template <bool kWave, bool kFirst, int kU>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
+// kW2 (with kWave): TWO waves per cluster. Wave h multiplies block slot h·64 + lane (one block per lane, not
+// two), stages only its half of the inverse's column groups and applies that half (split-K); the scalar
+// work, row sums and recurrences run in both waves (identical bits), wave 0 alone stores. Two LDS barriers
+// (products, M⁻¹ halves), no memory release.
+template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+__global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
-  __shared__ double s_v[kCD];
-  __shared__ float4 s_m[kCD * kCD / 4];
+  constexpr int kNH = kW2 ? 2 : 1;
+  __shared__ double s_v[kNH][kCD];
+  __shared__ float4 s_m[kCD * kCD / 4 + (kW2 ? 64 : 0)];   // kW2: a wave's last DMA may overrun its half
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
-  const int lane = threadIdx.x;
+  __shared__ double s_half[kW2 ? 64 : 1];
+  const int lane = threadIdx.x & 63;
+  const int hw = kW2 ? (int)(threadIdx.x >> 6) : 0;   // wave within the cluster's workgroup
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
   const int nw = g.nwg_row;
@@ -1429,16 +1438,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #endif
   int2 bl0 = make_int2(-1, 0), bl1 = make_int2(-1, 0);
   if (kWave) {
-    bl0 = g.wl[(int64_t)wv * kWL + lane];
-    bl1 = g.wl[(int64_t)wv * kWL + 64 + lane];
+    bl0 = g.wl[(int64_t)wv * kWL + 64 * hw + lane];
+    if (!kW2) bl1 = g.wl[(int64_t)wv * kWL + 64 + lane];
   }
   const int stop = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
   const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
+  if (kW2) {   // wave h: column groups [6h, 6h + 6) = float4 [288h, 288h + 288), 5 DMA instructions (clamped source)
+    constexpr int kHalf = kCD * kCD / 8;
 #pragma unroll
-  for (int k = 0; k < kMS; ++k)
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + k * 64 + lane), reinterpret_cast<void*>(s_m + k * 64), 16, 0, 0);
+    for (int k = 0; k < 5; ++k) {
+      const int f = kHalf * hw + k * 64;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + min(f + lane, kCD * kCD / 4 - 1)),
+                                       reinterpret_cast<void*>(s_m + f), 16, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kMS; ++k)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + k * 64 + lane), reinterpret_cast<void*>(s_m + k * 64), 16, 0, 0);
+  }
   double v[V_N];
   load_rec(g.st, o, v);
   const double m = mc[o];
@@ -1468,10 +1487,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #endif
   OFX_STAMP(1)
   // ---- trip 2: A blocks and gathered m (issued first; the scalar work below overlaps their flight)
-  double2 ab[kWave ? 2 : 1][18], xb[kWave ? 2 : 1][3];
+  constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
+  double2 ab[kNB][18], xb[kNB][3];
   if (kWave)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked later)
+    for (int j = 0; j < kNB; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked later)
       const int2 e = j ? bl1 : bl0;
       const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e.y);
       const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
@@ -1499,7 +1519,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   }
   const double gam = pa[0], del = pa[1], rr = pa[2];
   const double tol = g.prm.pcg_tol;
-  const bool lead = wv == 0 && lane == 0;
+  const bool lead = wv == 0 && lane == 0 && hw == 0;
+  const bool w0 = hw == 0;   // the wave that stores (kW2: both compute the same bits)
   if (kFirst && lead) g.scal[S_BB] = bb;
   double beta = 0.0, alpha;
   if (kFirst) {
@@ -1510,6 +1531,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   }
   const bool conv = rr <= tol * tol * bb || gam == 0.0;
   if (conv || !isfinite(alpha) || !(alpha > 0.0)) {   // converged, or breakdown (A SPD => alpha > 0): keep x
+    if (!w0) return;
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
     g.stopw[(int64_t)wv * 64 + lane] = 1;
     const bool ill = !conv && !isfinite(alpha);
@@ -1528,8 +1550,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   double nc;
   if (kWave) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < kNB; ++j) {
       const bool ok = (j ? bl1 : bl0).x >= 0;
+      const int slot = kW2 ? 64 * hw + lane : j * 64 + lane;
       double x[6];
 #pragma unroll
       for (int k = 0; k < 3; ++k) { x[2 * k] = xb[j][k].x; x[2 * k + 1] = xb[j][k].y; }
@@ -1537,11 +1560,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       for (int i = 0; i < 6; ++i) {   // (the PCG is not bit-pinned: fused multiply-adds)
         const double2 b01 = ab[j][3 * i], b23 = ab[j][3 * i + 1], b45 = ab[j][3 * i + 2];
         const double t = fma(b45.y, x[5], fma(b45.x, x[4], fma(b23.y, x[3], fma(b23.x, x[2], fma(b01.y, x[1], b01.x * x[0])))));
-        s_prod[(j * 64 + lane) * 6 + i] = ok ? t : 0.0;
+        s_prod[slot * 6 + i] = ok ? t : 0.0;
       }
     }
     OFX_STAMP(3)
-    wave_lds_sync();
+    if (kW2) {   // both waves' products: an LDS barrier (no memory release)
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+    } else {
+      wave_lds_sync();
+    }
     // row sums in CSR order (rows of at most kRowMax blocks; unrolled reads at immediate offsets,
     // masked; s_prod is padded so the reads past the wave's last block stay inside it)
     const int len = b1 - b0;
@@ -1570,27 +1598,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const double w2 = fma(-alpha, zz, v[V_W]);
     if (own) {
       const double nv[V_N] = {fma(alpha, p, v[V_X]), rn, un, zz, qq, sv, p, w2};
-      store_rec(g.st, o, nv);
-      s_v[6 * r + q] = w2;
+      if (w0) store_rec(g.st, o, nv);
+      s_v[hw][6 * r + q] = w2;
       d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
     }
   }
   OFX_STAMP(5)
   wave_lds_sync();
-  if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (inverse rows staged in LDS)
+  if (kW2) {      // split-K: wave h applies column groups [6h, 6h + 6); wave 0 adds the halves (fixed order)
+    double hsum = 0.0;
+    if (own) {
+      const float4* mrow = s_m + (6 * r + q);
+      double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < kCD / 8; ++kk) {
+        const int k = (kCD / 8) * hw + kk;
+        const float4 t = mrow[k * kCD];
+        a[0] = fma((double)t.x, s_v[hw][4 * k], a[0]);
+        a[1] = fma((double)t.y, s_v[hw][4 * k + 1], a[1]);
+        a[2] = fma((double)t.z, s_v[hw][4 * k + 2], a[2]);
+        a[3] = fma((double)t.w, s_v[hw][4 * k + 3], a[3]);
+      }
+      hsum = (a[0] + a[1]) + (a[2] + a[3]);
+    }
+    if (hw == 1) s_half[lane] = hsum;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (w0 && own) mn[o] = hsum + s_half[lane];
+  } else if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (inverse rows staged in LDS)
     const float4* mrow = s_m + (6 * r + q);
     double a[4] = {0.0, 0.0, 0.0, 0.0};   // four independent FMA chains
 #pragma unroll
     for (int k = 0; k < kCD / 4; ++k) {
       const float4 t = mrow[k * kCD];
-      a[0] = fma((double)t.x, s_v[4 * k], a[0]);
-      a[1] = fma((double)t.y, s_v[4 * k + 1], a[1]);
-      a[2] = fma((double)t.z, s_v[4 * k + 2], a[2]);
-      a[3] = fma((double)t.w, s_v[4 * k + 3], a[3]);
+      a[0] = fma((double)t.x, s_v[0][4 * k], a[0]);
+      a[1] = fma((double)t.y, s_v[0][4 * k + 1], a[1]);
+      a[2] = fma((double)t.z, s_v[0][4 * k + 2], a[2]);
+      a[3] = fma((double)t.w, s_v[0][4 * k + 3], a[3]);
     }
     mn[o] = (a[0] + a[1]) + (a[2] + a[3]);
   }
   OFX_STAMP(6)
+  if (!w0) return;
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
@@ -1835,6 +1884,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
                     : (small ? k_pcg_iter<false, true, 3> : k_pcg_iter<false, true, 17>);
   auto iter = wave ? (small ? k_pcg_iter<true, false, 3> : k_pcg_iter<true, false, 17>)
                    : (small ? k_pcg_iter<false, false, 3> : k_pcg_iter<false, false, 17>);
+  // two waves per cluster (wave-list SpMV, up to 384 waves)
+  const bool w2 = wave && small && g->pcg_w2;
+  if (w2) { iter0 = k_pcg_iter<true, true, 3, true>; iter = k_pcg_iter<true, false, 3, true>; }
+  const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
   // spins on it, so the next GN step is enqueued while the chunk's remaining (no-op) launches drain.
   // The chunk event only tells "all launched iterations ran without converging" -> launch more.
@@ -1854,7 +1907,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     const auto h0 = std::chrono::steady_clock::now();
 #endif
     for (int k = 0; k < n; ++k, ++it)
-      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block, 0, hs, pa, it & 1);
+      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, pa, it & 1);
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
     g->host_enqueued += n;
@@ -1897,6 +1950,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     return OFX_ERR_RANGE;
   }
   Gn* g = new Gn();
+  g->pcg_w2 = getenv("OFX_PCG_W1") ? 0 : 1;   // tuning / A-B: one wave per cluster
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
   // rows: clusters of <= kCS first-fit packed into groups of kCS; at most one group is at most half

@@ -302,6 +302,27 @@ def test_gn_repeatable(cuda, golden_dir):
     np.testing.assert_allclose(a["node_translations"].cpu().numpy(), b["node_translations"].cpu().numpy(), atol=1e-9)
 
 
+def test_gn_one_and_two_wave_pcg_agree(cuda, golden_dir, monkeypatch):
+    """The PCG iteration with two waves per cluster (default) and with one (OFX_PCG_W1=1, also the form for
+    large graphs) solve the same systems: transforms within the 1e-5 bar of the dense oracle and of each
+    other, each bitwise repeatable."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    two = GaussNewtonSolver(len(g["nodes"]), 1000)
+    monkeypatch.setenv("OFX_PCG_W1", "1")
+    one = GaussNewtonSolver(len(g["nodes"]), 1000)
+    outs = {}
+    for name, s in (("two", two), ("one", one)):
+        a = s.optimize(*_gn_inputs(g))
+        b = s.optimize(*_gn_inputs(g))
+        assert torch.equal(a["node_translations"], b["node_translations"]), name
+        assert torch.equal(a["node_rotations"], b["node_rotations"]), name
+        assert np.abs(a["node_translations"].cpu().numpy() - g["t"]).max() < 1e-5, name
+        outs[name] = a
+    assert (outs["two"]["node_translations"] - outs["one"]["node_translations"]).abs().max().item() < 1e-6
+    assert (outs["two"]["node_rotations"] - outs["one"]["node_rotations"]).abs().max().item() < 1e-6
+
+
 def test_gn_solver_reuse_across_graph_change(cuda, golden_dir):
     """A solver handle reused on a different graph of the same size (the row order is kept optimistically
     and checked on the device) gives exactly what a fresh handle gives."""

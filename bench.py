@@ -5,16 +5,30 @@ One step = one frame of the reference's fusion loop (lepard_nicp_test.py:test4):
 (DeformNet.optimize formulation, 10 iterations) -> update node transforms -> fused skin-cache warp +
 TSDF/weight/colour integrate of the new frame. All inputs are device-resident before timing.
 
-  python bench.py [--gpus N --steps K --warmup W] [--mode replicas|shard] [--dims 512] [--nodes 2000]
+  python bench.py [--gpus N --steps K --warmup W] [--config 1..5] [--mode replicas|shard]
+                  [--solve replicated|allreduce] [--dims 512] [--nodes 2000]
 
---mode replicas (default, BASELINE config 5): one independent 512³ scene per GPU, no collective,
+--gpus N > 1 without a torch.distributed environment: bench.py starts N ranks itself (a child
+    `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...` running this file,
+    started before anything touches the GPU) and exits with its status; under torchrun it checks
+    WORLD_SIZE == --gpus.
+--config (BASELINE.json configs): 3 (default) 512³ @4 mm, ~2k nodes, non-rigid + occluder; 2 256³ @4 mm,
+    ~1k nodes, rigid sequence; 1 128³ @8 mm, 200 nodes, 320x240 camera; 4 1024³ @2 mm, ~4k nodes;
+    5 = config 3 per GPU in replicas mode (what --gpus N runs by default).
+--mode replicas (default, BASELINE config 5): one independent scene per GPU, no collective,
     value = frames of all ranks / max-rank time (weak scaling).
---mode shard (BASELINE config 4 style): ONE volume x-sharded across ranks (bricks), matches sharded,
-    one RCCL all-reduce of the GN JᵀJ/Jᵀr accumulators per GN iteration; value = frames / time.
+--mode shard (BASELINE config 4 style): ONE volume, its bricks dealt to ranks by spatial hash bucket
+    (each rank skins and integrates only its bricks); the solve is replicated (--solve replicated: every
+    rank assembles all matches, no collective) or match-sharded (--solve allreduce: one RCCL all-reduce
+    of the GN JᵀJ/Jᵀr accumulators per GN iteration); value = frames / time (strong scaling).
+--launch-check: rank plumbing only (process group, barrier, max-over-ranks timing, per-rank gather) with
+    no device work — what tests/test_bench_launch.py runs on the CPU over gloo.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,15 +39,32 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
+
+# BASELINE.json configs -> (dims, voxel m, origin, nodes, scene motion, occluder, camera scale)
+CONFIGS = {
+    1: dict(dims=128, voxel=0.008, origin=(-0.512, -0.512, 0.9), nodes=200, motion="nonrigid", occluder=False,
+            cam_scale=2, seed=1),
+    2: dict(dims=256, voxel=0.004, origin=(-0.512, -0.512, 0.9), nodes=1000, motion="rigid", occluder=False,
+            cam_scale=1, seed=2),
+    3: dict(dims=512, voxel=0.004, origin=(-1.024, -1.024, 0.5), nodes=2000, motion="nonrigid", occluder=True,
+            cam_scale=1, seed=3),
+    4: dict(dims=1024, voxel=0.002, origin=(-1.024, -1.024, 0.5), nodes=4000, motion="nonrigid", occluder=True,
+            cam_scale=1, seed=4),
+}
+CONFIGS[5] = dict(CONFIGS[3])
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC summary (separate counter passes
-    cannot run inside the timed bench), or None."""
+    cannot run inside the timed bench) — only when that summary was measured on this very workload;
+    otherwise None."""
     try:
         with open(PMC_FILE) as f:
-            return json.load(f)["kernels"][kernel]["traffic_bytes"]
+            d = json.load(f)
+        if d.get("workload") != workload:
+            return None
+        return d["kernels"][kernel]["traffic_bytes"]
     except (OSError, KeyError, ValueError):
         return None
 
@@ -43,23 +74,83 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", type=int, choices=sorted(CONFIGS), default=3)
     p.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
-    p.add_argument("--dims", type=int, default=512)
-    p.add_argument("--voxel", type=float, default=0.004)
-    p.add_argument("--nodes", type=int, default=2000)
+    p.add_argument("--solve", choices=["replicated", "allreduce"], default="replicated",
+                   help="shard mode: replicated assembly (no collective) or match-sharded + all-reduce")
+    p.add_argument("--dims", type=int, default=None)
+    p.add_argument("--voxel", type=float, default=None)
+    p.add_argument("--nodes", type=int, default=None)
     p.add_argument("--matches", type=int, default=10000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 24)
     p.add_argument("--json-out", default=None)
-    p.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsals "
-                                                     "with several ranks on one device)")
-    return p.parse_args()
+    p.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL; gloo for "
+                                                   "CPU launch checks and rehearsals with ranks sharing a device)")
+    a = p.parse_args()
+    cfg = dict(CONFIGS[a.config])
+    for k in ("dims", "voxel", "nodes"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    a.cfg = cfg
+    if a.backend is None:
+        a.backend = "gloo" if a.launch_check else "nccl"
+    return a
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(a):
+    """Start --gpus ranks as fresh processes (torch.distributed.run, one per GPU) before any GPU call and
+    return their exit status. The child processes re-enter main() with WORLD_SIZE set."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(a, world, rank):
+    """Plumbing of the multi-rank bench without device work: the same barrier / max-over-ranks / gather."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(a.backend)
+        dist.barrier()
+    t0 = time.perf_counter()
+    x = torch.ones(1 << 16)
+    for _ in range(a.steps):
+        x = x * 1.0001
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64)
+    per_rank = [{"rank": rank, "pid": os.getpid(), "elapsed_s": elapsed}]
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "pid": os.getpid(), "elapsed_s": elapsed})
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "steps": a.steps, "mode": a.mode,
+                          "backend": a.backend, "max_elapsed_s": float(el.item()), "per_rank": per_rank}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE {world} != --gpus {a.gpus}")
+    if a.launch_check:
+        return launch_check(a, world, rank)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())   # rehearsals: several ranks may share one device
     torch.cuda.set_device(local)
@@ -74,10 +165,14 @@ def main():
     from occlusionfusion_amd import synthetic as S
     from occlusionfusion_amd.pipeline import FusionPipeline
 
+    cfg = a.cfg
     D = a.dims
-    origin = (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
-    seq = S.SyntheticSequence.build(a.nodes, seed=3)
-    shard = (rank, world) if (a.mode == "shard" and world > 1) else None
+    origin = cfg["origin"] if (a.dims, a.voxel) == (cfg["dims"], cfg["voxel"]) else \
+        (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
+    scene = S.SphereScene(motion=cfg["motion"], occluder=cfg["occluder"])
+    seq = S.SyntheticSequence.build(a.nodes, cam=S.bench_camera(cfg["cam_scale"]), seed=cfg["seed"], scene=scene)
+    sharded = a.mode == "shard" and world > 1
+    shard = (rank, world) if sharded else None
     pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)
     total = a.warmup + a.steps + 1
     frames = [pipe.prepare(t) for t in range(total)]
@@ -87,13 +182,14 @@ def main():
     K = cache.k
     n_skin_valid = int((cache.anchors.view(-1, 4)[:, K - 1] != -1).sum().item()) if cache.n_list else 0
     torch.cuda.synchronize()
+    allreduce = sharded and a.solve == "allreduce"
+    ar_events = []
 
     def solve(fi):
-        if a.mode == "shard" and world > 1:
-            g = pipe
-            out = pipe.solver.optimize_distributed(g.nodes_t, g.edges_t, g.ew_t, fi.tpos, fi.conf, fi.src, fi.anchors,
-                                                   fi.weights, fi.tgt, pipe.intr, prev_rot=pipe.prev_rot,
-                                                   prev_trans=pipe.prev_trans, sync=False)
+        if allreduce:
+            out = pipe.solver.optimize_distributed(pipe.nodes_t, pipe.edges_t, pipe.ew_t, fi.tpos, fi.conf, fi.src,
+                                                   fi.anchors, fi.weights, fi.tgt, pipe.intr, prev_rot=pipe.prev_rot,
+                                                   prev_trans=pipe.prev_trans, sync=False, timer=ar_events)
             pipe.prev_rot, pipe.prev_trans = out["node_rotations"], out["node_translations"]
             return out
         return pipe.solve(fi)
@@ -106,6 +202,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    ar_events.clear()
     marks = []
     upd = []
     pipe.solver.timing(True)               # arm hipEvent timing of the PCG loops (same stream)
@@ -128,7 +225,7 @@ def main():
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed_max = float(el.item())
     pcg_ms, pcg_launches, _ = pipe.solver.timing(False)
     N_, M_, nnzb, _T, rows = pipe.solver.info()
     t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
@@ -137,47 +234,72 @@ def main():
     gn_it = [int(m[3]["_status"][1].item()) for m in marks]
     valid = [int(m[3]["_status"][0].item()) for m in marks]
     U = float(np.mean([int(u.item()) for u in upd]))
-    t_kint = float(np.mean([a.elapsed_time(b) for a, b in pipe.vol.kernel_timer])) * 1e-3
+    t_kint = float(np.mean([x.elapsed_time(y) for x, y in pipe.vol.kernel_timer])) * 1e-3
     pipe.vol.kernel_timer = None
+    t_ar = (sum(x.elapsed_time(y) for x, y in ar_events) * 1e-3 / a.steps) if ar_events else 0.0
+    mine = {"rank": rank, "device": local, "ms_per_frame": 1e3 * elapsed / a.steps,
+            "solve_ms": 1e3 * float(np.mean(t_solve)), "allreduce_ms": 1e3 * t_ar,
+            "integrate_ms": 1e3 * float(np.mean(t_int)), "integrate_kernel_us": 1e6 * t_kint,
+            "listed_bricks": cache.n_list, "updated_voxels": U, "pcg_iters_per_frame": float(np.mean(pcg))}
+    per_rank = [mine]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     frames_done = a.steps * (world if a.mode == "replicas" else 1)
-    value = frames_done / elapsed
-    # algorithmic bytes of one integrate launch (DESIGN.md §Roofline): palette-rank anchors 4 B per voxel
+    value = frames_done / elapsed_max
+    # algorithmic bytes of one integrate launch (DESIGN.md §5): palette-rank anchors 4 B per voxel
     # of every listed brick + the brick's palette (64 x u16 + count); weights 16 B + tsdf/weight 8 B read
     # per skin-valid voxel; per updated voxel tsdf/weight write 8 B + colour read+write 8 B. Node records
     # and the depth/colour images are L2-resident and not counted.
     B = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
-    t_int_avg = float(np.mean(t_int))
     achieved = B / t_kint
-    # k_pcg_iter algorithmic (unique) bytes per launch: per JᵀJ block its 6x6 f64 values (288 B) + its
+    # k_pcg_iter algorithmic (unique) bytes per PCG iteration: per JᵀJ block its 6x6 f64 values (288 B) + its
     # (col, slot) wave-list entry (8 B); per PCG row (nodes in cluster order, padded) the cluster-inverse
     # rows (6 x 48 f32 = 1152 B), the 8-vector state read + written (2 x 384 B), m read (48 B; the
-    # neighbour gathers re-read these) and the new m written (48 B). DESIGN.md §5.
+    # neighbour gathers re-read these) and the new m written (48 B). DESIGN.md §5. Launches after the
+    # converging one (drained: they end after the first memory trip) move no algorithmic bytes, so the
+    # per-launch figure is iterations x bytes / launches, over the same launches rocprof averages.
     B_pcg = nnzb * 296 + rows * (1152 + 768 + 48 + 48)
-    t_pcg = pcg_ms * 1e-3 / max(1, pcg_launches)
-    ach_pcg = B_pcg / t_pcg
+    iters = float(np.sum(pcg))
+    launches = max(1, pcg_launches)
+    t_pcg = pcg_ms * 1e-3 / launches
+    B_launch = B_pcg * iters / launches
+    workload = (f"{D}^3 TSDF @{a.voxel * 1e3:g} mm, {seq.nodes.shape[0]} nodes, {a.matches} matches, "
+                f"{seq.cam.width}x{seq.cam.height} depth, {cfg['motion']}{' + occluder' if cfg['occluder'] else ''}, "
+                f"GN 10 it")
     res = {
-        "metric": "fusion frames/sec (warp+integrate+solve), 640x480 depth -> 512^3 TSDF",
+        "metric": f"fusion frames/sec (warp+integrate+solve), {640 // cfg['cam_scale']}x{480 // cfg['cam_scale']} depth "
+                  f"-> {D}^3 TSDF",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": 1e3 * elapsed / a.steps, "higher_is_better": True,
+        "ms_per_step": 1e3 * elapsed_max / a.steps, "higher_is_better": True,
         "scaling": "weak" if a.mode == "replicas" else "strong", "vs_baseline": None, "dtype": "f32/f64",
-        "data": "synthetic (seeded sphere+plane non-rigid sequence with a moving occluder hiding up to ~38 % of the object, 1 mm noise, matches from visible points; SURVEY §8(d), BASELINE config 3)",
-        "config": {"workload": f"{D}^3 TSDF @{a.voxel * 1e3:g} mm, {seq.nodes.shape[0]} nodes, "
-                               f"{a.matches} matches, 640x448 depth, GN 10 it",
-                   "mode": a.mode, "dims": D, "voxel_size_m": a.voxel, "nodes": int(seq.nodes.shape[0]),
-                   "matches": a.matches, "parallelism": f"{a.mode}{world}"},
-        "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * t_int_avg,
-                         "pcg_iters_per_frame": float(np.mean(pcg)), "gn_iters": float(np.mean(gn_it)),
-                         "valid_solves": int(np.sum(valid))},
-        "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster block-Jacobi apply)", "bound": "hbm",
-                     "achieved": ach_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": ach_pcg / PEAK_HBM,
-                     "traffic": pmc_traffic("k_pcg_iter"), "traffic_source": os.path.relpath(PMC_FILE, ROOT),
-                     "bytes_per_launch": B_pcg, "avg_launch_us": 1e6 * t_pcg,
-                     "launches_per_frame": pcg_launches / a.steps, "nnz_blocks": nnzb,
-                     "note": "dominant kernel by time; latency-bound (one launch per iteration: launch floor + two dependent memory trips + the wave's instruction stream)"},
+        "data": f"synthetic (seeded sphere+plane {cfg['motion']} sequence"
+                f"{' with a moving occluder hiding up to ~38 % of the object' if cfg['occluder'] else ''}, 1 mm noise, "
+                f"matches from visible points; SURVEY §8(d), BASELINE config {a.config})",
+        "config": {"workload": workload, "baseline_config": a.config, "mode": a.mode,
+                   "solve": (a.solve if sharded else "local"), "dims": D, "voxel_size_m": a.voxel,
+                   "nodes": int(seq.nodes.shape[0]), "matches": a.matches,
+                   "parallelism": f"{a.mode}{world}" + (f"-{a.solve}" if sharded else "")},
+        "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * float(np.mean(t_int)),
+                         "allreduce": 1e3 * t_ar, "pcg_iters_per_frame": float(np.mean(pcg)),
+                         "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid))},
+        "per_rank": per_rank,
+        "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster "
+                               "block-Jacobi apply)", "bound": "latency",
+                     "achieved": B_launch / t_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": B_launch / t_pcg / PEAK_HBM,
+                     "traffic": pmc_traffic("k_pcg_iter", workload), "traffic_source": os.path.relpath(PMC_FILE, ROOT),
+                     "bytes_per_iteration": B_pcg, "bytes_per_launch": B_launch, "avg_launch_us": 1e6 * t_pcg,
+                     "launches_per_frame": launches / a.steps, "iterations_per_frame": iters / a.steps,
+                     "us_per_iteration": 1e6 * pcg_ms * 1e-3 / max(1.0, iters), "nnz_blocks": nnzb,
+                     "note": "dominant kernel by time; latency-bound: one launch per iteration = the dispatch / "
+                             "kernel-boundary floor + two dependent memory trips + the wave's instruction stream "
+                             "(DESIGN.md §5); the 11-12 MB working set is L2/MALL-resident across launches. frac = "
+                             "bytes_per_launch / avg_launch_us / peak"},
         "roofline_integrate": {"kernel": "k_integrate<true,true> (fused warp+integrate, LDS node palette)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                               "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp"),
+                               "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp", workload),
                                "bytes_per_launch": B,
                                "avg_launch_us": 1e6 * t_kint, "listed_bricks": cache.n_list,
                                "skin_valid_voxels": n_skin_valid, "updated_voxels": U},
@@ -195,15 +317,30 @@ def main():
         dist.destroy_process_group()
 
 
+def cpu_model():
+    """`lscpu` model name of the host (from /proc/cpuinfo: the same field lscpu prints)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(pipe, fi, t, a):
-    """The oracle port on the host cores, on a bounded sample of the same frame:
+    """The oracle port on the host cores, on a bounded sample of the same frame (kind "port": the reference
+    Python cannot run here or travel; oracle/ restates it line for line):
     * warp+integrate: oracle/cpu_ref.c (C/OpenMP restatement of tsdf.py:378-494 + geometry.py:9-25) on a
       uniform random sample of the volume's voxels (skin precomputed, as the reference caches it), scaled
       to the whole volume;
     * solve: ONE Gauss-Newton step of the dense float64 restatement of DeformNet.optimize
       (oracle.fusion_oracle.gn_optimize, num_iter=1: dense J, JᵀJ, LU as model.py:222-859) on this frame's
       inputs and state, scaled x10 (the reference runs 10 GN iterations; the bench sequence never stops early).
-    CPU frames/s = 1 / (t_warp+integrate + 10 x t_gn_step)."""
+    CPU frames/s = 1 / (t_warp+integrate + 10 x t_gn_step), with all host threads (OMP_NUM_THREADS, BLAS
+    threads) and, as `single_thread`, with one: the integrate sample at one OpenMP thread and the GN step's
+    dominant dense JᵀJ product on 1/64 of J's columns at one BLAS thread (x64), plus the one-thread LU."""
     from oracle import cpu_ref
     from oracle import fusion_oracle as fo
     vol = pipe.vol
@@ -221,29 +358,69 @@ def cpu_baseline(pipe, fi, t, a):
                     (o[2] + vs * k.astype(np.float32).astype(np.float64))], 1).astype(np.float32)
     an, w, v = pipe.wf.skin_device(pts)
     an, w, v = an.cpu().numpy(), w.cpu().numpy(), v.cpu().numpy().astype(np.uint8)
-    tsdf, color, weight = (x.reshape(-1).copy() for x in vol.get_volume())
+    tsdf0, color0, weight0 = (x.reshape(-1).copy() for x in vol.get_volume())
     R = pipe.prev_rot.cpu().numpy().reshape(-1, 9)
     T = pipe.prev_trans.cpu().numpy()
     im = fi.im.cpu().numpy()
     depth, cim = fo.depth_of(im), fo.pack_color(im)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    t0 = time.perf_counter()
-    cpu_ref.integrate((Dx, Dy, Dz), vol._vol_origin, vol._voxel_size, vox, depth, cim, pipe.intr, tsdf, weight, color,
-                      warp=True, anchors=an, weights=w, valid=v, R=R, T=T, nodes=pipe.graph.nodes)
-    dt_int = time.perf_counter() - t0
+
+    def integrate_sample(nv):
+        tsdf, weight, color = tsdf0.copy(), weight0.copy(), color0.copy()
+        t0 = time.perf_counter()
+        cpu_ref.integrate((Dx, Dy, Dz), vol._vol_origin, vol._voxel_size, vox[:nv], depth, cim, pipe.intr, tsdf,
+                          weight, color, warp=True, anchors=an[:nv], weights=w[:nv], valid=v[:nv], R=R, T=T,
+                          nodes=pipe.graph.nodes)
+        return time.perf_counter() - t0
+
+    cpu_ref.set_threads(threads)
+    dt_int = integrate_sample(n)
     per_frame_int = dt_int * V / n
     g = pipe
+    gn_args = (g.graph.nodes, g.seq.edges, g.seq.edge_weights, fi.tpos.cpu().numpy(), fi.conf.cpu().numpy(),
+               fi.src.cpu().numpy(), fi.anchors.cpu().numpy(), fi.weights.cpu().numpy(), fi.tgt.cpu().numpy(),
+               pipe.intr)
     t0 = time.perf_counter()
-    fo.gn_optimize(g.graph.nodes, g.seq.edges, g.seq.edge_weights, fi.tpos.cpu().numpy(), fi.conf.cpu().numpy(),
-                   fi.src.cpu().numpy(), fi.anchors.cpu().numpy(), fi.weights.cpu().numpy(), fi.tgt.cpu().numpy(),
-                   pipe.intr, prev_rot=R.reshape(-1, 3, 3), prev_trans=T, num_iter=1)
+    fo.gn_optimize(*gn_args, prev_rot=R.reshape(-1, 3, 3), prev_trans=T, num_iter=1)
     dt_gn = time.perf_counter() - t0
     per_frame = per_frame_int + 10 * dt_gn
-    return {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"warp+integrate (oracle/cpu_ref.c, OpenMP) of {n} uniformly sampled voxels of the {Dx}^3 frame "
-                      f"(x{V / n:.0f} scaled, skin precomputed, {dt_int:.3f} s) + one dense float64 GN step "
-                      f"(oracle gn_optimize, numpy/LAPACK, {dt_gn:.2f} s) x 10 GN iterations",
-            "ms_per_frame_warp_integrate": 1e3 * per_frame_int, "s_per_gn_step": dt_gn}
+    out = {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
+           "sample": f"warp+integrate (oracle/cpu_ref.c, OpenMP) of {n} uniformly sampled voxels of the {Dx}^3 frame "
+                     f"(x{V / n:.0f} scaled, skin precomputed, {dt_int:.3f} s) + one dense float64 GN step "
+                     f"(oracle gn_optimize, numpy/LAPACK, {dt_gn:.2f} s) x 10 GN iterations",
+           "ms_per_frame_warp_integrate": 1e3 * per_frame_int, "s_per_gn_step": dt_gn}
+    # one thread: a 1/16 integrate sample, and the dense GN step's cost terms at one BLAS thread
+    try:
+        from threadpoolctl import threadpool_limits
+        cpu_ref.set_threads(1)
+        n1 = max(1, n // 16)
+        dt_int1 = integrate_sample(n1)
+        cpu_ref.set_threads(threads)
+        N6 = 6 * g.graph.nodes.shape[0]
+        rows = 3 * int(fi.src.shape[0]) + 3 * int((np.asarray(g.seq.edges) >= 0).sum()) + 3 * g.graph.nodes.shape[0]
+        Jr = np.random.default_rng(1).random((rows, N6))
+        cols = max(1, N6 // 64)
+        with threadpool_limits(limits=1):
+            t0 = time.perf_counter()
+            Jr.T @ Jr[:, :cols]
+            dt_mm = (time.perf_counter() - t0) * N6 / cols
+            from scipy.linalg import lu_factor
+            A = Jr[:N6].T @ Jr[:N6] + np.eye(N6)
+            t0 = time.perf_counter()
+            lu_factor(A)
+            dt_lu = time.perf_counter() - t0
+        del Jr
+        gn1 = dt_mm + dt_lu
+        pf1 = dt_int1 * V / n1 + 10 * gn1
+        out["single_thread"] = {"value": 1.0 / pf1, "unit": "frames/s", "cores": 1,
+                                "ms_per_frame_warp_integrate": 1e3 * dt_int1 * V / n1, "s_per_gn_step": gn1,
+                                "sample": f"integrate of {n1} sampled voxels at 1 OpenMP thread ({dt_int1:.3f} s, "
+                                          f"x{V / n1:.0f}); GN step = dense JᵀJ ({rows}x{N6}) measured on 1/64 of "
+                                          f"the columns at 1 BLAS thread ({dt_mm:.1f} s scaled) + LU of {N6}² "
+                                          f"({dt_lu:.1f} s)"}
+    except Exception as e:  # the reported baseline must not break the bench line
+        out["single_thread"] = {"error": repr(e)}
+    return out
 
 
 if __name__ == "__main__":

@@ -216,9 +216,11 @@ class GaussNewtonSolver:
 
     def optimize_distributed(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position,
                              node_confidence, source_points, anchors, weights, target_points, intrinsics,
-                             target_px=None, target_py=None, prev_rot=None, prev_trans=None, group=None, sync=True):
+                             target_px=None, target_py=None, prev_rot=None, prev_trans=None, group=None, sync=True,
+                             timer=None):
         """Match-sharded solve over torch.distributed: rank r assembles matches [r*M/W, (r+1)*M/W);
-        A and rhs are all-reduced (sum) once per GN iteration; rank 0 adds ARAP + motion rows."""
+        A and rhs are all-reduced (sum) once per GN iteration; rank 0 adds ARAP + motion rows.
+        timer: a list that receives (start, end) CUDA events around each GN step's all-reduce."""
         import torch.distributed as dist
         pb, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
                                  node_confidence, source_points, anchors, weights, target_points, intrinsics,
@@ -234,8 +236,15 @@ class GaussNewtonSolver:
         rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=self.device)
         for it in range(int(self.params["num_iter"])):
             call("ofx_gn_linearize", self._h, it, m0, m1, 1 if rank == 0 else 0, ptr(A), ptr(rhs), stream_ptr())
+            if timer is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             dist.all_reduce(A, group=group)
             dist.all_reduce(rhs, group=group)
+            if timer is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                timer.append((e0, e1))
             call("ofx_gn_step", self._h, it, ptr(A), ptr(rhs), stream_ptr())
         r, out = self._result(N)
         call("ofx_gn_finish", self._h, byref(r), stream_ptr())

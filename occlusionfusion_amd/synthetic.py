@@ -38,8 +38,18 @@ def bench_camera(scale=1):
     return Intrinsics(525.0 / scale, 525.0 / scale, 319.5 / scale, (239.5 - 16) / scale, 640 // scale, 448 // scale)
 
 
+def _axis_angle(axis, theta):
+    a = np.asarray(axis, np.float64)
+    a = a / np.linalg.norm(a)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return np.eye(3) + math.sin(theta) * K + (1.0 - math.cos(theta)) * (K @ K)
+
+
 @dataclass
 class SphereScene:
+    """motion="nonrigid" (BASELINE configs 3-5): the sphere breathes and drifts, the plane is static.
+    motion="rigid" (config 2): sphere + plane move as one rigid body about the sphere centre, at most
+    1.5° of rotation and 1 cm of translation per frame (≤2°, ≤1 cm)."""
     center: tuple = (0.0, 0.0, 1.4)
     radius: float = 0.35
     plane_z: float = 1.75
@@ -47,14 +57,26 @@ class SphereScene:
     occluder: bool = True
     occ_z: float = 0.9
     occ_half: float = 0.07
+    motion: str = "nonrigid"
 
     def occluder_x(self, t):
         """x centre of the occluding bar at frame t: out of view at t=0, over the sphere for t≈8..24."""
         return -0.75 + 0.375 * (1.0 - math.cos(0.2 * t))
 
+    def rigid_pose(self, t):
+        """(R_t, T_t): canonical (frame-0) point p -> R_t (p - c0) + c0 + T_t. R_0 = I, T_0 = 0."""
+        theta = math.radians(10.0) * math.sin(0.15 * t)          # |dθ/dt| <= 1.5° per frame
+        R = _axis_angle((0.3, 1.0, 0.2), theta)
+
+        def tr(s):
+            return np.array([0.05 * math.sin(0.12 * s), 0.03 * math.sin(0.15 * s + 0.5), 0.04 * math.sin(0.1 * s)])
+        return R, tr(t) - tr(0)                                     # |dT/dt| <= 0.9 cm per frame
+
     def frame_params(self, t):
-        """Sphere centre/radius at frame t (smooth non-rigid drift + breathing)."""
+        """Sphere centre/radius at frame t (smooth non-rigid drift + breathing; rigid: translated centre)."""
         c = np.array(self.center, np.float64)
+        if self.motion == "rigid":
+            return c + self.rigid_pose(t)[1], self.radius
         c = c + np.array([0.01 * math.sin(0.3 * t), 0.008 * math.sin(0.2 * t + 1.0), 0.012 * math.sin(0.25 * t)])
         r = self.radius * (1.0 + 0.03 * math.sin(0.35 * t))
         return c, r
@@ -62,6 +84,10 @@ class SphereScene:
     def deform_points(self, pts, t):
         """Ground-truth motion of canonical (frame-0) surface points to frame t."""
         pts = np.asarray(pts, np.float64)
+        if self.motion == "rigid":
+            R, T = self.rigid_pose(t)
+            c0 = np.array(self.center, np.float64)
+            return (pts - c0) @ R.T + c0 + T
         c0, r0 = self.frame_params(0)
         c, r = self.frame_params(t)
         out = pts.copy()
@@ -74,6 +100,8 @@ class SphereScene:
         u, v = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
         dx = (u - cam.cx) / cam.fx
         dy = (v - cam.cy) / cam.fy
+        if self.motion == "rigid":
+            return self._render_rigid(dx, dy, t, rng, noise)
         c, r = self.frame_params(t)
         # sphere: |z*(dx,dy,1) - c|^2 = r^2
         a = dx * dx + dy * dy + 1.0
@@ -89,10 +117,36 @@ class SphereScene:
             xo = self.occluder_x(t)
             hit = np.abs(dx * self.occ_z - xo) <= self.occ_half
             z = np.where(hit, np.minimum(z, self.occ_z), z)
+        return self._finish(z, rng, noise)
+
+    def _finish(self, z, rng, noise):
         if rng is not None and noise > 0:
             z = z + rng.normal(0.0, noise, z.shape)
         z = np.where(np.isfinite(z), np.round(z * 1000.0) / 1000.0, 0.0)
         return z.astype(np.float32)
+
+    def _render_rigid(self, dx, dy, t, rng, noise):
+        """Ray cast of the rigidly moved sphere + plane: rays z·(dx, dy, 1) taken into the canonical frame
+        (q = R_tᵀ (p - c0 - T_t) + c0 = z·R_tᵀ d + o) and intersected with the canonical scene."""
+        R, T = self.rigid_pose(t)
+        c0 = np.array(self.center, np.float64)
+        o = c0 - R.T @ (c0 + T)
+        d = np.stack([dx, dy, np.ones_like(dx)], -1) @ R          # rows: R_tᵀ d
+        oc = o - c0
+        a = (d * d).sum(-1)
+        b = 2.0 * (d @ oc)
+        cc = oc @ oc - self.radius ** 2
+        disc = b * b - 4 * a * cc
+        zs = np.where(disc >= 0, (-b - np.sqrt(np.maximum(disc, 0))) / (2 * a), np.inf)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            zp = (self.plane_z - o[2]) / d[..., 2]
+        qx, qy = o[0] + zp * d[..., 0], o[1] + zp * d[..., 1]
+        inplane = (zp > 0) & (np.abs(qx) <= self.plane_half[0]) & (np.abs(qy) <= self.plane_half[1])
+        z = np.minimum(zs, np.where(inplane, zp, np.inf))
+        if self.occluder:
+            hit = np.abs(dx * self.occ_z - self.occluder_x(t)) <= self.occ_half
+            z = np.where(hit, np.minimum(z, self.occ_z), z)
+        return self._finish(z, rng, noise)
 
 
 def backproject(depth, cam):
@@ -197,9 +251,11 @@ class SyntheticSequence:
     seed: int = 0
 
     @staticmethod
-    def build(n_nodes=2000, cam=None, seed=3, coverage=None):
+    def build(n_nodes=2000, cam=None, seed=3, coverage=None, scene=None):
+        """scene: SphereScene() (non-rigid with the occluder, configs 3-5) unless given, e.g.
+        SphereScene(motion="rigid", occluder=False) for config 2."""
         cam = cam or bench_camera()
-        scene = SphereScene()
+        scene = scene or SphereScene()
         d0 = scene.render(cam, 0, np.random.default_rng(seed))
         pts = backproject(d0, cam)
         cov = coverage if coverage is not None else coverage_for_nodes(pts, n_nodes, seed)

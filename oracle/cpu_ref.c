@@ -14,6 +14,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <omp.h>
 
 static inline float cdiv(float a, float b) { return (float)((double)a / (double)b); }
 
@@ -83,3 +84,6 @@ int64_t ofxref_integrate(int Dx, int Dy, int Dz, const float* origin, double vs,
   }
   return n_upd;
 }
+
+/* thread count of the OpenMP loop above (bench.py cpu_baseline: the 1-thread leg) */
+void ofxref_set_threads(int n) { omp_set_num_threads(n); }

@@ -30,6 +30,13 @@ def _lib():
 _F = None
 
 
+def set_threads(n):
+    """OpenMP thread count of the C restatement (bench.py's single-thread leg)."""
+    lib = ctypes.CDLL(LIB if os.path.exists(LIB) else build())
+    lib.ofxref_set_threads.argtypes = [ctypes.c_int]
+    lib.ofxref_set_threads(int(n))
+
+
 def _p(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 

@@ -268,8 +268,37 @@ def make_gn_small():
     print("gn_small:", nodes.shape[0], "nodes,", src.shape[0], "matches, loss", ci["total"][:3], "...")
 
 
+def config2_sequence():
+    """BASELINE config 2: rigid-motion sphere + plane, 640x448, ~1k nodes (seed 2)."""
+    scene = S.SphereScene(motion="rigid", occluder=False)
+    return S.SyntheticSequence.build(1000, seed=2, scene=scene)
+
+
+def make_gn_1k(t=1, n_matches=10000):
+    """gn_1k.npz — one DeformNet.optimize solve at a real config size (config 2: ~1k nodes, 10k matches,
+    J ≈ 57k x 6k dense) by the dense f64 oracle; pins the block-sparse assembly + PCG at that size."""
+    import time
+    seq = config2_sequence()
+    src, tgt, tpos, conf = seq.solver_inputs(t, n_matches)
+    a, w, v = fo.skin(src, seq.nodes, seq.node_coverage)
+    src, tgt, a, w = src[v], tgt[v], a[v], w[v]
+    intr = seq.cam.as_vec()
+    t0 = time.time()
+    out = fo.gn_optimize(seq.nodes, seq.edges, seq.edge_weights, tpos, conf, src, a, w, tgt, intr)
+    ci = out["convergence_info"]
+    np.savez_compressed(os.path.join(HERE, "gn_1k.npz"), nodes=seq.nodes, edges=seq.edges,
+                        edge_weights=seq.edge_weights, node_coverage=seq.node_coverage, tpos=tpos, conf=conf,
+                        src=src, anchors=a, weights=w, tgt=tgt, intr=intr, frame=t,
+                        R=out["node_rotations"], t=out["node_translations"], valid=out["valid_solve"],
+                        loss_total=np.array(ci["total"]))
+    print("gn_1k:", seq.nodes.shape[0], "nodes,", src.shape[0], "matches, loss", ci["total"][:3], "...",
+          f"{time.time() - t0:.0f} s")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn"]
+    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn", "gn1k"]
+    if "gn1k" in which:
+        make_gn_1k()
     if "skin" in which:
         make_skin_csrc()
     if "frontend" in which:

@@ -41,18 +41,7 @@ import torch  # noqa: E402
 PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
 
-# BASELINE.json configs -> (dims, voxel m, origin, nodes, scene motion, occluder, camera scale)
-CONFIGS = {
-    1: dict(dims=128, voxel=0.008, origin=(-0.512, -0.512, 0.9), nodes=200, motion="nonrigid", occluder=False,
-            cam_scale=2, seed=1),
-    2: dict(dims=256, voxel=0.004, origin=(-0.512, -0.512, 0.9), nodes=1000, motion="rigid", occluder=False,
-            cam_scale=1, seed=2),
-    3: dict(dims=512, voxel=0.004, origin=(-1.024, -1.024, 0.5), nodes=2000, motion="nonrigid", occluder=True,
-            cam_scale=1, seed=3),
-    4: dict(dims=1024, voxel=0.002, origin=(-1.024, -1.024, 0.5), nodes=4000, motion="nonrigid", occluder=True,
-            cam_scale=1, seed=4),
-}
-CONFIGS[5] = dict(CONFIGS[3])
+from occlusionfusion_amd.synthetic import BASELINE_CONFIGS as CONFIGS  # noqa: E402  (configs 1-5)
 
 
 def pmc_traffic(kernel, workload):
@@ -169,8 +158,7 @@ def main():
     D = a.dims
     origin = cfg["origin"] if (a.dims, a.voxel) == (cfg["dims"], cfg["voxel"]) else \
         (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
-    scene = S.SphereScene(motion=cfg["motion"], occluder=cfg["occluder"])
-    seq = S.SyntheticSequence.build(a.nodes, cam=S.bench_camera(cfg["cam_scale"]), seed=cfg["seed"], scene=scene)
+    seq = S.config_sequence(a.config, a.nodes)
     sharded = a.mode == "shard" and world > 1
     shard = (rank, world) if sharded else None
     pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)

@@ -379,6 +379,9 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
  * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
 int ofx_gn_info(void* handle, int64_t* info);
+/* Waves per PCG cluster workgroup of k_pcg_iter chosen at create: 2 (default) or 1 (environment
+ * OFX_PCG_W1 set to anything but "" / "0"; tuning and A/B only). */
+int ofx_gn_pcg_waves(void* handle, int32_t* waves);
 /* Per-GN-step statistics of the last solve: out (host f64[3*cap]) = [PCG iterations, |b|², loss] per
  * step (zeros for steps that did not run); synchronous D2H copy, at most 64 steps. */
 int ofx_gn_stats(void* handle, double* out, int32_t cap);

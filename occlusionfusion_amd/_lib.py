@@ -96,6 +96,7 @@ _SIGS = {
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
+    "ofx_gn_pcg_waves": [P, P],
     "ofx_gn_stats": [P, P, c_int32],
     "ofx_gn_row_order": [P, P, c_int32],
     "ofx_gn_setup": [P, P, P, P, P],

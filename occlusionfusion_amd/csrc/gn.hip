@@ -1163,8 +1163,11 @@ __global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict_
 // z = q = s = p = w = 0, u0 -> m1.
 __global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict__ rhs) {
   __shared__ double s_v[kCD];
-  if (g.flags[F_STOPPED]) return;
   const int lane = threadIdx.x;
+  if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
+    return;
+  }
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const int np = g.n_prev;
   const bool own = q < 6;
@@ -1242,8 +1245,11 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict
 // (γ0 = r·u, δ0 = w·u, r·r) -> parity 0, b·b -> part_b.
 __global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
   __shared__ double s_v[kCD];
-  if (g.flags[F_STOPPED]) return;
   const int lane = threadIdx.x;
+  if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
+    return;
+  }
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const bool own = q < 6;
   const int64_t o = 6 * (int64_t)row + q;
@@ -1415,7 +1421,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   constexpr int kNH = kW2 ? 2 : 1;
   __shared__ double s_v[kNH][kCD];
-  __shared__ float4 s_m[kCD * kCD / 4 + (kW2 ? 64 : 0)];   // kW2: a wave's last DMA may overrun its half
+  __shared__ float4 s_m[kCD * kCD / 4];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   __shared__ double s_half[kW2 ? 64 : 1];
   const int lane = threadIdx.x & 63;
@@ -1445,13 +1451,15 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
-  if (kW2) {   // wave h: column groups [6h, 6h + 6) = float4 [288h, 288h + 288), 5 DMA instructions (clamped source)
+  if (kW2) {   // wave h: column groups [6h, 6h + 6) = float4 [288h, 288h + 288), 5 DMA instructions; the last
+              // one is moved back to end at the half's end (it rewrites 32 of the wave's own float4 with the
+              // same bits), so no wave's DMA touches the other wave's half
     constexpr int kHalf = kCD * kCD / 8;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-      const int f = kHalf * hw + k * 64;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + min(f + lane, kCD * kCD / 4 - 1)),
-                                       reinterpret_cast<void*>(s_m + f), 16, 0, 0);
+      const int f = kHalf * hw + min(k * 64, kHalf - 64);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + f + lane), reinterpret_cast<void*>(s_m + f),
+                                       16, 0, 0);
     }
   } else {
 #pragma unroll
@@ -1535,7 +1543,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
     g.stopw[(int64_t)wv * 64 + lane] = 1;
     const bool ill = !conv && !isfinite(alpha);
-    if (g.fuse) fused_step(g, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
+    if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
     if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
       if (ill) g.flags[F_ILL] = 1;
@@ -1950,7 +1958,10 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     return OFX_ERR_RANGE;
   }
   Gn* g = new Gn();
-  g->pcg_w2 = getenv("OFX_PCG_W1") ? 0 : 1;   // tuning / A-B: one wave per cluster
+  {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster
+    const char* e = getenv("OFX_PCG_W1");
+    g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
+  }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
   // rows: clusters of <= kCS first-fit packed into groups of kCS; at most one group is at most half
@@ -2019,6 +2030,13 @@ int ofx_gn_info(void* handle, int64_t* info) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && info, "null handle/info");
   info[0] = g->N_real; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T; info[4] = g->N;
+  return OFX_OK;
+}
+
+int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && waves, "null handle/waves");
+  *waves = g->pcg_w2 ? 2 : 1;
   return OFX_OK;
 }
 

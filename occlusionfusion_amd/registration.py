@@ -70,6 +70,12 @@ class GaussNewtonSolver:
         call("ofx_gn_info", self._h, arr)
         return list(arr)
 
+    def pcg_waves(self):
+        """Waves per cluster workgroup of the PCG iteration kernel (2, or 1 under OFX_PCG_W1=1)."""
+        w = ctypes.c_int32()
+        call("ofx_gn_pcg_waves", self._h, byref(w))
+        return w.value
+
     def row_order(self):
         """PCG row -> node of the last setup (-1: padding row); the order of rhs / the state rows."""
         rows = self.info()[4]

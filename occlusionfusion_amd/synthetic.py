@@ -299,3 +299,25 @@ class SyntheticSequence:
             facing = facing & self.visible(tpos, t, tol=0.02)
         conf = np.where(facing, 1.0, occluded_conf).astype(np.float32)
         return src.astype(np.float32), tgt.astype(np.float32), tpos.astype(np.float32), conf
+
+
+# BASELINE.json configs: volume dims / voxel size / origin, graph size, motion, occluder, camera
+# scale (2: the 320x240 -> 320x224 camera of config 1) and the sequence seed (= config index).
+BASELINE_CONFIGS = {
+    1: dict(dims=128, voxel=0.008, origin=(-0.512, -0.512, 0.9), nodes=200, motion="nonrigid", occluder=False,
+            cam_scale=2, seed=1),
+    2: dict(dims=256, voxel=0.004, origin=(-0.512, -0.512, 0.9), nodes=1000, motion="rigid", occluder=False,
+            cam_scale=1, seed=2),
+    3: dict(dims=512, voxel=0.004, origin=(-1.024, -1.024, 0.5), nodes=2000, motion="nonrigid", occluder=True,
+            cam_scale=1, seed=3),
+    4: dict(dims=1024, voxel=0.002, origin=(-1.024, -1.024, 0.5), nodes=4000, motion="nonrigid", occluder=True,
+            cam_scale=1, seed=4),
+}
+BASELINE_CONFIGS[5] = dict(BASELINE_CONFIGS[3])   # 8 independent config-3 scenes, one per GPU
+
+
+def config_sequence(config, n_nodes=None):
+    """The seeded synthetic sequence of BASELINE config `config` (1..5)."""
+    c = BASELINE_CONFIGS[config]
+    scene = SphereScene(motion=c["motion"], occluder=c["occluder"])
+    return SyntheticSequence.build(n_nodes or c["nodes"], cam=bench_camera(c["cam_scale"]), seed=c["seed"], scene=scene)

@@ -16,6 +16,8 @@
                         compute_edges_geodesic in the three modes EDGraph uses, node_and_edge_clean_up,
                         compute_clusters, compute_edges_euclidean.
   gn_small.npz        — one DeformNet.optimize solve (N≈100, M=600) by the dense f64 oracle.
+  gn_1k.npz           — one DeformNet.optimize solve at BASELINE config 2's size (rigid sequence, 1025 nodes,
+                        10k matches, dense J ≈ 57k x 6k) by the dense f64 oracle (≈2 min on 8 cores).
   frontend_csrc.npz   — backproject_depth_float / _ushort and compute_mesh_from_depth outputs of the
                         REFERENCE's compiled C++ (csrc/cpu/image_proc.cpp:351-545) on a synthetic frame,
                         incl. max-distance thresholds that tie exactly with triangle edge lengths; plus the
@@ -270,8 +272,7 @@ def make_gn_small():
 
 def config2_sequence():
     """BASELINE config 2: rigid-motion sphere + plane, 640x448, ~1k nodes (seed 2)."""
-    scene = S.SphereScene(motion="rigid", occluder=False)
-    return S.SyntheticSequence.build(1000, seed=2, scene=scene)
+    return S.config_sequence(2)
 
 
 def make_gn_1k(t=1, n_matches=10000):

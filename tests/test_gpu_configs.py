@@ -1,0 +1,176 @@
+"""GPU: every BASELINE.json config on the HIP path against the oracle (SURVEY §8(d) workloads).
+
+* config 1 — 128³ @8 mm, 200 nodes, 320x240 camera: the WHOLE volume after the source frame and two
+  solver-driven warped frames equals the oracle run live on all 2.1M voxels (bit-exact tsdf / weight /
+  colour), and the GN solve of each frame is within 1e-5 of the dense f64 oracle (model.py:222-859).
+* config 2 — 256³ @4 mm, ~1k nodes, rigid sequence: GN against the committed dense-f64 fixture
+  tests/golden/gn_1k.npz (1025 nodes, 10k matches: the block-sparse assembly + PCG at a real size) within
+  1e-5; sampled-voxel integrate parity after a warped frame.
+* config 4 — 1024³ @2 mm, ~4k nodes, on one GPU (12.9 GB of volume): sampled-voxel integrate parity after a
+  warped frame, tight-vs-default GN within 1e-5 and bitwise-repeatable solves.
+(config 3 is tests/test_gpu_full.py; config 5 is config 3 per GPU — bench.py --gpus N replicas.)
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fusion_oracle as fo
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def make_pipe(config, cuda, n_nodes=None):
+    from occlusionfusion_amd import synthetic as S
+    from occlusionfusion_amd.pipeline import FusionPipeline
+    c = S.BASELINE_CONFIGS[config]
+    seq = S.config_sequence(config, n_nodes)
+    D = c["dims"]
+    pipe = FusionPipeline(seq, c["origin"], c["voxel"], (D, D, D), device=cuda)
+    pipe.integrate_source(pipe.prepare(0))
+    return pipe
+
+
+def voxel_positions(vol, vox):
+    """vox2world (tsdf.py:338-349) of C-order voxel ids."""
+    Dx, Dy, Dz = (int(d) for d in vol._vol_dim)
+    i, r = vox // (Dy * Dz), vox % (Dy * Dz)
+    j, k = r // Dz, r % Dz
+    o = vol._vol_origin.astype(np.float64)
+    vs = np.float64(vol._voxel_size)
+    return np.stack([(o[q] + vs * ax.astype(np.float32).astype(np.float64)) for q, ax in enumerate((i, j, k))],
+                    1).astype(np.float32)
+
+
+def sample_voxels(pipe, n, seed, whole_bricks=8):
+    vol = pipe.vol
+    Dx, Dy, Dz = (int(d) for d in vol._vol_dim)
+    rng = np.random.default_rng(seed)
+    vox = [rng.choice(Dx * Dy * Dz, n, replace=False)]
+    cache = pipe.wf.skin_tsdf_cache()
+    blist = cache.brick_list.cpu().numpy()[:cache.n_list]
+    nby, nbz = (Dy + 7) // 8, (Dz + 7) // 8
+    for b in blist[rng.choice(len(blist), min(whole_bricks, len(blist)), replace=False)]:
+        bx, by, bz = b // (nby * nbz), (b // nbz) % nby, b % nbz
+        ii, jj, kk = np.meshgrid(np.arange(8) + 8 * bx, np.arange(8) + 8 * by, np.arange(8) + 8 * bz, indexing="ij")
+        ok = (ii < Dx) & (jj < Dy) & (kk < Dz)
+        vox.append((ii * Dy * Dz + jj * Dz + kk)[ok].reshape(-1))
+    return np.unique(np.concatenate(vox))
+
+
+def fuse_and_compare(pipe, vox, frames):
+    """Source frame 0 (already fused by make_pipe) + the warped frames `frames` (each: GN solve on the device,
+    then integrate); the oracle replays the same frames on the voxels `vox` with the solver's transforms."""
+    seq, vol, intr = pipe.seq, pipe.vol, pipe.intr
+    pts = voxel_positions(vol, vox)
+    n = len(vox)
+    t, w, c = np.ones(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    im0 = pipe.prepare(0).im.cpu().numpy()
+    fo.integrate(t, w, c, pts, np.ones(n, bool), fo.depth_of(im0), fo.pack_color(im0), intr)
+    a, ww, v = fo.skin(pts, seq.nodes, seq.node_coverage)
+    for fr in frames:
+        f = pipe.prepare(fr)
+        pipe.step(f, fr)
+        R, T = pipe.prev_rot.cpu().numpy(), pipe.prev_trans.cpu().numpy()
+        x = fo.ed_warp(pts, a, ww, v, R, T, seq.nodes)
+        im = f.im.cpu().numpy()
+        fo.integrate(t, w, c, x, v, fo.depth_of(im), fo.pack_color(im), intr)
+    T1, C1, W1 = (q.reshape(-1)[vox] for q in vol.get_volume())
+    np.testing.assert_array_equal(T1, t)
+    np.testing.assert_array_equal(W1, w)
+    np.testing.assert_array_equal(C1, c)
+    return w
+
+
+def gn_vs_oracle(pipe, fr, tol=1e-5):
+    f = pipe.prepare(fr)
+    seq = pipe.seq
+    args = (seq.nodes, seq.edges, seq.edge_weights, f.tpos.cpu().numpy(), f.conf.cpu().numpy(), f.src.cpu().numpy(),
+            f.anchors.cpu().numpy(), f.weights.cpu().numpy(), f.tgt.cpu().numpy(), pipe.intr)
+    ref = fo.gn_optimize(*args)
+    from occlusionfusion_amd import GaussNewtonSolver
+    out = GaussNewtonSolver(len(seq.nodes), 10000).optimize(*args)
+    assert out["valid_solve"] == ref["valid_solve"] == 1
+    dr = np.abs(out["node_rotations"].cpu().numpy() - ref["node_rotations"]).max()
+    dt = np.abs(out["node_translations"].cpu().numpy() - ref["node_translations"]).max()
+    assert dr < tol and dt < tol, (dr, dt)
+    return dr, dt
+
+
+# ---------------------------------------------------------------- config 1
+def test_config1_whole_volume_matches_oracle(cuda):
+    pipe = make_pipe(1, cuda)
+    vol = pipe.vol
+    assert tuple(int(d) for d in vol._vol_dim) == (128, 128, 128) and pipe.seq.cam.width == 320
+    assert 150 <= pipe.seq.nodes.shape[0] <= 260
+    V = 128 ** 3
+    w = fuse_and_compare(pipe, np.arange(V), frames=(1, 2))
+    assert (w > 1).sum() > 10000          # the warped frames really integrated skinned voxels
+
+
+def test_config1_gn_matches_dense_oracle(cuda):
+    pipe = make_pipe(1, cuda)
+    gn_vs_oracle(pipe, 1)
+
+
+# ---------------------------------------------------------------- config 2
+def test_config2_gn_matches_dense_golden(cuda):
+    """gn_1k.npz: the dense f64 restatement of DeformNet.optimize on config 2's rigid frame 1 (1025 nodes,
+    10k matches). Transforms within the north star's 1e-5."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = np.load(os.path.join(GOLDEN, "gn_1k.npz"), allow_pickle=False)
+    assert g["nodes"].shape[0] > 900 and g["src"].shape[0] == 10000
+    s = GaussNewtonSolver(g["nodes"].shape[0], 10000)
+    out = s.optimize(g["nodes"], g["edges"], g["edge_weights"], g["tpos"], g["conf"], g["src"], g["anchors"],
+                     g["weights"], g["tgt"], g["intr"])
+    assert out["valid_solve"] == int(g["valid"]) == 1
+    assert out["convergence_info"]["gn_iterations"] == len(g["loss_total"])
+    np.testing.assert_allclose(out["convergence_info"]["total"], g["loss_total"], rtol=1e-6)
+    dr = np.abs(out["node_rotations"].cpu().numpy() - g["R"]).max()
+    dt = np.abs(out["node_translations"].cpu().numpy() - g["t"]).max()
+    assert dr < 1e-5 and dt < 1e-5, (dr, dt)
+
+
+def test_config2_rigid_integrate_matches_oracle_on_samples(cuda):
+    pipe = make_pipe(2, cuda)
+    assert tuple(int(d) for d in pipe.vol._vol_dim) == (256, 256, 256)
+    vox = sample_voxels(pipe, 300000, seed=2)
+    w = fuse_and_compare(pipe, vox, frames=(1,))
+    assert (w > 1).sum() > 1000
+
+
+# ---------------------------------------------------------------- config 4
+@pytest.fixture(scope="module")
+def pipe4(cuda):
+    p = make_pipe(4, cuda)
+    yield p
+    del p
+    torch.cuda.empty_cache()
+
+
+def test_config4_integrate_matches_oracle_on_samples(pipe4):
+    assert tuple(int(d) for d in pipe4.vol._vol_dim) == (1024, 1024, 1024)
+    assert 3500 <= pipe4.seq.nodes.shape[0] <= 4600
+    vox = sample_voxels(pipe4, 200000, seed=4)
+    w = fuse_and_compare(pipe4, vox, frames=(1,))
+    assert (w > 1).sum() > 1000
+
+
+def test_config4_gn_tolerance_and_determinism(pipe4):
+    from occlusionfusion_amd import GaussNewtonSolver
+    p = pipe4
+    f = p.prepare(2)
+    args = (p.nodes_t, p.edges_t, p.ew_t, f.tpos, f.conf, f.src, f.anchors, f.weights, f.tgt, p.intr)
+    N = len(p.seq.nodes)
+    tight = GaussNewtonSolver(N, 10000, pcg_tol=1e-11).optimize(*args)
+    s = GaussNewtonSolver(N, 10000)
+    a = s.optimize(*args)
+    b = s.optimize(*args)
+    assert a["valid_solve"] == 1 and tight["valid_solve"] == 1
+    assert torch.equal(a["node_translations"], b["node_translations"])
+    assert torch.equal(a["node_rotations"], b["node_rotations"])
+    dt = (a["node_translations"] - tight["node_translations"]).abs().max().item()
+    dr = (a["node_rotations"] - tight["node_rotations"]).abs().max().item()
+    assert dt < 1e-5 and dr < 1e-5, (dt, dr)

@@ -311,6 +311,9 @@ def test_gn_one_and_two_wave_pcg_agree(cuda, golden_dir, monkeypatch):
     two = GaussNewtonSolver(len(g["nodes"]), 1000)
     monkeypatch.setenv("OFX_PCG_W1", "1")
     one = GaussNewtonSolver(len(g["nodes"]), 1000)
+    monkeypatch.setenv("OFX_PCG_W1", "0")                 # parsed, not a presence test
+    two_again = GaussNewtonSolver(len(g["nodes"]), 1000)
+    assert (two.pcg_waves(), one.pcg_waves(), two_again.pcg_waves()) == (2, 1, 2)
     outs = {}
     for name, s in (("two", two), ("one", one)):
         a = s.optimize(*_gn_inputs(g))
@@ -321,6 +324,23 @@ def test_gn_one_and_two_wave_pcg_agree(cuda, golden_dir, monkeypatch):
         outs[name] = a
     assert (outs["two"]["node_translations"] - outs["one"]["node_translations"]).abs().max().item() < 1e-6
     assert (outs["two"]["node_rotations"] - outs["one"]["node_rotations"]).abs().max().item() < 1e-6
+
+
+def test_gn_stop_with_unconverged_pcg_keeps_the_stopping_step(cuda, golden_dir):
+    """PCG capped far below convergence (k_step runs as its own launch) plus a loss rule that stops at the
+    second GN step: the step enqueued before the host sees the stop must not move R/t (its iteration
+    launches end after trip 1 and the fused step is skipped). The result equals a solve that runs exactly
+    the accepted steps."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    a = GaussNewtonSolver(len(g["nodes"]), 1000, pcg_max_iter=2, stop_loss_diff=-1.0).optimize(*_gn_inputs(g))
+    k = a["convergence_info"]["gn_iterations"]
+    assert a["valid_solve"] == 1 and 1 <= k < 10
+    b = GaussNewtonSolver(len(g["nodes"]), 1000, pcg_max_iter=2, num_iter=k, stop_loss_diff=1e9).optimize(
+        *_gn_inputs(g))
+    assert b["convergence_info"]["gn_iterations"] == k
+    assert torch.equal(a["node_rotations"], b["node_rotations"])
+    assert torch.equal(a["node_translations"], b["node_translations"])
 
 
 def test_gn_solver_reuse_across_graph_change(cuda, golden_dir):

@@ -19,8 +19,8 @@ import math
 import numpy as np
 import torch
 
-from . import _lib
-from ._lib import call, ptr, stream_ptr, byref
+from . import _lib, ops  # noqa: F401  (ops registers torch.ops.ofx.*)
+from ._lib import call, byref
 from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
@@ -48,6 +48,7 @@ class GaussNewtonSolver:
             call("ofx_gn_create", self.max_nodes, self.max_matches, byref(h))
         self._h = h
         self._keep = []
+        self._state = torch.zeros(1, dtype=torch.int32, device=self.device)   # ofx::gn_* ordering token (ops.py)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -90,90 +91,64 @@ class GaussNewtonSolver:
         call("ofx_gn_stats", self._h, arr, n)
         return np.array(arr[:3 * n], dtype=np.float64).reshape(n, 3)
 
-    def _params(self):
-        p = _lib.GnParams()
+    def _plist(self, mode=0, pcg_tol=None):
+        """GN parameters as the ofx::gn_* operators take them (ops._gn_params)."""
         q = self.params
-        p.num_iter = int(q["num_iter"])
-        p.use_edge_weighting = int(bool(q["use_edge_weighting"]))
-        p.pcg_max_iter = int(q["pcg_max_iter"])
-        p.pcg_warm = int(bool(q["pcg_warm"]))
-        p.lambda_flow, p.lambda_depth = float(q["lambda_flow"]), float(q["lambda_depth"])
-        p.lambda_arap, p.lambda_motion = float(q["lambda_arap"]), float(q["lambda_motion"])
-        p.lm_factor, p.stop_loss_diff, p.pcg_tol = float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"])
-        p.mode = 0
-        p.precond_every = int(q.get("precond_every", 1))
-        return p
+        fp = [float(q["lambda_flow"]), float(q["lambda_depth"]), float(q["lambda_arap"]), float(q["lambda_motion"]),
+              float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"] if pcg_tol is None else pcg_tol)]
+        ip = [int(q["num_iter"]), int(bool(q["use_edge_weighting"])), int(q["pcg_max_iter"]), int(bool(q["pcg_warm"])),
+              int(mode), int(q.get("precond_every", 1))]
+        return fp, ip
 
     def _problem(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
                  source_points, anchors, weights, target_points, intrinsics, target_px, target_py, prev_rot,
                  prev_trans):
+        """Device tensors of one problem in the ofx::gn_* operators' argument order (+ N, M)."""
         d = self.device
-        ts = dict(nodes=_t(graph_nodes, d, torch.float32).reshape(-1, 3))
-        N = ts["nodes"].shape[0]
-        ts["edges"] = _t(graph_edges, d, torch.int32).reshape(N, -1)
-        ts["ew"] = _t(graph_edges_weights, d, torch.float32)
-        ts["tpos"] = (_t(target_node_position, d, torch.float32).reshape(N, 3) if target_node_position is not None
-                      else ts["nodes"].clone())
-        ts["conf"] = (_t(node_confidence, d, torch.float32).reshape(N) if node_confidence is not None
-                      else torch.zeros(N, device=d))
-        ts["src"] = _t(source_points, d, torch.float32).reshape(-1, 3)
-        M = ts["src"].shape[0]
-        ts["anc"] = _t(anchors, d, torch.int32).reshape(M, 4)
-        ts["wts"] = _t(weights, d, torch.float32).reshape(M, 4)
-        ts["tgt"] = _t(target_points, d, torch.float32).reshape(M, 3)
-        ts["tpx"] = _t(target_px, d, torch.float32)
-        ts["tpy"] = _t(target_py, d, torch.float32)
-        ts["prev_rot"] = _t(prev_rot, d, torch.float32)
-        ts["prev_trans"] = _t(prev_trans, d, torch.float32)
+        nodes = _t(graph_nodes, d, torch.float32).reshape(-1, 3)
+        N = nodes.shape[0]
+        src = _t(source_points, d, torch.float32).reshape(-1, 3)
+        M = src.shape[0]
         if N > self.max_nodes or M > self.max_matches:
             raise ValueError(f"problem ({N} nodes, {M} matches) exceeds solver capacity "
                              f"({self.max_nodes}, {self.max_matches})")
-        pb = _lib.GnProblem()
-        pb.n_nodes, pb.n_matches, pb.n_neighbors = N, M, ts["edges"].shape[1]
-        pb.nodes, pb.edges, pb.edge_weights = ptr(ts["nodes"]), ptr(ts["edges"]), ptr(ts["ew"])
-        pb.target_node_pos, pb.node_conf = ptr(ts["tpos"]), ptr(ts["conf"])
-        pb.src, pb.anchors, pb.weights, pb.tgt = ptr(ts["src"]), ptr(ts["anc"]), ptr(ts["wts"]), ptr(ts["tgt"])
-        pb.target_px, pb.target_py = ptr(ts["tpx"]), ptr(ts["tpy"])
-        pb.prev_rot, pb.prev_trans = ptr(ts["prev_rot"]), ptr(ts["prev_trans"])
-        fx, fy, cx, cy = (float(v) for v in np.asarray(intrinsics, np.float64).reshape(-1)[:4])
-        pb.fx, pb.fy, pb.cx, pb.cy = fx, fy, cx, cy
-        self._keep = ts  # keep inputs alive while the stream uses them
-        return pb, N, M
-
-    def _result(self, N):
-        d = self.device
-        out = dict(rot=torch.empty((N, 3, 3), device=d), trans=torch.empty((N, 3), device=d),
-                   status=torch.zeros(4, dtype=torch.int32, device=d),
-                   loss=torch.zeros((int(self.params["num_iter"]), 4), dtype=torch.float64, device=d))
-        r = _lib.GnResult()
-        r.rot, r.trans, r.status, r.loss_log = ptr(out["rot"]), ptr(out["trans"]), ptr(out["status"]), ptr(out["loss"])
-        return r, out
+        args = [nodes, _t(graph_edges, d, torch.int32).reshape(N, -1), _t(graph_edges_weights, d, torch.float32),
+                (_t(target_node_position, d, torch.float32).reshape(N, 3) if target_node_position is not None
+                 else nodes.clone()),
+                (_t(node_confidence, d, torch.float32).reshape(N) if node_confidence is not None
+                 else torch.zeros(N, device=d)),
+                src, _t(anchors, d, torch.int32).reshape(M, 4), _t(weights, d, torch.float32).reshape(M, 4),
+                _t(target_points, d, torch.float32).reshape(M, 3), _t(target_px, d, torch.float32),
+                _t(target_py, d, torch.float32), _t(prev_rot, d, torch.float32), _t(prev_trans, d, torch.float32),
+                [float(v) for v in np.asarray(intrinsics, np.float64).reshape(-1)[:4]]]
+        self._keep = args   # the last problem's inputs (arap reads prev_trans back)
+        return args, N, M
 
     @staticmethod
     def _pack(out, sync):
-        res = {"node_rotations": out["rot"], "node_translations": out["trans"], "_status": out["status"],
-               "_loss": out["loss"]}
+        rot, trans, status, loss = out
+        res = {"node_rotations": rot, "node_translations": trans, "_status": status, "_loss": loss}
         if sync:
-            st = out["status"].cpu().numpy()
-            loss = out["loss"].cpu().numpy()[:st[1]]
+            st = status.cpu().numpy()
+            loss = loss.cpu().numpy()[:st[1]]
             res["valid_solve"] = int(st[0])
             res["convergence_info"] = {"total": loss[:, 0].tolist(), "data": loss[:, 1].tolist(),
                                        "arap": loss[:, 2].tolist(), "motion": loss[:, 3].tolist(),
                                        "valid": int(st[0]), "gn_iterations": int(st[1]),
                                        "pcg_iterations": int(st[2]), "errors": (["Solver failed: Ill-posed system!"]
-                                                                                 if st[3] else [])}
+                                                                                if st[3] else [])}
         return res
 
     def optimize(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
                  source_points, anchors, weights, target_points, intrinsics, target_px=None, target_py=None,
                  prev_rot=None, prev_trans=None, sync=True):
-        """model.py:222-859 (batch item). Returns torch device tensors (+ host convergence info if sync)."""
-        pb, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
-                                 node_confidence, source_points, anchors, weights, target_points, intrinsics,
-                                 target_px, target_py, prev_rot, prev_trans)
-        r, out = self._result(N)
-        prm = self._params()
-        call("ofx_gn_solve", self._h, byref(pb), byref(prm), byref(r), stream_ptr())
+        """model.py:222-859 (batch item) through torch.ops.ofx.gn_solve. Returns torch device tensors (+ host
+        convergence info if sync)."""
+        args, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
+                                   node_confidence, source_points, anchors, weights, target_points, intrinsics,
+                                   target_px, target_py, prev_rot, prev_trans)
+        fp, ip = self._plist()
+        out = torch.ops.ofx.gn_solve(self._state, self._h.value, *args, fp, ip)
         return self._pack(out, sync)
 
     def arap(self, graph_nodes, source_node_position, target_node_position, valid_nodes_mask, original_graph_nodes,
@@ -201,16 +176,13 @@ class GaussNewtonSolver:
         tpos = torch.zeros((N, 3), device=d)
         tpos[vidx] = _t(target_node_position, d, torch.float32).reshape(-1, 3)
         z3 = np.zeros((0, 3), np.float32)
-        pb, N, _ = self._problem(nodes, graph_edges, graph_edges_weights, tpos, valid.float(), z3,
-                                 np.zeros((0, 4), np.int32), np.zeros((0, 4), np.float32), z3, (1.0, 1.0, 0.0, 0.0),
-                                 None, None, R_current, t_current)
-        r, out = self._result(N)
-        prm = self._params()
-        prm.mode = 1
-        prm.pcg_tol = float(pcg_tol)
-        call("ofx_gn_solve", self._h, byref(pb), byref(prm), byref(r), stream_ptr())
+        args, N, _ = self._problem(nodes, graph_edges, graph_edges_weights, tpos, valid.float(), z3,
+                                   np.zeros((0, 4), np.int32), np.zeros((0, 4), np.float32), z3, (1.0, 1.0, 0.0, 0.0),
+                                   None, None, R_current, t_current)
+        fp, ip = self._plist(mode=1, pcg_tol=pcg_tol)
+        out = torch.ops.ofx.gn_solve(self._state, self._h.value, *args, fp, ip)
         res = self._pack(out, sync)
-        t_init = self._keep["prev_trans"]
+        t_init = self._keep[12]                              # prev_trans as uploaded
         t0 = t_init[vidx] if t_init is not None else torch.zeros_like(src)
         res["deformed_nodes_to_target"] = src + t0          # valid nodes never move (model.py:1719,1961-1962)
         if sync:
@@ -228,20 +200,19 @@ class GaussNewtonSolver:
         A and rhs are all-reduced (sum) once per GN iteration; rank 0 adds ARAP + motion rows.
         timer: a list that receives (start, end) CUDA events around each GN step's all-reduce."""
         import torch.distributed as dist
-        pb, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
-                                 node_confidence, source_points, anchors, weights, target_points, intrinsics,
-                                 target_px, target_py, prev_rot, prev_trans)
-        prm = self._params()
-        nnz = _lib.c_int64()
-        call("ofx_gn_setup", self._h, byref(pb), byref(prm), byref(nnz), stream_ptr())
+        args, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
+                                   node_confidence, source_points, anchors, weights, target_points, intrinsics,
+                                   target_px, target_py, prev_rot, prev_trans)
+        fp, ip = self._plist()
+        h = self._h.value
+        nnz, rows = (int(v) for v in torch.ops.ofx.gn_setup(self._state, h, *args, fp, ip))
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         m0, m1 = match_range(M, rank, world)
-        A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=self.device)
-        rows = self.info()[4]        # nodes in cluster order, padded (include/ofx.h: ofx_gn_info)
-        rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=self.device)
+        A = torch.empty(nnz * 36, dtype=torch.float64, device=self.device)
+        rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=self.device)   # include/ofx.h: ofx_gn_linearize
         for it in range(int(self.params["num_iter"])):
-            call("ofx_gn_linearize", self._h, it, m0, m1, 1 if rank == 0 else 0, ptr(A), ptr(rhs), stream_ptr())
+            torch.ops.ofx.gn_linearize(self._state, h, it, m0, m1, rank == 0, A, rhs)
             if timer is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -251,9 +222,8 @@ class GaussNewtonSolver:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
                 timer.append((e0, e1))
-            call("ofx_gn_step", self._h, it, ptr(A), ptr(rhs), stream_ptr())
-        r, out = self._result(N)
-        call("ofx_gn_finish", self._h, byref(r), stream_ptr())
+            torch.ops.ofx.gn_step(self._state, h, it, A, rhs)
+        out = torch.ops.ofx.gn_finish(self._state, h, N, int(self.params["num_iter"]))
         return self._pack(out, sync)
 
 

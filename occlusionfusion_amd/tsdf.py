@@ -17,7 +17,7 @@ from types import SimpleNamespace
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, ops  # noqa: F401  (ops registers torch.ops.ofx.*)
 from ._lib import call, ptr, stream_ptr, byref
 from .sharding import shard_bricks  # noqa: F401  (re-exported: reference-style import path)
 
@@ -162,37 +162,36 @@ class TSDFVolume:
         self.integrate_device(obs_weight)
 
     def integrate_device(self, obs_weight=1., count_updates=False):
-        """Integrate the current (already updated) frame; no host synchronisation."""
+        """Integrate the current (already updated) frame through torch.ops.ofx.integrate; no host sync."""
         src = _opt(self.fopt, "source_frame", 0)
-        cam = self.camera()
-        cptr = ptr(self.color_b) if self.with_color else None
-        ciptr = ptr(self.color_t) if self.with_color else None
-        nu = ptr(self.n_updated) if count_updates else None
+        color = self.color_b if self.with_color else None
+        color_im = self.color_t if self.with_color else None
+        nu = self.n_updated if count_updates else None
+        d = self.desc
+        geo = ([int(v) for v in d.dim], [self.brick_x0, self.brick_x1], [float(v) for v in d.origin],
+               float(d.voxel_size), float(d.trunc_margin), int(d.semantics),
+               [float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1]), float(self.cam_intr[0, 2]),
+                float(self.cam_intr[1, 2])], float(obs_weight))
         if self.frame_id == src:
-            call("ofx_integrate", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, 0, None, 0, 1, None, 0,
-                 None, None, float(obs_weight), ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu, stream_ptr())
-        else:
-            if self.warpfield is None:
-                raise RuntimeError("non-source frame integrate needs tsdf.warpfield (WarpField) to be set")
-            cache = self.warpfield.skin_tsdf_cache()
-            nodes = self.warpfield.packed_nodes()
-            timer = self.kernel_timer
-            if timer is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            if self.use_palette and cache.pal_n is not None:
-                call("ofx_integrate_palette", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, ptr(nodes),
-                     self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
-                     ptr(cache.weights), ptr(cache.pal_ids), ptr(cache.pal_n), ptr(cache.local), float(obs_weight),
-                     ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu, stream_ptr())
-            else:
-                call("ofx_integrate", byref(self.desc), byref(cam), ptr(self.depth_t), ciptr, 1, ptr(nodes),
-                     self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
-                     ptr(cache.weights), float(obs_weight), ptr(self.tsdf_b), ptr(self.weight_b), cptr, nu,
-                     stream_ptr())
-            if timer is not None:
-                e1.record()
-                timer.append((e0, e1))
+            torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo,
+                                    None, 0, 1, None, 0, None, None, None, None, None)
+            return
+        if self.warpfield is None:
+            raise RuntimeError("non-source frame integrate needs tsdf.warpfield (WarpField) to be set")
+        cache = self.warpfield.skin_tsdf_cache()
+        nodes = self.warpfield.packed_nodes()
+        timer = self.kernel_timer
+        if timer is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        pal = self.use_palette and cache.pal_n is not None
+        torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo,
+                                nodes, self.warpfield.num_nodes, cache.k, cache.brick_list, cache.n_list,
+                                cache.anchors, cache.weights, cache.pal_ids if pal else None,
+                                cache.pal_n if pal else None, cache.local if pal else None)
+        if timer is not None:
+            e1.record()
+            timer.append((e0, e1))
 
     # ------------------------------------------------------------------ readback
     def _dense(self, t):

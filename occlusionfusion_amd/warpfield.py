@@ -11,7 +11,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, ops  # noqa: F401  (ops registers torch.ops.ofx.*)
 from ._lib import call, ptr, stream_ptr, byref
 
 log = logging.getLogger(__name__)
@@ -321,13 +321,7 @@ class WarpField:
         pts = _t(points, self.device, torch.float32).reshape(-1, 3)
         nd = self.nodes_t if nodes is None else _t(nodes, self.device, torch.float32).reshape(-1, 3)
         K = min(nd.shape[0], 4)
-        P = pts.shape[0]
-        anchors = torch.empty((P, K), dtype=torch.int32, device=self.device)
-        weights = torch.empty((P, K), dtype=torch.float32, device=self.device)
-        valid = torch.empty(P, dtype=torch.uint8, device=self.device)
-        call("ofx_skin_points", ptr(pts), P, ptr(nd), nd.shape[0], self.node_coverage, K, ptr(anchors), ptr(weights),
-             ptr(valid), stream_ptr())
-        return anchors, weights, valid.bool()
+        return torch.ops.ofx.skin_points(pts, nd, float(self.node_coverage), K)
 
     def skin(self, points, nodes=None, ensure_num_neigbours=False):
         """warpfield.py:83-129 (numpy in, numpy out)."""
@@ -447,10 +441,7 @@ class WarpField:
         a = _t(anchors, self.device, torch.int32)
         w = _t(weights, self.device, torch.float32)
         v = None if valid is None else _t(valid, self.device, torch.uint8)
-        out = torch.empty_like(pts)
-        call("ofx_deform_points", ptr(pts), pts.shape[0], ptr(a), ptr(w), ptr(v), a.shape[1], ptr(self.packed_nodes()),
-             self.num_nodes, 1 if normals else 0, ptr(out), stream_ptr())
-        return out
+        return torch.ops.ofx.deform_points(pts, a, w, v, self.packed_nodes(), bool(normals))
 
     def deform_lbs_device(self, node_rotations, node_translations, points, anchors, weights, valid_pts=None):
         """warpfield.py:208-231 deform_lbs (origin-form R x + t, weights == 0 skipped) on device."""

@@ -252,22 +252,20 @@ def test_gn_matches_dense_oracle(cuda, golden_dir):
 
 def test_gn_assembly_matches_dense_system(cuda, golden_dir):
     """ofx_gn_linearize's block-sparse A, b equal the dense oracle JᵀJ, -Jᵀr (node-major order)."""
-    from occlusionfusion_amd import GaussNewtonSolver, _lib
-    from occlusionfusion_amd._lib import call, ptr, stream_ptr, byref
+    from occlusionfusion_amd import GaussNewtonSolver
     g = _g(golden_dir, "gn_small.npz")
     N = len(g["nodes"])
     s = GaussNewtonSolver(N, 1000)
-    pb, N, M = s._problem(*_gn_inputs(g), None, None, None, None)
-    prm = s._params()
-    nnz = _lib.c_int64()
-    call("ofx_gn_setup", s._h, byref(pb), byref(prm), byref(nnz), stream_ptr())
-    rows = s.info()[4]
+    args, N, M = s._problem(*_gn_inputs(g), None, None, None, None)
+    fp, ip = s._plist()
+    nnz, rows = (int(v) for v in torch.ops.ofx.gn_setup(s._state, s._h.value, *args, fp, ip))
+    assert rows == s.info()[4]
     perm = s.row_order()
     assert len(perm) == rows and rows % 8 == 0 and rows <= 2 * N + 8
     assert sorted(perm[perm >= 0].tolist()) == list(range(N))   # every node exactly once
-    A = torch.empty(int(nnz.value) * 36, dtype=torch.float64, device=cuda)
+    A = torch.empty(nnz * 36, dtype=torch.float64, device=cuda)
     rhs = torch.empty(6 * rows + 4, dtype=torch.float64, device=cuda)
-    call("ofx_gn_linearize", s._h, 0, 0, M, 1, ptr(A), ptr(rhs), stream_ptr())
+    torch.ops.ofx.gn_linearize(s._state, s._h.value, 0, 0, M, True, A, rhs)
     torch.cuda.synchronize()
     lm = 1e-7   # linearize adds the LM damping λ_0·I to the diagonal blocks (model.py:418-419,641-662)
     sysd = fo.gn_system(g["nodes"], g["edges"], g["tpos"], g["conf"], g["src"], g["anchors"], g["weights"], g["tgt"],

@@ -22,6 +22,7 @@
  *   ofx_integrate           WarpField.deform_tsdf + TSDFVolume.integrate    warpfield.py:369-380, tsdf.py:378-494
  *                           (fused: skin cache -> ED warp -> project -> SDF/weight/colour update)
  *   ofx_integrate_palette   same, node records staged per brick in LDS      warpfield.py:369-380, tsdf.py:442-494
+ *   ofx_integrate_points    TSDFVolume.integrate of given (deformed) points  tsdf.py:442-494
  *   ofx_deform_points       ED_warp / deform_ED / deform_mesh / normals     NonRigidICP/model/geometry.py:9-25,
  *                                                                          registration_fusion.py:157-184, warpfield.py:312-367
  *   ofx_deform_points_lbs   WarpField.deform_lbs / deform_lbs_cuda (origin form) warpfield.py:208-266,270-305
@@ -170,6 +171,16 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
                           const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
                           double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
                           ofx_stream_t s);
+
+/* Integrate of explicit (already deformed) points: point p updates the voxel with C-order id voxel_ids[p]
+ * (i·Dy·Dz + j·Dz + k) as TSDFVolume.integrate does for pts from WarpField.deform_tsdf (tsdf.py:442-494,
+ * warpfield.py:369-380); valid (u8, may be NULL) masks points. Same arithmetic as ofx_integrate (CPU or
+ * pycuda semantics). Voxel ids must be distinct; ids outside this shard are ignored. n_updated (one u32,
+ * may be NULL) is incremented by the number of updated voxels. */
+int ofx_integrate_points(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
+                         const float* points, const int64_t* voxel_ids, const uint8_t* valid, int64_t n_points,
+                         double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
+                         ofx_stream_t s);
 
 /* ED warp of points: out = Σ w (R(x-g)+g+t) for valid points, x otherwise.
  * normals = 1: WarpField.deform_normals semantics (R only, renormalised). valid may be NULL (all valid). */

@@ -17,12 +17,15 @@
 // (64 B) and the depth/colour images are gathered through L1/L2. Voxels with invalid skin read 8 B
 // and stop. All arithmetic is un-contracted (-ffp-contract=off) so results are bit-identical to the
 // oracle restatement.
+#include <stdlib.h>
+
 #include "ofx_common.h"
 
 namespace ofx {
 
 struct CamD {
   double fx, fy, cx, cy;
+  float fxf, fyf, cxf, cyf;   // the same intrinsics as f32 (exact: ofx_camera is f32)
   int W, H;
 };
 
@@ -216,6 +219,92 @@ __device__ __forceinline__ int update_voxel_pycuda(const CamD& c, const float* _
   return 1;
 }
 
+// Pixel of a point (tsdf.py:351-364: u = int(round_half_even((X·fx)/Z + cx)) in f64, v likewise, in-bounds
+// test on the rounded values) computed in f32 where that is certified to give the f64 result, else in f64.
+// f32: su = f32(f32(f32(x·fx)·rcp(z)) + cx) with v_rcp_f32 (<= 1 ulp): |su - su64| <= 2^-22·|q|·(1+2^-20) +
+// 2^-24·|su| + 2^-52·(|q| + |su|) < 2.6e-7·(|q| + |su|) =: tol. If su lies farther than tol from every
+// half-integer, rint(su) = rint(su64) (no half-integer lies between them). z below 1e-30 (subnormal
+// reciprocals), values within tol of a tie, and |su| >= 2^22 (then tol > 0.5) take the exact f64 form.
+// Precondition z > 0. Returns the pixel index or -1 (outside the image).
+__device__ __forceinline__ int pixel_of(const CamD& c, float x, float y, float z) {
+  const float r = __builtin_amdgcn_rcpf(z);
+  const float qx = (x * c.fxf) * r, qy = (y * c.fyf) * r;
+  const float su = qx + c.cxf, sv = qy + c.cyf;
+  const float tu = 2.6e-7f * (fabsf(qx) + fabsf(su)), tv = 2.6e-7f * (fabsf(qy) + fabsf(sv));
+  const float du = fabsf((su - floorf(su)) - 0.5f), dv = fabsf((sv - floorf(sv)) - 0.5f);
+  float u, v;
+  if (__builtin_expect(!(z >= 1e-30f) || !(du > tu) || !(dv > tv), 0)) {
+    const double Z = z;
+    const double uu = rint(((double)x * c.fx) / Z + c.cx), vv = rint(((double)y * c.fy) / Z + c.cy);
+    if (!(uu >= 0.0 && uu < (double)c.W && vv >= 0.0 && vv < (double)c.H)) return -1;
+    return (int)vv * c.W + (int)uu;
+  }
+  u = rintf(su);
+  v = rintf(sv);
+  if (!(u >= 0.f && u < (float)c.W && v >= 0.f && v < (float)c.H)) return -1;
+  return (int)v * c.W + (int)u;
+}
+
+// TSDF + colour update of one voxel whose pixel, depth d and old values are known (tsdf.py:366-376,
+// 442-494; numba f64 promotion). Caller checked d > 0 and d - Z >= -trunc. The SDF quotient uses
+// num·(1/w_new) and dd·(1/trunc) with an error bound err (a few f64 ulp); its f32 rounding is taken
+// when the whole interval [t - err, t + err] rounds to it (|t - f| + err < |f|·2^-25 <= half the f32
+// spacing on either side of f), else the exact quotient runs. Bit-identical to update_voxel.
+__device__ __forceinline__ void sdf_color_update(double dd, double trunc, double itrunc, double obs, float w_old,
+                                                 float t_old, float nc, float oc, bool with_color, float& w_out,
+                                                 float& t_out, float& c_out) {
+  const float w_new = (float)((double)w_old + obs);
+  const float prod = w_old * t_old;
+  const double wn = (double)w_new;
+  const double inv = 1.0 / wn;
+  const double dist_a = fmin(1.0, dd * itrunc);
+  const double num_a = (double)prod + obs * dist_a;
+  const double t_a = num_a * inv;
+  const double err = 1e-15 * ((fabs(obs) + fabs(num_a)) * inv + fabs(t_a));
+  float t_new = (float)t_a;
+  if (__builtin_expect(!(fabs(t_a - (double)t_new) + err < fabs((double)t_new) * 0x1p-25), 0)) {
+    const double dist = fmin(1.0, dd / trunc);
+    t_new = (float)(((double)prod + obs * dist) / wn);
+  }
+  w_out = w_new;
+  t_out = t_new;
+  if (with_color) {
+    const float C = 65536.0f;
+    float ob = floorf(oc / C);
+    float og = floorf((oc - ob * C) / 256.0f);
+    float orr = (oc - ob * C) - og * 256.0f;
+    float nb = floorf(nc / C);
+    float ng = floorf((nc - nb * C) / 256.0f);
+    float nr = (nc - nb * C) - ng * 256.0f;
+    const float ow = (float)obs;
+    // f32(a · f64(1/w_new)) = the correctly rounded f32 a/w_new (see update_voxel)
+    float b2 = fminf(255.0f, rintf((float)((double)(w_old * ob + ow * nb) * inv)));
+    float g2 = fminf(255.0f, rintf((float)((double)(w_old * og + ow * ng) * inv)));
+    float r2 = fminf(255.0f, rintf((float)((double)(w_old * orr + ow * nr) * inv)));
+    c_out = (b2 * C + g2 * 256.0f) + r2;
+  }
+}
+
+// Brick coordinates of brick b (< 2^24) from magic reciprocals: q = (b · M) >> 40 with M = ceil(2^40 / d)
+// is floor(b / d) for b < 2^40 / d (d <= 2^16): no 64-bit integer division in the kernel prologue.
+struct BrickDiv {
+  uint64_t mz, my;
+};
+static BrickDiv make_div(const BrickGeom& g) {
+  BrickDiv d;
+  d.mz = ((1ull << 40) + (uint64_t)g.nbz - 1) / (uint64_t)g.nbz;
+  d.my = ((1ull << 40) + (uint64_t)g.nby - 1) / (uint64_t)g.nby;
+  return d;
+}
+__device__ __forceinline__ void brick_coords(const BrickGeom& g, const BrickDiv& d, uint32_t b, int& i0, int& j0,
+                                             int& k0) {
+  const uint32_t r = (uint32_t)(((uint64_t)b * d.mz) >> 40);
+  const uint32_t bz = b - r * (uint32_t)g.nbz;
+  const uint32_t bx = (uint32_t)(((uint64_t)r * d.my) >> 40);
+  const uint32_t by = r - bx * (uint32_t)g.nby;
+  i0 = (int)(bx + (uint32_t)g.bx0) * kBrick; j0 = (int)by * kBrick; k0 = (int)bz * kBrick;
+}
+
 // per-workgroup (= per-brick) update count, plain store: no contended atomics in the hot kernel
 __device__ __forceinline__ void count_updates(int n, uint32_t* counts) {
   if (!counts) return;
@@ -295,6 +384,146 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     else n_upd += update_voxel(c, depth, color_im, trunc, 1.0 / trunc, obs, x, y, z, b * kBrickVox + l, tsdf, weight, color);
   }
   count_updates(n_upd, counter);
+}
+
+// The fused warp + integrate of the skinned bricks for K = 4 anchors and the reference CPU semantics (the
+// bench / pipeline case): one 512-thread workgroup per listed brick, one voxel per thread, three dependent
+// memory trips —
+//   1. brick id, palette count / ids, the voxel's palette ranks;
+//   2. (skin-valid voxels only, exec-masked) weights and old tsdf / weight; the palette's node records into
+//      LDS (one barrier);
+//   3. (projected voxels) depth, colour image and old colour at the pixel / voxel;
+// then the stores. Warp with the anchors unrolled (no dynamic register indexing), pixel in certified f32
+// (pixel_of), SDF rounding certified cheaply (sdf_color_update); bit-identical to k_integrate<1,1,0>.
+template <bool COLOR>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) void k_integrate_pal4(
+    BrickGeom g, BrickDiv bd, CamD c, const float* __restrict__ depth, const float* __restrict__ color_im,
+    const float4* __restrict__ nodes, int n_nodes, const int32_t* __restrict__ list,
+    const ushort4* __restrict__ anchors, const float4* __restrict__ weights, const uint16_t* __restrict__ pal_ids,
+    const int32_t* __restrict__ pal_n, const uchar4* __restrict__ local, double trunc, double itrunc, double obs,
+    float* __restrict__ tsdf, float* __restrict__ weight, float* __restrict__ color, uint32_t* counter) {
+  __shared__ float4 s_node[4 * kPal];
+  const int l = threadIdx.x;
+  const int64_t slot = blockIdx.x;
+  // ---- trip 1 (unconditional loads: a branch would split the trip)
+  const uint32_t b = (uint32_t)list[slot];
+  const int pn = pal_n[slot];
+  const int pid = pal_ids[slot * kPal + ((l >> 2) & (kPal - 1))];
+  const uchar4 la = local[slot * kBrickVox + l];
+  asm volatile("" ::: "memory");
+  int i0, j0, k0;
+  brick_coords(g, bd, b, i0, j0, k0);
+  const bool use_pal = pn <= kPal;
+  const int i = i0 + (l >> 6), j = j0 + ((l >> 3) & 7), k = k0 + (l & 7);
+  const uint32_t vi = b * (uint32_t)kBrickVox + (uint32_t)l;   // voxel slot (the host checks n_slots < 2^31)
+  bool act = i < g.Dx && j < g.Dy && k < g.Dz;
+  ushort4 ga = make_ushort4(0, 0, 0, 0);
+  if (use_pal) {
+    act = act && la.w != kNoLocal;
+  } else {   // palette overflow (> kPal distinct anchors in the brick): global anchors, one more trip
+    ga = anchors[slot * kBrickVox + l];
+    act = act && ga.w != kNoAnchor;
+  }
+  // ---- trip 2: the palette's node records (unconditional, clamped id) + the skin-valid voxels' weights and
+  // old tsdf / weight (exec-masked); the records go to LDS once they land
+  const float4 nrec = nodes[4 * (int64_t)min(pid, n_nodes - 1) + (l & 3)];
+  float4 ww = make_float4(0.f, 0.f, 0.f, 0.f);
+  float t_old = 0.f, w_old = 0.f;
+  if (act) {
+    ww = weights[slot * kBrickVox + l];
+    t_old = tsdf[vi];
+    w_old = weight[vi];
+  }
+  if (use_pal && l < 4 * pn) s_node[l] = nrec;
+  __syncthreads();
+  int pix = -1;
+  float px = vox2world(g.ox, g.vs, i), py = vox2world(g.oy, g.vs, j), pz = vox2world(g.oz, g.vs, k);
+  if (act) {
+    const float w[4] = {ww.x, ww.y, ww.z, ww.w};
+    if (use_pal) {
+      const int ids[4] = {la.x, la.y, la.z, la.w};
+      ed_warp(s_node, ids, w, 4, px, py, pz);
+    } else {
+      const int ids[4] = {ga.x, ga.y, ga.z, ga.w};
+      ed_warp(nodes, ids, w, 4, px, py, pz);
+    }
+    if (pz > 0.f) pix = pixel_of(c, px, py, pz);
+  }
+  // ---- trip 3 (skin-valid voxels; pixel 0 stands in for the unprojected ones)
+  float d = 0.f, nc = 0.f, oc = 0.f;
+  if (act) {
+    const int pc = pix >= 0 ? pix : 0;
+    d = depth[pc];
+    if (COLOR) { nc = color_im[pc]; oc = color[vi]; }
+  }
+  asm volatile("" ::: "memory");
+  int n_upd = 0;
+  if (pix >= 0) {
+    const double dd = (double)d - (double)pz;
+    if (d > 0.f && dd >= -trunc) {
+      float wn, tn, cn;
+      sdf_color_update(dd, trunc, itrunc, obs, w_old, t_old, nc, oc, COLOR, wn, tn, cn);
+      weight[vi] = wn;
+      tsdf[vi] = tn;
+      if (COLOR) color[vi] = cn;
+      n_upd = 1;
+    }
+  }
+  if (counter) {
+    __shared__ int s_w[8];
+    for (int off = 32; off > 0; off >>= 1) n_upd += __shfl_xor(n_upd, off, 64);
+    if ((l & 63) == 0) s_w[l >> 6] = n_upd;
+    __syncthreads();
+    if (l == 0) counter[blockIdx.x] = (uint32_t)(((s_w[0] + s_w[1]) + (s_w[2] + s_w[3])) + ((s_w[4] + s_w[5]) + (s_w[6] + s_w[7])));
+  }
+}
+
+// Integrate of explicit points (TSDFVolume.integrate on already deformed points: tsdf.py:442-494 with pts
+// from WarpField.deform_tsdf, warpfield.py:369-380): point p updates voxel vox[p] (C-order id), with the
+// same arithmetic as the fused kernels (pixel_of / sdf_color_update, or the pycuda form). Points of voxels
+// outside this shard are ignored. Voxel ids must be distinct (one writer per voxel).
+template <bool PYC>
+__global__ __launch_bounds__(256) void k_integrate_points(BrickGeom g, CamD c, const float* __restrict__ depth,
+                                                          const float* __restrict__ color_im,
+                                                          const float* __restrict__ pts, const int64_t* __restrict__ vox,
+                                                          const uint8_t* __restrict__ valid, int64_t n, double trunc,
+                                                          double itrunc, double obs, float* __restrict__ tsdf,
+                                                          float* __restrict__ weight, float* __restrict__ color,
+                                                          uint32_t* n_updated) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int upd = 0;
+  if (p < n && (!valid || valid[p])) {
+    const int64_t v = vox[p];
+    const int64_t DyDz = (int64_t)g.Dy * g.Dz;
+    const int i = (int)(v / DyDz), j = (int)((v / g.Dz) % g.Dy), k = (int)(v % g.Dz);
+    if (v >= 0 && i < g.Dx && (i >> 3) >= g.bx0 && (i >> 3) < g.bx1) {
+      const int64_t b = ((int64_t)((i >> 3) - g.bx0) * g.nby + (j >> 3)) * g.nbz + (k >> 3);
+      const int64_t vi = b * kBrickVox + ((i & 7) * 8 + (j & 7)) * 8 + (k & 7);
+      const float x = pts[3 * p], y = pts[3 * p + 1], z = pts[3 * p + 2];
+      if (PYC) {
+        upd = update_voxel_pycuda(c, depth, color_im, (float)trunc, (float)obs, x, y, z, vi, tsdf, weight, color);
+      } else if (z > 0.f) {
+        const int pix = pixel_of(c, x, y, z);
+        if (pix >= 0) {
+          const float d = depth[pix];
+          const double dd = (double)d - (double)z;
+          if (d > 0.f && dd >= -trunc) {
+            float wn, tn, cn;
+            sdf_color_update(dd, trunc, itrunc, obs, weight[vi], tsdf[vi], color ? color_im[pix] : 0.f,
+                             color ? color[vi] : 0.f, color != nullptr, wn, tn, cn);
+            weight[vi] = wn;
+            tsdf[vi] = tn;
+            if (color) color[vi] = cn;
+            upd = 1;
+          }
+        }
+      }
+    }
+  }
+  if (n_updated) {
+    for (int off = 32; off > 0; off >>= 1) upd += __shfl_xor(upd, off, 64);
+    if ((threadIdx.x & 63) == 0 && upd) atomicAdd(n_updated, (uint32_t)upd);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_deform_points(const float* __restrict__ pts, int64_t n,
@@ -381,6 +610,7 @@ __global__ void k_visibility(const float* __restrict__ pts, int64_t n, CamD c, c
 static CamD make_cam(const ofx_camera* cam) {
   CamD c;
   c.fx = cam->fx; c.fy = cam->fy; c.cx = cam->cx; c.cy = cam->cy;
+  c.fxf = cam->fx; c.fyf = cam->fy; c.cxf = cam->cx; c.cyf = cam->cy;
   c.W = cam->width; c.H = cam->height;
   return c;
 }
@@ -444,10 +674,45 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
   OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights && pal_ids && pal_n && local_anchors,
                 "null warp/palette buffer");
   OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
+  if (desc->semantics == OFX_SEM_CPU && k == 4 && g.n_bricks * kBrickVox < (1ll << 31) && !getenv("OFX_INT_GENERIC")) {
+    if (color)
+      hipLaunchKernelGGL(k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(512), 0, as_stream(s), g, make_div(g),
+                         make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
+                         (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
+                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+    else
+      hipLaunchKernelGGL(k_integrate_pal4<false>, dim3((unsigned)n_list), dim3(512), 0, as_stream(s), g, make_div(g),
+                         make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
+                         (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
+                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+    OFX_LAUNCH_CHECK();
+    return OFX_OK;
+  }
   hipLaunchKernelGGL(desc->semantics == OFX_SEM_PYCUDA ? (k_integrate<true, true, true>) : (k_integrate<true, true, false>),
                      dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_cam(cam),
                      depth, color_im, (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors,
                      (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,
+                     obs_weight, tsdf, weight, color, n_updated);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_integrate_points(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
+                         const float* points, const int64_t* voxel_ids, const uint8_t* valid, int64_t n_points,
+                         double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
+                         ofx_stream_t s) {
+  BrickGeom g;
+  int st = make_geom(desc, &g);
+  if (st) return st;
+  OFX_CHECK_ARG(cam && depth && tsdf && weight && n_points >= 0, "null buffer / bad size");
+  OFX_CHECK_ARG(cam->width > 0 && cam->height > 0, "bad camera size");
+  OFX_CHECK_ARG((color == nullptr) == (color_im == nullptr), "color and color_im must both be set or both NULL");
+  OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
+  if (n_points == 0) return OFX_OK;
+  OFX_CHECK_ARG(points && voxel_ids, "null points / voxel ids");
+  hipLaunchKernelGGL(desc->semantics == OFX_SEM_PYCUDA ? (k_integrate_points<true>) : (k_integrate_points<false>),
+                     dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), g, make_cam(cam), depth,
+                     color_im, points, voxel_ids, valid, n_points, desc->trunc_margin, 1.0 / desc->trunc_margin,
                      obs_weight, tsdf, weight, color, n_updated);
   OFX_LAUNCH_CHECK();
   return OFX_OK;

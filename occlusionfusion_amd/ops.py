@@ -81,6 +81,27 @@ def _(tsdf, weight, color, n_updated, depth, color_im, dims, brick_range, origin
     return None
 
 
+@torch.library.custom_op(f"{_NS}::integrate_points", mutates_args=("tsdf", "weight", "color", "n_updated"),
+                         device_types="cuda")
+def integrate_points(tsdf: Tensor, weight: Tensor, color: Optional[Tensor], n_updated: Optional[Tensor],
+                     depth: Tensor, color_im: Optional[Tensor], dims: List[int], brick_range: List[int],
+                     origin: List[float], voxel_size: float, trunc_margin: float, semantics: int, intr: List[float],
+                     obs_weight: float, points: Tensor, voxel_ids: Tensor, valid: Optional[Tensor]) -> None:
+    """TSDFVolume.integrate of given (already deformed) points into the voxels `voxel_ids` (C-order ids,
+    distinct): tsdf.py:442-494 with pts from WarpField.deform_tsdf (warpfield.py:369-380)."""
+    desc = _volume_desc(dims, brick_range, origin, voxel_size, trunc_margin, semantics)
+    cam = _camera(intr, depth.shape[0], depth.shape[1])
+    call("ofx_integrate_points", byref(desc), byref(cam), ptr(depth), ptr(color_im), ptr(points), ptr(voxel_ids),
+         ptr(valid), points.shape[0], float(obs_weight), ptr(tsdf), ptr(weight), ptr(color), ptr(n_updated),
+         _stream(tsdf))
+
+
+@integrate_points.register_fake
+def _(tsdf, weight, color, n_updated, depth, color_im, dims, brick_range, origin, voxel_size, trunc_margin, semantics,
+      intr, obs_weight, points, voxel_ids, valid):
+    return None
+
+
 # --------------------------------------------------------------------------------------------- skinning
 @torch.library.custom_op(f"{_NS}::skin_points", mutates_args=(), device_types="cuda")
 def skin_points(points: Tensor, nodes: Tensor, node_coverage: float, k: int) -> Tuple[Tensor, Tensor, Tensor]:
@@ -242,4 +263,4 @@ def _(state, handle, n_nodes, num_iter):
             state.new_empty((4,), dtype=torch.int32), state.new_empty((num_iter, 4), dtype=torch.float64))
 
 
-OPS = ("integrate", "skin_points", "deform_points", "gn_solve", "gn_setup", "gn_linearize", "gn_step", "gn_finish")
+OPS = ("integrate", "integrate_points", "skin_points", "deform_points", "gn_solve", "gn_setup", "gn_linearize", "gn_step", "gn_finish")

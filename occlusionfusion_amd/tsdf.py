@@ -193,6 +193,25 @@ class TSDFVolume:
             e1.record()
             timer.append((e0, e1))
 
+    def integrate_points(self, points, voxel_ids, valid=None, obs_weight=1., count_updates=False):
+        """tsdf.py:442-494 on explicit points: point p (already warped, e.g. WarpField.deform_tsdf) updates the
+        voxel with C-order id voxel_ids[p] against the current frame (update() first). Voxel ids must be
+        distinct; ids outside this shard are ignored. Returns the update count (device u32 tensor) if asked."""
+        d = self.desc
+        pts = torch.as_tensor(points, dtype=torch.float32, device=self.device).reshape(-1, 3).contiguous()
+        vox = torch.as_tensor(voxel_ids, dtype=torch.int64, device=self.device).reshape(-1).contiguous()
+        if vox.shape[0] != pts.shape[0]:
+            raise ValueError(f"{pts.shape[0]} points but {vox.shape[0]} voxel ids")
+        v = None if valid is None else torch.as_tensor(valid, device=self.device).reshape(-1).to(torch.uint8)
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.device) if count_updates else None
+        torch.ops.ofx.integrate_points(
+            self.tsdf_b, self.weight_b, self.color_b if self.with_color else None, cnt, self.depth_t,
+            self.color_t if self.with_color else None, [int(x) for x in d.dim], [self.brick_x0, self.brick_x1],
+            [float(x) for x in d.origin], float(d.voxel_size), float(d.trunc_margin), int(d.semantics),
+            [float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1]), float(self.cam_intr[0, 2]),
+             float(self.cam_intr[1, 2])], float(obs_weight), pts, vox, v)
+        return cnt
+
     # ------------------------------------------------------------------ readback
     def _dense(self, t):
         Dy, Dz = int(self._vol_dim[1]), int(self._vol_dim[2])

@@ -89,10 +89,14 @@ def test_integrate_source_and_warped_frames_bitexact(cuda, golden_dir):
     np.testing.assert_array_equal(c, g["color1"].reshape(D))
 
 
-def test_skin_palette_and_fallback(cuda, golden_dir):
+@pytest.mark.parametrize("kernel", ["pal4", "generic"])
+def test_skin_palette_and_fallback(cuda, golden_dir, kernel, monkeypatch):
     """Node palette = ascending distinct anchors of each brick's skin-valid voxels, local ranks map back
-    to the anchors; palette path, forced-overflow fallback and global path integrate identically."""
+    to the anchors; palette path, forced-overflow fallback and global path integrate identically — with the
+    specialised K = 4 kernel (k_integrate_pal4) and with the generic one (OFX_INT_GENERIC=1)."""
     from occlusionfusion_amd import WarpField, _lib
+    if kernel == "generic":
+        monkeypatch.setenv("OFX_INT_GENERIC", "1")
     g = _g(golden_dir, "integrate_small.npz")
     P = _lib.PALETTE
     vols = []

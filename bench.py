@@ -160,7 +160,7 @@ def main():
         (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
     seq = S.config_sequence(a.config, a.nodes)
     sharded = a.mode == "shard" and world > 1
-    shard = (rank, world) if sharded else None
+    shard = (rank, world, "hash") if sharded else None   # spatial-hash brick buckets (sharding.hash_owner)
     pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)
     total = a.warmup + a.steps + 1
     frames = [pipe.prepare(t) for t in range(total)]
@@ -194,7 +194,7 @@ def main():
     marks = []
     upd = []
     pipe.solver.timing(True)               # arm hipEvent timing of the PCG loops (same stream)
-    pipe.vol.kernel_timer = []             # hipEvents around each warped integrate launch
+    pipe.vol.integrate_timing(True)        # library hipEvents around each warped integrate launch (same stream)
     t0 = time.perf_counter()
     for t in range(1 + a.warmup, total):
         e0, e1, e2 = ev(), ev(), ev()
@@ -222,8 +222,8 @@ def main():
     gn_it = [int(m[3]["_status"][1].item()) for m in marks]
     valid = [int(m[3]["_status"][0].item()) for m in marks]
     U = float(np.mean([int(u.item()) for u in upd]))
-    t_kint = float(np.mean([x.elapsed_time(y) for x, y in pipe.vol.kernel_timer])) * 1e-3
-    pipe.vol.kernel_timer = None
+    kint_ms, kint_n = pipe.vol.integrate_timing(False)
+    t_kint = kint_ms * 1e-3 / max(1, kint_n)
     t_ar = (sum(x.elapsed_time(y) for x, y in ar_events) * 1e-3 / a.steps) if ar_events else 0.0
     mine = {"rank": rank, "device": local, "ms_per_frame": 1e3 * elapsed / a.steps,
             "solve_ms": 1e3 * float(np.mean(t_solve)), "allreduce_ms": 1e3 * t_ar,

@@ -152,10 +152,12 @@ int ofx_pack_nodes(const float* R, const float* T, const float* g, int32_t n_nod
                    ofx_stream_t s);
 
 /* Fused warp + integrate of one frame into the shard.
- *   warp = 0 : source frame — every voxel, world position, no skin (tsdf.py:395-398)
+ *   warp = 0 : source frame — every voxel, world position, no skin (tsdf.py:395-398); with brick_list
+ *              non-NULL (CPU semantics only) just the n_list listed bricks (a hash-bucket shard's own)
  *   warp = 1 : bricks in brick_list, ED-warped positions, skin-valid voxels only (tsdf.py:401,464)
  * color_im / color may be NULL (no colour integration). n_updated (device u32, one entry per launched
- * brick: n_list when warp, all shard bricks otherwise) receives per-brick update counts, may be NULL. */
+ * brick: n_list when a list is given, all shard bricks otherwise) receives per-brick update counts, may
+ * be NULL. */
 int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
                   int32_t warp, const float* packed_nodes, int32_t n_nodes, int32_t k,
                   const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
@@ -171,6 +173,12 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
                           const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
                           double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
                           ofx_stream_t s);
+
+/* Profiling hook (process-wide): returns (and resets) the device time of the warped integrate kernel launches
+ * (ofx_integrate warp = 1, ofx_integrate_palette) recorded since the last call, from hipEvents recorded by the
+ * library around each launch on its stream (synchronises on them), and their count; `enable` switches
+ * recording for the following launches. */
+int ofx_integrate_timing(int32_t enable, double* kernel_ms, int64_t* launches);
 
 /* Integrate of explicit (already deformed) points: point p updates the voxel with C-order id voxel_ids[p]
  * (i·Dy·Dz + j·Dz + k) as TSDFVolume.integrate does for pts from WarpField.deform_tsdf (tsdf.py:442-494,
@@ -393,6 +401,11 @@ int ofx_gn_info(void* handle, int64_t* info);
 /* Waves per PCG cluster workgroup of k_pcg_iter chosen at create: 2 (default) or 1 (environment
  * OFX_PCG_W1 set to anything but "" / "0"; tuning and A/B only). */
 int ofx_gn_pcg_waves(void* handle, int32_t* waves);
+/* The solve's stop flag as the host sees it (host-mapped, no synchronisation): 1 once a GN step's loss rule
+ * (model.py:726-732) or an ill-posed solve stopped it. After ofx_gn_step(i + 1) returns it reflects step i's
+ * decision on every rank alike (that step's PCG poll waited for it), so a stepped multi-rank loop can leave
+ * after the same step everywhere, as ofx_gn_solve does. */
+int ofx_gn_stopped(void* handle, int32_t* stopped);
 /* Per-GN-step statistics of the last solve: out (host f64[3*cap]) = [PCG iterations, |b|², loss] per
  * step (zeros for steps that did not run); synchronous D2H copy, at most 64 steps. */
 int ofx_gn_stats(void* handle, double* out, int32_t cap);

@@ -59,6 +59,7 @@ _SIGS = {
     "ofx_skin_volume_to_dense": [P, P, c_int32, P, P, c_int32, P, P, P, P],
     "ofx_pack_nodes": [P, P, P, c_int32, P, P],
     "ofx_integrate": [P, P, P, P, c_int32, P, c_int32, c_int32, P, c_int32, P, P, c_double, P, P, P, P, P],
+    "ofx_integrate_timing": [c_int32, P, P],
     "ofx_integrate_points": [P, P, P, P, P, P, P, c_int64, c_double, P, P, P, P, P],
     "ofx_integrate_palette": [P, P, P, P, P, c_int32, c_int32, P, c_int32, P, P, P, P, P, c_double, P, P, P, P, P],
     "ofx_deform_points": [P, c_int64, P, P, P, c_int32, P, c_int32, c_int32, P, P],
@@ -98,6 +99,7 @@ _SIGS = {
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
     "ofx_gn_pcg_waves": [P, P],
+    "ofx_gn_stopped": [P, P],
     "ofx_gn_stats": [P, P, c_int32],
     "ofx_gn_row_order": [P, P, c_int32],
     "ofx_gn_setup": [P, P, P, P, P],

@@ -2033,6 +2033,13 @@ int ofx_gn_info(void* handle, int64_t* info) {
   return OFX_OK;
 }
 
+int ofx_gn_stopped(void* handle, int32_t* stopped) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && stopped, "null handle/stopped");
+  *stopped = ((const volatile int32_t*)g->host_flags)[H_STOPPED] ? 1 : 0;
+  return OFX_OK;
+}
+
 int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && waves, "null handle/waves");

@@ -19,6 +19,10 @@
 // oracle restatement.
 #include <stdlib.h>
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "ofx_common.h"
 
 namespace ofx {
@@ -256,7 +260,13 @@ __device__ __forceinline__ void sdf_color_update(double dd, double trunc, double
   const float w_new = (float)((double)w_old + obs);
   const float prod = w_old * t_old;
   const double wn = (double)w_new;
-  const double inv = 1.0 / wn;
+  // 1/w_new; skipped for a wave whose voxels are all first observations (w_new == 1: the source frame)
+  double inv = 1.0;
+  if (__ballot(w_new != 1.0f)) {
+    double w = wn;
+    asm volatile("" : "+v"(w));   // opaque: the compiler would otherwise fold the branch away (1/1 == 1)
+    inv = 1.0 / w;
+  }
   const double dist_a = fmin(1.0, dd * itrunc);
   const double num_a = (double)prod + obs * dist_a;
   const double t_a = num_a * inv;
@@ -387,94 +397,215 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 }
 
 // The fused warp + integrate of the skinned bricks for K = 4 anchors and the reference CPU semantics (the
-// bench / pipeline case): one 512-thread workgroup per listed brick, one voxel per thread, three dependent
-// memory trips —
-//   1. brick id, palette count / ids, the voxel's palette ranks;
-//   2. (skin-valid voxels only, exec-masked) weights and old tsdf / weight; the palette's node records into
-//      LDS (one barrier);
-//   3. (projected voxels) depth, colour image and old colour at the pixel / voxel;
+// bench / pipeline case): one 256-thread workgroup per listed brick, voxels l and l + 256 per thread (same
+// y and z), three dependent memory trips —
+//   1. brick id, palette count / ids, the voxels' palette ranks;
+//   2. the palette's node records (into LDS, one barrier) + the skin-valid voxels' weights and old
+//      tsdf / weight (exec-masked);
+//   3. depth, colour image and old colour of the skin-valid voxels;
 // then the stores. Warp with the anchors unrolled (no dynamic register indexing), pixel in certified f32
-// (pixel_of), SDF rounding certified cheaply (sdf_color_update); bit-identical to k_integrate<1,1,0>.
+// (pixel_of), SDF rounding certified cheaply (sdf_color_update), per-wave update counts by ballot;
+// bit-identical to k_integrate<1,1,0>. The kernel is VALU-bound: every per-wave instruction
+// is shared by two voxels.
 template <bool COLOR>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) void k_integrate_pal4(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_integrate_pal4(
     BrickGeom g, BrickDiv bd, CamD c, const float* __restrict__ depth, const float* __restrict__ color_im,
     const float4* __restrict__ nodes, int n_nodes, const int32_t* __restrict__ list,
     const ushort4* __restrict__ anchors, const float4* __restrict__ weights, const uint16_t* __restrict__ pal_ids,
     const int32_t* __restrict__ pal_n, const uchar4* __restrict__ local, double trunc, double itrunc, double obs,
     float* __restrict__ tsdf, float* __restrict__ weight, float* __restrict__ color, uint32_t* counter) {
   __shared__ float4 s_node[4 * kPal];
-  const int l = threadIdx.x;
-  const int64_t slot = blockIdx.x;
+  __shared__ float s_xyz[3 * kBrick];   // vox2world of the brick's 8 x, y and z coordinates
+  __shared__ uint32_t s_cnt[4];
+  const int tid = threadIdx.x;
+  const uint32_t slot = blockIdx.x;
   // ---- trip 1 (unconditional loads: a branch would split the trip)
   const uint32_t b = (uint32_t)list[slot];
   const int pn = pal_n[slot];
-  const int pid = pal_ids[slot * kPal + ((l >> 2) & (kPal - 1))];
-  const uchar4 la = local[slot * kBrickVox + l];
+  const int pid = pal_ids[slot * kPal + (tid >> 2)];
+  uchar4 la[2];
+  la[0] = local[slot * kBrickVox + tid];
+  la[1] = local[slot * kBrickVox + tid + 256];
   asm volatile("" ::: "memory");
   int i0, j0, k0;
   brick_coords(g, bd, b, i0, j0, k0);
   const bool use_pal = pn <= kPal;
-  const int i = i0 + (l >> 6), j = j0 + ((l >> 3) & 7), k = k0 + (l & 7);
-  const uint32_t vi = b * (uint32_t)kBrickVox + (uint32_t)l;   // voxel slot (the host checks n_slots < 2^31)
-  bool act = i < g.Dx && j < g.Dy && k < g.Dz;
-  ushort4 ga = make_ushort4(0, 0, 0, 0);
-  if (use_pal) {
-    act = act && la.w != kNoLocal;
-  } else {   // palette overflow (> kPal distinct anchors in the brick): global anchors, one more trip
-    ga = anchors[slot * kBrickVox + l];
-    act = act && ga.w != kNoAnchor;
-  }
-  // ---- trip 2: the palette's node records (unconditional, clamped id) + the skin-valid voxels' weights and
-  // old tsdf / weight (exec-masked); the records go to LDS once they land
-  const float4 nrec = nodes[4 * (int64_t)min(pid, n_nodes - 1) + (l & 3)];
-  float4 ww = make_float4(0.f, 0.f, 0.f, 0.f);
-  float t_old = 0.f, w_old = 0.f;
-  if (act) {
-    ww = weights[slot * kBrickVox + l];
-    t_old = tsdf[vi];
-    w_old = weight[vi];
-  }
-  if (use_pal && l < 4 * pn) s_node[l] = nrec;
-  __syncthreads();
-  int pix = -1;
-  float px = vox2world(g.ox, g.vs, i), py = vox2world(g.oy, g.vs, j), pz = vox2world(g.oz, g.vs, k);
-  if (act) {
-    const float w[4] = {ww.x, ww.y, ww.z, ww.w};
+  const int j = j0 + ((tid >> 3) & 7), k = k0 + (tid & 7);
+  const bool in_yz = j < g.Dy && k < g.Dz;
+  const uint32_t vb = b * (uint32_t)kBrickVox + (uint32_t)tid;   // voxel slot of l = tid (n_slots < 2^31)
+  bool act[2];
+  ushort4 ga[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    act[h] = in_yz && i0 + (tid >> 6) + 4 * h < g.Dx;
     if (use_pal) {
-      const int ids[4] = {la.x, la.y, la.z, la.w};
+      act[h] = act[h] && la[h].w != kNoLocal;
+    } else {   // palette overflow (> kPal distinct anchors in the brick): global anchors, one more trip
+      ga[h] = anchors[slot * kBrickVox + tid + 256 * h];
+      act[h] = act[h] && ga[h].w != kNoAnchor;
+    }
+  }
+  // ---- trip 2
+  const float4 nrec = nodes[4 * (int64_t)min(pid, n_nodes - 1) + (tid & 3)];
+  float4 ww[2];
+  float t_old[2], w_old[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (act[h]) {
+      ww[h] = weights[slot * kBrickVox + tid + 256 * h];
+      t_old[h] = tsdf[vb + 256 * h];
+      w_old[h] = weight[vb + 256 * h];
+    }
+  }
+  if (use_pal && tid < 4 * pn) s_node[tid] = nrec;
+  if (tid >= 256 - 3 * kBrick) {   // the last 24 lanes (one wave): x, y, z world coordinates of the brick
+    const int q = tid - (256 - 3 * kBrick), ax = q >> 3, o = q & 7;
+    s_xyz[q] = ax == 0 ? vox2world(g.ox, g.vs, i0 + o) : ax == 1 ? vox2world(g.oy, g.vs, j0 + o)
+                                                               : vox2world(g.oz, g.vs, k0 + o);
+  }
+  __syncthreads();
+  const float y0 = s_xyz[kBrick + ((tid >> 3) & 7)], z0 = s_xyz[2 * kBrick + (tid & 7)];
+  int pix[2];
+  float zw[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    pix[h] = -1;
+    zw[h] = 0.f;
+    if (!act[h]) continue;
+    float px = s_xyz[(tid >> 6) + 4 * h], py = y0, pz = z0;
+    const float w[4] = {ww[h].x, ww[h].y, ww[h].z, ww[h].w};
+    if (use_pal) {
+      const int ids[4] = {la[h].x, la[h].y, la[h].z, la[h].w};
       ed_warp(s_node, ids, w, 4, px, py, pz);
     } else {
-      const int ids[4] = {ga.x, ga.y, ga.z, ga.w};
+      const int ids[4] = {ga[h].x, ga[h].y, ga[h].z, ga[h].w};
       ed_warp(nodes, ids, w, 4, px, py, pz);
     }
-    if (pz > 0.f) pix = pixel_of(c, px, py, pz);
+    zw[h] = pz;
+    if (pz > 0.f) pix[h] = pixel_of(c, px, py, pz);
   }
   // ---- trip 3 (skin-valid voxels; pixel 0 stands in for the unprojected ones)
-  float d = 0.f, nc = 0.f, oc = 0.f;
-  if (act) {
-    const int pc = pix >= 0 ? pix : 0;
-    d = depth[pc];
-    if (COLOR) { nc = color_im[pc]; oc = color[vi]; }
-  }
-  asm volatile("" ::: "memory");
-  int n_upd = 0;
-  if (pix >= 0) {
-    const double dd = (double)d - (double)pz;
-    if (d > 0.f && dd >= -trunc) {
-      float wn, tn, cn;
-      sdf_color_update(dd, trunc, itrunc, obs, w_old, t_old, nc, oc, COLOR, wn, tn, cn);
-      weight[vi] = wn;
-      tsdf[vi] = tn;
-      if (COLOR) color[vi] = cn;
-      n_upd = 1;
+  float d[2], nc[2], oc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (act[h]) {
+      const int pc = pix[h] >= 0 ? pix[h] : 0;
+      d[h] = depth[pc];
+      if (COLOR) { nc[h] = color_im[pc]; oc[h] = color[vb + 256 * h]; }
     }
   }
+  asm volatile("" ::: "memory");
+  uint32_t n_upd = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bool upd = false;
+    if (pix[h] >= 0) {
+      const double dd = (double)d[h] - (double)zw[h];
+      if (d[h] > 0.f && dd >= -trunc) {
+        float wn, tn, cn;
+        sdf_color_update(dd, trunc, itrunc, obs, w_old[h], t_old[h], COLOR ? nc[h] : 0.f, COLOR ? oc[h] : 0.f,
+                         COLOR, wn, tn, cn);
+        weight[vb + 256 * h] = wn;
+        tsdf[vb + 256 * h] = tn;
+        if (COLOR) color[vb + 256 * h] = cn;
+        upd = true;
+      }
+    }
+    n_upd += (uint32_t)__popcll(__ballot(upd));   // per-wave count: scalar, no lane shuffles
+  }
   if (counter) {
-    __shared__ int s_w[8];
-    for (int off = 32; off > 0; off >>= 1) n_upd += __shfl_xor(n_upd, off, 64);
-    if ((l & 63) == 0) s_w[l >> 6] = n_upd;
+    if ((tid & 63) == 0) s_cnt[tid >> 6] = n_upd;
     __syncthreads();
-    if (l == 0) counter[blockIdx.x] = (uint32_t)(((s_w[0] + s_w[1]) + (s_w[2] + s_w[3])) + ((s_w[4] + s_w[5]) + (s_w[6] + s_w[7])));
+    if (tid == 0) counter[blockIdx.x] = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+  }
+}
+
+// Source frame (tsdf.py:395-398: every voxel at its world position, all valid) with per-brick projection
+// tables: on the voxel grid u depends only on (i, k) and v only on (j, k), so one workgroup computes the
+// brick's 8x8 u-table and 8x8 v-table exactly in f64 (the reference expression, 128 lanes, one each) plus
+// the 24 world coordinates, and every voxel then looks its pixel up in LDS. brick_list (may be NULL: all
+// bricks of the shard) restricts the pass to the listed bricks (hash-bucket shards). 2 voxels per thread.
+template <bool COLOR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_integrate_src(
+    BrickGeom g, BrickDiv bd, CamD c, const float* __restrict__ depth, const float* __restrict__ color_im,
+    const int32_t* __restrict__ list, double trunc, double itrunc, double obs, float* __restrict__ tsdf,
+    float* __restrict__ weight, float* __restrict__ color, uint32_t* counter) {
+  __shared__ int s_u[kBrick * kBrick], s_v[kBrick * kBrick];
+  __shared__ float s_xyz[3 * kBrick];
+  __shared__ uint32_t s_cnt[4];
+  const int tid = threadIdx.x;
+  const uint32_t b = list ? (uint32_t)list[blockIdx.x] : (uint32_t)blockIdx.x;
+  int i0, j0, k0;
+  brick_coords(g, bd, b, i0, j0, k0);
+  const uint32_t vb = b * (uint32_t)kBrickVox + (uint32_t)tid;
+  // old values first (every in-volume voxel: the reference reads them all), then the tables
+  const int j = j0 + ((tid >> 3) & 7), k = k0 + (tid & 7);
+  bool in[2];
+  float t_old[2], w_old[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    in[h] = j < g.Dy && k < g.Dz && i0 + (tid >> 6) + 4 * h < g.Dx;
+    if (in[h]) { t_old[h] = tsdf[vb + 256 * h]; w_old[h] = weight[vb + 256 * h]; }
+  }
+  if (tid < 2 * kBrick * kBrick) {   // u(i, k) for tid < 64, v(j, k) for 64 <= tid < 128 (tsdf.py:351-364)
+    const int q = tid & 63, a = q >> 3, kk = q & 7;
+    const double Z = (double)vox2world(g.oz, g.vs, k0 + kk);
+    int r = -1;
+    if (tid < 64) {
+      const double X = (double)vox2world(g.ox, g.vs, i0 + a);
+      const double u = rint((X * c.fx) / Z + c.cx);
+      if (Z > 0.0 && u >= 0.0 && u < (double)c.W) r = (int)u;
+      s_u[q] = r;
+    } else {
+      const double Y = (double)vox2world(g.oy, g.vs, j0 + a);
+      const double v = rint((Y * c.fy) / Z + c.cy);
+      if (Z > 0.0 && v >= 0.0 && v < (double)c.H) r = (int)v;
+      s_v[q] = r;
+    }
+  } else if (tid >= 256 - kBrick) {
+    s_xyz[tid - (256 - kBrick)] = vox2world(g.oz, g.vs, k0 + (tid - (256 - kBrick)));
+  }
+  __syncthreads();
+  const int lz = tid & 7, ly = (tid >> 3) & 7;
+  const int vv = s_v[ly * kBrick + lz];
+  const float z = s_xyz[lz];
+  int pix[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int uu = s_u[((tid >> 6) + 4 * h) * kBrick + lz];
+    pix[h] = (in[h] && uu >= 0 && vv >= 0) ? vv * c.W + uu : -1;
+  }
+  float d[2], nc[2], oc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (pix[h] >= 0) {
+      d[h] = depth[pix[h]];
+      if (COLOR) { nc[h] = color_im[pix[h]]; oc[h] = color[vb + 256 * h]; }
+    }
+  }
+  asm volatile("" ::: "memory");
+  uint32_t n_upd = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bool upd = false;
+    if (pix[h] >= 0) {
+      const double dd = (double)d[h] - (double)z;
+      if (d[h] > 0.f && dd >= -trunc) {
+        float wn, tn, cn;
+        sdf_color_update(dd, trunc, itrunc, obs, w_old[h], t_old[h], COLOR ? nc[h] : 0.f, COLOR ? oc[h] : 0.f,
+                         COLOR, wn, tn, cn);
+        weight[vb + 256 * h] = wn;
+        tsdf[vb + 256 * h] = tn;
+        if (COLOR) color[vb + 256 * h] = cn;
+        upd = true;
+      }
+    }
+    n_upd += (uint32_t)__popcll(__ballot(upd));
+  }
+  if (counter) {
+    if ((tid & 63) == 0) s_cnt[tid >> 6] = n_upd;
+    __syncthreads();
+    if (tid == 0) counter[blockIdx.x] = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
   }
 }
 
@@ -619,7 +750,49 @@ static CamD make_cam(const ofx_camera* cam) {
 
 using namespace ofx;
 
+namespace {
+// profiling hook state (ofx_integrate_timing): hipEvent pairs around the warped integrate kernel launches
+std::mutex g_int_mu;
+bool g_int_timing = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_int_ev;
+
+struct IntTimer {
+  hipStream_t s;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  explicit IntTimer(hipStream_t st) : s(st) {
+    std::lock_guard<std::mutex> lk(g_int_mu);
+    if (!g_int_timing) return;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { e0 = e1 = nullptr; return; }
+    (void)hipEventRecord(e0, s);
+  }
+  ~IntTimer() {
+    if (!e0) return;
+    (void)hipEventRecord(e1, s);
+    std::lock_guard<std::mutex> lk(g_int_mu);
+    g_int_ev.emplace_back(e0, e1);
+  }
+};
+}  // namespace
+
 extern "C" {
+
+int ofx_integrate_timing(int32_t enable, double* kernel_ms, int64_t* launches) {
+  std::lock_guard<std::mutex> lk(g_int_mu);
+  double ms = 0.0;
+  for (auto& e : g_int_ev) {
+    float t = 0.f;
+    OFX_HIP(hipEventSynchronize(e.second));
+    OFX_HIP(hipEventElapsedTime(&t, e.first, e.second));
+    ms += t;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (kernel_ms) *kernel_ms = ms;
+  if (launches) *launches = (int64_t)g_int_ev.size();
+  g_int_ev.clear();
+  g_int_timing = enable != 0;
+  return OFX_OK;
+}
 
 int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth, const float* color_im,
                   int32_t warp, const float* packed_nodes, int32_t n_nodes, int32_t k, const int32_t* brick_list,
@@ -635,7 +808,19 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
   hipStream_t hs = as_stream(s);
   OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
   const bool pyc = desc->semantics == OFX_SEM_PYCUDA;
-  if (!warp) {
+  if (!warp && !pyc && g.n_bricks * kBrickVox < (1ll << 31) && !getenv("OFX_INT_GENERIC")) {
+    const unsigned nb = brick_list ? (unsigned)n_list : (unsigned)g.n_bricks;
+    if (nb == 0) return OFX_OK;
+    if (color)
+      hipLaunchKernelGGL(k_integrate_src<true>, dim3(nb), dim3(256), 0, hs, g, make_div(g), c, depth, color_im,
+                         brick_list, desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color,
+                         n_updated);
+    else
+      hipLaunchKernelGGL(k_integrate_src<false>, dim3(nb), dim3(256), 0, hs, g, make_div(g), c, depth, color_im,
+                         brick_list, desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color,
+                         n_updated);
+  } else if (!warp) {
+    OFX_CHECK_ARG(brick_list == nullptr, "a source-frame brick list needs the CPU semantics");
     hipLaunchKernelGGL(pyc ? (k_integrate<false, false, true>) : (k_integrate<false, false, false>),
                        dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth,
                        color_im, (const float4*)nullptr, 1, (const int32_t*)nullptr, (const ushort4*)nullptr,
@@ -646,6 +831,7 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
     OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
     if (n_list == 0) return OFX_OK;
     OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights, "null warp buffer");
+    IntTimer timer(hs);
     hipLaunchKernelGGL(pyc ? (k_integrate<true, false, true>) : (k_integrate<true, false, false>), dim3((unsigned)n_list),
                        dim3(256), 0, hs, g, c, depth, color_im,
                        (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors, (const float4*)weights,
@@ -674,14 +860,15 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
   OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights && pal_ids && pal_n && local_anchors,
                 "null warp/palette buffer");
   OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
+  IntTimer timer(as_stream(s));
   if (desc->semantics == OFX_SEM_CPU && k == 4 && g.n_bricks * kBrickVox < (1ll << 31) && !getenv("OFX_INT_GENERIC")) {
     if (color)
-      hipLaunchKernelGGL(k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(512), 0, as_stream(s), g, make_div(g),
+      hipLaunchKernelGGL(k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
                          (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
                          desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
     else
-      hipLaunchKernelGGL(k_integrate_pal4<false>, dim3((unsigned)n_list), dim3(512), 0, as_stream(s), g, make_div(g),
+      hipLaunchKernelGGL(k_integrate_pal4<false>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
                          (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
                          desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);

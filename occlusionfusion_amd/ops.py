@@ -62,9 +62,9 @@ def integrate(tsdf: Tensor, weight: Tensor, color: Optional[Tensor], n_updated: 
     desc = _volume_desc(dims, brick_range, origin, voxel_size, trunc_margin, semantics)
     cam = _camera(intr, depth.shape[0], depth.shape[1])
     s = _stream(tsdf)
-    if packed_nodes is None:
-        call("ofx_integrate", byref(desc), byref(cam), ptr(depth), ptr(color_im), 0, None, 0, 1, None, 0, None, None,
-             float(obs_weight), ptr(tsdf), ptr(weight), ptr(color), ptr(n_updated), s)
+    if packed_nodes is None:   # source frame; brick_list: a hash shard's own bricks (None: all of the shard)
+        call("ofx_integrate", byref(desc), byref(cam), ptr(depth), ptr(color_im), 0, None, 0, 1, ptr(brick_list),
+             n_list, None, None, float(obs_weight), ptr(tsdf), ptr(weight), ptr(color), ptr(n_updated), s)
     elif pal_ids is not None:
         call("ofx_integrate_palette", byref(desc), byref(cam), ptr(depth), ptr(color_im), ptr(packed_nodes), n_nodes, k,
              ptr(brick_list), n_list, ptr(anchors), ptr(weights), ptr(pal_ids), ptr(pal_n), ptr(local),

@@ -71,6 +71,12 @@ class GaussNewtonSolver:
         call("ofx_gn_info", self._h, arr)
         return list(arr)
 
+    def stopped(self):
+        """The solve's stop flag as the host sees it (ofx_gn_stopped: no synchronisation)."""
+        f = ctypes.c_int32()
+        call("ofx_gn_stopped", self._h, byref(f))
+        return bool(f.value)
+
     def pcg_waves(self):
         """Waves per cluster workgroup of the PCG iteration kernel (2, or 1 under OFX_PCG_W1=1)."""
         w = ctypes.c_int32()
@@ -223,6 +229,8 @@ class GaussNewtonSolver:
                 e1.record()
                 timer.append((e0, e1))
             torch.ops.ofx.gn_step(self._state, h, it, A, rhs)
+            if self.stopped():   # step it-1's stop rule, seen alike by every rank (include/ofx.h ofx_gn_stopped)
+                break
         out = torch.ops.ofx.gn_finish(self._state, h, N, int(self.params["num_iter"]))
         return self._pack(out, sync)
 
@@ -283,7 +291,9 @@ class Registration:
         nodes_t = torch.as_tensor(self.graph.nodes, device=self.device)
         self.warpfield.set_node_transforms(R, T)
         warped = self.warpfield.deform_device(self.source_pcd, self.point_anchors, self.anchor_weight)
-        res = {"warped_verts": warped, "node_rotations": R.cpu().numpy(), "node_translations": T.cpu(),
+        # dtypes as registration_fusion.py:363-377: rotations numpy f64 (scipy as_matrix), translations a CPU
+        # tensor, deformed nodes and warped vertices device tensors
+        res = {"warped_verts": warped, "node_rotations": R.cpu().numpy().astype(np.float64), "node_translations": T.cpu(),
                "deformed_nodes_to_target": nodes_t + T, "convergence_info": out["convergence_info"],
                "valid_solve": out["valid_solve"],
                "source_frame_id": optical_flow_data["source_id"], "target_frame_id": optical_flow_data["target_id"]}

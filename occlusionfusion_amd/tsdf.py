@@ -89,9 +89,20 @@ class TSDFVolume:
         self.gpu_mode = True
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         nbx = int((self._vol_dim[0] + 7) // 8)
-        rank, world = shard if shard is not None else (0, 1)
+        rank, world, kind = (tuple(shard) + ("slab",))[:3] if shard is not None else (0, 1, "slab")
+        if kind not in ("slab", "hash"):
+            raise ValueError(f"shard kind must be 'slab' or 'hash', got {kind!r}")
         self.shard = (rank, world)
-        self.brick_x0, self.brick_x1 = shard_bricks(nbx, rank, world)
+        self.shard_kind = kind
+        self.owned_bricks = None    # hash shards: int32 device list of this rank's bricks
+        self.owned_mask = None      # hash shards: bool device mask over all bricks
+        if kind == "hash":          # whole brick address space, own bricks by spatial hash (sharding.hash_owner)
+            from .sharding import hash_owner
+            self.brick_x0, self.brick_x1 = 0, nbx
+            self.brick_owner = hash_owner(nbx, int((self._vol_dim[1] + 7) // 8), int((self._vol_dim[2] + 7) // 8),
+                                          world)
+        else:
+            self.brick_x0, self.brick_x1 = shard_bricks(nbx, rank, world)
         self.desc = _lib.VolumeDesc()
         self.desc.dim[:] = [int(d) for d in self._vol_dim]
         self.desc.brick_x0, self.desc.brick_x1 = self.brick_x0, self.brick_x1
@@ -114,8 +125,11 @@ class TSDFVolume:
         self.weight_b = torch.empty(self.n_slots, **kw)
         self.color_b = torch.empty(self.n_slots, **kw)
         self.n_updated = torch.zeros(max(1, self.n_bricks), dtype=torch.int32, device=self.device)  # per brick
+        if kind == "hash":
+            mask = self.brick_owner == rank
+            self.owned_mask = torch.from_numpy(mask).to(self.device)
+            self.owned_bricks = torch.from_numpy(np.nonzero(mask)[0].astype(np.int32)).to(self.device)
         self.with_color = True
-        self.kernel_timer = None   # list -> (start, end) torch events around each warped integrate launch
         self.use_palette = True    # warped integrate through the skin cache's LDS node palette
         call("ofx_volume_reset", byref(self.desc), ptr(self.tsdf_b), ptr(self.weight_b), ptr(self.color_b), stream_ptr())
         self.warpfield = None
@@ -173,25 +187,19 @@ class TSDFVolume:
                [float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1]), float(self.cam_intr[0, 2]),
                 float(self.cam_intr[1, 2])], float(obs_weight))
         if self.frame_id == src:
+            ob = self.owned_bricks
             torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo,
-                                    None, 0, 1, None, 0, None, None, None, None, None)
+                                    None, 0, 1, ob, 0 if ob is None else int(ob.shape[0]), None, None, None, None, None)
             return
         if self.warpfield is None:
             raise RuntimeError("non-source frame integrate needs tsdf.warpfield (WarpField) to be set")
         cache = self.warpfield.skin_tsdf_cache()
         nodes = self.warpfield.packed_nodes()
-        timer = self.kernel_timer
-        if timer is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
         pal = self.use_palette and cache.pal_n is not None
         torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo,
                                 nodes, self.warpfield.num_nodes, cache.k, cache.brick_list, cache.n_list,
                                 cache.anchors, cache.weights, cache.pal_ids if pal else None,
                                 cache.pal_n if pal else None, cache.local if pal else None)
-        if timer is not None:
-            e1.record()
-            timer.append((e0, e1))
 
     def integrate_points(self, points, voxel_ids, valid=None, obs_weight=1., count_updates=False):
         """tsdf.py:442-494 on explicit points: point p (already warped, e.g. WarpField.deform_tsdf) updates the
@@ -211,6 +219,14 @@ class TSDFVolume:
             [float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1]), float(self.cam_intr[0, 2]),
              float(self.cam_intr[1, 2])], float(obs_weight), pts, vox, v)
         return cnt
+
+    @staticmethod
+    def integrate_timing(enable=True):
+        """(kernel ms, launches) of the warped integrate kernels since the last call, from hipEvents the library
+        records around each launch on its stream (ofx_integrate_timing); then (re)arm or disarm recording."""
+        ms, n = _lib.c_double(), _lib.c_int64()
+        call("ofx_integrate_timing", 1 if enable else 0, byref(ms), byref(n))
+        return ms.value, n.value
 
     # ------------------------------------------------------------------ readback
     def _dense(self, t):
@@ -326,9 +342,15 @@ class TSDFVolume:
         """Voxel slots of one brick column (one x-brick of the bricked layout: ny·nz bricks of 512)."""
         return int((self._vol_dim[1] + 7) // 8) * int((self._vol_dim[2] + 7) // 8) * 512
 
+    def _need_slab(self, what):
+        if self.shard_kind != "slab":
+            raise ValueError(f"{what} needs x-slab shards (a hash-bucket shard holds scattered bricks): gather the "
+                             "volume (sharding.merge_hash_shards) or shard it as (rank, world, 'slab')")
+
     def boundary_columns(self):
         """(first, last) brick columns of this shard as (2, slots) device tensors [tsdf; colour] — what the
         neighbouring shards need as marching-cubes halo (sharding.exchange_boundary)."""
+        self._need_slab("boundary_columns")
         c = self.brick_column_slots()
         first = torch.stack([self.tsdf_b[:c], self.color_b[:c]])
         last = torch.stack([self.tsdf_b[-c:], self.color_b[-c:]])
@@ -342,6 +364,7 @@ class TSDFVolume:
         [tsdf; colour] tensors (None at the volume's ends). sharding.merge_shard_meshes of the parts in rank
         order is the whole volume's extract_mesh_device + get_mesh colours, bit for bit (include/ofx.h
         ofx_mesh_count_range)."""
+        self._need_slab("extract_mesh_shard")
         nbx = int((self._vol_dim[0] + 7) // 8)
         x0, x1 = self.brick_x0, self.brick_x1
         if (x0 > 0) != (lo is not None) or (x1 < nbx) != (hi is not None):

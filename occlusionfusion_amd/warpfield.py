@@ -410,6 +410,11 @@ class WarpField:
             call("ofx_skin_volume_bricks", byref(t.desc), ptr(self.nodes_t), self.num_nodes, self.node_coverage, K,
                  ptr(blist), ptr(cnt), stream_ptr())
             n_list = int(cnt.item())
+            if t.owned_mask is not None:   # hash shard: only this rank's bricks (sharding.hash_owner)
+                own = blist[:n_list][t.owned_mask[blist[:n_list].long()]]
+                n_list = int(own.shape[0])
+                blist = torch.zeros(max(1, t.n_bricks), dtype=torch.int32, device=self.device)
+                blist[:n_list] = own
             anchors = torch.empty(max(1, n_list) * 512 * 4, dtype=torch.int16, device=self.device)
             weights = torch.empty(max(1, n_list) * 512 * 4, dtype=torch.float32, device=self.device)
             call("ofx_skin_volume", byref(t.desc), ptr(self.nodes_t), self.num_nodes, self.node_coverage, K, ptr(blist),

@@ -152,6 +152,39 @@ def test_sharded_volume_equals_full(cuda, golden_dir):
         np.testing.assert_array_equal(full, g[key].reshape(D))
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_hash_sharded_volume_equals_full(cuda, golden_dir, world):
+    """Spatial-hash brick ownership (sharding.hash_owner; each shard keeps the whole address space and fuses
+    only its own bricks — the source frame through the brick-list pass, warped frames through its share of the
+    skin cache): the owners' voxels merged reproduce the full volume exactly, and every shard's skin cache
+    lists exactly its own bricks of the full cache."""
+    from occlusionfusion_amd import WarpField
+    from occlusionfusion_amd.sharding import merge_hash_shards
+    g = _g(golden_dir, "integrate_small.npz")
+    parts, lists = [], []
+    for r in range(world):
+        vol = _small_volume(g, shard=(r, world, "hash"))
+        vol.integrate({"im": g["im0"], "id": 0})
+        wf = WarpField(_graph(g), vol)
+        c = wf.skin_tsdf_cache()
+        lists.append(c.brick_list[:c.n_list].cpu().numpy())
+        wf.frame_id = 1
+        wf.set_node_transforms(g["R"], g["T"])
+        vol.integrate({"im": g["im1"], "id": 1})
+        parts.append(vol.get_volume())
+    full = _small_volume(g)
+    full.integrate({"im": g["im0"], "id": 0})
+    fc = WarpField(_graph(g), full).skin_tsdf_cache()
+    owners = vol.brick_owner
+    all_listed = fc.brick_list[:fc.n_list].cpu().numpy()
+    for r in range(world):
+        np.testing.assert_array_equal(lists[r], all_listed[owners[all_listed] == r])
+    merged = merge_hash_shards(parts, owners)
+    D = tuple(g["dims"])
+    for i, key in enumerate(("tsdf1", "color1", "weight1")):
+        np.testing.assert_array_equal(merged[i], g[key].reshape(D))
+
+
 def test_deform_points_and_visibility(cuda, golden_dir):
     from occlusionfusion_amd import WarpField
     g = _g(golden_dir, "integrate_small.npz")

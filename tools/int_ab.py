@@ -27,12 +27,34 @@ for rep in range(30):
             os.environ["OFX_INT_GENERIC"] = "1"
         else:
             os.environ.pop("OFX_INT_GENERIC", None)
-        pipe.vol.kernel_timer = []
+        pipe.vol.integrate_timing(True)
         pipe.integrate(f1, t)
         t += 1
         torch.cuda.synchronize()
-        a, b = pipe.vol.kernel_timer[0]
-        res[var].append(a.elapsed_time(b) * 1e3)
+        ms, n = pipe.vol.integrate_timing(False)
+        res[var].append(ms * 1e3 / n)
+# source frame (dense pass) on a scratch volume of the same grid, both kernels interleaved
+from occlusionfusion_amd import TSDFVolume  # noqa: E402
+scratch = TSDFVolume.from_grid(c["origin"], c["voxel"], (D, D, D), pipe.intr, pipe.fopt, device=dev)
+f0 = pipe.prepare(0)
+res.update({"src_generic": [], "src_table": []})
+for rep in range(12):
+    for var in ("src_generic", "src_table"):
+        if var == "src_generic":
+            os.environ["OFX_INT_GENERIC"] = "1"
+        else:
+            os.environ.pop("OFX_INT_GENERIC", None)
+        if hasattr(scratch, "frame_id"):
+            del scratch.frame_id
+        scratch.update(f0.im, 0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        scratch.integrate_device()
+        e1.record()
+        torch.cuda.synchronize()
+        res[var].append(e0.elapsed_time(e1) * 1e3)
+os.environ.pop("OFX_INT_GENERIC", None)
 for k, v in res.items():
     v = np.array(v[3:])
     print(f"{k}: median {np.median(v):.1f} us  min {v.min():.1f} us", flush=True)

@@ -23,6 +23,7 @@
  *                           (fused: skin cache -> ED warp -> project -> SDF/weight/colour update)
  *   ofx_integrate_palette   same, node records staged per brick in LDS      warpfield.py:369-380, tsdf.py:442-494
  *   ofx_integrate_points    TSDFVolume.integrate of given (deformed) points  tsdf.py:442-494
+ *   ofx_raycast             (new) depth / normal / colour images of the TSDF  — (no reference twin)
  *   ofx_deform_points       ED_warp / deform_ED / deform_mesh / normals     NonRigidICP/model/geometry.py:9-25,
  *                                                                          registration_fusion.py:157-184, warpfield.py:312-367
  *   ofx_deform_points_lbs   WarpField.deform_lbs / deform_lbs_cuda (origin form) warpfield.py:208-266,270-305
@@ -189,6 +190,17 @@ int ofx_integrate_points(const ofx_volume_desc* desc, const ofx_camera* cam, con
                          const float* points, const int64_t* voxel_ids, const uint8_t* valid, int64_t n_points,
                          double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
                          ofx_stream_t s);
+
+/* TSDF raycast (new capability; the reference has none — parity unpinned, restated by the oracle): per pixel
+ * of `cam` (identity pose), march the ray from max(z_near, volume entry) to min(z_far, volume exit) through the
+ * trilinear tsdf (unobserved voxels and the outside count as +1), coarse steps of 0.8·trunc while the sample
+ * is >= 0.999, one-voxel steps otherwise; the first + -> - sign change, linearly refined, is the surface.
+ * depth f32[H*W] (z, 0 = miss); normals f32[H*W*3] (normalised central differences, may be NULL); colors
+ * f32[H*W] (packed colour of the nearest voxel, may be NULL; color may be NULL then). Needs the whole volume
+ * (brick range [0, nbx)). */
+int ofx_raycast(const ofx_volume_desc* desc, const ofx_camera* cam, const float* tsdf, const float* weight,
+                const float* color, float z_near, float z_far, float* depth, float* normals, float* colors,
+                ofx_stream_t s);
 
 /* ED warp of points: out = Σ w (R(x-g)+g+t) for valid points, x otherwise.
  * normals = 1: WarpField.deform_normals semantics (R only, renormalised). valid may be NULL (all valid). */

@@ -102,6 +102,28 @@ def _(tsdf, weight, color, n_updated, depth, color_im, dims, brick_range, origin
     return None
 
 
+@torch.library.custom_op(f"{_NS}::raycast", mutates_args=(), device_types="cuda")
+def raycast(tsdf: Tensor, weight: Tensor, color: Optional[Tensor], dims: List[int], origin: List[float],
+            voxel_size: float, trunc_margin: float, intr: List[float], height: int, width: int, z_near: float,
+            z_far: float) -> Tuple[Tensor, Tensor, Tensor]:
+    """Depth (H,W), normals (H,W,3) and packed colours (H,W) of the fused surface seen from the camera
+    (ofx_raycast; new capability, no reference twin)."""
+    nbx = (int(dims[0]) + 7) // 8
+    desc = _volume_desc(dims, [0, nbx], origin, voxel_size, trunc_margin, 0)
+    cam = _camera(intr, height, width)
+    depth = torch.empty((height, width), dtype=torch.float32, device=tsdf.device)
+    normals = torch.empty((height, width, 3), dtype=torch.float32, device=tsdf.device)
+    colors = torch.empty((height, width), dtype=torch.float32, device=tsdf.device)
+    call("ofx_raycast", byref(desc), byref(cam), ptr(tsdf), ptr(weight), ptr(color), float(z_near), float(z_far),
+         ptr(depth), ptr(normals), ptr(colors), _stream(tsdf))
+    return depth, normals, colors
+
+
+@raycast.register_fake
+def _(tsdf, weight, color, dims, origin, voxel_size, trunc_margin, intr, height, width, z_near, z_far):
+    return (tsdf.new_empty((height, width)), tsdf.new_empty((height, width, 3)), tsdf.new_empty((height, width)))
+
+
 # --------------------------------------------------------------------------------------------- skinning
 @torch.library.custom_op(f"{_NS}::skin_points", mutates_args=(), device_types="cuda")
 def skin_points(points: Tensor, nodes: Tensor, node_coverage: float, k: int) -> Tuple[Tensor, Tensor, Tensor]:
@@ -263,4 +285,4 @@ def _(state, handle, n_nodes, num_iter):
             state.new_empty((4,), dtype=torch.int32), state.new_empty((num_iter, 4), dtype=torch.float64))
 
 
-OPS = ("integrate", "integrate_points", "skin_points", "deform_points", "gn_solve", "gn_setup", "gn_linearize", "gn_step", "gn_finish")
+OPS = ("integrate", "integrate_points", "raycast", "skin_points", "deform_points", "gn_solve", "gn_setup", "gn_linearize", "gn_step", "gn_finish")

@@ -220,6 +220,22 @@ class TSDFVolume:
              float(self.cam_intr[1, 2])], float(obs_weight), pts, vox, v)
         return cnt
 
+    def raycast(self, cam_intr=None, height=None, width=None, z_near=0.1, z_far=10.0):
+        """Depth (H,W) f32 (0 = miss), normals (H,W,3) f32 and packed colours (H,W) f32 of the fused surface seen
+        from the camera (identity pose) — device tensors (ofx_raycast). New capability: the reference renders
+        no TSDF (its surfaces come from marching cubes); parity with oracle.raycast, unpinned against the
+        reference. Needs the whole volume (an unsharded volume or shard world 1)."""
+        if self.shard[1] != 1:
+            raise ValueError("raycast needs the whole volume: gather a sharded volume first")
+        K = self.cam_intr
+        intr = [float(v) for v in (cam_intr if cam_intr is not None else (K[0, 0], K[1, 1], K[0, 2], K[1, 2]))[:4]]
+        if height is None or width is None:
+            height, width = (int(x) for x in self.depth_t.shape)
+        d = self.desc
+        return torch.ops.ofx.raycast(self.tsdf_b, self.weight_b, self.color_b if self.with_color else None,
+                                     [int(x) for x in d.dim], [float(x) for x in d.origin], float(d.voxel_size),
+                                     float(d.trunc_margin), intr, int(height), int(width), float(z_near), float(z_far))
+
     @staticmethod
     def integrate_timing(enable=True):
         """(kernel ms, launches) of the warped integrate kernels since the last call, from hipEvents the library

@@ -1382,3 +1382,101 @@ def _np_sum_f32(a):
     for x in a[i:]:
         s = f32(s + x)
     return s
+
+
+# ----------------------------------------------------------------------------
+# (new capability) TSDF raycast — no reference twin: the restatement of csrc/raycast.hip op for op (f32,
+# un-contracted), so the GPU kernel can be checked bit for bit. Parity against the reference is unpinned.
+# ----------------------------------------------------------------------------
+def raycast(tsdf, weight, color, origin, voxel_size, intr, height, width, z_near=0.1, z_far=10.0,
+            trunc=TRUNC_MARGIN, rows=None):
+    """Depth (H,W), normals (H,W,3), colours (H,W) of dense C-order volumes (Dx,Dy,Dz) seen from the identity
+    camera: trilinear tsdf march (unobserved / outside = +1), coarse steps 0.8·trunc while >= 0.999, else one
+    voxel; first + -> - change refined linearly; central-difference normals; nearest-voxel colour.
+    rows: optional subset of image rows (the other rows stay 0)."""
+    tsdf = np.asarray(tsdf, F32)
+    weight = np.asarray(weight, F32)
+    D = tsdf.shape
+    lo = np.asarray(origin, F32)
+    hi = np.array([F32(float(origin[a]) + float(voxel_size) * D[a]) for a in range(3)], F32)
+    inv_vs = F32(1.0 / float(voxel_size))
+    step_c, step_f = F32(0.8 * trunc), F32(float(voxel_size))
+    fx, fy, cx, cy = (F32(v) for v in intr)
+    rows = np.arange(height) if rows is None else np.asarray(rows)
+    vv, uu = np.meshgrid(rows, np.arange(width), indexing="ij")
+    u, v = uu.reshape(-1), vv.reshape(-1)
+    dx = (u.astype(F32) - cx) / fx
+    dy = (v.astype(F32) - cy) / fy
+    n = u.size
+    z0 = np.full(n, F32(z_near), F32)
+    z1 = np.full(n, F32(z_far), F32)
+    miss = np.zeros(n, bool)
+    for a, d in enumerate((dx, dy, np.ones(n, F32))):
+        zero = d == 0
+        miss |= zero & ~((F32(0) >= lo[a]) & (F32(0) <= hi[a]))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ta = np.where(zero, F32(0), lo[a] / np.where(zero, F32(1), d)).astype(F32)
+            tb = np.where(zero, F32(0), hi[a] / np.where(zero, F32(1), d)).astype(F32)
+        z0 = np.where(zero, z0, np.maximum(z0, np.minimum(ta, tb)))
+        z1 = np.where(zero, z1, np.minimum(z1, np.maximum(ta, tb)))
+
+    def voxel(i, j, k):
+        ok = (i >= 0) & (j >= 0) & (k >= 0) & (i < D[0]) & (j < D[1]) & (k < D[2])
+        ic, jc, kc = (np.clip(x, 0, D[q] - 1) for q, x in enumerate((i, j, k)))
+        t = tsdf[ic, jc, kc]
+        w = weight[ic, jc, kc]
+        return np.where(ok & (w > 0), t, F32(1)).astype(F32)
+
+    def trilinear(qx, qy, qz):
+        f0 = [np.floor(q) for q in (qx, qy, qz)]
+        ax, ay, az = (q - f for q, f in zip((qx, qy, qz), f0))
+        i, j, k = (f.astype(np.int64) for f in f0)
+        t000, t100, t010, t110 = voxel(i, j, k), voxel(i + 1, j, k), voxel(i, j + 1, k), voxel(i + 1, j + 1, k)
+        t001, t101, t011, t111 = (voxel(i, j, k + 1), voxel(i + 1, j, k + 1), voxel(i, j + 1, k + 1),
+                                  voxel(i + 1, j + 1, k + 1))
+        bx, by, bz = F32(1) - ax, F32(1) - ay, F32(1) - az
+        c00, c10 = t000 * bx + t100 * ax, t010 * bx + t110 * ax
+        c01, c11 = t001 * bx + t101 * ax, t011 * bx + t111 * ax
+        c0, c1 = c00 * by + c10 * ay, c01 * by + c11 * ay
+        return (c0 * bz + c1 * az).astype(F32)
+
+    hit = np.zeros(n, F32)
+    act = np.nonzero(~miss & (z0 <= z1))[0]
+    z, zp, sp = z0[act].copy(), z0[act].copy(), np.ones(act.size, F32)
+    while act.size:
+        run = z <= z1[act]
+        act, z, zp, sp = act[run], z[run], zp[run], sp[run]
+        if not act.size:
+            break
+        s = trilinear((z * dx[act] - lo[0]) * inv_vs, (z * dy[act] - lo[1]) * inv_vs, (z - lo[2]) * inv_vs)
+        h = (sp > 0) & (s < 0)
+        hit[act[h]] = zp[h] + (z[h] - zp[h]) * (sp[h] / (sp[h] - s[h]))
+        keep = ~h
+        act, z, s = act[keep], z[keep], s[keep]
+        zp, sp = z.copy(), s
+        z = (z + np.where(s >= F32(0.999), step_c, step_f)).astype(F32)
+    nrm = np.zeros((n, 3), F32)
+    col = np.zeros(n, F32)
+    hh = np.nonzero(hit > 0)[0]
+    if hh.size:
+        zh = hit[hh]
+        qx, qy, qz = (zh * dx[hh] - lo[0]) * inv_vs, (zh * dy[hh] - lo[1]) * inv_vs, (zh - lo[2]) * inv_vs
+        one = F32(1)
+        g = np.stack([trilinear(qx + one, qy, qz) - trilinear(qx - one, qy, qz),
+                      trilinear(qx, qy + one, qz) - trilinear(qx, qy - one, qz),
+                      trilinear(qx, qy, qz + one) - trilinear(qx, qy, qz - one)], 1).astype(F32)
+        ln = np.sqrt((g[:, 0] * g[:, 0] + g[:, 1] * g[:, 1]) + g[:, 2] * g[:, 2])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            nrm[hh] = np.where((ln > 0)[:, None], g / np.where(ln > 0, ln, one)[:, None], F32(0))
+        if color is not None:
+            ii, jj, kk = (np.floor(q + F32(0.5)).astype(np.int64) for q in (qx, qy, qz))
+            ok = (ii >= 0) & (jj >= 0) & (kk >= 0) & (ii < D[0]) & (jj < D[1]) & (kk < D[2])
+            cv = np.asarray(color, F32)[np.clip(ii, 0, D[0] - 1), np.clip(jj, 0, D[1] - 1), np.clip(kk, 0, D[2] - 1)]
+            col[hh] = np.where(ok, cv, F32(0))
+    out_d = np.zeros((height, width), F32)
+    out_n = np.zeros((height, width, 3), F32)
+    out_c = np.zeros((height, width), F32)
+    out_d[rows] = hit.reshape(rows.size, width)
+    out_n[rows] = nrm.reshape(rows.size, width, 3)
+    out_c[rows] = col.reshape(rows.size, width)
+    return out_d, out_n, out_c

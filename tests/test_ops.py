@@ -35,6 +35,10 @@ def test_fake_kernels():
         assert info.shape == (2,) and info.dtype == torch.int64
         R2, _, _, loss2 = torch.ops.ofx.gn_finish(st, 0, 37, 10)
         assert R2.shape == (37, 3, 3) and loss2.shape == (10, 4)
+        dd, nn, cc = torch.ops.ofx.raycast(torch.empty(512 * 8), torch.empty(512 * 8), None, [16, 16, 16],
+                                           [0.0, 0.0, 1.0], 0.004, 0.04, [525.0, 525.0, 319.5, 223.5], 448, 640,
+                                           0.1, 10.0)
+        assert dd.shape == (448, 640) and nn.shape == (448, 640, 3) and cc.shape == (448, 640)
         vol = torch.empty(512 * 8)
         assert torch.ops.ofx.integrate(vol, vol.clone(), None, None, torch.empty(448, 640), None, [16, 16, 16],
                                        [0, 2], [0.0, 0.0, 1.0], 0.004, 0.04, 0, [525.0, 525.0, 319.5, 223.5], 1.0,

@@ -4,7 +4,10 @@ tools/pmc_traffic.sh -> JSON (bench.py reads it into roofline.traffic).
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of
 16-B/lane coalesced reads, so traffic = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KB).
 
-  python tools/pmc_summary.py gpurun_out profiles/r01_pmc_traffic.json
+  python tools/pmc_summary.py gpurun_out profiles/r02_pmc_traffic.json
+
+The workload the counters were collected on is taken from the bench line the profiled run printed
+(gpurun_out/pmc_FETCH_SIZE.log); bench.py uses `traffic` only when that workload equals its own.
 """
 import collections
 import csv
@@ -14,18 +17,29 @@ import sys
 
 import numpy as np
 
-KERNELS = {"k_pcg_iter": "ofx::k_pcg_iter<true, false", "k_integrate_warp": "ofx::k_integrate<true, true"}
+KERNELS = {"k_pcg_iter": ("ofx::k_pcg_iter<true, false",),
+           "k_integrate_warp": ("ofx::k_integrate_pal4<true>", "ofx::k_integrate<true, true")}
+
+
+def workload(d):
+    try:
+        for line in open(os.path.join(d, "pmc_FETCH_SIZE.log")):
+            if line.startswith("{"):
+                return json.loads(line)["config"]["workload"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
 
 
 def main(d, out):
     res = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), median over dispatches; "
                      "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
-           "kernels": {}}
+           "workload": workload(d), "kernels": {}}
     vals = collections.defaultdict(dict)
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         rows = list(csv.DictReader(open(os.path.join(d, f"pmc_{c}", "run_counter_collection.csv"))))
-        for key, pat in KERNELS.items():
-            v = [float(r["Counter_Value"]) for r in rows if pat in r["Kernel_Name"]]
+        for key, pats in KERNELS.items():
+            v = [float(r["Counter_Value"]) for r in rows if any(p in r["Kernel_Name"] for p in pats)]
             if v:
                 vals[key][c] = (float(np.median(v)), len(v))
     for key, v in vals.items():

@@ -17,6 +17,7 @@
 // (64 B) and the depth/colour images are gathered through L1/L2. Voxels with invalid skin read 8 B
 // and stop. All arithmetic is un-contracted (-ffp-contract=off) so results are bit-identical to the
 // oracle restatement.
+#include <hip/hip_ext.h>
 #include <stdlib.h>
 
 #include <mutex>
@@ -756,22 +757,28 @@ std::mutex g_int_mu;
 bool g_int_timing = false;
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_int_ev;
 
+// events recorded by the dispatch itself (hipExtLaunchKernel: the kernel's own start / end), so host gaps
+// before a launch never count
 struct IntTimer {
-  hipStream_t s;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  explicit IntTimer(hipStream_t st) : s(st) {
+  IntTimer() {
     std::lock_guard<std::mutex> lk(g_int_mu);
     if (!g_int_timing) return;
-    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { e0 = e1 = nullptr; return; }
-    (void)hipEventRecord(e0, s);
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) e0 = e1 = nullptr;
   }
   ~IntTimer() {
     if (!e0) return;
-    (void)hipEventRecord(e1, s);
     std::lock_guard<std::mutex> lk(g_int_mu);
     g_int_ev.emplace_back(e0, e1);
   }
 };
+#define OFX_TIMED_LAUNCH(T, kernel, grid, block, shm, stream, ...)                                         \
+  do {                                                                                                    \
+    if ((T).e0)                                                                                           \
+      hipExtLaunchKernelGGL(kernel, grid, block, shm, stream, (T).e0, (T).e1, 0, __VA_ARGS__);            \
+    else                                                                                                  \
+      hipLaunchKernelGGL(kernel, grid, block, shm, stream, __VA_ARGS__);                                  \
+  } while (0)
 }  // namespace
 
 extern "C" {
@@ -831,8 +838,8 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
     OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
     if (n_list == 0) return OFX_OK;
     OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights, "null warp buffer");
-    IntTimer timer(hs);
-    hipLaunchKernelGGL(pyc ? (k_integrate<true, false, true>) : (k_integrate<true, false, false>), dim3((unsigned)n_list),
+    IntTimer timer;
+    OFX_TIMED_LAUNCH(timer, pyc ? (k_integrate<true, false, true>) : (k_integrate<true, false, false>), dim3((unsigned)n_list),
                        dim3(256), 0, hs, g, c, depth, color_im,
                        (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors, (const float4*)weights,
                        (const uint16_t*)nullptr, (const int32_t*)nullptr, (const uchar4*)nullptr,
@@ -860,22 +867,22 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
   OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights && pal_ids && pal_n && local_anchors,
                 "null warp/palette buffer");
   OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
-  IntTimer timer(as_stream(s));
+  IntTimer timer;
   if (desc->semantics == OFX_SEM_CPU && k == 4 && g.n_bricks * kBrickVox < (1ll << 31) && !getenv("OFX_INT_GENERIC")) {
     if (color)
-      hipLaunchKernelGGL(k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
+      OFX_TIMED_LAUNCH(timer, k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
                          (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
                          desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
     else
-      hipLaunchKernelGGL(k_integrate_pal4<false>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
+      OFX_TIMED_LAUNCH(timer, k_integrate_pal4<false>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
                          (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
                          desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
     OFX_LAUNCH_CHECK();
     return OFX_OK;
   }
-  hipLaunchKernelGGL(desc->semantics == OFX_SEM_PYCUDA ? (k_integrate<true, true, true>) : (k_integrate<true, true, false>),
+  OFX_TIMED_LAUNCH(timer, desc->semantics == OFX_SEM_PYCUDA ? (k_integrate<true, true, true>) : (k_integrate<true, true, false>),
                      dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_cam(cam),
                      depth, color_im, (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors,
                      (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,

@@ -9,6 +9,7 @@ bash tools/pmc_traffic.sh
 python tools/pmc_summary.py gpurun_out gpurun_out/${TAG}_pmc_traffic.json
 cp gpurun_out/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_traffic.json
 bash tools/pmc_valu.sh
+python tools/pmc_valu_summary.py gpurun_out/pmc_valu/run_counter_collection.csv gpurun_out/${TAG}_pmc_valu.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_final -o run -- python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/bench_rocprof.log 2>&1
 cd $R

@@ -103,7 +103,6 @@ struct Gn {
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
   int32_t nw_pad = 0;            // stride of the iteration partial streams: 128·pcg_ku, zero beyond nwg_row
   int32_t pcg_w2 = 1;            // two waves per cluster in k_pcg_iter (OFX_PCG_W1=1: one)
-  int32_t pcg_stream = 0;        // progress-paced enqueue of the PCG launches (OFX_PCG_STREAM=W: lead window W)
   int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (3: <= 384 waves, else 17)
   double* scal = nullptr;
   int32_t* flags = nullptr;
@@ -138,7 +137,7 @@ struct Gn {
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
 enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
-enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_PROG = 3, H_COUNT = 4 };
+enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_COUNT = 4 };
 __device__ __forceinline__ void host_flag(const int32_t* hf, int k, int v) {
   __hip_atomic_store(const_cast<int32_t*>(hf) + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1324,7 +1323,7 @@ struct PcgIt {
   const StepArgs* sa;
   const double* tail;           // rhs + 6N: [loss² total, data, arap, motion, nonfinite]
   double stop_loss_diff;
-  int32_t fuse, gn_iter, N, mode, n_iter_log, warm, stream;
+  int32_t fuse, gn_iter, N, mode, n_iter_log, warm;
 };
 static PcgIt pcg_args(const Gn* g) {
   PcgIt a;
@@ -1335,7 +1334,6 @@ static PcgIt pcg_args(const Gn* g) {
   a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol;
   a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff;
   a.fuse = 0; a.gn_iter = 0; a.N = g->N; a.mode = g->prm.mode; a.n_iter_log = 64; a.warm = g->prm.pcg_warm;
-  a.stream = g->pcg_stream;
   return a;
 }
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
@@ -1554,10 +1552,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     }
     return;
   }
-  if (lead) {
-    g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1;
-    if (g.stream) host_flag(g.hflags, H_PROG, cnt + 1);   // progress for the paced enqueue (posted store)
-  }
+  if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
   OFX_STAMP(2)
   // ---- n = A m (own component)
   double nc;
@@ -1914,36 +1909,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   g->step_fused = false;
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
-  if (g->pcg_stream > 0) {
-    // progress-paced enqueue: keep at most W launches queued ahead of the iteration the GPU is running
-    // (H_PROG, stored by every live launch), so at most W launches drain after convergence
-    const int W = g->pcg_stream;
-    hf[H_PROG] = 0;
-    bool done = false;
-    while (!done) {
-      const int target = std::min(max_it, hf[H_PROG] + W + 1);
-      for (; it < target; ++it) hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, pa, it & 1);
-      OFX_LAUNCH_CHECK();
-      if (it >= max_it) break;            // all launched: the chunk wait below decides
-      for (int spin = 0; spin < 4096; ++spin) {
-        if (hf[H_DONE] || hf[H_STOPPED]) { done = true; break; }
-        if (hf[H_PROG] + W + 1 > it) break;
-      }
-    }
-    if (done) {
-      if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
-      if (hf[H_DONE] && !hf[H_STOPPED]) {
-        g->last_pcg[gn_iter & 63] = hf[H_PCG_IT];
-        g->step_fused = pa.fuse != 0;
-      }
-      g->n_iter_launches += it;
-      if (g->timing) g->ev.emplace_back(e0, e1);
-      return OFX_OK;
-    }
-    chunk = 0;   // max_it launched without convergence: fall through to the event wait
-  }
-  while (it < max_it || chunk == 0) {
-    if (chunk == 0) chunk = 8;
+  while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
 #ifdef OFX_STAMPS
     const auto h0 = std::chrono::steady_clock::now();
@@ -1995,8 +1961,6 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster
     const char* e = getenv("OFX_PCG_W1");
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
-    const char* st = getenv("OFX_PCG_STREAM");   // paced enqueue with a lead window of W launches
-    g->pcg_stream = st ? atoi(st) : 0;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;

@@ -292,7 +292,7 @@ def main():
                                "avg_launch_us": 1e6 * t_kint, "listed_bricks": cache.n_list,
                                "skin_valid_voxels": n_skin_valid, "updated_voxels": U},
     }
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:   # the CPU baseline is an N=1 datapoint
         res["cpu_baseline"] = cpu_baseline(pipe, frames[total - 1], total - 1, a)
     if rank == 0:
         line = json.dumps(res)
@@ -315,6 +315,29 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def dense_gn_terms(rows, N6, threads):
+    """The dense GN step's two dominant costs (model.py:641-709: JᵀJ of the rows x N6 Jacobian, LU of N6²),
+    measured at the current BLAS thread count on bounded sub-problems and scaled by their flop counts: JᵀJ of a
+    (rs x m) slab (m = min(N6, 4096), rs <= rows) -> GFLOP/s -> 2·rows·N6² flops; LU of min(N6, 6000)² scaled by the
+    cube. Returns (t_JtJ, t_LU, GEMM GFLOP/s)."""
+    from scipy.linalg import lu_factor
+    m = min(N6, 4096)
+    rs = int(min(rows, max(m, (12e9 * max(1, threads) / 25.0) // (2.0 * m * m))))   # ~0.5 s per thread-equivalent
+    J = np.random.default_rng(1).random((rs, m))
+    J.T @ J[:, :64]
+    t0 = time.perf_counter()
+    J.T @ J
+    rate = 2.0 * rs * m * m / (time.perf_counter() - t0)
+    t_mm = 2.0 * rows * N6 * N6 / rate
+    n = min(N6, 6000)
+    A = np.random.default_rng(2).random((n, n)) + n * np.eye(n)
+    del J
+    t0 = time.perf_counter()
+    lu_factor(A)
+    t_lu = (time.perf_counter() - t0) * (N6 / n) ** 3
+    return t_mm, t_lu, rate / 1e9
 
 
 def cpu_baseline(pipe, fi, t, a):
@@ -368,14 +391,23 @@ def cpu_baseline(pipe, fi, t, a):
     gn_args = (g.graph.nodes, g.seq.edges, g.seq.edge_weights, fi.tpos.cpu().numpy(), fi.conf.cpu().numpy(),
                fi.src.cpu().numpy(), fi.anchors.cpu().numpy(), fi.weights.cpu().numpy(), fi.tgt.cpu().numpy(),
                pipe.intr)
-    t0 = time.perf_counter()
-    fo.gn_optimize(*gn_args, prev_rot=R.reshape(-1, 3, 3), prev_trans=T, num_iter=1)
-    dt_gn = time.perf_counter() - t0
+    N6 = 6 * g.graph.nodes.shape[0]
+    rows = 3 * int(fi.src.shape[0]) + 3 * int((np.asarray(g.seq.edges) >= 0).sum()) + 3 * g.graph.nodes.shape[0]
+    if N6 <= 12600:     # up to ~2.1k nodes: one real dense GN step of the oracle (≈ 11 s at 2k nodes, 16 threads)
+        t0 = time.perf_counter()
+        fo.gn_optimize(*gn_args, prev_rot=R.reshape(-1, 3, 3), prev_trans=T, num_iter=1)
+        dt_gn = time.perf_counter() - t0
+        gn_how = "one dense float64 GN step (oracle gn_optimize, numpy/LAPACK)"
+    else:               # larger graphs: the step's dominant terms, each on a bounded slice, scaled
+        dt_mm, dt_lu, gf = dense_gn_terms(rows, N6, threads)
+        dt_gn = dt_mm + dt_lu
+        gn_how = (f"dense GN step estimated from its dominant terms at {threads} BLAS threads: JᵀJ ({rows}x{N6}) "
+                  f"at the measured {gf:.0f} GFLOP/s of a 4096-column slab + LU scaled from a 6000² factorisation")
     per_frame = per_frame_int + 10 * dt_gn
     out = {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port", "cpu": cpu_model(),
            "sample": f"warp+integrate (oracle/cpu_ref.c, OpenMP) of {n} uniformly sampled voxels of the {Dx}^3 frame "
-                     f"(x{V / n:.0f} scaled, skin precomputed, {dt_int:.3f} s) + one dense float64 GN step "
-                     f"(oracle gn_optimize, numpy/LAPACK, {dt_gn:.2f} s) x 10 GN iterations",
+                     f"(x{V / n:.0f} scaled, skin precomputed, {dt_int:.3f} s) + {gn_how} ({dt_gn:.2f} s) x 10 GN "
+                     f"iterations",
            "ms_per_frame_warp_integrate": 1e3 * per_frame_int, "s_per_gn_step": dt_gn}
     # one thread: a 1/16 integrate sample, and the dense GN step's cost terms at one BLAS thread
     try:
@@ -384,28 +416,16 @@ def cpu_baseline(pipe, fi, t, a):
         n1 = max(1, n // 16)
         dt_int1 = integrate_sample(n1)
         cpu_ref.set_threads(threads)
-        N6 = 6 * g.graph.nodes.shape[0]
-        rows = 3 * int(fi.src.shape[0]) + 3 * int((np.asarray(g.seq.edges) >= 0).sum()) + 3 * g.graph.nodes.shape[0]
-        Jr = np.random.default_rng(1).random((rows, N6))
-        cols = max(1, N6 // 64)
         with threadpool_limits(limits=1):
-            t0 = time.perf_counter()
-            Jr.T @ Jr[:, :cols]
-            dt_mm = (time.perf_counter() - t0) * N6 / cols
-            from scipy.linalg import lu_factor
-            A = Jr[:N6].T @ Jr[:N6] + np.eye(N6)
-            t0 = time.perf_counter()
-            lu_factor(A)
-            dt_lu = time.perf_counter() - t0
-        del Jr
+            dt_mm, dt_lu, gf1 = dense_gn_terms(rows, N6, 1)
         gn1 = dt_mm + dt_lu
         pf1 = dt_int1 * V / n1 + 10 * gn1
         out["single_thread"] = {"value": 1.0 / pf1, "unit": "frames/s", "cores": 1,
                                 "ms_per_frame_warp_integrate": 1e3 * dt_int1 * V / n1, "s_per_gn_step": gn1,
                                 "sample": f"integrate of {n1} sampled voxels at 1 OpenMP thread ({dt_int1:.3f} s, "
-                                          f"x{V / n1:.0f}); GN step = dense JᵀJ ({rows}x{N6}) measured on 1/64 of "
-                                          f"the columns at 1 BLAS thread ({dt_mm:.1f} s scaled) + LU of {N6}² "
-                                          f"({dt_lu:.1f} s)"}
+                                          f"x{V / n1:.0f}); GN step = dense JᵀJ ({rows}x{N6}) at the measured "
+                                          f"{gf1:.0f} GFLOP/s of a 4096-column slab at 1 BLAS thread ({dt_mm:.1f} s) + "
+                                          f"LU of {N6}² ({dt_lu:.1f} s, scaled from at most 6000²)"}
     except Exception as e:  # the reported baseline must not break the bench line
         out["single_thread"] = {"error": repr(e)}
     return out

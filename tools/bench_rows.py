@@ -80,6 +80,28 @@ def main():
     rows = {"workload": f"{D}^3 TSDF @{a.voxel * 1e3:g} mm after {a.frames} fused frames; 640x448 depth; "
                         f"{seq.nodes.shape[0]} nodes", "reps": a.reps}
 
+    # ---- a7: source-frame integrate (the dense pass, once per sequence) on a scratch volume of the same grid
+    from occlusionfusion_amd import TSDFVolume
+    scratch = TSDFVolume.from_grid(vol._vol_origin, vol._voxel_size, vol._vol_dim, pipe.intr, pipe.fopt, device=dev)
+
+    def src_pass():
+        if hasattr(scratch, "frame_id"):
+            del scratch.frame_id
+        scratch.update(frames[0].im, 0)
+        scratch.integrate_device(count_updates=True)
+    t_src, _ = timed(src_pass, a.reps)
+    U_src = int(scratch.n_updated[:scratch.n_bricks].sum().item())
+    B_src = V * 8 + U_src * 16
+    rows["a7_source_frame_integrate"] = {"ms": 1e3 * t_src, "updated_voxels": U_src, "bytes": B_src,
+                                         "GBps": B_src / t_src / 1e9, "frac_hbm": B_src / t_src / PEAK,
+                                         "bytes_note": "tsdf + weight read 8 B per voxel, tsdf/weight/colour "
+                                                       "write + colour read 16 B per updated voxel (SURVEY 8(d))"}
+    del scratch
+    # ---- new capability: raycast of the fused volume (no reference twin)
+    t_rc, rc = timed(lambda: vol.raycast(), a.reps)
+    rows["new_raycast"] = {"ms": 1e3 * t_rc, "pixels": int(rc[0].numel()), "hits": int((rc[0] > 0).sum().item()),
+                           "note": "depth + normals + colours, trilinear march (coarse 0.8 trunc / fine 1 voxel)"}
+
     # ---- f1: surface extraction
     t_tr, _ = timed(lambda: vol.truncated_region_device(1.2), a.reps)
     B_tr = vol.n_slots * (4 + 1)

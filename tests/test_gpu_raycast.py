@@ -68,3 +68,26 @@ def test_raycast_config_volume(cuda, config):
     m[np.setdiff1d(np.arange(H), rows)] = False
     assert m.sum() > 1000
     assert np.median(np.abs(d[m] - dep[m])) < c["voxel"]
+
+
+def test_raycast_axis_rays_and_inside_camera(cuda):
+    """Edge cases of the slab test: integer principal point (the centre column / row has dx = 0 / dy = 0 exactly:
+    the axis-parallel branch), a volume that contains the camera (entry clamped by z_near) and one that does not
+    (rays whose box interval is empty)."""
+    from types import SimpleNamespace
+    from occlusionfusion_amd import TSDFVolume
+    from occlusionfusion_amd import synthetic as S
+    cam = S.Intrinsics(100.0, 100.0, 40.0, 30.0, 80, 60)
+    depth = S.SphereScene(occluder=False).render(cam, 0, np.random.default_rng(0))
+    im = S.make_image(depth)
+    for origin in ((-0.6, -0.5, 0.9), (-0.6, -0.5, -0.2)):          # in front of / around the camera
+        vol = TSDFVolume.from_grid(origin, 0.02, (64, 50, 60), (cam.fx, cam.fy, cam.cx, cam.cy),
+                                   SimpleNamespace(source_frame=0, skip_rate=1), device=cuda)
+        vol.integrate({"im": im, "id": 0})
+        for zn, zf in ((0.1, 10.0), (1.2, 1.5), (0.05, 0.06)):
+            d = _compare(vol, z_near=zn, z_far=zf)
+            if (zn, zf) == (0.1, 10.0) and origin[2] > 0:
+                assert (d > 0).sum() > 500
+            if zf < 0.5:
+                assert not (d > 0).any()
+

@@ -242,6 +242,9 @@ def main():
     # and the depth/colour images are L2-resident and not counted.
     B = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
     achieved = B / t_kint
+    # SURVEY §8(d)'s per-unit figure over the voxels this launch processes (every voxel of a listed brick):
+    # 32 B skin + 8 B tsdf/weight read per voxel, 8 B tsdf/weight write per updated voxel (colour separately)
+    B_survey = cache.n_list * 512 * 40 + U * 8
     # k_pcg_iter algorithmic (unique) bytes per PCG iteration: per JᵀJ block its 6x6 f64 values (288 B) + its
     # (col, slot) wave-list entry (8 B); per PCG row (nodes in cluster order, padded) the cluster-inverse
     # rows (6 x 48 f32 = 1152 B), the 8-vector state read + written (2 x 384 B), m read (48 B; the
@@ -285,10 +288,14 @@ def main():
                              "kernel-boundary floor + two dependent memory trips + the wave's instruction stream "
                              "(DESIGN.md §5); the 11-12 MB working set is L2/MALL-resident across launches. frac = "
                              "bytes_per_launch / avg_launch_us / peak"},
-        "roofline_integrate": {"kernel": "k_integrate<true,true> (fused warp+integrate, LDS node palette)", "bound": "hbm",
+        "roofline_integrate": {"kernel": "k_integrate_pal4 (fused warp+integrate, LDS node palette; VALU-bound: "
+                                         "DESIGN.md section 5)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp", workload),
                                "bytes_per_launch": B,
+                               "bytes_note": "this layout's minimal bytes (palette ranks, reads for skin-valid voxels "
+                                             "only); SURVEY 8(d)'s per-unit figure over the processed voxels below",
+                               "survey_bytes_per_launch": B_survey, "frac_survey_bytes": B_survey / t_kint / PEAK_HBM,
                                "avg_launch_us": 1e6 * t_kint, "listed_bricks": cache.n_list,
                                "skin_valid_voxels": n_skin_valid, "updated_voxels": U},
     }

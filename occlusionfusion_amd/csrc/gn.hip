@@ -37,6 +37,7 @@
 #include <string.h>
 #include <algorithm>
 #include <chrono>
+#include <type_traits>
 #include <utility>
 #include <cstdlib>
 #include <vector>
@@ -51,15 +52,15 @@ constexpr int kProj = 4;      // warm start: Galerkin projection on the last kPr
 constexpr int kCS = 8;        // nodes per preconditioner cluster (= PCG rows per wave)
 constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² entries
 
-struct Gn {
+// Everything the kernels read: trivially copyable, passed by value as the kernel argument (host-only
+// members live in Gn below, so a launch copies these bytes and nothing else).
+struct GnDev {
   int max_nodes = 0, max_matches = 0;
   int N = 0, M = 0, NB = 0;    // N: PCG rows (nodes in cluster order, padded to whole clusters)
   int N_real = 0;              // caller's node count
   int max_pad = 0;             // capacity of the node-indexed arrays (2·max_nodes + kCS)
   int32_t *perm = nullptr;     // row -> caller node (-1: padding), N entries
   int32_t *iperm = nullptr;    // caller node -> row, N_real entries
-  std::vector<float> h_nodes;          // host copy of the graph the current order was built from
-  std::vector<int32_t> h_edges, h_perm;
   int64_t T = 0;        // terms = M + N*NB + N
   ofx_gn_params prm{};
   float fx = 0, fy = 0, cx = 0, cy = 0;
@@ -130,8 +131,15 @@ struct Gn {
   bool setup_done = false;
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   int64_t n_iter_launches = 0;
+};
+static_assert(std::is_trivially_copyable<GnDev>::value, "kernel argument");
+
+// The solver handle: the kernel-visible state plus host-only members.
+struct Gn : GnDev {
+  std::vector<float> h_nodes;          // host copy of the graph the current order was built from
+  std::vector<int32_t> h_edges, h_perm;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // timing events of the PCG loops
 };
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
@@ -237,13 +245,13 @@ struct Upload {
   int64_t old_nnzb, n;
 };
 // caller node -> row (negative ids stay negative)
-__device__ __forceinline__ int to_row(const Gn& g, int a) { return a >= 0 ? g.iperm[a] : a; }
+__device__ __forceinline__ int to_row(const GnDev& g, int a) { return a >= 0 ? g.iperm[a] : a; }
 // edge k of row i in row numbering (-1: none, also for padding rows)
-__device__ __forceinline__ int edge_row(const Gn& g, const Upload& u, int i, int k) {
+__device__ __forceinline__ int edge_row(const GnDev& g, const Upload& u, int i, int k) {
   const int p = g.perm[i];
   return p >= 0 ? to_row(g, u.edges[(int64_t)p * g.NB + k]) : -1;
 }
-__global__ __launch_bounds__(256) void k_upload(Gn g, Upload u) {
+__global__ __launch_bounds__(256) void k_upload(GnDev g, Upload u) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= u.n) return;
   const int N = g.N, M = g.M, NB = g.NB;
@@ -316,7 +324,7 @@ __device__ __forceinline__ int block_exscan(int v, int* s_w, int& total) {
   return base + x - v;
 }
 
-__global__ void k_mark(Gn g) {
+__global__ void k_mark(GnDev g) {
   int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= g.T) return;
   const int32_t* n = g.term_node + t * 4;
@@ -349,7 +357,7 @@ __global__ __launch_bounds__(256) void k_wave_max(int nwave, const int32_t* __re
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w < nwave) atomicMax(out, row_ptr[(w + 1) * kCS] - row_ptr[w * kCS]);
 }
-__global__ __launch_bounds__(256) void k_wave_list(Gn g) {
+__global__ __launch_bounds__(256) void k_wave_list(GnDev g) {
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e >= (int64_t)(g.N / kCS) * kWL) return;
   const int w = (int)(e / kWL), k = (int)(e % kWL);
@@ -425,7 +433,7 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
     }
 }
 
-__global__ void k_pair_count(Gn g) {
+__global__ void k_pair_count(GnDev g) {
   int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= g.T) return;
   const int32_t* n = g.term_node + t * 4;
@@ -438,7 +446,7 @@ __global__ void k_pair_count(Gn g) {
 }
 
 // scatter (order fixed later by k_seg_sort); blk_cnt/node_cnt are reused as cursors (zeroed first)
-__global__ void k_pair_scatter(Gn g) {
+__global__ void k_pair_scatter(GnDev g) {
   int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= g.T) return;
   const int32_t* n = g.term_node + t * 4;
@@ -477,7 +485,7 @@ struct DataCoef {
   double lf, ld, la, lm, fx, fy, cx, cy;
 };
 
-__device__ void data_jacobian(const Gn& g, const DataCoef& dc, int64_t m, int k, const double p[3], double zinv,
+__device__ void data_jacobian(const GnDev& g, const DataCoef& dc, int64_t m, int k, const double p[3], double zinv,
                               double* __restrict__ J) {
   int a = g.anc[m * 4 + k];
   double w = g.wts[m * 4 + k];
@@ -503,7 +511,7 @@ __device__ void data_jacobian(const Gn& g, const DataCoef& dc, int64_t m, int k,
   J[15] = 0.0; J[16] = 0.0; J[17] = dc.ld * w;
 }
 
-__device__ void deformed_point(const Gn& g, int64_t m, double p[3]) {
+__device__ void deformed_point(const GnDev& g, int64_t m, double p[3]) {
   p[0] = p[1] = p[2] = 0.0;
   for (int k = 0; k < 4; ++k) {
     int a = g.anc[m * 4 + k];
@@ -523,7 +531,7 @@ __device__ void deformed_point(const Gn& g, int64_t m, double p[3]) {
 // recompute the deformed point (identical bits) so the four anchor Jacobians run in parallel.
 // Terms outside this rank's share (data matches outside [m0,m1), regularisers when !add_reg) are
 // written as exact zeros so the fixed contribution lists stay valid.
-__global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m1, int add_reg) {
+__global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, int m1, int add_reg) {
   const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t t = id >> 2;
   const int k = (int)(id & 3);
@@ -619,7 +627,7 @@ __global__ __launch_bounds__(kBlk) void k_terms(Gn g, DataCoef dc, int m0, int m
 // block, loads both 3x6 Jacobian blocks of the entry whole (16-B accesses) and accumulates the full
 // 6x6 product; 16-lane DPP sums (fixed pairing) finish the block and lane 0 of the group stores it.
 // Deterministic; forward declared helpers live in the PCG section.
-__device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A, int64_t wg, double lm) {
+__device__ __forceinline__ void blocks_body(const GnDev& g, double* __restrict__ A, int64_t wg, double lm) {
   const int64_t s = wg * (kBlk / 16) + (threadIdx.x >> 4);
   const int q = threadIdx.x & 15;
   double acc[36];
@@ -661,7 +669,7 @@ __device__ __forceinline__ void blocks_body(const Gn& g, double* __restrict__ A,
 
 // b = -Jᵀr: one wave per node, entry-parallel (below). WG 0 also reduces the loss partials into the
 // rhs tail.
-__device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, int wg) {
+__device__ __forceinline__ void rhs_body(const GnDev& g, double* __restrict__ rhs, int wg) {
   if (wg == 0 && threadIdx.x < 64) {   // the loss partials of k_terms, 4 streams in one pass, fixed order
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     for (int i = threadIdx.x; i < g.nwg_terms; i += 64) {
@@ -723,7 +731,7 @@ __device__ __forceinline__ void rhs_body(const Gn& g, double* __restrict__ rhs, 
 // the chunk in list order. A block's cost is its share of the workgroup's entries, not its own list length
 // (the 16-lane form took ceil(len/16) dependent trips: ~6 for a busy node's diagonal block).
 constexpr int kCoop = 128;
-__device__ __forceinline__ void blocks_coop(const Gn& g, double* __restrict__ A, int64_t wg, double lm) {
+__device__ __forceinline__ void blocks_coop(const GnDev& g, double* __restrict__ A, int64_t wg, double lm) {
   __shared__ double s_prod[36 * (kCoop + 1)];
   __shared__ int s_off[17];
   const int tid = threadIdx.x;
@@ -793,7 +801,7 @@ __device__ __forceinline__ void blocks_coop(const Gn& g, double* __restrict__ A,
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
-__global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A, double* __restrict__ rhs, int nwb,
+__global__ __launch_bounds__(kBlk) void k_assemble(GnDev g, double* __restrict__ A, double* __restrict__ rhs, int nwb,
                                                   double lm) {
   const int nrw = (int)gridDim.x - nwb;
   if ((int)blockIdx.x < nrw) rhs_body(g, rhs, blockIdx.x);
@@ -804,14 +812,14 @@ __global__ __launch_bounds__(kBlk) void k_assemble(Gn g, double* __restrict__ A,
 #endif
 }
 #ifdef OFX_SPLIT_ASSEMBLE
-__global__ __launch_bounds__(kBlk) void k_assemble_blocks(Gn g, double* __restrict__ A, double lm) {
+__global__ __launch_bounds__(kBlk) void k_assemble_blocks(GnDev g, double* __restrict__ A, double lm) {
 #ifdef OFX_ASSEMBLE_LANES
   blocks_body(g, A, blockIdx.x, lm);
 #else
   blocks_coop(g, A, blockIdx.x, lm);
 #endif
 }
-__global__ __launch_bounds__(kBlk) void k_assemble_rhs(Gn g, double* __restrict__ rhs) { rhs_body(g, rhs, blockIdx.x); }
+__global__ __launch_bounds__(kBlk) void k_assemble_rhs(GnDev g, double* __restrict__ rhs) { rhs_body(g, rhs, blockIdx.x); }
 #endif
 
 // ---------------------------------------------------------------------------- PCG
@@ -975,7 +983,7 @@ __device__ __forceinline__ int64_t mcl_idx(int64_t cluster, int i, int j) {
   return cluster * kCD * kCD + ((j >> 2) * kCD + i) * 4 + (j & 3);
 }
 // The row's (r, c) f32 row of the cluster inverse, 12 x 16-B loads.
-__device__ __forceinline__ void load_mrow(const Gn& g, int64_t o, float4 mr[kCD / 4]) {
+__device__ __forceinline__ void load_mrow(const GnDev& g, int64_t o, float4 mr[kCD / 4]) {
   const float4* p = reinterpret_cast<const float4*>(g.Mcl + mcl_idx(o / kCD, (int)(o % kCD), 0));
 #pragma unroll
   for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k * kCD];
@@ -997,7 +1005,7 @@ __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const dou
 // in registers for all 48 (unrolled) steps; step k fetches the old row k / column k entries it needs
 // from their owner lanes by cross-lane permutes and the pivot by a lane read — no LDS, no barrier.
 // Cold start also: x = 0, r = b, u = M⁻¹ b, z = q = s = p = w = 0, u -> m1.
-__global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __restrict__ A,
+__global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __restrict__ A,
                                                  const double* __restrict__ rhs, int invert) {
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1087,7 +1095,7 @@ __global__ __launch_bounds__(64) void k_pcg_prep(Gn g, double lm, double* __rest
 constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
 __device__ __forceinline__ constexpr int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
 
-__global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict__ rhs) {
+__global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restrict__ rhs) {
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {   // PCG bookkeeping of this GN step (also in k_pcg_prep)
     g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
@@ -1161,7 +1169,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj(Gn g, const double* __restrict_
 // identical bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get
 // c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0 (cluster, via LDS),
 // z = q = s = p = w = 0, u0 -> m1.
-__global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict__ rhs) {
+__global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restrict__ rhs) {
   __shared__ double s_v[kCD];
   const int lane = threadIdx.x;
   if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
@@ -1243,7 +1251,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(Gn g, const double* __restrict
 
 // w0 = A u0 (u0 gathered from m1), m0 = M⁻¹ w0 (cluster, via LDS); per-wave partials
 // (γ0 = r·u, δ0 = w·u, r·r) -> parity 0, b·b -> part_b.
-__global__ __launch_bounds__(64) void k_pcg_w0(Gn g, const double* __restrict__ rhs) {
+__global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict__ rhs) {
   __shared__ double s_v[kCD];
   const int lane = threadIdx.x;
   if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
@@ -1660,7 +1668,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 // (flags set by the PCG, this step's rhs tail, step_state[k]); workgroup 0 alone writes the
 // bookkeeping (flags, loss log, step_state[k+1], statistics). xsave (nullable): ring slot receiving
 // this step's solution for the following steps' warm start.
-__global__ __launch_bounds__(256) void k_step(Gn g, const double* __restrict__ rhs, int n_iter_log, int pcg_max,
+__global__ __launch_bounds__(256) void k_step(GnDev g, const double* __restrict__ rhs, int n_iter_log, int pcg_max,
                                               int gn_iter, double* __restrict__ xsave) {
   if (g.flags[F_STOPPED]) return;
   const double* tail = rhs + 6 * (int64_t)g.N;
@@ -1730,7 +1738,7 @@ __global__ __launch_bounds__(256) void k_step(Gn g, const double* __restrict__ r
 // arap mode, lambda_flow = 0: remove each connected component's mean translation from the PCG
 // solution (one wave per component, fixed-order sums). A·n = λ_LM·n for that common translation n and
 // b ⊥ n, so the dense LU solution has no n component; CG barely resolves the λ_LM eigenvalue.
-__global__ __launch_bounds__(64) void k_null_project(Gn g) {
+__global__ __launch_bounds__(64) void k_null_project(GnDev g) {
   const int c = blockIdx.x;
   const int b = g.comp_off[c], e = g.comp_off[c + 1];
   double s[3] = {0.0, 0.0, 0.0};
@@ -1749,7 +1757,7 @@ __global__ __launch_bounds__(64) void k_null_project(Gn g) {
   }
 }
 
-__global__ void k_finish(Gn g, float* __restrict__ rot, float* __restrict__ trans, int32_t* __restrict__ status,
+__global__ void k_finish(GnDev g, float* __restrict__ rot, float* __restrict__ trans, int32_t* __restrict__ status,
                          double* __restrict__ loss_out, int n_log) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = !g.flags[F_ILL] && !g.flags[F_RES_NONFINITE];

@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--nodes", type=int, default=None)
     p.add_argument("--matches", type=int, default=10000)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-prefetch", dest="prefetch", action="store_false",
+                   help="set up each frame's solve inline instead of prefetching it during the previous frame")
     p.add_argument("--cpu-sample", type=int, default=1 << 24)
     p.add_argument("--json-out", default=None)
     p.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
@@ -163,7 +165,7 @@ def main():
     shard = (rank, world, "hash") if sharded else None   # spatial-hash brick buckets (sharding.hash_owner)
     pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)
     total = a.warmup + a.steps + 1
-    frames = [pipe.prepare(t) for t in range(total)]
+    frames = [pipe.prepare(t) for t in range(total + 1)]   # + the frame the last timed step prefetches
     torch.cuda.synchronize()
     pipe.integrate_source(frames[0])
     cache = pipe.wf.skin_tsdf_cache()
@@ -173,19 +175,23 @@ def main():
     allreduce = sharded and a.solve == "allreduce"
     ar_events = []
 
-    def solve(fi):
+    prefetch = a.prefetch and not allreduce
+
+    def solve(fi, nxt):
         if allreduce:
             out = pipe.solver.optimize_distributed(pipe.nodes_t, pipe.edges_t, pipe.ew_t, fi.tpos, fi.conf, fi.src,
                                                    fi.anchors, fi.weights, fi.tgt, pipe.intr, prev_rot=pipe.prev_rot,
                                                    prev_trans=pipe.prev_trans, sync=False, timer=ar_events)
             pipe.prev_rot, pipe.prev_trans = out["node_rotations"], out["node_translations"]
             return out
-        return pipe.solve(fi)
+        # software pipelining: frame t+1's solver setup runs on the other solver slot while frame t solves
+        return pipe.solve(fi, nxt if prefetch else None)
 
     ev = lambda: torch.cuda.Event(enable_timing=True)
     for t in range(1, 1 + a.warmup):
-        solve(frames[t])
+        solve(frames[t], frames[t + 1])
         pipe.integrate(frames[t], t)
+    pipe.solver.drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -199,12 +205,13 @@ def main():
     for t in range(1 + a.warmup, total):
         e0, e1, e2 = ev(), ev(), ev()
         e0.record()
-        out = solve(frames[t])
+        out = solve(frames[t], frames[t + 1])
         e1.record()
         pipe.integrate(frames[t], t, count_updates=True)
         e2.record()
         upd.append(pipe.vol.n_updated[:cache.n_list].sum())   # device-side sum, read after timing
         marks.append((e0, e1, e2, out))
+    pipe.solver.drain()   # the last step's prefetched setup (of a frame not timed) counts inside the region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -215,6 +222,7 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed_max = float(el.item())
     pcg_ms, pcg_launches, _ = pipe.solver.timing(False)
+    pf_used, pf_missed = pipe.solver.prefetch_stats()
     N_, M_, nnzb, _T, rows = pipe.solver.info()
     t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
     t_int = np.array([m[1].elapsed_time(m[2]) for m in marks]) * 1e-3
@@ -271,10 +279,12 @@ def main():
         "config": {"workload": workload, "baseline_config": a.config, "mode": a.mode,
                    "solve": (a.solve if sharded else "local"), "dims": D, "voxel_size_m": a.voxel,
                    "nodes": int(seq.nodes.shape[0]), "matches": a.matches,
-                   "parallelism": f"{a.mode}{world}" + (f"-{a.solve}" if sharded else "")},
+                   "parallelism": f"{a.mode}{world}" + (f"-{a.solve}" if sharded else ""),
+                   "setup_prefetch": prefetch},
         "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * float(np.mean(t_int)),
                          "allreduce": 1e3 * t_ar, "pcg_iters_per_frame": float(np.mean(pcg)),
-                         "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid))},
+                         "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid)),
+                         "prefetched_setups_used": pf_used, "prefetched_setups_missed": pf_missed},
         "per_rank": per_rank,
         "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster "
                                "block-Jacobi apply)", "bound": "latency",

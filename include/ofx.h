@@ -443,6 +443,21 @@ int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s);
 /* setup + num_iter x (linearize + step) + finish, single device */
 int ofx_gn_solve(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params,
                  const ofx_gn_result* res, ofx_stream_t s);
+/* Prefetch the setup of the NEXT problem on this handle (software pipelining across frames; no reference
+ * twin — the reference sets up every solve inline, model.py:222-415). Returns at once: the setup (upload,
+ * JᵀJ pattern, contribution lists, with its one host sync) runs on a host thread and on the handle's own
+ * stream, ordered after everything enqueued on `s` so far, concurrently with the caller's other work (the
+ * current frame's solve on another handle). The following ofx_gn_solve on this handle with the same problem
+ * (same buffers and sizes, same params; prev_rot / prev_trans may differ: they are read by the solve)
+ * skips its setup, waits for the prefetched one on its own stream and loads the pose. A different problem,
+ * or a prefetch that failed, falls back to the inline setup. The problem's buffers must stay allocated and
+ * unchanged until that solve. */
+int ofx_gn_prepare(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params, ofx_stream_t s);
+/* Wait (host) until a prefetch on this handle has been enqueued, and order stream `s` after it: a
+ * synchronisation of `s` afterwards covers the prefetched setup. */
+int ofx_gn_prepare_wait(void* handle, ofx_stream_t s);
+/* Solves on this handle that used a prefetched setup / discarded one (a different problem or a failure). */
+int ofx_gn_prefetch_stats(void* handle, int64_t* used, int64_t* missed);
 
 #ifdef __cplusplus
 }

@@ -108,6 +108,9 @@ _SIGS = {
     "ofx_gn_step": [P, c_int32, P, P, P],
     "ofx_gn_finish": [P, P, P],
     "ofx_gn_solve": [P, P, P, P, P],
+    "ofx_gn_prepare": [P, P, P, P],
+    "ofx_gn_prepare_wait": [P, P],
+    "ofx_gn_prefetch_stats": [P, P, P],
 }
 
 

@@ -37,6 +37,7 @@
 #include <string.h>
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <cstdlib>
@@ -140,6 +141,16 @@ struct Gn : GnDev {
   std::vector<float> h_nodes;          // host copy of the graph the current order was built from
   std::vector<int32_t> h_edges, h_perm;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // timing events of the PCG loops
+  // prefetched setup (ofx_gn_prepare): the next problem's setup runs on a host thread, on the handle's own
+  // stream, while the caller's stream still works on the current problem (of another handle)
+  std::thread prep;
+  int prep_status = 0;
+  bool prepared = false;            // the setup of prep_pb / prep_prm is (being) enqueued on `side`
+  ofx_gn_problem prep_pb{};
+  ofx_gn_params prep_prm{};
+  hipStream_t side = nullptr;
+  hipEvent_t ev_in = nullptr, ev_prep = nullptr;   // caller's stream at prepare -> side; side's setup done
+  int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
 };
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
@@ -295,6 +306,21 @@ __global__ __launch_bounds__(256) void k_upload(GnDev g, Upload u) {
   if (i < S_COUNT) g.scal[i] = 0.0;
   if (i < 3 * kMaxLog) g.stat[i] = 0.0;
   if (i < 2 * (kMaxLog + 1)) g.step_state[i] = 0.0;
+}
+
+// The previous frame's transforms into the state (k_upload's R / t rows) for a setup that was prefetched
+// before they existed (ofx_gn_prepare uploads the problem with identity / zero).
+__global__ __launch_bounds__(256) void k_pose(GnDev g, const float* __restrict__ prev_R, const float* __restrict__ prev_t) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int N = g.N;
+  if (i < 3 * (int64_t)N) {
+    const int p = g.perm[i / 3];
+    g.t[i] = (p >= 0 && prev_t) ? (double)prev_t[3 * (int64_t)p + i % 3] : 0.0;
+  }
+  if (i < 9 * (int64_t)N) {
+    const int p = g.perm[i / 9];
+    g.R[i] = (p >= 0 && prev_R) ? (double)prev_R[9 * (int64_t)p + i % 9] : ((i % 9) % 4 == 0 ? 1.0 : 0.0);
+  }
 }
 
 // exclusive scan of one int per thread over the workgroup (wave shuffles + one LDS pass); total out
@@ -1953,6 +1979,29 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   return OFX_OK;
 }
 
+static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, int64_t* nnz_blocks, ofx_stream_t s);
+
+// the prefetch thread of this handle has finished enqueuing (its status stays in prep_status)
+static void prep_wait(Gn* g) {
+  if (g->prep.joinable()) g->prep.join();
+}
+
+static bool same_problem(const ofx_gn_problem& a, const ofx_gn_problem& b) {   // all but the pose
+  return a.n_nodes == b.n_nodes && a.n_matches == b.n_matches && a.n_neighbors == b.n_neighbors &&
+         a.nodes == b.nodes && a.edges == b.edges && a.edge_weights == b.edge_weights &&
+         a.target_node_pos == b.target_node_pos && a.node_conf == b.node_conf && a.src == b.src &&
+         a.anchors == b.anchors && a.weights == b.weights && a.tgt == b.tgt && a.target_px == b.target_px &&
+         a.target_py == b.target_py && a.fx == b.fx && a.fy == b.fy && a.cx == b.cx && a.cy == b.cy;
+}
+
+static bool same_params(const ofx_gn_params& a, const ofx_gn_params& b) {
+  return a.num_iter == b.num_iter && a.use_edge_weighting == b.use_edge_weighting &&
+         a.pcg_max_iter == b.pcg_max_iter && a.pcg_warm == b.pcg_warm && a.lambda_flow == b.lambda_flow &&
+         a.lambda_depth == b.lambda_depth && a.lambda_arap == b.lambda_arap && a.lambda_motion == b.lambda_motion &&
+         a.lm_factor == b.lm_factor && a.stop_loss_diff == b.stop_loss_diff && a.pcg_tol == b.pcg_tol &&
+         a.mode == b.mode && a.precond_every == b.precond_every;
+}
+
 }  // namespace ofx
 
 using namespace ofx;
@@ -2015,6 +2064,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
 
 int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g, "null handle");
   double ms = 0.0;
   for (auto& e : g->ev) {
@@ -2036,6 +2086,7 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 
 int ofx_gn_info(void* handle, int64_t* info) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && info, "null handle/info");
   info[0] = g->N_real; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T; info[4] = g->N;
   return OFX_OK;
@@ -2057,6 +2108,7 @@ int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
 
 int ofx_gn_stats(void* handle, double* out, int32_t cap) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && out && cap >= 0, "bad gn_stats args");
   int n = cap < kMaxLog ? cap : kMaxLog;
   if (n > 0) OFX_HIP(hipMemcpy(out, g->stat, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
@@ -2065,6 +2117,7 @@ int ofx_gn_stats(void* handle, double* out, int32_t cap) {
 
 int ofx_gn_row_order(void* handle, int32_t* perm, int32_t cap) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && g->setup_done && perm, "gn_setup not called / null perm");
   OFX_CHECK_ARG(cap >= (int)g->h_perm.size(), "cap %d < rows %d", cap, (int)g->h_perm.size());
   memcpy(perm, g->h_perm.data(), g->h_perm.size() * sizeof(int32_t));
@@ -2092,7 +2145,11 @@ int ofx_gn_stamps(void* handle, uint64_t* out, int64_t n) {
 int ofx_gn_destroy(void* handle) {
   if (!handle) return OFX_OK;
   Gn* g = (Gn*)handle;
+  prep_wait(g);
   (void)hipDeviceSynchronize();
+  if (g->side) (void)hipStreamDestroy(g->side);
+  if (g->ev_in) (void)hipEventDestroy(g->ev_in);
+  if (g->ev_prep) (void)hipEventDestroy(g->ev_prep);
   free_all(g);
   delete g;
   return OFX_OK;
@@ -2101,6 +2158,65 @@ int ofx_gn_destroy(void* handle) {
 int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* prm, int64_t* nnz_blocks,
                  ofx_stream_t s) {
   Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g, "null handle");
+  prep_wait(g);            // an explicit setup replaces a prefetched one
+  g->prepared = false;
+  g->prep_status = OFX_OK;
+  return gn_setup(g, pb, prm, nnz_blocks, s);
+}
+
+int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* prm, ofx_stream_t s) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && pb && prm, "null handle/problem/params");
+  prep_wait(g);
+  g->prepared = false;
+  g->prep_status = OFX_OK;
+  if (!g->side) {
+    OFX_HIP(hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking));
+    OFX_HIP(hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming));
+    OFX_HIP(hipEventCreateWithFlags(&g->ev_prep, hipEventDisableTiming));
+  }
+  int dev = 0;
+  OFX_HIP(hipGetDevice(&dev));
+  // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve)
+  // comes before the prefetched setup
+  OFX_HIP(hipEventRecord(g->ev_in, as_stream(s)));
+  g->prep_pb = *pb;
+  g->prep_pb.prev_rot = nullptr;    // the pose is loaded by the solve (k_pose)
+  g->prep_pb.prev_trans = nullptr;
+  g->prep_prm = *prm;
+  g->prepared = true;
+  g->prep = std::thread([g, dev]() {
+    int r = (hipSetDevice(dev) == hipSuccess && hipStreamWaitEvent(g->side, g->ev_in, 0) == hipSuccess) ? OFX_OK
+                                                                                                           : OFX_ERR_HIP;
+    if (r == OFX_OK) r = gn_setup(g, &g->prep_pb, &g->prep_prm, nullptr, (ofx_stream_t)g->side);
+    if (r == OFX_OK && hipEventRecord(g->ev_prep, g->side) != hipSuccess) r = OFX_ERR_HIP;
+    g->prep_status = r;
+  });
+  return OFX_OK;
+}
+
+int ofx_gn_prefetch_stats(void* handle, int64_t* used, int64_t* missed) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && used && missed, "null handle/outputs");
+  *used = g->pf_used;
+  *missed = g->pf_missed;
+  return OFX_OK;
+}
+
+int ofx_gn_prepare_wait(void* handle, ofx_stream_t s) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g, "null handle");
+  prep_wait(g);
+  if (g->prepared && g->prep_status == OFX_OK) OFX_HIP(hipStreamWaitEvent(as_stream(s), g->ev_prep, 0));
+  return OFX_OK;
+}
+
+}  // extern "C"
+
+namespace ofx {
+
+static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, int64_t* nnz_blocks, ofx_stream_t s) {
   OFX_CHECK_ARG(g && pb && prm, "null handle/problem/params");
   OFX_CHECK_ARG(pb->n_nodes >= 1 && pb->n_nodes <= g->max_nodes, "n_nodes %d outside [1,%d]", pb->n_nodes, g->max_nodes);
   OFX_CHECK_ARG(pb->n_matches >= 0 && pb->n_matches <= g->max_matches, "n_matches %d > max %d", pb->n_matches, g->max_matches);
@@ -2275,7 +2391,7 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     g->pat_N = 0;
     g->pat_nnzb = 0;
     g->h_perm.clear();
-    return ofx_gn_setup(handle, pb, prm, nnz_blocks, s);
+    return gn_setup(g, pb, prm, nnz_blocks, s);
   }
   g->max_deg = lens[0];
   g->max_wave = lens[1];
@@ -2316,9 +2432,14 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   return OFX_OK;
 }
 
+}  // namespace ofx
+
+extern "C" {
+
 int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int32_t add_reg, double* A, double* rhs,
                      ofx_stream_t s) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && g->setup_done, "gn_setup not called");
   OFX_CHECK_ARG(A && rhs, "null A/rhs");
   OFX_CHECK_ARG(m0 >= 0 && m1 <= g->M && m0 <= m1, "bad match range [%d,%d) of %d", m0, m1, g->M);
@@ -2345,6 +2466,7 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
 
 int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_stream_t s) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && g->setup_done, "gn_setup not called");
   OFX_CHECK_ARG(A && rhs, "null A/rhs");
   hipStream_t hs = as_stream(s);
@@ -2361,6 +2483,7 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
 
 int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s) {
   Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && g->setup_done && res && res->rot && res->trans, "bad gn_finish args");
   int n_log = g->prm.num_iter;
   int64_t n = g->N > 4 * n_log ? g->N : 4 * n_log;
@@ -2373,9 +2496,27 @@ int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s) {
 int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* prm, const ofx_gn_result* res,
                  ofx_stream_t s) {
   Gn* g = (Gn*)handle;
-  int64_t nnz = 0;
-  int st = ofx_gn_setup(handle, pb, prm, &nnz, s);
-  if (st) return st;
+  OFX_CHECK_ARG(g && pb && prm && res, "null handle/problem/params/result");
+  prep_wait(g);
+  // a setup prefetched for exactly this problem (ofx_gn_prepare): wait for it on the caller's stream and load
+  // the pose; otherwise (none, another problem, or it failed) set up here
+  const bool use = g->prepared && g->prep_status == OFX_OK && same_problem(g->prep_pb, *pb) &&
+                   same_params(g->prep_prm, *prm);
+  if (g->prepared) ++(use ? g->pf_used : g->pf_missed);
+  g->prepared = false;
+  g->prep_status = OFX_OK;
+  int st = OFX_OK;
+  if (use) {
+    hipStream_t hs = as_stream(s);
+    OFX_HIP(hipStreamWaitEvent(hs, g->ev_prep, 0));
+    if (pb->prev_rot || pb->prev_trans)
+      hipLaunchKernelGGL(k_pose, dim3(grid_for(9 * (int64_t)g->N, 256)), dim3(256), 0, hs, *g, pb->prev_rot,
+                         pb->prev_trans);
+    OFX_LAUNCH_CHECK();
+  } else {
+    st = gn_setup(g, pb, prm, nullptr, s);
+    if (st) return st;
+  }
   for (int it = 0; it < prm->num_iter; ++it) {
     st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, s);
     if (st) return st;

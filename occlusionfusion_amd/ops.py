@@ -249,6 +249,23 @@ def _(state, handle, nodes, edges, edge_weights, tpos, conf, src, anchors, weigh
             nodes.new_empty((int(iparams[0]), 4), dtype=torch.float64))
 
 
+@_op("gn_prepare", mutates_args=("state",))
+def gn_prepare(state: Tensor, handle: int, nodes: Tensor, edges: Tensor, edge_weights: Tensor, tpos: Tensor,
+               conf: Tensor, src: Tensor, anchors: Tensor, weights: Tensor, tgt: Tensor, target_px: Optional[Tensor],
+               target_py: Optional[Tensor], intr: List[float], fparams: List[float], iparams: List[int]) -> None:
+    """ofx_gn_prepare: prefetch the setup of the next gn_solve on this handle (host thread + the handle's own
+    stream, ordered after the current stream's work); returns at once. The tensors must stay alive and
+    unchanged until that solve."""
+    pb = _gn_problem(nodes, edges, edge_weights, tpos, conf, src, anchors, weights, tgt, target_px, target_py,
+                     None, None, intr)
+    call("ofx_gn_prepare", _lib.c_void_p(handle), byref(pb), byref(_gn_params(fparams, iparams)), _stream(nodes))
+
+
+@gn_prepare.register_fake
+def _(state, handle, nodes, *rest):
+    return None
+
+
 @_op("gn_setup", mutates_args=("state",))
 def gn_setup(state: Tensor, handle: int, nodes: Tensor, edges: Tensor, edge_weights: Tensor, tpos: Tensor,
              conf: Tensor, src: Tensor, anchors: Tensor, weights: Tensor, tgt: Tensor, target_px: Optional[Tensor],
@@ -312,4 +329,5 @@ def _(state, handle, n_nodes, num_iter):
             state.new_empty((4,), dtype=torch.int32), state.new_empty((num_iter, 4), dtype=torch.float64))
 
 
-OPS = ("integrate", "integrate_points", "raycast", "skin_points", "deform_points", "gn_solve", "gn_setup", "gn_linearize", "gn_step", "gn_finish")
+OPS = ("integrate", "integrate_points", "raycast", "skin_points", "deform_points", "gn_solve", "gn_prepare", "gn_setup",
+       "gn_linearize", "gn_step", "gn_finish")

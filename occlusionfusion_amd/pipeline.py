@@ -65,10 +65,17 @@ class FusionPipeline:
         self.vol.integrate({"im": fi.im, "id": 0})
         self.wf.skin_tsdf_cache()
 
-    def solve(self, fi):
+    def problem(self, fi):
+        """Frame fi's GN problem as GaussNewtonSolver.optimize(prefetch=) takes it."""
+        return dict(graph_nodes=self.nodes_t, graph_edges=self.edges_t, graph_edges_weights=self.ew_t,
+                    target_node_position=fi.tpos, node_confidence=fi.conf, source_points=fi.src, anchors=fi.anchors,
+                    weights=fi.weights, target_points=fi.tgt)
+
+    def solve(self, fi, next_fi=None):
+        """GN solve of frame fi; next_fi: the next frame, whose solver setup is prefetched concurrently."""
         out = self.solver.optimize(self.nodes_t, self.edges_t, self.ew_t, fi.tpos, fi.conf, fi.src, fi.anchors,
                                    fi.weights, fi.tgt, self.intr, prev_rot=self.prev_rot, prev_trans=self.prev_trans,
-                                   sync=False)
+                                   sync=False, prefetch=None if next_fi is None else self.problem(next_fi))
         self.prev_rot, self.prev_trans = out["node_rotations"], out["node_translations"]
         return out
 
@@ -78,7 +85,7 @@ class FusionPipeline:
         self.vol.update(fi.im, t)
         self.vol.integrate_device(count_updates=count_updates)
 
-    def step(self, fi, t, count_updates=False):
-        self.last = self.solve(fi)
+    def step(self, fi, t, count_updates=False, next_fi=None):
+        self.last = self.solve(fi, next_fi)
         self.integrate(fi, t, count_updates)
         return self.last

@@ -43,27 +43,56 @@ class GaussNewtonSolver:
         self.params = dict(GN_DEFAULTS)
         self.params.update(params)
         self.max_nodes, self.max_matches = int(max_nodes), int(max_matches)
+        self._keep = []
+        # solver slots (handle, ordering token): a second one is made by the first prefetch (optimize(prefetch=)),
+        # which sets up the next problem on the slot the current solve does not use
+        self._slots = [self._new_slot()]
+        self._cur = 0                   # slot of the next optimize()
+        self._pending = [None, None]    # a prefetched problem's tensors, alive until its solve
+        self._side = None               # torch stream that orders a prefetch before the current solve
+        self._h, self._state = self._slots[0]   # the last solve's slot (info / stats / stopped / arap / distributed)
+
+    def _new_slot(self):
         h = _lib.c_void_p()
         with torch.cuda.device(self.device):
             call("ofx_gn_create", self.max_nodes, self.max_matches, byref(h))
-        self._h = h
-        self._keep = []
-        self._state = torch.zeros(1, dtype=torch.int32, device=self.device)   # ofx::gn_* ordering token (ops.py)
+        return h, torch.zeros(1, dtype=torch.int32, device=self.device)   # ofx::gn_* ordering token (ops.py)
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            try:
-                _lib.lib.ofx_gn_destroy(h)
-            except Exception:
-                pass
-            self._h = None
+        for h, _ in getattr(self, "_slots", []):
+            if h is not None and h.value:
+                try:
+                    _lib.lib.ofx_gn_destroy(h)
+                except Exception:
+                    pass
+        self._slots = []
+        self._h = None
 
     def timing(self, enable=True):
-        """(pcg_ms, k_pcg_iter launches, timed PCG solves) recorded since the last call; then (re)arm."""
-        ms, n, ns = _lib.c_double(), _lib.c_int64(), _lib.c_int64()
-        call("ofx_gn_timing", self._h, 1 if enable else 0, byref(ms), byref(n), byref(ns))
-        return ms.value, n.value, ns.value
+        """(pcg_ms, k_pcg_iter launches, timed PCG solves) recorded since the last call over all slots; then
+        (re)arm."""
+        tot = [0.0, 0, 0]
+        for h, _ in self._slots:
+            ms, n, ns = _lib.c_double(), _lib.c_int64(), _lib.c_int64()
+            call("ofx_gn_timing", h, 1 if enable else 0, byref(ms), byref(n), byref(ns))
+            tot = [tot[0] + ms.value, tot[1] + n.value, tot[2] + ns.value]
+        return tuple(tot)
+
+    def prefetch_stats(self):
+        """(solves that used a prefetched setup, solves that discarded one) over all slots."""
+        used = missed = 0
+        for h, _ in self._slots:
+            u, m = _lib.c_int64(), _lib.c_int64()
+            call("ofx_gn_prefetch_stats", h, byref(u), byref(m))
+            used, missed = used + u.value, missed + m.value
+        return used, missed
+
+    def drain(self):
+        """Order the current stream after any prefetched setup still in flight (ofx_gn_prepare_wait): a
+        synchronisation afterwards covers it."""
+        s = _lib.stream_ptr(torch.cuda.current_stream(self.device))
+        for h, _ in self._slots:
+            call("ofx_gn_prepare_wait", h, s)
 
     def info(self):
         """[n_nodes, n_matches, JᵀJ block count, residual terms, PCG rows] of the last solve's setup."""
@@ -108,7 +137,7 @@ class GaussNewtonSolver:
 
     def _problem(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
                  source_points, anchors, weights, target_points, intrinsics, target_px, target_py, prev_rot,
-                 prev_trans):
+                 prev_trans, keep=True):
         """Device tensors of one problem in the ofx::gn_* operators' argument order (+ N, M)."""
         d = self.device
         nodes = _t(graph_nodes, d, torch.float32).reshape(-1, 3)
@@ -127,7 +156,8 @@ class GaussNewtonSolver:
                 _t(target_points, d, torch.float32).reshape(M, 3), _t(target_px, d, torch.float32),
                 _t(target_py, d, torch.float32), _t(prev_rot, d, torch.float32), _t(prev_trans, d, torch.float32),
                 [float(v) for v in np.asarray(intrinsics, np.float64).reshape(-1)[:4]]]
-        self._keep = args   # the last problem's inputs (arap reads prev_trans back)
+        if keep:
+            self._keep = args   # the last problem's inputs (arap reads prev_trans back)
         return args, N, M
 
     @staticmethod
@@ -147,14 +177,49 @@ class GaussNewtonSolver:
 
     def optimize(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
                  source_points, anchors, weights, target_points, intrinsics, target_px=None, target_py=None,
-                 prev_rot=None, prev_trans=None, sync=True):
+                 prev_rot=None, prev_trans=None, sync=True, prefetch=None):
         """model.py:222-859 (batch item) through torch.ops.ofx.gn_solve. Returns torch device tensors (+ host
-        convergence info if sync)."""
+        convergence info if sync).
+
+        prefetch: the NEXT frame's problem as a dict of this method's argument names (graph_nodes ...
+        target_points, optional target_px / target_py; intrinsics default to this call's; no pose). Its setup
+        (upload, JᵀJ pattern, with the setup's host sync) is started on the other solver slot when this solve's
+        host loop returns, ordered before this solve, and runs concurrently with this frame's tail
+        (torch.ops.ofx.gn_prepare); the next optimize() with that problem (the same device tensors) then skips
+        its setup. The prefetched tensors must not change until
+        that call."""
         args, N, M = self._problem(graph_nodes, graph_edges, graph_edges_weights, target_node_position,
                                    node_confidence, source_points, anchors, weights, target_points, intrinsics,
                                    target_px, target_py, prev_rot, prev_trans)
         fp, ip = self._plist()
-        out = torch.ops.ofx.gn_solve(self._state, self._h.value, *args, fp, ip)
+        cur = self._cur
+        h, st = self._slots[cur]
+        if prefetch is not None:
+            # the prefetch is ordered after the work enqueued so far (its inputs, the other slot's last solve)
+            # but not after this solve: it is started when this solve's host loop returns, so its kernels
+            # overlap this frame's tail (the drained PCG launches, the integrate) instead of the PCG chain
+            before = torch.cuda.Event()
+            before.record()
+        out = torch.ops.ofx.gn_solve(st, h.value, *args, fp, ip)
+        self._pending[cur] = None
+        self._h, self._state = h, st
+        if prefetch is not None:
+            nxt = 1 - cur
+            if len(self._slots) < 2:
+                self._slots.append(self._new_slot())
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            q = dict(prefetch)
+            pa, _, _ = self._problem(q["graph_nodes"], q["graph_edges"], q["graph_edges_weights"],
+                                     q["target_node_position"], q["node_confidence"], q["source_points"],
+                                     q["anchors"], q["weights"], q["target_points"], q.get("intrinsics", intrinsics),
+                                     q.get("target_px"), q.get("target_py"), None, None, keep=False)
+            h1, st1 = self._slots[nxt]
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(before)
+                torch.ops.ofx.gn_prepare(st1, h1.value, *pa[:11], pa[13], fp, ip)
+            self._pending[nxt] = pa
+            self._cur = nxt
         return self._pack(out, sync)
 
     def arap(self, graph_nodes, source_node_position, target_node_position, valid_nodes_mask, original_graph_nodes,

@@ -37,6 +37,8 @@
 #include <string.h>
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <type_traits>
 #include <utility>
@@ -143,7 +145,11 @@ struct Gn : GnDev {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // timing events of the PCG loops
   // prefetched setup (ofx_gn_prepare): the next problem's setup runs on a host thread, on the handle's own
   // stream, while the caller's stream still works on the current problem (of another handle)
-  std::thread prep;
+  std::thread worker;               // persistent (created by the first prefetch): no per-frame thread start
+  std::mutex mu;
+  std::condition_variable cv;
+  bool job = false, quit = false;   // guarded by mu: a prefetch is queued / running; shut down
+  int prep_dev = 0;
   int prep_status = 0;
   bool prepared = false;            // the setup of prep_pb / prep_prm is (being) enqueued on `side`
   ofx_gn_problem prep_pb{};
@@ -1981,9 +1987,28 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
 
 static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, int64_t* nnz_blocks, ofx_stream_t s);
 
-// the prefetch thread of this handle has finished enqueuing (its status stays in prep_status)
+// the prefetch worker of this handle has finished enqueuing the queued setup (its status is in prep_status)
 static void prep_wait(Gn* g) {
-  if (g->prep.joinable()) g->prep.join();
+  if (!g->worker.joinable()) return;
+  std::unique_lock<std::mutex> lk(g->mu);
+  g->cv.wait(lk, [g] { return !g->job; });
+}
+
+static void prep_worker(Gn* g) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  for (;;) {
+    g->cv.wait(lk, [g] { return g->job || g->quit; });
+    if (g->quit) return;
+    lk.unlock();
+    int r = (hipSetDevice(g->prep_dev) == hipSuccess && hipStreamWaitEvent(g->side, g->ev_in, 0) == hipSuccess)
+                ? OFX_OK : OFX_ERR_HIP;
+    if (r == OFX_OK) r = gn_setup(g, &g->prep_pb, &g->prep_prm, nullptr, (ofx_stream_t)g->side);
+    if (r == OFX_OK && hipEventRecord(g->ev_prep, g->side) != hipSuccess) r = OFX_ERR_HIP;
+    lk.lock();
+    g->prep_status = r;
+    g->job = false;
+    g->cv.notify_all();
+  }
 }
 
 static bool same_problem(const ofx_gn_problem& a, const ofx_gn_problem& b) {   // all but the pose
@@ -2146,6 +2171,14 @@ int ofx_gn_destroy(void* handle) {
   if (!handle) return OFX_OK;
   Gn* g = (Gn*)handle;
   prep_wait(g);
+  if (g->worker.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      g->quit = true;
+    }
+    g->cv.notify_all();
+    g->worker.join();
+  }
   (void)hipDeviceSynchronize();
   if (g->side) (void)hipStreamDestroy(g->side);
   if (g->ev_in) (void)hipEventDestroy(g->ev_in);
@@ -2176,8 +2209,7 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
     OFX_HIP(hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming));
     OFX_HIP(hipEventCreateWithFlags(&g->ev_prep, hipEventDisableTiming));
   }
-  int dev = 0;
-  OFX_HIP(hipGetDevice(&dev));
+  OFX_HIP(hipGetDevice(&g->prep_dev));
   // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve)
   // comes before the prefetched setup
   OFX_HIP(hipEventRecord(g->ev_in, as_stream(s)));
@@ -2186,13 +2218,12 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
   g->prep_pb.prev_trans = nullptr;
   g->prep_prm = *prm;
   g->prepared = true;
-  g->prep = std::thread([g, dev]() {
-    int r = (hipSetDevice(dev) == hipSuccess && hipStreamWaitEvent(g->side, g->ev_in, 0) == hipSuccess) ? OFX_OK
-                                                                                                           : OFX_ERR_HIP;
-    if (r == OFX_OK) r = gn_setup(g, &g->prep_pb, &g->prep_prm, nullptr, (ofx_stream_t)g->side);
-    if (r == OFX_OK && hipEventRecord(g->ev_prep, g->side) != hipSuccess) r = OFX_ERR_HIP;
-    g->prep_status = r;
-  });
+  if (!g->worker.joinable()) g->worker = std::thread(prep_worker, g);
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->job = true;
+  }
+  g->cv.notify_all();
   return OFX_OK;
 }
 

@@ -456,6 +456,10 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* prob, const ofx_gn_params
 /* Wait (host) until a prefetch on this handle has been enqueued, and order stream `s` after it: a
  * synchronisation of `s` afterwards covers the prefetched setup. */
 int ofx_gn_prepare_wait(void* handle, ofx_stream_t s);
+/* Make `handle` use `other`'s per-GN-step PCG iteration history (it sizes the first chunk of iteration
+ * launches; results do not depend on it): the solver slots of one frame loop then predict from the previous
+ * frame whichever slot solved it. */
+int ofx_gn_share_history(void* handle, void* other);
 /* Solves on this handle that used a prefetched setup / discarded one (a different problem or a failure). */
 int ofx_gn_prefetch_stats(void* handle, int64_t* used, int64_t* missed);
 

@@ -37,7 +37,9 @@
 #include <string.h>
 #include <algorithm>
 #include <chrono>
+#include <array>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <type_traits>
@@ -130,7 +132,6 @@ struct GnDev {
   hipEvent_t poll_ev = nullptr;   // recorded after each chunk of PCG launches
   double host_enqueue_us = 0.0;   // tuning build: host time spent enqueuing PCG iterations
   int64_t host_enqueued = 0;
-  int last_pcg[64] = {0};   // converged PCG iteration count of the previous solve, per GN step
   bool setup_done = false;
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
   bool timing = false;
@@ -143,6 +144,9 @@ struct Gn : GnDev {
   std::vector<float> h_nodes;          // host copy of the graph the current order was built from
   std::vector<int32_t> h_edges, h_perm;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // timing events of the PCG loops
+  // converged PCG iteration count of the previous solve, per GN step (sizes the first chunk of launches);
+  // shared by the solver slots of one frame loop (ofx_gn_share_history)
+  std::shared_ptr<std::array<int, 64>> last_pcg = std::make_shared<std::array<int, 64>>();
   // prefetched setup (ofx_gn_prepare): the next problem's setup runs on a host thread, on the handle's own
   // stream, while the caller's stream still works on the current problem (of another handle)
   std::thread worker;               // persistent (created by the first prefetch): no per-frame thread start
@@ -1923,7 +1927,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // covers the previous frame's count for this GN step plus a small margin. (A hipGraph replay of
   // parity-pair chunks was measured: no gain over plain launches for this kernel.)
   const int max_it = g->prm.pcg_max_iter;
-  const int lp = g->last_pcg[gn_iter & 63];
+  const int lp = (*g->last_pcg)[gn_iter & 63];
   const dim3 grid(g->nwg_row), block(64);
   // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width for up to 384 / 2176 waves
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
@@ -1938,7 +1942,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
   // spins on it, so the next GN step is enqueued while the chunk's remaining (no-op) launches drain.
-  // The chunk event only tells "all launched iterations ran without converging" -> launch more.
+  // The chunk event only tells "all launched iterations ran without converging" -> launch more. (Measured
+  // and dropped: a first chunk of exactly the previous count, topped up by 4 from a marker event 3 launches
+  // before each chunk's end — 690.5 instead of 694.3 launches per frame, but 5.15 instead of 5.06-5.12 us per
+  // launch with the marker in the stream: -0.5 %, A/B x3.)
   volatile int32_t* hf = g->host_flags;
   hf[H_DONE] = 0;   // the previous step's converged launch has run (we saw it); prep also clears it
   PcgIt pa = pcg_args(g);
@@ -1973,7 +1980,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     if (hf[H_STOPPED]) break;
     if (hf[H_DONE]) {
-      g->last_pcg[gn_iter & 63] = hf[H_PCG_IT];
+      (*g->last_pcg)[gn_iter & 63] = hf[H_PCG_IT];
       g->step_fused = pa.fuse != 0;
       break;
     }
@@ -2224,6 +2231,14 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
     g->job = true;
   }
   g->cv.notify_all();
+  return OFX_OK;
+}
+
+int ofx_gn_share_history(void* handle, void* other) {
+  Gn* g = (Gn*)handle;
+  Gn* o = (Gn*)other;
+  OFX_CHECK_ARG(g && o, "null handle");
+  g->last_pcg = o->last_pcg;
   return OFX_OK;
 }
 

@@ -207,6 +207,7 @@ class GaussNewtonSolver:
             nxt = 1 - cur
             if len(self._slots) < 2:
                 self._slots.append(self._new_slot())
+                call("ofx_gn_share_history", self._slots[1][0], self._slots[0][0])
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
             q = dict(prefetch)

@@ -410,8 +410,9 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
  * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
 int ofx_gn_info(void* handle, int64_t* info);
-/* Waves per PCG cluster workgroup of k_pcg_iter chosen at create: 2 (default) or 1 (environment
- * OFX_PCG_W1 set to anything but "" / "0"; tuning and A/B only). */
+/* Waves per PCG cluster workgroup of k_pcg_iter for the last setup (before any: for a small problem): 2 up to
+ * 384 clusters (default) or 1 (environment OFX_PCG_W1 set to anything but "" / "0" at create; tuning and A/B
+ * only); larger problems always run one wave per cluster. */
 int ofx_gn_pcg_waves(void* handle, int32_t* waves);
 /* The solve's stop flag as the host sees it (host-mapped, no synchronisation): 1 once a GN step's loss rule
  * (model.py:726-732) or an ill-posed solve stopped it. After ofx_gn_step(i + 1) returns it reflects step i's

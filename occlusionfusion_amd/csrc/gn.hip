@@ -109,7 +109,7 @@ struct GnDev {
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
   int32_t nw_pad = 0;            // stride of the iteration partial streams: 128·pcg_ku, zero beyond nwg_row
   int32_t pcg_w2 = 1;            // two waves per cluster in k_pcg_iter (OFX_PCG_W1=1: one)
-  int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (3: <= 384 waves, else 17)
+  int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (pcg_ku_for)
   double* scal = nullptr;
   int32_t* flags = nullptr;
   // DeformNet.arap mode with lambda_flow = 0: rows of each multi-node connected graph component
@@ -1897,6 +1897,37 @@ static void order_rows(int N, int NB, const float* nodes, const int32_t* edges, 
   }
 }
 
+// Partial pairs per lane and stream of k_pcg_iter for a cluster (wave) count: the streams are 2·64·kU wide, so
+// fewer loads and adds per lane for fewer clusters (3: <= 384, 4: <= 512, 8: <= 1024, 17: <= 2176 clusters).
+// OFX_PCG_KU=<3|4|8|17> forces one (A/B; it must still cover the count).
+static int pcg_ku_for(int waves) {
+  int ku = waves <= 384 ? 3 : waves <= 512 ? 4 : waves <= 1024 ? 8 : 17;
+  if (const char* e = getenv("OFX_PCG_KU")) {
+    const int f = atoi(e);
+    if ((f == 3 || f == 4 || f == 8 || f == 17) && 128 * f >= waves) ku = f;
+  }
+  return ku;
+}
+
+using PcgKernel = void (*)(PcgIt, int);
+template <int KU>
+static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
+  if constexpr (KU == 3) {
+    if (wave && w2) {
+      first = k_pcg_iter<true, true, 3, true>;
+      rest = k_pcg_iter<true, false, 3, true>;
+      return;
+    }
+  }
+  if (wave) {
+    first = k_pcg_iter<true, true, KU>;
+    rest = k_pcg_iter<true, false, KU>;
+  } else {
+    first = k_pcg_iter<false, true, KU>;
+    rest = k_pcg_iter<false, false, KU>;
+  }
+}
+
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
   g->warm_now = 0;
@@ -1929,16 +1960,20 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const int max_it = g->prm.pcg_max_iter;
   const int lp = (*g->last_pcg)[gn_iter & 63];
   const dim3 grid(g->nwg_row), block(64);
-  // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width for up to 384 / 2176 waves
+  // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width kU for the cluster count (pcg_ku_for);
+  // two waves per cluster only up to 384 clusters (kU = 3): config 4's 490 clusters ran 5.38 us per launch
+  // with one wave and kU = 4, 5.58 with two; kU = 8: 5.66 vs 5.91; kU = 17: 6.35 vs 6.93 (A/B, 1278.9
+  // iterations per frame; one wave per cluster and kU = 17 was the round-1 form for > 384 clusters: 95 vs 111
+  // frames/s)
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
-  const bool small = g->pcg_ku == 3;
-  auto iter0 = wave ? (small ? k_pcg_iter<true, true, 3> : k_pcg_iter<true, true, 17>)
-                    : (small ? k_pcg_iter<false, true, 3> : k_pcg_iter<false, true, 17>);
-  auto iter = wave ? (small ? k_pcg_iter<true, false, 3> : k_pcg_iter<true, false, 17>)
-                   : (small ? k_pcg_iter<false, false, 3> : k_pcg_iter<false, false, 17>);
-  // two waves per cluster (wave-list SpMV, up to 384 waves)
-  const bool w2 = wave && small && g->pcg_w2;
-  if (w2) { iter0 = k_pcg_iter<true, true, 3, true>; iter = k_pcg_iter<true, false, 3, true>; }
+  const bool w2 = wave && g->pcg_w2 && g->pcg_ku == 3;
+  PcgKernel iter0 = nullptr, iter = nullptr;
+  switch (g->pcg_ku) {
+    case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
+    case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
+    case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
+    default: pcg_pick<17>(wave, w2, iter0, iter); break;
+  }
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
   // spins on it, so the next GN step is enqueued while the chunk's remaining (no-op) launches drain.
@@ -2134,7 +2169,7 @@ int ofx_gn_stopped(void* handle, int32_t* stopped) {
 int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && waves, "null handle/waves");
-  *waves = g->pcg_w2 ? 2 : 1;
+  *waves = (g->pcg_w2 && g->pcg_ku == 3) ? 2 : 1;   // the last setup's form (two only up to 384 clusters)
   return OFX_OK;
 }
 
@@ -2376,7 +2411,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
   g->nwg_row = N / kRW;
-  g->pcg_ku = g->nwg_row <= 2 * 64 * 3 ? 3 : 17;
+  g->pcg_ku = pcg_ku_for(g->nwg_row);
   g->nw_pad = 128 * g->pcg_ku;
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);

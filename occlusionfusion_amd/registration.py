@@ -107,7 +107,8 @@ class GaussNewtonSolver:
         return bool(f.value)
 
     def pcg_waves(self):
-        """Waves per cluster workgroup of the PCG iteration kernel (2, or 1 under OFX_PCG_W1=1)."""
+        """Waves per cluster workgroup of the PCG iteration kernel in the last setup (2 up to 384 clusters, else 1;
+        1 under OFX_PCG_W1=1)."""
         w = ctypes.c_int32()
         call("ofx_gn_pcg_waves", self._h, byref(w))
         return w.value

@@ -33,6 +33,8 @@ def _t(x, device, dtype):
     if x is None:
         return None
     if isinstance(x, torch.Tensor):
+        if x.dtype == dtype and x.device == device and x.is_contiguous():
+            return x   # per-frame fast path (host time: no .to / .contiguous dispatch)
         return x.to(device=device, dtype=dtype).contiguous()
     return torch.as_tensor(np.ascontiguousarray(x), device=device).to(dtype).contiguous()
 

@@ -209,7 +209,7 @@ def main():
         e1.record()
         pipe.integrate(frames[t], t, count_updates=True)
         e2.record()
-        upd.append(pipe.vol.n_updated[:cache.n_list].sum())   # device-side sum, read after timing
+        upd.append(pipe.vol.n_updated[:cache.n_list].sum(dtype=torch.int32))   # one device reduce, read after timing
         marks.append((e0, e1, e2, out))
     pipe.solver.drain()   # the last step's prefetched setup (of a frame not timed) counts inside the region
     torch.cuda.synchronize()

@@ -1009,6 +1009,53 @@ __device__ __forceinline__ void row_spmv(const G& g, int b0, int b1, int q, cons
 #pragma unroll
   for (int i = 0; i < 6; ++i) n[i] = slot_sum(n[i]);
 }
+// row_spmv with the first two slots' blocks and gathers issued together (two dependent trips for rows of
+// <= 2·kSL blocks), the same accumulation order
+template <class G>
+__device__ __forceinline__ void row_spmv_2(const G& g, int b0, int b1, int q, const double* __restrict__ v,
+                                           double n[6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) n[i] = 0.0;
+  const int bi0 = b0 + q, bi1 = bi0 + kSL;
+  const bool ok0 = bi0 < b1, ok1 = bi1 < b1;
+  const int e[2] = {ok0 ? bi0 : 0, ok1 ? bi1 : 0};
+  double x[2][6];
+  double2 bb[2][18];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e[h]);
+    const double2* vc = reinterpret_cast<const double2*>(v + 6 * (int64_t)g.col[e[h]]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { const double2 t = vc[j]; x[h][2 * j] = t.x; x[h][2 * j + 1] = t.y; }
+#pragma unroll
+    for (int k = 0; k < 18; ++k) bb[h][k] = blk[k];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 0 ? ok0 : ok1) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double2 b01 = bb[h][3 * i], b23 = bb[h][3 * i + 1], b45 = bb[h][3 * i + 2];
+        n[i] += ((b01.x * x[h][0] + b01.y * x[h][1]) + (b23.x * x[h][2] + b23.y * x[h][3])) +
+                (b45.x * x[h][4] + b45.y * x[h][5]);
+      }
+    }
+  }
+  for (int bi = b0 + q + 2 * kSL; bi < b1; bi += kSL) {
+    const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)bi);
+    const double2* vc = reinterpret_cast<const double2*>(v + 6 * (int64_t)g.col[bi]);
+    double xx[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { const double2 t = vc[j]; xx[2 * j] = t.x; xx[2 * j + 1] = t.y; }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double2 b01 = blk[3 * i], b23 = blk[3 * i + 1], b45 = blk[3 * i + 2];
+      n[i] += ((b01.x * xx[0] + b01.y * xx[1]) + (b23.x * xx[2] + b23.y * xx[3])) + (b45.x * xx[4] + b45.y * xx[5]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) n[i] = slot_sum(n[i]);
+}
 __device__ __forceinline__ void load_rec(const double* __restrict__ st, int64_t o, double v[V_N]) {
   const double2* p = reinterpret_cast<const double2*>(st + V_N * o);
 #pragma unroll
@@ -1138,14 +1185,32 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
 constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
 __device__ __forceinline__ constexpr int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
 
+// t_j += A_blk x_j (block bk, gathered history rows x) for the stored solutions j < np, in the loop's order
+__device__ __forceinline__ void proj_accumulate(const double bk[36], const double x[kProj][6], int np,
+                                                double n[kProj][6]) {
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) {
+    if (j < np) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) t += bk[6 * i + k] * x[j][k];
+        n[j][i] += t;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restrict__ rhs) {
+  const int lane = threadIdx.x;
+  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
+  const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];   // issued with the stop flag: one trip
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {   // PCG bookkeeping of this GN step (also in k_pcg_prep)
     g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
     host_flag(g.hflags, H_DONE, 0);
   }
-  const int lane = threadIdx.x;
-  const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int np = g.n_prev;
   const int64_t stride = 6 * (int64_t)g.N;
   double n[kProj][6];
@@ -1153,8 +1218,24 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
   for (int j = 0; j < kProj; ++j)
 #pragma unroll
     for (int i = 0; i < 6; ++i) n[j][i] = 0.0;
-  const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-  for (int bi = b0 + q; bi < b1; bi += kSL) {
+  {   // the first two slots' blocks, then all their history gathers, issued together (rows of <= 2·kSL blocks:
+      // two dependent trips instead of four); unconditional loads (clamped entry, every history row exists)
+    const int bi0 = b0 + q, bi1 = bi0 + kSL;
+    const bool ok0 = bi0 < b1, ok1 = bi1 < b1;
+    const int e0 = ok0 ? bi0 : 0, e1 = ok1 ? bi1 : 0;
+    const int64_t cc0 = 6 * (int64_t)g.col[e0], cc1 = 6 * (int64_t)g.col[e1];
+    double bk0[36], bk1[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) { bk0[k] = g.Aop[36 * (int64_t)e0 + k]; bk1[k] = g.Aop[36 * (int64_t)e1 + k]; }
+    double x0[kProj][6], x1[kProj][6];
+#pragma unroll
+    for (int j = 0; j < kProj; ++j)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { x0[j][k] = g.xh[j * stride + cc0 + k]; x1[j][k] = g.xh[j * stride + cc1 + k]; }
+    if (ok0) proj_accumulate(bk0, x0, np, n);
+    if (ok1) proj_accumulate(bk1, x1, np, n);
+  }
+  for (int bi = b0 + q + 2 * kSL; bi < b1; bi += kSL) {
     const double* blk = g.Aop + 36 * (int64_t)bi;
     const int64_t cc = 6 * (int64_t)g.col[bi];
     double bk[36];
@@ -1297,11 +1378,12 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restr
 __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict__ rhs) {
   __shared__ double s_v[kCD];
   const int lane = threadIdx.x;
+  const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
+  const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];   // issued with the stop flag: one trip
   if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
     g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
     return;
   }
-  const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const bool own = q < 6;
   const int64_t o = 6 * (int64_t)row + q;
   float4 mr[kCD / 4];
@@ -1309,7 +1391,7 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
   double b = 0.0;
   if (own) { load_mrow(g, o, mr); load_rec(g.st, o, v); b = rhs[o]; }
   double n[6];
-  row_spmv(g, g.row_ptr[row], g.row_ptr[row + 1], q, g.m1, n);
+  row_spmv_2(g, rb0, rb1, q, g.m1, n);
   const double w = pick6(n, q);
   if (own) s_v[6 * r + q] = w;
   __syncthreads();

@@ -1296,18 +1296,28 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
 __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restrict__ rhs) {
   __shared__ double s_v[kCD];
   const int lane = threadIdx.x;
-  if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
-    g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
-    return;
-  }
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const int np = g.n_prev;
   const bool own = q < 6;
   const int64_t o = 6 * (int64_t)row + q;
+  const int64_t oc = 6 * (int64_t)row + (own ? q : 5);   // every lane loads (clamped): one memory trip in all
+  const int64_t stride = 6 * (int64_t)g.N;
   float4 mr[kCD / 4];
-  if (own) load_mrow(g, o, mr);
+  load_mrow(g, oc, mr);
+  const double rb = rhs[oc];
+  double xo[kProj], to[kProj];
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) { xo[j] = g.xh[j * stride + oc]; to[j] = g.th[j * stride + oc]; }
+  double pt[kProjP][8];
+  load_streams<kProjP, 8>(g.part_p, g.nwg_row, pt);
+  const int stopped = g.flags[F_STOPPED];
+  asm volatile("" ::: "memory");   // keep the loads above the exit test (one trip with the flag)
+  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
+    return;
+  }
   double p[kProjP];
-  sum_streams<kProjP, 8>(g.part_p, g.nwg_row, p);
+  reduce_streams<kProjP, 8>(g.part_p, g.nwg_row, pt, p);
   // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
   double L[kProj][kProj], y[kProj], c[kProj];
   bool use[kProj];
@@ -1355,13 +1365,12 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restr
   bool fin = true;
 #pragma unroll
   for (int j = 0; j < kProj; ++j) fin = fin && isfinite(c[j]);
-  const int64_t stride = 6 * (int64_t)g.N;
   double xv = 0.0, rv = 0.0;
   if (own) {
-    rv = rhs[o];
+    rv = rb;
 #pragma unroll
     for (int j = 0; j < kProj; ++j)
-      if (j < np && fin) { xv += c[j] * g.xh[j * stride + o]; rv -= c[j] * g.th[j * stride + o]; }
+      if (j < np && fin) { xv += c[j] * xo[j]; rv -= c[j] * to[j]; }
     s_v[6 * r + q] = rv;
   }
   __syncthreads();
@@ -1379,17 +1388,23 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
   __shared__ double s_v[kCD];
   const int lane = threadIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
-  const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];   // issued with the stop flag: one trip
-  if (g.flags[F_STOPPED]) {   // the solve already stopped: this step's iteration launches end after trip 1
+  const bool own = q < 6;
+  const int64_t o = 6 * (int64_t)row + q;
+  const int64_t oc = 6 * (int64_t)row + (own ? q : 5);   // every lane loads (clamped)
+  // row bounds, own state, M⁻¹ row and b issued with the stop flag: one trip
+  const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];
+  float4 mr[kCD / 4];
+  double v[V_N];
+  load_mrow(g, oc, mr);
+  load_rec(g.st, oc, v);
+  const double bo = rhs[oc];
+  const int stopped = g.flags[F_STOPPED];
+  asm volatile("" ::: "memory");
+  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
     g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
     return;
   }
-  const bool own = q < 6;
-  const int64_t o = 6 * (int64_t)row + q;
-  float4 mr[kCD / 4];
-  double v[V_N];
-  double b = 0.0;
-  if (own) { load_mrow(g, o, mr); load_rec(g.st, o, v); b = rhs[o]; }
+  const double b = own ? bo : 0.0;
   double n[6];
   row_spmv_2(g, rb0, rb1, q, g.m1, n);
   const double w = pick6(n, q);

@@ -12,9 +12,12 @@ TSDF/weight/colour integrate of the new frame. All inputs are device-resident be
     `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...` running this file,
     started before anything touches the GPU) and exits with its status; under torchrun it checks
     WORLD_SIZE == --gpus.
---config (BASELINE.json configs): 3 (default) 512³ @4 mm, ~2k nodes, non-rigid + occluder; 2 256³ @4 mm,
-    ~1k nodes, rigid sequence; 1 128³ @8 mm, 200 nodes, 320x240 camera; 4 1024³ @2 mm, ~4k nodes;
-    5 = config 3 per GPU in replicas mode (what --gpus N runs by default).
+--config (BASELINE.json configs): 3 (default at --gpus 1) 512³ @4 mm, ~2k nodes, non-rigid + occluder; 2 256³
+    @4 mm, ~1k nodes, rigid sequence; 1 128³ @8 mm, 200 nodes, 320x240 camera; 4 1024³ @2 mm, ~4k nodes;
+    5 (default at --gpus N > 1) = one independent config-3-class scene per GPU in replicas mode: rank 0 runs
+    config 3 itself, rank r its own seeded scene (synthetic.config_scene), so N=1 and rank 0 are the same workload.
+    Every graph is the SURVEY §8(d) depth-mesh graph of the source frame (sample_nodes + 8 geodesic edges, built on
+    the device: synthetic.depth_graph).
 --mode replicas (default, BASELINE config 5): one independent scene per GPU, no collective,
     value = frames of all ranks / max-rank time (weak scaling).
 --mode shard (BASELINE config 4 style): ONE volume, its bricks dealt to ranks by spatial hash bucket
@@ -63,7 +66,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, choices=sorted(CONFIGS), default=3)
+    p.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None)
     p.add_argument("--mode", choices=["replicas", "shard"], default="replicas")
     p.add_argument("--solve", choices=["replicated", "allreduce"], default="replicated",
                    help="shard mode: replicated assembly (no collective) or match-sharded + all-reduce")
@@ -80,6 +83,8 @@ def parse():
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL; gloo for "
                                                    "CPU launch checks and rehearsals with ranks sharing a device)")
     a = p.parse_args()
+    if a.config is None:
+        a.config = 5 if a.gpus > 1 and a.mode == "replicas" else 3
     cfg = dict(CONFIGS[a.config])
     for k in ("dims", "voxel", "nodes"):
         if getattr(a, k) is None:
@@ -119,11 +124,15 @@ def launch_check(a, world, rank):
         x = x * 1.0001
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64)
-    per_rank = [{"rank": rank, "pid": os.getpid(), "elapsed_s": elapsed}]
+    from occlusionfusion_amd.synthetic import config_scene
+    scene, seed = config_scene(a.config, rank if a.mode == "replicas" else 0)   # the workload this rank would run
+    mine = {"rank": rank, "pid": os.getpid(), "elapsed_s": elapsed, "config": a.config, "scene_seed": seed,
+            "scene": {"center": list(scene.center), "radius": scene.radius, "phase": scene.phase}}
+    per_rank = [mine]
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         per_rank = [None] * world
-        dist.all_gather_object(per_rank, {"rank": rank, "pid": os.getpid(), "elapsed_s": elapsed})
+        dist.all_gather_object(per_rank, mine)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "steps": a.steps, "mode": a.mode,
                           "backend": a.backend, "max_elapsed_s": float(el.item()), "per_rank": per_rank}), flush=True)
@@ -160,7 +169,8 @@ def main():
     D = a.dims
     origin = cfg["origin"] if (a.dims, a.voxel) == (cfg["dims"], cfg["voxel"]) else \
         (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
-    seq = S.config_sequence(a.config, a.nodes)
+    seq = S.config_sequence(a.config, a.nodes, rank=rank if a.mode == "replicas" else 0, device=dev)
+    scene_seed = int(seq.seed)
     sharded = a.mode == "shard" and world > 1
     shard = (rank, world, "hash") if sharded else None   # spatial-hash brick buckets (sharding.hash_owner)
     pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)
@@ -248,7 +258,8 @@ def main():
     vol.tsdf_b, vol.weight_b, vol.color_b = keep
     t_kint = kiso_ms * 1e-3 / max(1, kiso_n)
     t_ar = (sum(x.elapsed_time(y) for x, y in ar_events) * 1e-3 / a.steps) if ar_events else 0.0
-    mine = {"rank": rank, "device": local, "ms_per_frame": 1e3 * elapsed / a.steps,
+    mine = {"rank": rank, "device": local, "scene_seed": scene_seed, "nodes": int(seq.nodes.shape[0]),
+            "ms_per_frame": 1e3 * elapsed / a.steps,
             "solve_ms": 1e3 * float(np.mean(t_solve)), "allreduce_ms": 1e3 * t_ar,
             "integrate_ms": 1e3 * float(np.mean(t_int)), "integrate_kernel_us": 1e6 * t_kint_loop,
             "listed_bricks": cache.n_list, "updated_voxels": U, "pcg_iters_per_frame": float(np.mean(pcg))}

@@ -160,8 +160,30 @@ struct Gn : GnDev {
   ofx_gn_params prep_prm{};
   hipStream_t side = nullptr;
   hipEvent_t ev_in = nullptr, ev_prep = nullptr;   // caller's stream at prepare -> side; side's setup done
+  // side-stream work of a prefetch that no caller stream has been ordered after yet: the worker returns before
+  // its last kernels (row assignment, contribution lists, ...) have run, and they write this handle's buffers
+  bool side_dirty = false;
+  hipEvent_t ev_side = nullptr;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
 };
+
+// Order stream hs after everything the prefetch worker enqueued on the handle's side stream (call after
+// prep_wait: the worker has finished enqueuing). Every entry point that touches the handle's buffers on a
+// caller stream does this first, whether or not the prefetched setup is used.
+static int fence_side(Gn* g, hipStream_t hs) {
+  if (!g->side || !g->side_dirty) return OFX_OK;
+  OFX_HIP(hipEventRecord(g->ev_side, g->side));
+  OFX_HIP(hipStreamWaitEvent(hs, g->ev_side, 0));
+  g->side_dirty = false;
+  return OFX_OK;
+}
+// the same for host reads of device buffers (synchronous copies do not order after a non-blocking stream)
+static int sync_side(Gn* g) {
+  if (!g->side || !g->side_dirty) return OFX_OK;
+  OFX_HIP(hipStreamSynchronize(g->side));
+  g->side_dirty = false;
+  return OFX_OK;
+}
 
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
@@ -2283,6 +2305,8 @@ int ofx_gn_stats(void* handle, double* out, int32_t cap) {
   Gn* g = (Gn*)handle;
   if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && out && cap >= 0, "bad gn_stats args");
+  const int ss = sync_side(g);
+  if (ss) return ss;
   int n = cap < kMaxLog ? cap : kMaxLog;
   if (n > 0) OFX_HIP(hipMemcpy(out, g->stat, 3 * (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
   return OFX_OK;
@@ -2331,6 +2355,7 @@ int ofx_gn_destroy(void* handle) {
   if (g->side) (void)hipStreamDestroy(g->side);
   if (g->ev_in) (void)hipEventDestroy(g->ev_in);
   if (g->ev_prep) (void)hipEventDestroy(g->ev_prep);
+  if (g->ev_side) (void)hipEventDestroy(g->ev_side);
   free_all(g);
   delete g;
   return OFX_OK;
@@ -2343,6 +2368,8 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   prep_wait(g);            // an explicit setup replaces a prefetched one
   g->prepared = false;
   g->prep_status = OFX_OK;
+  const int fs = fence_side(g, as_stream(s));   // its side-stream kernels write the buffers this setup reuses
+  if (fs) return fs;
   return gn_setup(g, pb, prm, nnz_blocks, s);
 }
 
@@ -2356,6 +2383,7 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
     OFX_HIP(hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking));
     OFX_HIP(hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming));
     OFX_HIP(hipEventCreateWithFlags(&g->ev_prep, hipEventDisableTiming));
+    OFX_HIP(hipEventCreateWithFlags(&g->ev_side, hipEventDisableTiming));
   }
   OFX_HIP(hipGetDevice(&g->prep_dev));
   // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve)
@@ -2366,6 +2394,7 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
   g->prep_pb.prev_trans = nullptr;
   g->prep_prm = *prm;
   g->prepared = true;
+  g->side_dirty = true;
   if (!g->worker.joinable()) g->worker = std::thread(prep_worker, g);
   {
     std::lock_guard<std::mutex> lk(g->mu);
@@ -2395,8 +2424,7 @@ int ofx_gn_prepare_wait(void* handle, ofx_stream_t s) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g, "null handle");
   prep_wait(g);
-  if (g->prepared && g->prep_status == OFX_OK) OFX_HIP(hipStreamWaitEvent(as_stream(s), g->ev_prep, 0));
-  return OFX_OK;
+  return fence_side(g, as_stream(s));   // all of the prefetch's side-stream work, whatever its status
 }
 
 }  // extern "C"
@@ -2632,6 +2660,8 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   OFX_CHECK_ARG(m0 >= 0 && m1 <= g->M && m0 <= m1, "bad match range [%d,%d) of %d", m0, m1, g->M);
   // A: nnz_blocks x 36 f64, rhs: 6·rows + 4 f64 (rows = ofx_gn_info()[4])
   hipStream_t hs = as_stream(s);
+  const int fs = fence_side(g, hs);
+  if (fs) return fs;
   DataCoef dc;
   dc.lf = sqrt(g->prm.lambda_flow); dc.ld = sqrt(g->prm.lambda_depth);
   dc.la = sqrt(g->prm.lambda_arap); dc.lm = sqrt(g->prm.lambda_motion);
@@ -2657,6 +2687,8 @@ int ofx_gn_step(void* handle, int32_t gn_iter, double* A, double* rhs, ofx_strea
   OFX_CHECK_ARG(g && g->setup_done, "gn_setup not called");
   OFX_CHECK_ARG(A && rhs, "null A/rhs");
   hipStream_t hs = as_stream(s);
+  const int fs = fence_side(g, hs);
+  if (fs) return fs;
   int st = gn_pcg(g, gn_iter, A, rhs, hs);
   if (st) return st;
   if (g->step_fused) return OFX_OK;   // the converging PCG launch took the step (fused_step)
@@ -2672,6 +2704,8 @@ int ofx_gn_finish(void* handle, const ofx_gn_result* res, ofx_stream_t s) {
   Gn* g = (Gn*)handle;
   if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && g->setup_done && res && res->rot && res->trans, "bad gn_finish args");
+  const int fs = fence_side(g, as_stream(s));
+  if (fs) return fs;
   int n_log = g->prm.num_iter;
   int64_t n = g->N > 4 * n_log ? g->N : 4 * n_log;
   hipLaunchKernelGGL(k_finish, dim3(grid_for(n, 256)), dim3(256), 0, as_stream(s), *g, res->rot, res->trans,
@@ -2692,10 +2726,12 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   if (g->prepared) ++(use ? g->pf_used : g->pf_missed);
   g->prepared = false;
   g->prep_status = OFX_OK;
-  int st = OFX_OK;
+  // used or not, the prefetch's side-stream kernels may still be writing this handle's buffers: the caller's
+  // stream waits for all of them before anything here reuses the handle (a discarded prefetch included)
+  int st = fence_side(g, as_stream(s));
+  if (st) return st;
   if (use) {
     hipStream_t hs = as_stream(s);
-    OFX_HIP(hipStreamWaitEvent(hs, g->ev_prep, 0));
     if (pb->prev_rot || pb->prev_trans)
       hipLaunchKernelGGL(k_pose, dim3(grid_for(9 * (int64_t)g->N, 256)), dim3(256), 0, hs, *g, pb->prev_rot,
                          pb->prev_trans);

@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                                                     float* __restrict__ color, uint32_t* counter) {
   __shared__ float4 s_node[PAL ? 4 * kPal : 1];
   const int64_t slot = blockIdx.x;
-  const int64_t b = WARP ? (int64_t)list[slot] : slot;
+  const int64_t b = (WARP || list) ? (int64_t)list[slot] : slot;   // source frame: optional brick list (hash shard)
   int64_t bz = b % g.nbz;
   int64_t r = b / g.nbz;
   int64_t by = r % g.nby;
@@ -827,10 +827,14 @@ int ofx_integrate(const ofx_volume_desc* desc, const ofx_camera* cam, const floa
                          brick_list, desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color,
                          n_updated);
   } else if (!warp) {
-    OFX_CHECK_ARG(brick_list == nullptr, "a source-frame brick list needs the CPU semantics");
+    // generic source-frame form: pycuda semantics, shards of >= 2^31 voxels, or the OFX_INT_GENERIC A/B; a brick
+    // list (hash shard) is walked as in the warped form
+    OFX_CHECK_ARG(brick_list == nullptr || (n_list >= 0 && n_list <= g.n_bricks), "bad n_list");
+    const unsigned nb = brick_list ? (unsigned)n_list : (unsigned)g.n_bricks;
+    if (nb == 0) return OFX_OK;
     hipLaunchKernelGGL(pyc ? (k_integrate<false, false, true>) : (k_integrate<false, false, false>),
-                       dim3((unsigned)g.n_bricks), dim3(256), 0, hs, g, c, depth,
-                       color_im, (const float4*)nullptr, 1, (const int32_t*)nullptr, (const ushort4*)nullptr,
+                       dim3(nb), dim3(256), 0, hs, g, c, depth,
+                       color_im, (const float4*)nullptr, 1, brick_list, (const ushort4*)nullptr,
                        (const float4*)nullptr, (const uint16_t*)nullptr, (const int32_t*)nullptr,
                        (const uchar4*)nullptr, desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
   } else {

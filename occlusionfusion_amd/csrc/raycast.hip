@@ -8,7 +8,8 @@
 // z runs from the entry into the volume box (and >= z_near) to the exit (and <= z_far), sampling the tsdf
 // trilinearly (unobserved voxels — weight 0 — and voxels outside the volume count as +1, empty space) with a
 // coarse step while the sample is truncated (>= 0.999) and a fine step (one voxel) otherwise. The first
-// sign change + -> - is the surface: z* = z0 + (z1 - z0)·s0/(s0 - s1). Normal: normalised central
+// sign change + -> - between two taken samples is the surface: z* = z0 + (z1 - z0)·s0/(s0 - s1) (a ray whose
+// first sample is already negative has no positive sample before it: no hit there). Normal: normalised central
 // differences of the trilinear tsdf at p(z*) (+-1 voxel per axis). Colour: the packed colour of the voxel
 // nearest p(z*). Misses give depth 0, normal 0, colour 0.
 //
@@ -89,13 +90,17 @@ __global__ __launch_bounds__(256) void k_raycast(RayGeom r, const float* __restr
   }
   float hit = 0.0f;
   if (!miss && z0 <= z1) {
+    // a sign change needs a real positive sample before it: a ray that enters the volume (or starts at z_near)
+    // inside an observed negative region reports no surface at the entry plane
     float z = z0, zp = z0, sp = 1.0f;
+    bool have_prev = false;
     for (int n = 0; n < r.max_steps && z <= z1; ++n) {
       const float s = ray_sample(r, tsdf, weight, dx, dy, z);
-      if (sp > 0.0f && s < 0.0f) {
+      if (have_prev && sp > 0.0f && s < 0.0f) {
         hit = zp + (z - zp) * rdiv(sp, sp - s);
         break;
       }
+      have_prev = true;
       zp = z;
       sp = s;
       z = z + (s >= 0.999f ? r.step_coarse : r.step_fine);

@@ -198,9 +198,17 @@ class GaussNewtonSolver:
         cur = self._cur
         h, st = self._slots[cur]
         if prefetch is not None:
-            # the prefetch is ordered after the work enqueued so far (its inputs, the other slot's last solve)
-            # but not after this solve: it is started when this solve's host loop returns, so its kernels
-            # overlap this frame's tail (the drained PCG launches, the integrate) instead of the PCG chain
+            # The prefetch problem's tensors are made first (any conversion / default it needs runs on the current
+            # stream), then the prefetch is ordered after the work enqueued so far (those producers, its inputs,
+            # the other slot's last solve) but not after this solve: it is started when this solve's host loop
+            # returns, so its kernels overlap this frame's tail (the drained PCG launches, the integrate) instead
+            # of the PCG chain. Inputs that need conversion are new tensors on every call, so such a prefetch is
+            # correct but never matches the next solve (it is set up inline then: prefetch_stats counts a miss).
+            q = dict(prefetch)
+            pa, _, _ = self._problem(q["graph_nodes"], q["graph_edges"], q["graph_edges_weights"],
+                                     q["target_node_position"], q["node_confidence"], q["source_points"],
+                                     q["anchors"], q["weights"], q["target_points"], q.get("intrinsics", intrinsics),
+                                     q.get("target_px"), q.get("target_py"), None, None, keep=False)
             before = torch.cuda.Event()
             before.record()
         out = torch.ops.ofx.gn_solve(st, h.value, *args, fp, ip)
@@ -213,11 +221,6 @@ class GaussNewtonSolver:
                 call("ofx_gn_share_history", self._slots[1][0], self._slots[0][0])
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
-            q = dict(prefetch)
-            pa, _, _ = self._problem(q["graph_nodes"], q["graph_edges"], q["graph_edges_weights"],
-                                     q["target_node_position"], q["node_confidence"], q["source_points"],
-                                     q["anchors"], q["weights"], q["target_points"], q.get("intrinsics", intrinsics),
-                                     q.get("target_px"), q.get("target_py"), None, None, keep=False)
             h1, st1 = self._slots[nxt]
             with torch.cuda.stream(self._side):
                 self._side.wait_event(before)
@@ -298,7 +301,12 @@ class GaussNewtonSolver:
                 e1.record()
                 timer.append((e0, e1))
             torch.ops.ofx.gn_step(self._state, h, it, A, rhs)
-            if self.stopped():   # step it-1's stop rule, seen alike by every rank (include/ofx.h ofx_gn_stopped)
+            # The stop decision of step `it` is identical on every rank (identical all-reduced systems), but the host
+            # flag that carries it is written asynchronously when the step is not fused into the converging PCG
+            # launch (k_step after pcg_max_iter launches): read it only after the step has run, so that every rank
+            # leaves the loop after the same step and the collectives stay matched.
+            torch.cuda.current_stream(self.device).synchronize()
+            if self.stopped():
                 break
         out = torch.ops.ofx.gn_finish(self._state, h, N, int(self.params["num_iter"]))
         return self._pack(out, sync)

@@ -37,15 +37,36 @@ def hash_owner(nbx, nby, nbz, world):
     return (h % np.uint64(world)).astype(np.int32).reshape(-1)
 
 
+def _brick_view(a, nb):
+    """(nbx, nby, nbz, 8, 8, 8) view of a C-order volume whose dims are whole bricks (nb = brick counts)."""
+    return a.reshape(nb[0], 8, nb[1], 8, nb[2], 8).transpose(0, 2, 4, 1, 3, 5)
+
+
 def merge_hash_shards(parts, owners):
     """Whole-volume (tsdf, color, weight) from the full-size get_volume() of every hash shard (rank order) and
-    the brick owner array: each voxel is taken from the rank owning its brick."""
+    the brick owner array: each brick is copied from the rank that owns it (any world size; no voxel-level index
+    grids — dims that are not whole bricks are padded only for the copy)."""
     import numpy as np
-    Dx, Dy, Dz = parts[0][0].shape
-    nby, nbz = (Dy + 7) // 8, (Dz + 7) // 8
-    i, j, k = np.meshgrid(np.arange(Dx) // 8, np.arange(Dy) // 8, np.arange(Dz) // 8, indexing="ij")
-    own = np.asarray(owners)[(i * nby + j) * nbz + k]
-    return tuple(np.choose(own, [p[q] for p in parts]) for q in range(3))
+    D = parts[0][0].shape
+    nb = tuple((d + 7) // 8 for d in D)
+    own = np.asarray(owners).reshape(nb)
+    whole = all(d == 8 * n for d, n in zip(D, nb))
+    out = []
+    for q in range(3):
+        dst = np.empty(tuple(8 * n for n in nb), dtype=parts[0][q].dtype)
+        dv = _brick_view(dst, nb)
+        for r, p in enumerate(parts):
+            m = own == r
+            if not m.any():
+                continue
+            src = p[q]
+            if not whole:
+                pad = np.zeros(dst.shape, dtype=src.dtype)
+                pad[: D[0], : D[1], : D[2]] = src
+                src = pad
+            dv[m] = _brick_view(np.ascontiguousarray(src), nb)[m]
+        out.append(dst if whole else np.ascontiguousarray(dst[: D[0], : D[1], : D[2]]))
+    return tuple(out)
 
 
 def match_range(n_matches, rank, world):

@@ -10,8 +10,13 @@ enters from the left after frame 0 and sweeps over the sphere and back (up to ~3
 pixels hidden); matches come only from surface points visible in the target frame, and the motion
 term confidence is 1 for visible nodes, 0.3 for occluded ones.
 
-Graphs: greedy coverage sampling of surface points (the rule of csrc sample_nodes,
-csrc/cpu/graph_proc.cpp:79-136, with a spatial hash instead of the O(N²) scan) and 8 Euclidean
+Graphs (config_sequence): the reference's create_graph_from_depth
+(embedded_deformation_graph.py:95-256) on the source frame, on the device — backprojected depth ->
+compute_mesh_from_depth (max triangle distance 0.05) -> erode_mesh -> sample_nodes (no shuffle) -> 8 geodesic
+edges -> node_and_edge_clean_up + reduced graph (EDGraph.from_mesh: csrc-pinned kernels), with the node coverage
+tuned per config to its node count (BASELINE_CONFIGS[c]["coverage"]). SyntheticSequence.build's default
+(graph="euclidean", kept for the tuning tools) is a greedy coverage sampler of surface points (the rule of csrc
+sample_nodes, csrc/cpu/graph_proc.cpp:79-136, with a spatial hash instead of the O(N²) scan) with 8 Euclidean
 nearest-node edges (csrc compute_edges_euclidean semantics, graph_proc.cpp:302-356).
 """
 import math
@@ -58,10 +63,21 @@ class SphereScene:
     occ_z: float = 0.9
     occ_half: float = 0.07
     motion: str = "nonrigid"
+    phase: float = 0.0          # time offset of the non-rigid motion and the occluder sweep (independent scenes)
+
+    @staticmethod
+    def variant(seed):
+        """An independent non-rigid scene with the occluder (BASELINE config 5: one scene per GPU): sphere centre,
+        radius, occluder depth and motion phase drawn from the seed; the same size class as config 3."""
+        rng = np.random.default_rng(seed)
+        return SphereScene(center=(float(rng.uniform(-0.08, 0.08)), float(rng.uniform(-0.06, 0.06)),
+                                   float(rng.uniform(1.3, 1.5))),
+                           radius=float(rng.uniform(0.3, 0.38)), occ_z=float(rng.uniform(0.8, 1.0)),
+                           phase=float(rng.uniform(0.0, 30.0)))
 
     def occluder_x(self, t):
         """x centre of the occluding bar at frame t: out of view at t=0, over the sphere for t≈8..24."""
-        return -0.75 + 0.375 * (1.0 - math.cos(0.2 * t))
+        return -0.75 + 0.375 * (1.0 - math.cos(0.2 * (t + self.phase)))
 
     def rigid_pose(self, t):
         """(R_t, T_t): canonical (frame-0) point p -> R_t (p - c0) + c0 + T_t. R_0 = I, T_0 = 0."""
@@ -77,8 +93,9 @@ class SphereScene:
         c = np.array(self.center, np.float64)
         if self.motion == "rigid":
             return c + self.rigid_pose(t)[1], self.radius
-        c = c + np.array([0.01 * math.sin(0.3 * t), 0.008 * math.sin(0.2 * t + 1.0), 0.012 * math.sin(0.25 * t)])
-        r = self.radius * (1.0 + 0.03 * math.sin(0.35 * t))
+        s = t + self.phase
+        c = c + np.array([0.01 * math.sin(0.3 * s), 0.008 * math.sin(0.2 * s + 1.0), 0.012 * math.sin(0.25 * s)])
+        r = self.radius * (1.0 + 0.03 * math.sin(0.35 * s))
         return c, r
 
     def deform_points(self, pts, t):
@@ -222,6 +239,26 @@ def euclidean_edges(nodes, k=8):
     return edges, w
 
 
+def depth_graph(depth, cam, coverage, device=None, max_triangle_distance=0.05, n_neighbours=8):
+    """SURVEY §8(d) graph of one depth frame on the device: the reference's create_graph_from_depth
+    (embedded_deformation_graph.py:95-256) — backproject_depth (csrc/cpu/image_proc.cpp:351-401),
+    compute_mesh_from_depth (image_proc.cpp:405-545), then EDGraph.from_mesh (erode_mesh, sample_nodes without
+    shuffle, compute_edges_geodesic, node_and_edge_clean_up + get_reduced_graph, compute_clusters;
+    graph_proc.cpp:17-481). -> (nodes (N,3) f32, edges (N,K) i32, edge weights (N,K) f32)."""
+    import torch
+    from .image_proc import backproject_depth_device, compute_mesh_from_depth_device
+    from .warpfield import EDGraph
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    d = torch.from_numpy(np.ascontiguousarray(depth, np.float32)).to(dev)
+    pimg = backproject_depth_device(d, cam.fx, cam.fy, cam.cx, cam.cy)
+    mesh = compute_mesh_from_depth_device(pimg, max_triangle_distance, with_pixels=False)
+    g = EDGraph.from_mesh(mesh["vertices"], mesh["faces"],
+                          {"node_coverage": float(coverage), "num_neighbours": int(n_neighbours),
+                           "max_triangle_distance": float(max_triangle_distance)}, device=dev)
+    return (np.ascontiguousarray(g.nodes, np.float32), np.ascontiguousarray(g.edges, np.int32),
+            np.ascontiguousarray(g.edges_weights, np.float32))
+
+
 def coverage_for_nodes(points, target_nodes, seed=0, iters=8):
     """Bisection on node coverage to hit ~target_nodes."""
     lo, hi = 0.002, 0.5
@@ -238,6 +275,16 @@ def coverage_for_nodes(points, target_nodes, seed=0, iters=8):
     return best
 
 
+def frame_depth(scene, cam, seed, t):
+    """Depth of frame t of the seeded sequence (noise stream seed·1000 + t)."""
+    return scene.render(cam, t, np.random.default_rng(seed * 1000 + t))
+
+
+def source_depth(scene, cam, seed):
+    """The source frame's depth (frame 0): the canonical surface, and what the depth-mesh graph is built on."""
+    return frame_depth(scene, cam, seed, 0)
+
+
 @dataclass
 class SyntheticSequence:
     """A seeded sequence: frames, canonical surface, graph and per-frame solver inputs."""
@@ -251,22 +298,38 @@ class SyntheticSequence:
     seed: int = 0
 
     @staticmethod
-    def build(n_nodes=2000, cam=None, seed=3, coverage=None, scene=None):
+    def build(n_nodes=2000, cam=None, seed=3, coverage=None, scene=None, graph="euclidean", device=None):
         """scene: SphereScene() (non-rigid with the occluder, configs 3-5) unless given, e.g.
-        SphereScene(motion="rigid", occluder=False) for config 2."""
+        SphereScene(motion="rigid", occluder=False) for config 2.
+        graph: "euclidean" — greedy sampling of a 60k-point subset of a noisy frame-0 render (coverage bisected to
+        n_nodes) + 8 Euclidean edges; "geodesic" — depth_graph() of the source frame (frame 0, as fused) on
+        `device` with the given coverage; or a given (nodes, edges, edge_weights) triple built
+        from the source frame the same way (coverage given; e.g. the reference's compiled C++ in the CPU fixture
+        generator). The matches are drawn from the canonical points: the backprojected source frame."""
         cam = cam or bench_camera()
         scene = scene or SphereScene()
-        d0 = scene.render(cam, 0, np.random.default_rng(seed))
-        pts = backproject(d0, cam)
-        cov = coverage if coverage is not None else coverage_for_nodes(pts, n_nodes, seed)
-        sub = pts[np.random.default_rng(seed).permutation(pts.shape[0])[:60000]]
-        nodes = sample_nodes(sub, cov, seed)
-        edges, ew = euclidean_edges(nodes, 8)
-        return SyntheticSequence(cam, scene, nodes, edges, ew, float(cov), pts, seed)
+        if isinstance(graph, str) and graph == "euclidean":
+            d0 = scene.render(cam, 0, np.random.default_rng(seed))
+            pts = backproject(d0, cam)
+            cov = coverage if coverage is not None else coverage_for_nodes(pts, n_nodes, seed)
+            sub = pts[np.random.default_rng(seed).permutation(pts.shape[0])[:60000]]
+            nodes = sample_nodes(sub, cov, seed)
+            edges, ew = euclidean_edges(nodes, 8)
+            return SyntheticSequence(cam, scene, nodes, edges, ew, float(cov), pts, seed)
+        if coverage is None:
+            raise ValueError("a depth-mesh graph needs its node coverage")
+        d0 = source_depth(scene, cam, seed)
+        if isinstance(graph, str):
+            if graph != "geodesic":
+                raise ValueError(f"unknown graph kind {graph!r}")
+            nodes, edges, ew = depth_graph(d0, cam, coverage, device)
+        else:
+            nodes, edges, ew = (np.ascontiguousarray(graph[0], np.float32), np.ascontiguousarray(graph[1], np.int32),
+                                np.ascontiguousarray(graph[2], np.float32))
+        return SyntheticSequence(cam, scene, nodes, edges, ew, float(coverage), backproject(d0, cam), seed)
 
     def frame(self, t):
-        rng = np.random.default_rng(self.seed * 1000 + t)
-        return make_image(self.scene.render(self.cam, t, rng))
+        return make_image(frame_depth(self.scene, self.cam, self.seed, t))
 
     def visible(self, pts_t, t, tol=0.01):
         """Points (already at frame t) seen by the camera in frame t: the noise-free rendered depth at
@@ -302,22 +365,48 @@ class SyntheticSequence:
 
 
 # BASELINE.json configs: volume dims / voxel size / origin, graph size, motion, occluder, camera
-# scale (2: the 320x240 -> 320x224 camera of config 1) and the sequence seed (= config index).
+# scale (2: the 320x240 -> 320x224 camera of config 1), the sequence seed (= config index) and the node coverage of
+# the depth-mesh graph that gives the config's node count (measured with the reference's compiled C++ on the
+# source frame, tools/graph_coverage.py: 199 / 1020 / 1998 / 4016 nodes, 8 edges each).
 BASELINE_CONFIGS = {
     1: dict(dims=128, voxel=0.008, origin=(-0.512, -0.512, 0.9), nodes=200, motion="nonrigid", occluder=False,
-            cam_scale=2, seed=1),
+            cam_scale=2, seed=1, coverage=0.1),
     2: dict(dims=256, voxel=0.004, origin=(-0.512, -0.512, 0.9), nodes=1000, motion="rigid", occluder=False,
-            cam_scale=1, seed=2),
+            cam_scale=1, seed=2, coverage=0.043),
     3: dict(dims=512, voxel=0.004, origin=(-1.024, -1.024, 0.5), nodes=2000, motion="nonrigid", occluder=True,
-            cam_scale=1, seed=3),
+            cam_scale=1, seed=3, coverage=0.03),
     4: dict(dims=1024, voxel=0.002, origin=(-1.024, -1.024, 0.5), nodes=4000, motion="nonrigid", occluder=True,
-            cam_scale=1, seed=4),
+            cam_scale=1, seed=4, coverage=0.0205),
 }
-BASELINE_CONFIGS[5] = dict(BASELINE_CONFIGS[3])   # 8 independent config-3 scenes, one per GPU
+# 8 independent config-3-class scenes, one per GPU: rank 0 is config 3 itself, rank r > 0 its own seeded scene
+# (SphereScene.variant(5000 + r)) and noise stream (seed 5000 + r)
+BASELINE_CONFIGS[5] = dict(BASELINE_CONFIGS[3])
 
 
-def config_sequence(config, n_nodes=None):
-    """The seeded synthetic sequence of BASELINE config `config` (1..5)."""
+def config_scene(config, rank=0):
+    """(scene, seed) of BASELINE config `config`; config 5: rank r's independent scene."""
     c = BASELINE_CONFIGS[config]
-    scene = SphereScene(motion=c["motion"], occluder=c["occluder"])
-    return SyntheticSequence.build(n_nodes or c["nodes"], cam=bench_camera(c["cam_scale"]), seed=c["seed"], scene=scene)
+    if config == 5 and rank > 0:
+        return SphereScene.variant(5000 + rank), 5000 + rank
+    return SphereScene(motion=c["motion"], occluder=c["occluder"]), c["seed"]
+
+
+def config_coverage(config, n_nodes=None):
+    """Node coverage of the config's depth-mesh graph; another node count scales it as 1/sqrt(nodes) (surface
+    sampling)."""
+    c = BASELINE_CONFIGS[config]
+    cov = c["coverage"]
+    if n_nodes and int(n_nodes) != c["nodes"]:
+        cov = cov * math.sqrt(c["nodes"] / float(n_nodes))
+    return cov
+
+
+def config_sequence(config, n_nodes=None, rank=0, device=None, graph="geodesic"):
+    """The seeded synthetic sequence of BASELINE config `config` (1..5; config 5: the scene of `rank`). Its graph
+    is the SURVEY §8(d) depth-mesh graph of the source frame built on `device` (graph="geodesic"), a given
+    (nodes, edges, edge_weights) triple of that graph (CPU fixture generators), or graph="euclidean"."""
+    c = BASELINE_CONFIGS[config]
+    scene, seed = config_scene(config, rank)
+    cov = config_coverage(config, n_nodes) if not (isinstance(graph, str) and graph == "euclidean") else None
+    return SyntheticSequence.build(n_nodes or c["nodes"], cam=bench_camera(c["cam_scale"]), seed=seed, scene=scene,
+                                   coverage=cov, graph=graph, device=device)

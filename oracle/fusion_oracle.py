@@ -540,6 +540,151 @@ def gn_optimize(graph_nodes, graph_edges, graph_edges_weights, target_node_posit
     return dict(node_rotations=R, node_translations=t, valid_solve=int(valid), convergence_info=conv)
 
 
+def gn_optimize_sparse(graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
+                       source_points, anchors, weights, target_points, intrinsics,
+                       target_px=None, target_py=None, prev_rot=None, prev_trans=None, **params):
+    """gn_optimize (model.py:222-859) with the same Jacobian entries held as a sparse f64 matrix: JᵀJ and Jᵀr by
+    sparse products, then the reference's dense LU of the 6N x 6N system (model.py:59-86,694-709). Identical rows,
+    columns, LM schedule, early stop and update; only the f64 summation order of JᵀJ differs from the dense J
+    (tests/test_oracle.py checks the two against each other). For graphs whose dense J does not fit (2k-4k
+    nodes: J is (3M+3E+3N) x 6N, 8.5 GB at 2k nodes)."""
+    import scipy.sparse as sp
+    from scipy.linalg import lu_factor, lu_solve
+    p = dict(GN_DEFAULTS)
+    p.update(params)
+    g = np.asarray(graph_nodes, F64)
+    N = g.shape[0]
+    src = np.asarray(source_points, F64)
+    M = src.shape[0]
+    anc = np.asarray(anchors, np.int64)
+    wts = np.asarray(weights, F64)
+    tgt = np.asarray(target_points, F64)
+    tpos = np.asarray(target_node_position, F64)
+    conf = np.asarray(node_confidence, F64).reshape(-1)
+    fx, fy, cx, cy = (float(v) for v in intrinsics)
+    tpx = np.zeros(M) if target_px is None else np.asarray(target_px, F64).reshape(-1)
+    tpy = np.zeros(M) if target_py is None else np.asarray(target_py, F64).reshape(-1)
+    edges, (ei, ek) = gn_edges(graph_edges)
+    E = edges.shape[0]
+    n_nb = np.asarray(graph_edges).shape[1]
+    ew = np.ones(E)
+    if p['use_edge_weighting']:
+        ew = float(n_nb) * np.asarray(graph_edges_weights, F64)[ei, ek]
+    lf, ld = math.sqrt(p['lambda_flow']), math.sqrt(p['lambda_depth'])
+    lm_, la = math.sqrt(p['lambda_motion']), math.sqrt(p['lambda_arap'])
+    lm_factor = p['lm_factor']
+    R = np.tile(np.eye(3), (N, 1, 1)) if prev_rot is None else np.asarray(prev_rot, F64).reshape(N, 3, 3).copy()
+    t = np.zeros((N, 3)) if prev_trans is None else np.asarray(prev_trans, F64).reshape(N, 3).copy()
+    conv = dict(total=[], data=[], arap=[], motion=[], errors=[])
+    ill_posed = False
+    rowsM = np.arange(M) * 3
+    nrow = 3 * M + 3 * E + 3 * N
+    res = None
+    for gn_i in range(p['num_iter']):
+        if gn_i % 3 == 2:
+            lm_factor /= 2
+        rr, cc, vv = [], [], []
+
+        def put(r, c, v):
+            rr.append(np.asarray(r, np.int64).reshape(-1))
+            cc.append(np.asarray(c, np.int64).reshape(-1))
+            vv.append(np.broadcast_to(np.asarray(v, F64), np.shape(r)).reshape(-1))
+        defp = np.zeros((M, 3))
+        for k in range(4):
+            nk = anc[:, k]
+            rot = np.einsum('mij,mj->mi', R[nk], src - g[nk])
+            defp += wts[:, k:k + 1] * (rot + g[nk] + t[nk])
+        zinv = 1.0 / (defp[:, 2] + 1e-7)
+        fx_mul_x, fy_mul_y = fx * defp[:, 0], fy * defp[:, 1]
+        fx_div_z, fy_div_z = fx * zinv, fy * zinv
+        fx_mul_x_div_z, fy_mul_y_div_z = fx_mul_x * zinv, fy_mul_y * zinv
+        mfx = -fx_mul_x_div_z * zinv
+        mfy = -fy_mul_y_div_z * zinv
+        for k in range(4):
+            nk = anc[:, k]
+            wk = wts[:, k]
+            rot = np.einsum('mij,mj->mi', R[nk], src - g[nk])
+            S = -skew(wk[:, None] * rot)
+            ct = 3 * N + 3 * nk
+            put(rowsM, ct + 0, lf * wk * fx_div_z)
+            put(rowsM, ct + 2, lf * wk * mfx)
+            put(rowsM + 1, ct + 1, lf * wk * fy_div_z)
+            put(rowsM + 1, ct + 2, lf * wk * mfy)
+            put(rowsM, ct + 0, ld * wk)
+            put(rowsM + 1, ct + 1, ld * wk)
+            put(rowsM + 2, ct + 2, ld * wk)
+            cr = 3 * nk
+            for j in range(3):      # flow part with the reference's precedence quirk (model.py:505-510)
+                put(rowsM, cr + j, lf * fx_div_z * S[:, 0, j] + mfx * S[:, 2, j])
+                put(rowsM + 1, cr + j, lf * fy_div_z * S[:, 1, j] + mfy * S[:, 2, j])
+            for i in range(3):
+                for j in range(3):
+                    put(rowsM + i, cr + j, ld * S[:, i, j])
+        rd = np.zeros(M * 3)
+        rd[rowsM] = lf * (fx_mul_x_div_z + cx - tpx)
+        rd[rowsM + 1] = lf * (fy_mul_y_div_z + cy - tpy)
+        rd[rowsM] += ld * (defp[:, 0] - tgt[:, 0])
+        rd[rowsM + 1] += ld * (defp[:, 1] - tgt[:, 1])
+        rd[rowsM + 2] += ld * (defp[:, 2] - tgt[:, 2])
+        blocks_r = [rd]
+        ra = None
+        if E > 0:
+            i0, i1 = edges[:, 0], edges[:, 1]
+            rowsE = 3 * M + np.arange(E) * 3
+            delta = np.einsum('eij,ej->ei', R[i0], g[i1] - g[i0])
+            ra = (la * ew[:, None] * (delta + g[i0] + t[i0] - (g[i1] + t[i1]))).reshape(-1)
+            for c in range(3):
+                put(rowsE + c, 3 * N + 3 * i0 + c, la * ew)
+                put(rowsE + c, 3 * N + 3 * i1 + c, -la * ew)
+            Sa = -la * ew[:, None, None] * skew(delta)
+            for i in range(3):
+                for j in range(3):
+                    put(rowsE + i, 3 * i0 + j, Sa[:, i, j])
+            blocks_r.append(ra)
+        ids = np.arange(N)
+        for c in range(3):
+            put(3 * M + 3 * E + ids * 3 + c, 3 * N + 3 * ids + c, lm_ * conf)
+        rm = (lm_ * conf[:, None] * (t + g - tpos)).reshape(-1)
+        blocks_r.append(rm)
+        J = sp.csr_matrix((np.concatenate(vv), (np.concatenate(rr), np.concatenate(cc))), shape=(nrow, 6 * N))
+        res = np.concatenate(blocks_r, 0)
+        JT = J.T.tocsr()
+        A = (JT @ J).toarray()
+        A[np.diag_indices(6 * N)] += lm_factor
+        b = -(JT @ res)
+        try:
+            x = lu_solve(lu_factor(A, overwrite_a=True), b)
+        except Exception:
+            ill_posed = True
+            conv['errors'].append("Solver failed: Ill-posed system!")
+            break
+        del A
+        if not np.all(np.isfinite(x)):
+            ill_posed = True
+            conv['errors'].append("Solver failed: Non-finite solution x!")
+            break
+        loss_total = float(np.linalg.norm(res))
+        if len(conv['total']):
+            if loss_total - conv['total'][-1] > p['stop_loss_diff']:
+                break
+            if loss_total == conv['total'][-1]:
+                break
+        conv['data'].append(float(np.linalg.norm(rd)))
+        conv['total'].append(loss_total)
+        R_inc = angle_axis_to_rotation_matrix(x[:3 * N].reshape(N, 3))
+        R = R_inc @ R
+        t = t + x[3 * N:].reshape(N, 3)
+        if ra is not None:
+            conv['arap'].append(float(np.linalg.norm(ra)))
+        conv['motion'].append(float(np.linalg.norm(rm)))
+    valid = (not ill_posed) and res is not None and bool(np.all(np.isfinite(res)))
+    if not valid:
+        R = np.tile(np.eye(3), (N, 1, 1))
+        t = np.zeros((N, 3))
+    conv['valid'] = int(valid)
+    return dict(node_rotations=R, node_translations=t, valid_solve=int(valid), convergence_info=conv)
+
+
 def gn_arap(graph_nodes, source_node_position, target_node_position, valid_nodes_mask, original_graph_nodes,
             graph_edges, graph_edges_weights, R_current, t_current, **params):
     """DeformNet.arap (model/model.py:1639-1986), dense float64: data rows per valid node with the
@@ -1443,17 +1588,18 @@ def raycast(tsdf, weight, color, origin, voxel_size, intr, height, width, z_near
     hit = np.zeros(n, F32)
     act = np.nonzero(~miss & (z0 <= z1))[0]
     z, zp, sp = z0[act].copy(), z0[act].copy(), np.ones(act.size, F32)
+    have = np.zeros(act.size, bool)   # a sign change needs a real sample before it (no hit at the entry plane)
     while act.size:
         run = z <= z1[act]
-        act, z, zp, sp = act[run], z[run], zp[run], sp[run]
+        act, z, zp, sp, have = act[run], z[run], zp[run], sp[run], have[run]
         if not act.size:
             break
         s = trilinear((z * dx[act] - lo[0]) * inv_vs, (z * dy[act] - lo[1]) * inv_vs, (z - lo[2]) * inv_vs)
-        h = (sp > 0) & (s < 0)
+        h = have & (sp > 0) & (s < 0)
         hit[act[h]] = zp[h] + (z[h] - zp[h]) * (sp[h] / (sp[h] - s[h]))
         keep = ~h
         act, z, s = act[keep], z[keep], s[keep]
-        zp, sp = z.copy(), s
+        zp, sp, have = z.copy(), s, np.ones(act.size, bool)
         z = (z + np.where(s >= F32(0.999), step_c, step_f)).astype(F32)
     nrm = np.zeros((n, 3), F32)
     col = np.zeros(n, F32)

@@ -18,6 +18,10 @@
   gn_small.npz        — one DeformNet.optimize solve (N≈100, M=600) by the dense f64 oracle.
   gn_1k.npz           — one DeformNet.optimize solve at BASELINE config 2's size (rigid sequence, 1025 nodes,
                         10k matches, dense J ≈ 57k x 6k) by the dense f64 oracle (≈2 min on 8 cores).
+  gn_2k.npz           — the headline config's solve (config 3: occluded non-rigid frames 10 and 11, the second
+                        chained from the first, ~2k nodes of the SURVEY §8(d) depth-mesh graph built by the
+                        reference's C++, 10k matches) by the f64 oracle with a sparse JᵀJ + dense LU.
+  gn_4k.npz           — the same at config 4's graph (~4k nodes, frame 10).
   frontend_csrc.npz   — backproject_depth_float / _ushort and compute_mesh_from_depth outputs of the
                         REFERENCE's compiled C++ (csrc/cpu/image_proc.cpp:351-545) on a synthetic frame,
                         incl. max-distance thresholds that tie exactly with triangle edge lengths; plus the
@@ -270,6 +274,58 @@ def make_gn_small():
     print("gn_small:", nodes.shape[0], "nodes,", src.shape[0], "matches, loss", ci["total"][:3], "...")
 
 
+_REF = None
+
+
+def _ref():
+    """The reference's compiled C++ (oracle/_ref, built from /root/reference by oracle/build_ref.py)."""
+    global _REF
+    if _REF is None:
+        from oracle.build_ref import build, load_prebuilt
+        _REF = load_prebuilt() or build()
+    return _REF
+
+
+def csrc_depth_graph(depth, cam, coverage, max_triangle_distance=0.05, K=8):
+    """SURVEY §8(d) graph of a depth frame by the REFERENCE's compiled C++, in EDGraph.from_mesh's order (the
+    reference's create_graph_from_depth, embedded_deformation_graph.py:95-256): backproject_depth_float ->
+    compute_mesh_from_depth -> erode_mesh(1, 3) -> sample_nodes(no shuffle, valid vertices only) ->
+    compute_edges_geodesic(K, enforce) -> node_and_edge_clean_up -> the oracle's get_reduced_graph. The device
+    twin is occlusionfusion_amd.synthetic.depth_graph (tests/test_gpu_golden_gn.py checks the two agree)."""
+    m = _ref()
+    bf = np.zeros((3,) + depth.shape, np.float32)
+    m.backproject_depth_float(np.ascontiguousarray(depth, np.float32), bf, float(cam.fx), float(cam.fy),
+                              float(cam.cx), float(cam.cy))
+    v, px, f = np.zeros((0,), np.float32), np.zeros((0,), np.int32), np.zeros((0,), np.int32)
+    m.compute_mesh_from_depth(bf, float(max_triangle_distance), v, px, f)
+    v, f = v.reshape(-1, 3), f.reshape(-1, 3)
+    ne = m.erode_mesh(v, f, 1, 3)
+    npos, nidx = np.zeros((0,), np.float32), np.zeros((0,), np.int32)
+    n = m.sample_nodes(v, ne, npos, nidx, float(coverage), True, False)
+    npos, nidx = npos[:n], nidx[:n]
+    E = -np.ones((n, K), np.int32)
+    W = np.zeros((n, K), np.float32)
+    Dd = np.zeros((n, K), np.float32)
+    D = -np.ones((n, v.shape[0]), np.float32)
+    m.compute_edges_geodesic(v, np.ones((v.shape[0], 1), bool), f, nidx, K, float(coverage), E, W, Dd, D, True, True)
+    del D
+    valid = np.ones((n, 1), bool)
+    m.node_and_edge_clean_up(E, valid)
+    nodes, E, W, _, _ = fo.reduced_graph(npos, E, W, Dd, -np.ones((n, 1), np.int32), valid)
+    return nodes.astype(np.float32), E.astype(np.int32), W.astype(np.float32)
+
+
+def config_sequence_cpu(config, rank=0):
+    """BASELINE config `config`'s synthetic sequence with its SURVEY §8(d) depth-mesh graph built by the
+    reference's compiled C++ (the bench builds the same graph on the device)."""
+    c = S.BASELINE_CONFIGS[config]
+    scene, seed = S.config_scene(config, rank)
+    cam = S.bench_camera(c["cam_scale"])
+    cov = S.config_coverage(config)
+    g = csrc_depth_graph(S.source_depth(scene, cam, seed), cam, cov)
+    return S.config_sequence(config, rank=rank, graph=g)
+
+
 def config2_sequence():
     """BASELINE config 2: rigid-motion sphere + plane, 640x448, ~1k nodes (seed 2)."""
     return S.config_sequence(2)
@@ -296,8 +352,49 @@ def make_gn_1k(t=1, n_matches=10000):
           f"{time.time() - t0:.0f} s")
 
 
+def _frame_problem(seq, t, n_matches=10000):
+    """Frame t's GN inputs exactly as FusionPipeline.prepare builds them: seeded matches + node targets, then the
+    skin of the source points (oracle skin == the device skin, tests/test_gpu_parity.py) keeping the valid ones."""
+    src, tgt, tpos, conf = seq.solver_inputs(t, n_matches)
+    a, w, v = fo.skin(src, seq.nodes, seq.node_coverage)
+    return dict(src=src[v], tgt=tgt[v], tpos=tpos, conf=conf, anchors=a[v], weights=w[v])
+
+
+def make_gn_chain(name, config, frames, n_matches=10000):
+    """gn_2k.npz / gn_4k.npz — DeformNet.optimize (model.py:222-859) at the headline sizes by the f64 oracle
+    (gn_optimize_sparse: the dense restatement's rows with a sparse JᵀJ, then the reference's dense LU), on
+    BASELINE config `config`'s occluded non-rigid frames with its SURVEY §8(d) depth-mesh graph (the reference's
+    compiled C++). frames = (t0, t1, ...): t0 starts from the identity, every later frame from the previous
+    frame's oracle result (the frame loop's prev_rot / prev_trans)."""
+    import time
+    seq = config_sequence_cpu(config)
+    intr = seq.cam.as_vec()
+    out = dict(nodes=seq.nodes, edges=seq.edges, edge_weights=seq.edge_weights, node_coverage=seq.node_coverage,
+               intr=intr, config=config, frames=np.array(frames, np.int32), seed=seq.seed)
+    R = T = None
+    for q, t in enumerate(frames):
+        pb = _frame_problem(seq, t, n_matches)
+        t0 = time.time()
+        res = fo.gn_optimize_sparse(seq.nodes, seq.edges, seq.edge_weights, pb["tpos"], pb["conf"], pb["src"],
+                                    pb["anchors"], pb["weights"], pb["tgt"], intr, prev_rot=R, prev_trans=T)
+        R, T = res["node_rotations"], res["node_translations"]
+        ci = res["convergence_info"]
+        for k, v in pb.items():
+            out[f"f{q}_{k}"] = v
+        out.update({f"f{q}_R": R, f"f{q}_t": T, f"f{q}_valid": res["valid_solve"],
+                    f"f{q}_loss_total": np.array(ci["total"]), f"f{q}_loss_data": np.array(ci["data"])})
+        print(f"{name} frame {t}: {seq.nodes.shape[0]} nodes, {pb['src'].shape[0]} matches, "
+              f"{int((pb['conf'] < 1).sum())} low-confidence nodes, {len(ci['total'])} GN steps, loss "
+              f"{ci['total'][0]:.6f} -> {ci['total'][-1]:.6f} ({time.time() - t0:.0f} s)", flush=True)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn", "gn1k"]
+    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn", "gn1k", "gn2k", "gn4k"]
+    if "gn2k" in which:
+        make_gn_chain("gn_2k", 3, (10, 11))
+    if "gn4k" in which:
+        make_gn_chain("gn_4k", 4, (10,))
     if "gn1k" in which:
         make_gn_1k()
     if "skin" in which:

@@ -8,7 +8,8 @@
   1e-5; sampled-voxel integrate parity after a warped frame.
 * config 4 — 1024³ @2 mm, ~4k nodes, on one GPU (12.9 GB of volume): sampled-voxel integrate parity after a
   warped frame, tight-vs-default GN within 1e-5 and bitwise-repeatable solves.
-(config 3 is tests/test_gpu_full.py; config 5 is config 3 per GPU — bench.py --gpus N replicas.)
+(config 3 is tests/test_gpu_full.py and, against the oracle at full size, tests/test_gpu_golden_gn.py; config 5 is
+one independent config-3-class scene per GPU — bench.py --gpus N replicas.)
 """
 import os
 
@@ -26,7 +27,7 @@ def make_pipe(config, cuda, n_nodes=None):
     from occlusionfusion_amd import synthetic as S
     from occlusionfusion_amd.pipeline import FusionPipeline
     c = S.BASELINE_CONFIGS[config]
-    seq = S.config_sequence(config, n_nodes)
+    seq = S.config_sequence(config, n_nodes, device=cuda)
     D = c["dims"]
     pipe = FusionPipeline(seq, c["origin"], c["voxel"], (D, D, D), device=cuda)
     pipe.integrate_source(pipe.prepare(0))

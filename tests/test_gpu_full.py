@@ -18,9 +18,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def seq():
+def seq(cuda):
     from occlusionfusion_amd import synthetic as S
-    return S.SyntheticSequence.build(2000, seed=3)
+    return S.config_sequence(3, device=cuda)     # the bench's sequence and depth-mesh graph
 
 
 @pytest.fixture(scope="module")

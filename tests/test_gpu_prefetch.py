@@ -56,3 +56,37 @@ def test_prefetch_for_another_problem_is_discarded(cuda):
     torch.cuda.synchronize()
     assert pipe.solver.prefetch_stats() == (0, 1)
     assert torch.equal(pipe.prev_rot, ref.prev_rot) and torch.equal(pipe.prev_trans, ref.prev_trans)
+
+
+def test_discarded_larger_prefetch_is_ordered_before_the_inline_setup(cuda):
+    """A prefetch is discarded while its side-stream setup may still run, and that setup reallocates the slot's
+    buffers (its problem is larger than any the slot held): the miss solve, issued right away, must wait for all of
+    it (ofx_gn_solve fences the side stream whether or not the prefetch is used) and equal the plain solve."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    from occlusionfusion_amd.pipeline import FusionPipeline, FrameInputs
+    from occlusionfusion_amd import synthetic as S
+    c = S.BASELINE_CONFIGS[1]
+    seq = S.config_sequence(1, device=cuda)
+    D = c["dims"]
+
+    def pipeline():
+        p = FusionPipeline(seq, c["origin"], c["voxel"], (D, D, D), n_matches=3000, device=cuda)
+        p.solver = GaussNewtonSolver(len(seq.nodes), 10000, cuda)   # room for the larger prefetched problem
+        fr = [p.prepare(t) for t in range(6)]
+        p.integrate_source(fr[0])
+        return p, fr
+
+    pipe, frames = pipeline()
+    ref, rframes = pipeline()
+    big = FrameInputs(im=frames[3].im, tpos=frames[3].tpos, conf=frames[3].conf,
+                      **{k: torch.cat([getattr(frames[t], k) for t in (3, 4, 5)])
+                         for k in ("src", "anchors", "weights", "tgt")})
+    assert big.src.shape[0] > 2 * frames[1].src.shape[0]
+    pipe.solve(frames[1], frames[2])          # slot 1 set up for frame 2
+    pipe.solve(frames[2], big)                # frame 2 uses it; slot 0 (sized for frame 1) prefetches 3x the matches
+    pipe.solve(frames[3])                     # miss, issued at once: inline setup on slot 0
+    for t in (1, 2, 3):
+        ref.solve(rframes[t])
+    torch.cuda.synchronize()
+    assert pipe.solver.prefetch_stats() == (1, 1)
+    assert torch.equal(pipe.prev_rot, ref.prev_rot) and torch.equal(pipe.prev_trans, ref.prev_trans)

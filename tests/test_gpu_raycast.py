@@ -91,3 +91,26 @@ def test_raycast_axis_rays_and_inside_camera(cuda):
             if zf < 0.5:
                 assert not (d > 0).any()
 
+
+
+def test_raycast_entering_inside_the_negative_band_reports_no_entry_hit(cuda):
+    """Rays that start (z_near) behind the fused front surface, inside its observed negative band, have no
+    positive sample before their first one: no surface is reported at the entry plane (a spurious hit at z_near
+    before the fix), and the result still equals the oracle bit for bit."""
+    from types import SimpleNamespace
+    from occlusionfusion_amd import TSDFVolume
+    from occlusionfusion_amd import synthetic as S
+    cam = S.Intrinsics(100.0, 100.0, 40.0, 30.0, 80, 60)
+    depth = S.SphereScene(occluder=False).render(cam, 0, np.random.default_rng(0))
+    vol = TSDFVolume.from_grid((-0.6, -0.5, 0.9), 0.01, (128, 100, 100), (cam.fx, cam.fy, cam.cx, cam.cy),
+                               SimpleNamespace(source_frame=0, skip_rate=1), device=cuda)
+    vol.integrate({"im": S.make_image(depth), "id": 0})
+    full = _compare(vol)
+    zc = float(full[30, 40])
+    assert zc > 0
+    zn = zc + 0.01                       # 1 cm behind the front surface: inside the 4 cm truncation band
+    d = _compare(vol, z_near=zn, z_far=10.0)
+    inside = np.abs(full - zc) < 0.004   # pixels whose surface lies (about) where the centre ray's does
+    assert inside.sum() > 10
+    assert not (d[inside] == np.float32(zn)).any()
+    assert not ((d > 0) & (d <= np.float32(zn))).any()

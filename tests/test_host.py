@@ -37,6 +37,22 @@ def test_match_range_partition():
         assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
 
 
+@pytest.mark.parametrize("dims,world", [((16, 24, 8), 2), ((13, 21, 18), 3), ((40, 40, 40), 70)])
+def test_merge_hash_shards_takes_each_brick_from_its_owner(dims, world):
+    """Brick-wise merge of hash shards: any world size (np.choose capped it at 32/64 choices) and dims that are
+    not whole bricks; every voxel comes from the rank owning its 8³ brick."""
+    from occlusionfusion_amd.sharding import hash_owner, merge_hash_shards
+    nb = [(d + 7) // 8 for d in dims]
+    owners = hash_owner(*nb, world)
+    parts = [tuple(np.full(dims, 10 * r + q, np.float32) for q in range(3)) for r in range(world)]
+    merged = merge_hash_shards(parts, owners)
+    i, j, k = np.meshgrid(*[np.arange(d) // 8 for d in dims], indexing="ij")
+    own = owners[(i * nb[1] + j) * nb[2] + k]
+    for q in range(3):
+        assert merged[q].shape == tuple(dims) and merged[q].flags.c_contiguous
+        np.testing.assert_array_equal(merged[q], (10 * own + q).astype(np.float32))
+
+
 def test_synthetic_graph_properties():
     from occlusionfusion_amd import synthetic as S
     cam = S.bench_camera(4)

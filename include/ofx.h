@@ -218,6 +218,10 @@ int ofx_deform_points_lbs(const float* points, int64_t n_points, const int32_t* 
 /* check_visibility: valid u8[P], depth_diff f64[P] */
 int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
                    double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s);
+/* The same check with the projection in f32, as numba runs cam2pix on an f32 point array: get_visible_nodes on
+ * the f32 deformed nodes (tsdf.py:614-638 -> 599-612 -> 351-364); depth lookup and depth_diff in f64 */
+int ofx_visibility_f32(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
+                       double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s);
 
 /* ---------------- Surface extraction ----------------
  * Voxel-index coordinates as skimage returns. ofx_truncated_region / ofx_mesh_count take the whole volume;
@@ -404,8 +408,9 @@ typedef struct ofx_gn_result {
 /* max_nodes <= 8192 (the JᵀJ slot map is dense over the padded rows) */
 int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle);
 /* Profiling hook: returns (and resets) the device time of the PCG iteration loops recorded since the
- * last call (hipEvents on the solve stream; synchronises on them), the number of k_pcg_iter launches
- * and of timed solves; `enable` switches recording for the following steps. */
+ * last call (hipEvents on the solve stream; synchronises on them), the number of PCG launches (k_pcg_iter
+ * launches, or one k_pcg_persist launch per GN step) and of timed solves; `enable` switches recording for the
+ * following steps. */
 int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves);
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
  * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
@@ -414,10 +419,17 @@ int ofx_gn_info(void* handle, int64_t* info);
  * 384 clusters (default) or 1 (environment OFX_PCG_W1 set to anything but "" / "0" at create; tuning and A/B
  * only); larger problems always run one wave per cluster. */
 int ofx_gn_pcg_waves(void* handle, int32_t* waves);
+/* PCG form of the last setup: form (host int32[3]) = [1 if each GN step's PCG is ONE persistent launch
+ * (k_pcg_persist: A blocks in LDS, state in registers, m and the dot-product partials handed between workgroups)
+ * else 0 (one k_pcg_iter launch per iteration), workgroups of the persistent launch, clusters per workgroup].
+ * Persistent when selected (environment OFX_PCG_PERSIST=1 at create) unless a workgroup's blocks exceed its LDS, a
+ * cluster has more than 128 blocks or a row more than 20, more than min(128, CUs) workgroups would be needed,
+ * pcg_max_iter >= 4096, or an earlier persistent solve of the handle timed out (it then reported valid_solve = 0). */
+int ofx_gn_pcg_form(void* handle, int32_t* form);
 /* The solve's stop flag as the host sees it (host-mapped, no synchronisation): 1 once a GN step's loss rule
- * (model.py:726-732) or an ill-posed solve stopped it. After ofx_gn_step(i + 1) returns it reflects step i's
- * decision on every rank alike (that step's PCG poll waited for it), so a stepped multi-rank loop can leave
- * after the same step everywhere, as ofx_gn_solve does. */
+ * (model.py:726-732) or an ill-posed solve stopped it. The device writes it asynchronously: a stepped multi-rank
+ * loop reads it only after synchronising the stream behind ofx_gn_step(i), so that every rank leaves after the
+ * same step (GaussNewtonSolver.optimize_distributed). */
 int ofx_gn_stopped(void* handle, int32_t* stopped);
 /* Per-GN-step statistics of the last solve: out (host f64[3*cap]) = [PCG iterations, |b|², loss] per
  * step (zeros for steps that did not run); synchronous D2H copy, at most 64 steps. */

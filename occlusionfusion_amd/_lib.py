@@ -66,6 +66,7 @@ _SIGS = {
     "ofx_deform_points": [P, c_int64, P, P, P, c_int32, P, c_int32, c_int32, P, P],
     "ofx_deform_points_lbs": [P, c_int64, P, P, P, c_int32, P, P, c_int32, P, P],
     "ofx_visibility": [P, c_int64, P, P, c_double, P, P, P],
+    "ofx_visibility_f32": [P, c_int64, P, P, c_double, P, P, P],
     "ofx_truncated_region": [P, P, c_double, P, P],
     "ofx_mesh_create": [P],
     "ofx_mesh_destroy": [P],
@@ -100,6 +101,7 @@ _SIGS = {
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
     "ofx_gn_pcg_waves": [P, P],
+    "ofx_gn_pcg_form": [P, P],
     "ofx_gn_stopped": [P, P],
     "ofx_gn_stats": [P, P, c_int32],
     "ofx_gn_row_order": [P, P, c_int32],

@@ -136,6 +136,11 @@ struct GnDev {
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
   bool timing = false;
   int64_t n_iter_launches = 0;
+  // persistent PCG (k_pcg_persist): cluster -> workgroup partition, m double buffer, partial granules, abort word
+  int32_t* p_wg_cl = nullptr;
+  unsigned long long* p_mgr = nullptr;
+  unsigned long long* p_gran = nullptr;
+  int32_t* p_abort = nullptr;
 };
 static_assert(std::is_trivially_copyable<GnDev>::value, "kernel argument");
 
@@ -164,6 +169,11 @@ struct Gn : GnDev {
   // its last kernels (row assignment, contribution lists, ...) have run, and they write this handle's buffers
   bool side_dirty = false;
   hipEvent_t ev_side = nullptr;
+  // persistent PCG: enabled for this setup, workgroups, clusters per workgroup, A blocks of the largest workgroup
+  bool p_on = false, p_disabled = false;
+  int p_G = 0, p_C = 4, p_lds_blocks = 0, p_cus = 0;
+  uint32_t p_epoch = 0;
+  std::vector<int32_t> h_wg_cl;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
 };
 
@@ -1826,6 +1836,329 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   OFX_STAMP(7)
 }
 
+// ---------------------------------------------------------------------------- persistent PCG
+// The same pipelined PCG as k_pcg_iter, as ONE launch per solve (GN step) instead of one per iteration. Why: a
+// launch re-reads the iteration's whole working set (A blocks, cluster inverses, state: ~11 MB at 2k nodes) from
+// beyond L2 and pays the kernel boundary; a bare launch that only reads 44 KB per workgroup already takes ~4.5 us
+// back to back on this part (tools/sync_micro.hip), the iteration kernel 5.1 us. Here every workgroup keeps its
+// clusters' A blocks in LDS, its rows' recurrence state and cluster-inverse rows in registers for the whole solve,
+// and only m (48 doubles per cluster) and the three dot-product partials (per workgroup) cross workgroups:
+//  * workgroup = up to kPersistMaxC compute waves (one cluster each) + one poll wave; G <= 128 workgroups (two
+//    producers per lane in the partial sweep), all co-resident (host: G <= CUs, one workgroup's LDS per CU);
+//  * SpMV as the iteration kernel's wave-list form: lane l multiplies the cluster's blocks l and l + 64 (balanced
+//    whatever the row lengths), the products meet in LDS and each row sums its blocks in CSR order; the cluster's
+//    A blocks sit in LDS element-major (element e of block s at e·nb + s), so every read is one contiguous,
+//    bank-conflict-free wave access;
+//  * hand-offs carry their own flag (MI355X_MICROARCH.md, visibility, R2 granules): every double travels as two
+//    8-byte granules {tag | 32-bit half}, each written by one sc1 store and read by sc1 loads until the tag matches.
+//    m_{it+1} (per row component) is published as soon as M⁻¹ has produced it, the workgroup's partials of
+//    iteration it + 1 (its clusters summed in order) right after;
+//  * iteration it: the compute waves gather m_it of their blocks' columns (spinning on the granules of just those
+//    rows) and multiply from LDS while the poll wave sweeps every workgroup's partials — the neighbour hop and the
+//    global reduction overlap; one barrier hands the scalars to the compute waves;
+//  * m and the partials are double-buffered by iteration parity: a producer writes iteration it + 2 only after it
+//    has seen every workgroup's partials of it + 1, which each consumer publishes after it has read iteration it;
+//  * tags = (launch epoch << 12) | iteration: no per-launch memset, stale granules never match;
+//  * scalars: every workgroup sums the G partials in the same fixed order, so all of them take the same
+//    convergence / breakdown / cap decision at the same iteration and leave the loop together; the converging
+//    iteration takes the GN step (fused_step) for the workgroup's rows;
+//  * every spin is bounded: a timeout marks the solve ill-posed (valid_solve = 0), records the epoch in abort_word
+//    (the host then stays on the per-iteration launches) and the waits of the other workgroups time out in turn.
+// Deterministic: fixed-order sums everywhere (not bit-identical to k_pcg_iter, whose partial tree differs).
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr int kPersistMaxC = 4;         // compute waves (clusters) per workgroup, + 1 poll wave
+constexpr int kPersistRowMax = kRowMax; // longest block row (row sums over the products in LDS)
+constexpr int kPersistMaxG = 128;
+constexpr unsigned kPersistSpin = 1u << 20;   // polls before a wait gives up (~1 s)
+constexpr int kPersistLds = 126 * 1024;       // dynamic LDS budget per workgroup: A blocks + their columns
+
+struct PcgPersist {
+  PcgIt b;                  // the iteration kernel's arguments: operator, state, flags, fused GN step
+  const int32_t* wg_cl;     // per workgroup its first cluster (G + 1 entries)
+  unsigned long long* mgr;  // [2][6N][2] m granules of iteration it >= 1 at parity it & 1
+  unsigned long long* gran; // [2][G][8] partial granules
+  int32_t* abort_word;      // epoch of a launch that timed out
+  int32_t G, max_it, lds_blocks, C;
+  uint32_t epoch;
+};
+
+__device__ __forceinline__ uint32_t persist_tag(uint32_t epoch, int it) { return (epoch << 12) | (uint32_t)it; }
+__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long* p) {
+  return __hip_atomic_load((gu64*)const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_gran(unsigned long long* p, uint32_t tag, uint32_t v) {
+  __hip_atomic_store((gu64*)p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_gran_double(unsigned long long* p, uint32_t tag, double v) {
+  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+  st_gran(p, tag, (uint32_t)bits);
+  st_gran(p + 1, tag, (uint32_t)(bits >> 32));
+}
+__device__ __forceinline__ double gran_double(unsigned long long lo, unsigned long long hi) {
+  return __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
+}
+__device__ __forceinline__ bool gran_tag_is(unsigned long long lo, unsigned long long hi, uint32_t tag) {
+  return (uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag;
+}
+__device__ __forceinline__ bool persist_give_up(const PcgPersist& P, unsigned spins) {
+  return spins > kPersistSpin ||
+         ((spins & 255) == 255 &&
+          __hip_atomic_load(P.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int32_t)P.epoch);
+}
+
+#ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every workgroup for the first 64 iterations
+#define OFX_PSTAMP(cond, k)                                                                                     \
+  if ((cond) && lane == 0 && g.stamps && it < 64)                                                              \
+    g.stamps[((int64_t)it * g.nwg_row + wg) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OFX_PSTAMP(cond, k)
+#endif
+__global__ __launch_bounds__(64 * (kPersistMaxC + 1)) void k_pcg_persist(PcgPersist P) {
+  extern __shared__ double s_A[];                 // the workgroup's A blocks (CSR order), then their columns
+  __shared__ double s_v[kPersistMaxC][kCD];
+  __shared__ double s_sc[4];                      // gamma, delta, r.r of the iteration; |b|^2
+  __shared__ double s_part[kPersistMaxC][3];
+  __shared__ double s_prod[kPersistMaxC][(kWL + kRowMax) * 6];   // block products, slot-major
+  __shared__ int s_cb[kPersistMaxC + 1];          // the clusters' first blocks (workgroup-relative)
+  __shared__ int s_abort;
+  const PcgIt& g = P.b;
+  const int wg = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (g.flags[F_STOPPED]) return;                 // the solve already stopped: this GN step is a no-op (uniform)
+  const int c0 = P.wg_cl[wg], c1 = P.wg_cl[wg + 1], ncl = c1 - c0;
+  const bool poller = w == P.C;                   // the workgroup's poll wave (no cluster)
+  const bool act = w < ncl;
+  const int cl = c0 + (act ? w : 0);
+  const int r = lane / kSL, q = lane % kSL, row = cl * kRW + r;
+  const bool own = q < 6;
+  const int qc = own ? q : 5;
+  const int64_t o = 6 * (int64_t)row + qc;
+  const int64_t n6 = 6 * (int64_t)g.N;
+  const int bw = g.row_ptr[c0 * kRW];
+  const int nblk = g.row_ptr[c1 * kRW] - bw;
+  int* s_col = reinterpret_cast<int*>(s_A + 36 * (size_t)P.lds_blocks);
+  if (tid <= ncl) s_cb[tid] = g.row_ptr[(c0 + tid) * kRW] - bw;
+  __syncthreads();
+  {   // stage the workgroup's A blocks (element-major per cluster) and columns (earlier launches wrote them)
+    const double* src = g.Aop + 36 * (int64_t)bw;
+    for (int i = tid; i < nblk * 36; i += blockDim.x) {
+      const int b = i / 36, e = i - 36 * b;
+      int j = 0;
+#pragma unroll
+      for (int k = 1; k < kPersistMaxC; ++k) j += (k < ncl && b >= s_cb[k]) ? 1 : 0;
+      const int nb = s_cb[j + 1] - s_cb[j];
+      s_A[36 * s_cb[j] + e * nb + (b - s_cb[j])] = src[i];
+    }
+    for (int i = tid; i < nblk; i += blockDim.x) s_col[i] = g.col[bw + i];
+  }
+  const int cb = s_cb[act ? w : 0], cnb = s_cb[act ? w + 1 : 1] - cb;   // this wave's cluster: first block, blocks
+  const int b0 = g.row_ptr[row] - bw - cb, b1 = g.row_ptr[row + 1] - bw - cb;   // the row's blocks, cluster-relative
+  double v[V_N];
+  load_rec(g.st, o, v);
+  double mown = g.m0[o];                          // the own row's m of the current iteration (k_pcg_w0 wrote m_0)
+  float4 mr[kCD / 4];                             // this lane's row of its cluster inverse, for the whole solve
+  {
+    const float4* p = reinterpret_cast<const float4*>(g.Mcl + mcl_idx(cl, 6 * r + qc, 0));
+#pragma unroll
+    for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k * kCD];
+  }
+  if (w == 0) {   // iteration 0's scalars and |b|^2 from k_pcg_w0's per-cluster partials, fixed order
+    const int nc = g.nwg_row, ns = g.nw_pad;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = lane; i < nc; i += 64) {
+      a[0] += g.part_p[i]; a[1] += g.part_p[ns + i]; a[2] += g.part_p[2 * ns + i]; a[3] += g.part_b[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = wave_sum(a[k]);
+    if (lane == 0) { s_sc[0] = a[0]; s_sc[1] = a[1]; s_sc[2] = a[2]; s_sc[3] = a[3]; s_abort = 0; }
+  }
+  __syncthreads();
+  const double bb = s_sc[3];
+  const double tol = g.prm.pcg_tol;
+  const bool lead = wg == 0 && tid == 0;
+  if (lead) g.scal[S_BB] = bb;
+  double rgam = 1.0, ralpha = 1.0;
+  for (int it = 0;; ++it) {
+    const uint32_t tag = persist_tag(P.epoch, it);
+    OFX_PSTAMP(w == 0, 0)
+    double nc = 0.0;
+    if (act) {   // ---- n = A m_it (own component): the cluster's blocks lane and lane + 64, products via LDS
+      double xm[2][6];
+      bool okb[2];
+      int64_t c6[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int sl = lane + 64 * k;
+        okb[k] = sl < cnb;
+        c6[k] = 6 * (int64_t)s_col[cb + (okb[k] ? sl : 0)];
+      }
+      if (it == 0) {   // m_0: written by k_pcg_w0 (an earlier launch)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int j = 0; j < 6; ++j) xm[k][j] = g.m0[c6[k] + j];
+      } else {         // m_it: the producers' granules, spun on until all carry this iteration's tag
+        const unsigned long long* mg = P.mgr + (size_t)(it & 1) * n6 * 2;
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+              const unsigned long long lo = ld_gran(mg + 2 * (c6[k] + j)), hi = ld_gran(mg + 2 * (c6[k] + j) + 1);
+              ok &= !okb[k] || gran_tag_is(lo, hi, tag);
+              xm[k][j] = gran_double(lo, hi);
+            }
+          if (__all(ok)) break;
+          if (persist_give_up(P, spins)) {
+            if (lane == 0) s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      OFX_PSTAMP(w == 0, 1)
+      const double* sa = s_A + 36 * (size_t)cb;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int sl = lane + 64 * k;
+        const int slc = okb[k] ? sl : 0;
+        double a[36];
+#pragma unroll
+        for (int e = 0; e < 36; ++e) a[e] = sa[e * cnb + slc];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double t = fma(a[6 * i + 5], xm[k][5], fma(a[6 * i + 4], xm[k][4], fma(a[6 * i + 3], xm[k][3],
+                           fma(a[6 * i + 2], xm[k][2], fma(a[6 * i + 1], xm[k][1], a[6 * i] * xm[k][0])))));
+          s_prod[w][sl * 6 + i] = okb[k] ? t : 0.0;
+        }
+      }
+      wave_lds_sync();
+      {   // row sums in CSR order (rows of at most kRowMax blocks; masked reads inside the padded array)
+        const int len = b1 - b0;
+        const double* sp = s_prod[w] + b0 * 6 + qc;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < kRowMax; ++k) {
+          const double t = sp[6 * k];
+          acc += k < len ? t : 0.0;
+        }
+        nc = acc;
+      }
+      OFX_PSTAMP(w == 0, 2)
+    }
+    if (poller && it > 0) {   // ---- meanwhile: the partials of iteration it from every workgroup, fixed order
+      const unsigned long long* gs = P.gran + (size_t)(it & 1) * P.G * 8;
+      double a[3] = {0.0, 0.0, 0.0};
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+        double sx[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int p = lane + 64 * u;
+          const int pc = p < P.G ? p : 0;
+          unsigned long long x[6];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) x[k] = ld_gran(gs + (size_t)pc * 8 + k);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            ok &= p >= P.G || gran_tag_is(x[2 * k], x[2 * k + 1], tag);
+            sx[k] += p < P.G ? gran_double(x[2 * k], x[2 * k + 1]) : 0.0;
+          }
+        }
+        if (__all(ok)) { a[0] = sx[0]; a[1] = sx[1]; a[2] = sx[2]; break; }
+        if (persist_give_up(P, spins)) {
+          if (lane == 0) s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a[k] = wave_sum(a[k]);
+      if (lane == 0) { s_sc[0] = a[0]; s_sc[1] = a[1]; s_sc[2] = a[2]; }
+      OFX_PSTAMP(true, 3)
+    }
+    __syncthreads();   // the scalars (and any timeout) reach every wave
+    OFX_PSTAMP(w == 0, 4)
+    if (s_abort) {     // a wait timed out: this solve is invalid (the host falls back for the next ones)
+      if (tid == 0) __hip_atomic_store(P.abort_word, (int32_t)P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lead) g.flags[F_ILL] = 1;
+      return;
+    }
+    const double gam = s_sc[0], del = s_sc[1], rr = s_sc[2];
+    // ---- scalars (identical in every workgroup) and the stop decision
+    double beta = 0.0, alpha;
+    if (it == 0) {
+      alpha = gam / del;
+    } else {
+      beta = gam * rgam;
+      alpha = gam / (del - beta * gam * ralpha);
+    }
+    const bool conv = rr <= tol * tol * bb || gam == 0.0;
+    const bool brk = !isfinite(alpha) || !(alpha > 0.0);
+    if (conv || brk || it >= P.max_it) {
+      const bool ill = !conv && brk && !isfinite(alpha);
+      const bool done = conv || brk;
+      if (act) {
+        if (own) g.st[V_N * o + V_X] = v[V_X];
+        if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, cl, lane, r, q, own, o, row, v[V_X], ill, it, bb);
+      }
+      if (lead && !g.flags[F_STOPPED] && (done || g.fuse)) {
+        g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
+        if (ill) g.flags[F_ILL] = 1;
+        host_flag(g.hflags, H_PCG_IT, it);
+        __hip_atomic_store(g.hflags + H_DONE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (lead) g.flags[F_PCG_CNT] = it;
+      break;
+    }
+    rgam = 1.0 / gam;
+    ralpha = 1.0 / alpha;
+    // ---- recurrences (own components), m_{it+1} = M⁻¹ w_new (cluster-local, LDS), published at once
+    const uint32_t tag1 = persist_tag(P.epoch, it + 1);
+    if (act) {
+      double d[3] = {0.0, 0.0, 0.0};
+      const double zz = fma(beta, v[V_Z], nc);
+      const double qq = fma(beta, v[V_Q], mown);
+      const double sv = fma(beta, v[V_S], v[V_W]);
+      const double p = fma(beta, v[V_P], v[V_U]);
+      const double rn = fma(-alpha, sv, v[V_R]);
+      const double un = fma(-alpha, qq, v[V_U]);
+      const double w2 = fma(-alpha, zz, v[V_W]);
+      v[V_X] = fma(alpha, p, v[V_X]); v[V_R] = rn; v[V_U] = un; v[V_Z] = zz; v[V_Q] = qq; v[V_S] = sv; v[V_P] = p;
+      v[V_W] = w2;
+      if (own) {
+        s_v[w][6 * r + q] = w2;
+        d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
+      }
+      wave_lds_sync();
+      if (own) {
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < kCD / 4; ++k) {
+          a4[0] = fma((double)mr[k].x, s_v[w][4 * k], a4[0]);
+          a4[1] = fma((double)mr[k].y, s_v[w][4 * k + 1], a4[1]);
+          a4[2] = fma((double)mr[k].z, s_v[w][4 * k + 2], a4[2]);
+          a4[3] = fma((double)mr[k].w, s_v[w][4 * k + 3], a4[3]);
+        }
+        mown = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        st_gran_double(P.mgr + ((size_t)((it + 1) & 1) * n6 + o) * 2, tag1, mown);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
+      if (lane == 0) { s_part[w][0] = d[0]; s_part[w][1] = d[1]; s_part[w][2] = d[2]; }
+      OFX_PSTAMP(w == 0, 5)
+    }
+    __syncthreads();   // the clusters' partials -> compute wave 0 publishes the workgroup's before it gathers again
+    OFX_PSTAMP(w == 0, 6)
+    if (w == 0 && lane < 3) {
+      double sum = 0.0;
+      for (int c = 0; c < ncl; ++c) sum += s_part[c][lane];
+      st_gran_double(P.gran + ((size_t)((it + 1) & 1) * P.G + wg) * 8 + 2 * lane, tag1, sum);
+    }
+    OFX_PSTAMP(w == 0, 7)
+  }
+}
+
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
 // if accepted, the kornia 0.7.0 angle_axis_to_rotation_matrix + left-multiplicative update
 // (model.py:744-748) — one launch. Every workgroup derives the same decision from read-only inputs
@@ -1954,7 +2287,8 @@ static void free_all(Gn* g) {
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
-                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off};
+                  g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
+                  g->p_wg_cl, g->p_mgr, g->p_gran, g->p_abort};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -2110,13 +2444,33 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // before each chunk's end — 690.5 instead of 694.3 launches per frame, but 5.15 instead of 5.06-5.12 us per
   // launch with the marker in the stream: -0.5 %, A/B x3.)
   volatile int32_t* hf = g->host_flags;
-  hf[H_DONE] = 0;   // the previous step's converged launch has run (we saw it); prep also clears it
   PcgIt pa = pcg_args(g);
   // the converging launch also takes the GN step (not when arap's null-space projection must run first)
   pa.fuse = g->n_comp == 0 ? 1 : 0;
   pa.gn_iter = gn_iter;
   pa.tail = rhs + 6 * (int64_t)g->N;
   g->step_fused = false;
+  if (g->p_on) {   // the whole solve in one launch (k_pcg_persist); no host polling, nothing drains
+    PcgPersist pp;
+    pp.b = pa;
+    pp.wg_cl = g->p_wg_cl; pp.mgr = g->p_mgr; pp.gran = g->p_gran; pp.abort_word = g->p_abort;
+    pp.G = g->p_G; pp.max_it = max_it; pp.lds_blocks = g->p_lds_blocks; pp.C = g->p_C;
+    if (++g->p_epoch >= (1u << 20)) {   // tag space wrapped: clear the granules once
+      OFX_HIP(hipMemsetAsync(g->p_gran, 0, (size_t)2 * kPersistMaxG * 8 * sizeof(unsigned long long), hs));
+      OFX_HIP(hipMemsetAsync(g->p_mgr, 0, (size_t)2 * 6 * g->max_pad * 2 * sizeof(unsigned long long), hs));
+      g->p_epoch = 1;
+    }
+    pp.epoch = g->p_epoch;
+    const size_t lds = (size_t)g->p_lds_blocks * (36 * sizeof(double) + sizeof(int32_t));
+    hipLaunchKernelGGL(k_pcg_persist, dim3(g->p_G), dim3(64 * (g->p_C + 1)), lds, hs, pp);
+    OFX_LAUNCH_CHECK();
+    if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
+    g->step_fused = pa.fuse != 0;
+    g->n_iter_launches += 1;
+    if (g->timing) g->ev.emplace_back(e0, e1);
+    return OFX_OK;
+  }
+  hf[H_DONE] = 0;   // the previous step's converged launch has run (we saw it); prep also clears it
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
@@ -2237,9 +2591,31 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->part_p, (6 * max_ns > kProjP * max_row_wg ? 6 * max_ns : kProjP * max_row_wg)); ALLOC(g->part_b, max_ns);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
+  ALLOC(g->p_wg_cl, N / kCS + 2); ALLOC(g->p_mgr, 2 * 6 * N * 2); ALLOC(g->p_gran, 2 * kPersistMaxG * 8); ALLOC(g->p_abort, 1);
 #undef ALLOC
-  if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess) {   // pattern entries are cleared per setup
+  if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess ||   // pattern entries are cleared per setup
+      hipMemset(g->p_gran, 0, (size_t)2 * kPersistMaxG * 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(g->p_mgr, 0, (size_t)2 * 6 * N * 2 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(g->p_abort, 0, sizeof(int32_t)) != hipSuccess) {
     free_all(g); delete g; set_error("hipMemset failed"); return OFX_ERR_HIP;
+  }
+  {   // persistent PCG: CU count (all workgroups must be resident), dynamic LDS beyond the default 64 KB;
+      // OFX_PCG_PERSIST=1 selects it (default: the per-iteration launches), OFX_PCG_PERSIST_C=<1..4> sets the
+      // clusters per workgroup
+    int dev = 0;
+    const char* e = getenv("OFX_PCG_PERSIST");
+    g->p_disabled = !(e && strcmp(e, "1") == 0);
+    if (const char* c = getenv("OFX_PCG_PERSIST_C")) {
+      const int v = atoi(c);
+      if (v >= 1 && v <= kPersistMaxC) g->p_C = v;
+    }
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g->p_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_pcg_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kPersistLds) != hipSuccess) {
+      g->p_disabled = true;
+      (void)hipGetLastError();
+    }
   }
   if (hipHostMalloc((void**)&g->host_flags, H_COUNT * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess ||
@@ -2298,6 +2674,16 @@ int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && waves, "null handle/waves");
   *waves = (g->pcg_w2 && g->pcg_ku == 3) ? 2 : 1;   // the last setup's form (two only up to 384 clusters)
+  return OFX_OK;
+}
+
+int ofx_gn_pcg_form(void* handle, int32_t* form) {
+  Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
+  OFX_CHECK_ARG(g && form, "null handle/form");
+  form[0] = g->p_on ? 1 : 0;
+  form[1] = g->p_on ? g->p_G : 0;
+  form[2] = g->p_C;
   return OFX_OK;
 }
 
@@ -2596,11 +2982,18 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N);
   hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
-  int32_t nnz = 0, lens[2] = {0, 0}, gdiff = 0;
+  int32_t nnz = 0, lens[2] = {0, 0}, gdiff = 0, aborted = 0;
+  std::vector<int32_t> hrp(N + 1);   // row pointers: the persistent PCG's cluster -> workgroup partition
   OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipMemcpyAsync(lens, g->row_cnt + N, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipMemcpyAsync(hrp.data(), g->row_ptr, (N + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  OFX_HIP(hipMemcpyAsync(&aborted, g->p_abort, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   if (optimistic) OFX_HIP(hipMemcpyAsync(&gdiff, g->d_gdiff, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
   OFX_HIP(hipStreamSynchronize(hs));
+  if (aborted) {   // a persistent solve timed out earlier (it marked itself ill-posed): per-iteration launches from now on
+    g->p_disabled = true;
+    OFX_HIP(hipMemsetAsync(g->p_abort, 0, sizeof(int32_t), hs));
+  }
   if (gdiff) {   // the graph changed: clear the slot map marked with the stale order and start over
     OFX_HIP(hipMemsetAsync(g->map, 0, (size_t)g->max_pad * g->max_pad * sizeof(int32_t), hs));
     g->pat_N = 0;
@@ -2610,6 +3003,36 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   }
   g->max_deg = lens[0];
   g->max_wave = lens[1];
+  {   // persistent PCG: consecutive clusters (one wave each) packed into workgroups of <= p_C clusters whose A blocks
+      // fit the LDS budget; enabled when every row fits three lane passes and all workgroups can be resident
+    const int nc = N / kCS;
+    const int budget = kPersistLds / (int)(36 * sizeof(double) + sizeof(int32_t));
+    g->h_wg_cl.assign(1, 0);
+    int cur = 0, n_in = 0, maxb = 0;
+    bool fits = true;
+    for (int c = 0; c < nc; ++c) {
+      const int bc = hrp[(c + 1) * kCS] - hrp[c * kCS];
+      fits = fits && bc <= budget;
+      if (n_in == g->p_C || (n_in > 0 && cur + bc > budget)) {
+        g->h_wg_cl.push_back(c);
+        maxb = cur > maxb ? cur : maxb;
+        cur = 0;
+        n_in = 0;
+      }
+      cur += bc;
+      ++n_in;
+    }
+    g->h_wg_cl.push_back(nc);
+    maxb = cur > maxb ? cur : maxb;
+    g->p_G = (int)g->h_wg_cl.size() - 1;
+    g->p_lds_blocks = maxb;
+    const int cap = g->p_cus < kPersistMaxG ? g->p_cus : kPersistMaxG;
+    g->p_on = !g->p_disabled && fits && nc > 0 && g->max_deg <= kPersistRowMax && g->max_wave <= kWL && g->p_G <= cap &&
+              prm->pcg_max_iter < 4096;
+    if (g->p_on)
+      OFX_HIP(hipMemcpyAsync(g->p_wg_cl, g->h_wg_cl.data(), g->h_wg_cl.size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, hs));
+  }
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
     for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->blk_off,
                     (void**)&g->blk_cnt})

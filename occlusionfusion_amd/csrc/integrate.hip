@@ -727,12 +727,30 @@ __global__ __launch_bounds__(256) void k_deform_lbs(const float* __restrict__ pt
   out[3 * p] = ox; out[3 * p + 1] = oy; out[3 * p + 2] = oz;
 }
 
+// F32: the projection of f32 points as numba types cam2pix on an f32 array (tsdf.py:351-364 called from
+// get_visible_nodes with the f32 deformed nodes, tsdf.py:614-638): (x·fx)/z + cx in f32 with the f32 intrinsics,
+// np.round (half-even) in f32, int(); the depth lookup and the difference stay f64 as get_depth_from_image's
+// np.zeros array makes them (tsdf.py:576-612). F32 = false: the f64 form of the integrate path (f64 cam_pts).
+__device__ __forceinline__ int64_t project_f32(const CamD& c, float x, float y, float z) {
+  const float su = cdiv(x * c.fxf, z) + c.cxf, sv = cdiv(y * c.fyf, z) + c.cyf;
+  const float u = rintf(su), v = rintf(sv);
+  if (!(u >= 0.0f && u < (float)c.W && v >= 0.0f && v < (float)c.H && z > 0.0f)) return -1;
+  return (int64_t)v * c.W + (int64_t)u;
+}
+
+template <bool F32>
 __global__ void k_visibility(const float* __restrict__ pts, int64_t n, CamD c, const float* __restrict__ depth,
                              double trunc, uint8_t* __restrict__ valid, double* __restrict__ ddiff) {
   int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (p >= n) return;
   double Z;
-  int64_t pix = project(c, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], Z);
+  int64_t pix;
+  if (F32) {
+    Z = pts[3 * p + 2];
+    pix = project_f32(c, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]);
+  } else {
+    pix = project(c, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], Z);
+  }
   double dv = pix >= 0 ? (double)depth[pix] : 0.0;
   double dd = dv - Z;
   valid[p] = (dv > 0.0 && dd >= -trunc) ? 1 : 0;
@@ -945,7 +963,18 @@ int ofx_visibility(const float* points, int64_t n_points, const ofx_camera* cam,
   OFX_CHECK_ARG(cam && n_points >= 0, "bad args");
   if (n_points == 0) return OFX_OK;
   OFX_CHECK_ARG(points && depth && valid, "null buffer");
-  hipLaunchKernelGGL(k_visibility, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
+  hipLaunchKernelGGL(k_visibility<false>, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
+                     n_points, make_cam(cam), depth, trunc_margin, valid, depth_diff);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_visibility_f32(const float* points, int64_t n_points, const ofx_camera* cam, const float* depth,
+                       double trunc_margin, uint8_t* valid, double* depth_diff, ofx_stream_t s) {
+  OFX_CHECK_ARG(cam && n_points >= 0, "bad args");
+  if (n_points == 0) return OFX_OK;
+  OFX_CHECK_ARG(points && depth && valid, "null buffer");
+  hipLaunchKernelGGL(k_visibility<true>, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
                      n_points, make_cam(cam), depth, trunc_margin, valid, depth_diff);
   OFX_LAUNCH_CHECK();
   return OFX_OK;

@@ -115,6 +115,13 @@ class GaussNewtonSolver:
         call("ofx_gn_pcg_waves", self._h, byref(w))
         return w.value
 
+    def pcg_form(self):
+        """(persistent, workgroups, clusters per workgroup) of the last setup's PCG: persistent = one k_pcg_persist
+        launch per GN step, else one k_pcg_iter launch per iteration (include/ofx.h ofx_gn_pcg_form)."""
+        f = (ctypes.c_int32 * 3)()
+        call("ofx_gn_pcg_form", self._h, f)
+        return bool(f[0]), int(f[1]), int(f[2])
+
     def row_order(self):
         """PCG row -> node of the last setup (-1: padding row); the order of rhs / the state rows."""
         rows = self.info()[4]

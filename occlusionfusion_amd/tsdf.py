@@ -288,20 +288,27 @@ class TSDFVolume:
         return self._world_pts
 
     def check_visibility(self, points):
-        """tsdf.py:599-612 -> (valid bool (P,), depth_diff f64 (P,))."""
-        pts = torch.as_tensor(np.ascontiguousarray(points, np.float32), device=self.device)
+        """tsdf.py:599-612 -> (valid bool (P,), depth_diff f64 (P,)). numba types cam2pix by the array it gets
+        (tsdf.py:351-364): float32 points (get_visible_nodes' deformed nodes) project in f32 (ofx_visibility_f32),
+        float64 points (the integrate path's rigid_transform output) in f64 (ofx_visibility; their values must be
+        f32-representable, as vox2world / ED-warp positions are)."""
+        f32 = isinstance(points, np.ndarray) and points.dtype == np.float32 or (
+            isinstance(points, torch.Tensor) and points.dtype == torch.float32)
+        pts = torch.as_tensor(np.ascontiguousarray(points, np.float32) if isinstance(points, np.ndarray) else points,
+                              device=self.device).to(torch.float32).contiguous()
         P = pts.shape[0]
         valid = torch.empty(P, dtype=torch.uint8, device=self.device)
         dd = torch.empty(P, dtype=torch.float64, device=self.device)
         cam = self.camera()
-        call("ofx_visibility", ptr(pts), P, byref(cam), ptr(self.depth_t), float(self._trunc_margin), ptr(valid),
-             ptr(dd), stream_ptr())
+        call("ofx_visibility_f32" if f32 else "ofx_visibility", ptr(pts), P, byref(cam), ptr(self.depth_t),
+             float(self._trunc_margin), ptr(valid), ptr(dd), stream_ptr())
         return valid.cpu().numpy().astype(bool), dd.cpu().numpy()
 
     def get_visible_nodes(self):
-        """tsdf.py:614-638 (without the .npy side file)."""
+        """tsdf.py:614-638 (without the .npy side file): the warp field's f32 deformed nodes (g + T) checked
+        against this frame's depth with the f32 projection numba gives them."""
         assert self.warpfield.frame_id == self.frame_id
-        visible, _ = self.check_visibility(self.warpfield.get_deformed_nodes())
+        visible, _ = self.check_visibility(np.asarray(self.warpfield.get_deformed_nodes(), np.float32))
         return visible
 
     # ------------------------------------------------------------------ surface extraction (SURVEY §8(f) row 1)

@@ -234,6 +234,27 @@ def check_visibility(cam_pts_f64, depth_im, intr, trunc=TRUNC_MARGIN):
     return valid_pts, depth_diff, pxi, pyi
 
 
+def check_visibility_f32(points_f32, depth_im, intr, trunc=TRUNC_MARGIN):
+    """tsdf.py:599-612 on an f32 point array (get_visible_nodes, tsdf.py:614-638): numba types cam2pix
+    (tsdf.py:351-364) in f32 — (x·fx)/z + cx with f32 intrinsics, np.round half-even in f32, int() — while
+    get_depth_from_image's depth array is f64 (np.zeros), so depth_diff = f64(depth) - f32 z. -> (valid, depth_diff)."""
+    p = np.asarray(points_f32, F32)
+    fx, fy, cx, cy = (F32(v) for v in intr)
+    H, W = depth_im.shape
+    with np.errstate(divide='ignore', invalid='ignore', over='ignore'):
+        su = ((p[:, 0] * fx) / p[:, 2] + cx).astype(F32)
+        sv = ((p[:, 1] * fy) / p[:, 2] + cy).astype(F32)
+        u, v = np.rint(su), np.rint(sv)
+    z = p[:, 2]
+    valid_pix = (u >= 0) & (u < W) & (v >= 0) & (v < H) & (z > 0)
+    ui = np.where(valid_pix, u, 0).astype(np.int64)
+    vi = np.where(valid_pix, v, 0).astype(np.int64)
+    depth_val = np.zeros(p.shape[0], F64)
+    depth_val[valid_pix] = depth_im[vi[valid_pix], ui[valid_pix]]
+    depth_diff = depth_val - z
+    return (depth_val > 0) & (depth_diff >= -trunc), depth_diff
+
+
 def integrate(tsdf, weight, color, pts, valid_points, depth_im, color_im, intr,
               obs_weight=1.0, trunc=TRUNC_MARGIN, with_color=True):
     """In-place CPU integrate over flat f32 volumes (V,). Returns number of updated voxels.

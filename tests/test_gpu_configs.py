@@ -141,11 +141,12 @@ def test_gn_1k_every_partial_width_matches_dense_oracle(cuda, ku, monkeypatch):
     waves per cluster."""
     from occlusionfusion_amd import GaussNewtonSolver
     monkeypatch.setenv("OFX_PCG_KU", str(ku))
+    monkeypatch.setenv("OFX_PCG_PERSIST", "0")          # the per-iteration launch form (k_pcg_iter)
     g = np.load(os.path.join(GOLDEN, "gn_1k.npz"), allow_pickle=False)
     s = GaussNewtonSolver(g["nodes"].shape[0], 10000)
     out = s.optimize(g["nodes"], g["edges"], g["edge_weights"], g["tpos"], g["conf"], g["src"], g["anchors"],
                      g["weights"], g["tgt"], g["intr"])
-    assert s.pcg_waves() == (2 if ku == 3 else 1)
+    assert s.pcg_waves() == (2 if ku == 3 else 1) and s.pcg_form()[0] is False
     assert out["valid_solve"] == 1
     dr = np.abs(out["node_rotations"].cpu().numpy() - g["R"]).max()
     dt = np.abs(out["node_translations"].cpu().numpy() - g["t"]).max()

@@ -9,6 +9,8 @@ reference's dense LU), from committed fixtures made by tests/golden/make_golden.
   loaded from frame 10's device result) and inline; transforms within 1e-5, the per-step loss log within 1e-6
   relative.
 * gn_4k.npz — BASELINE config 4's graph (~4k nodes), frame 10.
+* Both PCG forms — one persistent launch per GN step (k_pcg_persist, the default) and one launch per iteration
+  (k_pcg_iter, OFX_PCG_PERSIST=0) — meet the same bars on gn_2k, and the persistent solve is bitwise repeatable.
 * The device graph builder (synthetic.depth_graph: EDGraph.from_mesh on the depth mesh) reproduces the fixture's
   graph (the bench's graph) exactly.
 """
@@ -51,10 +53,10 @@ def _check(out, g, q):
     return dr, dt
 
 
-def _chain(g, cuda, prefetch):
+def _chain(g, cuda, prefetch, n_frames=None):
     from occlusionfusion_amd import GaussNewtonSolver
     N = g["nodes"].shape[0]
-    frames = [_frame(g, q, cuda) for q in range(len(g["frames"]))]
+    frames = [_frame(g, q, cuda) for q in range(n_frames or len(g["frames"]))]
     probs = [_problem(g, f, cuda) for f in frames]
     s = GaussNewtonSolver(N, 10000)
     intr = tuple(float(v) for v in g["intr"])
@@ -105,3 +107,19 @@ def test_gn_4k_matches_oracle(cuda):
     assert 3500 <= g["nodes"].shape[0] <= 4600
     _, outs = _chain(g, cuda, prefetch=False)
     _check(outs[0], g, 0)
+
+
+@pytest.mark.parametrize("persist", ["1", "0"])
+def test_gn_2k_both_pcg_forms_match_oracle(cuda, persist, monkeypatch):
+    monkeypatch.setenv("OFX_PCG_PERSIST", persist)
+    g = _load("gn_2k.npz")
+    s, outs = _chain(g, cuda, prefetch=False, n_frames=1)
+    form = s.pcg_form()
+    assert form[0] is (persist == "1")
+    if form[0]:
+        assert 1 <= form[1] <= 128 and form[2] == 4
+    _check(outs[0], g, 0)
+    if persist == "1":   # bitwise repeatable: fixed-order sums whatever the workgroup placement and timing
+        _, again = _chain(g, cuda, prefetch=False, n_frames=1)
+        assert torch.equal(outs[0]["node_rotations"], again[0]["node_rotations"])
+        assert torch.equal(outs[0]["node_translations"], again[0]["node_translations"])

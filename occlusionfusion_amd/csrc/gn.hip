@@ -1843,7 +1843,8 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 // back to back on this part (tools/sync_micro.hip), the iteration kernel 5.1 us. Here every workgroup keeps its
 // clusters' A blocks in LDS, its rows' recurrence state and cluster-inverse rows in registers for the whole solve,
 // and only m (48 doubles per cluster) and the three dot-product partials (per workgroup) cross workgroups:
-//  * workgroup = up to kPersistMaxC compute waves (one cluster each) + one poll wave; G <= 128 workgroups (two
+//  * workgroup = up to kPersistMaxC waves (one cluster each; at most one wave per SIMD, so the kernel has the
+//    whole register file: a fifth, polling wave capped it at 256 VGPRs and spilled); G <= 128 workgroups (two
 //    producers per lane in the partial sweep), all co-resident (host: G <= CUs, one workgroup's LDS per CU);
 //  * SpMV as the iteration kernel's wave-list form: lane l multiplies the cluster's blocks l and l + 64 (balanced
 //    whatever the row lengths), the products meet in LDS and each row sums its blocks in CSR order; the cluster's
@@ -1853,9 +1854,9 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 //    8-byte granules {tag | 32-bit half}, each written by one sc1 store and read by sc1 loads until the tag matches.
 //    m_{it+1} (per row component) is published as soon as M⁻¹ has produced it, the workgroup's partials of
 //    iteration it + 1 (its clusters summed in order) right after;
-//  * iteration it: the compute waves gather m_it of their blocks' columns (spinning on the granules of just those
-//    rows) and multiply from LDS while the poll wave sweeps every workgroup's partials — the neighbour hop and the
-//    global reduction overlap; one barrier hands the scalars to the compute waves;
+//  * iteration it: every wave gathers m_it of its blocks' columns (spinning on the granules of just those rows) and
+//    multiplies from LDS; wave 0 then sweeps every workgroup's partials (published with the m granules, so the
+//    global reduction overlaps the neighbour hop and the SpMV); one barrier hands the scalars to every wave;
 //  * m and the partials are double-buffered by iteration parity: a producer writes iteration it + 2 only after it
 //    has seen every workgroup's partials of it + 1, which each consumer publishes after it has read iteration it;
 //  * tags = (launch epoch << 12) | iteration: no per-launch memset, stale granules never match;
@@ -1913,7 +1914,7 @@ __device__ __forceinline__ bool persist_give_up(const PcgPersist& P, unsigned sp
 #else
 #define OFX_PSTAMP(cond, k)
 #endif
-__global__ __launch_bounds__(64 * (kPersistMaxC + 1)) void k_pcg_persist(PcgPersist P) {
+__global__ __launch_bounds__(64 * kPersistMaxC) void k_pcg_persist(PcgPersist P) {
   extern __shared__ double s_A[];                 // the workgroup's A blocks (CSR order), then their columns
   __shared__ double s_v[kPersistMaxC][kCD];
   __shared__ double s_sc[4];                      // gamma, delta, r.r of the iteration; |b|^2
@@ -1925,7 +1926,7 @@ __global__ __launch_bounds__(64 * (kPersistMaxC + 1)) void k_pcg_persist(PcgPers
   const int wg = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   if (g.flags[F_STOPPED]) return;                 // the solve already stopped: this GN step is a no-op (uniform)
   const int c0 = P.wg_cl[wg], c1 = P.wg_cl[wg + 1], ncl = c1 - c0;
-  const bool poller = w == P.C;                   // the workgroup's poll wave (no cluster)
+  const bool poller = w == 0;                     // compute wave 0 also sweeps the partials (after its SpMV)
   const bool act = w < ncl;
   const int cl = c0 + (act ? w : 0);
   const int r = lane / kSL, q = lane % kSL, row = cl * kRW + r;
@@ -2013,7 +2014,7 @@ __global__ __launch_bounds__(64 * (kPersistMaxC + 1)) void k_pcg_persist(PcgPers
             if (lane == 0) s_abort = 1;
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+          __builtin_amdgcn_s_sleep(2);
         }
       }
       OFX_PSTAMP(w == 0, 1)
@@ -2155,6 +2156,8 @@ __global__ __launch_bounds__(64 * (kPersistMaxC + 1)) void k_pcg_persist(PcgPers
       for (int c = 0; c < ncl; ++c) sum += s_part[c][lane];
       st_gran_double(P.gran + ((size_t)((it + 1) & 1) * P.G + wg) * 8 + 2 * lane, tag1, sum);
     }
+    // the partial stores leave before the other waves' next gather loads fill this CU's memory queue
+    __syncthreads();
     OFX_PSTAMP(w == 0, 7)
   }
 }
@@ -2462,7 +2465,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     pp.epoch = g->p_epoch;
     const size_t lds = (size_t)g->p_lds_blocks * (36 * sizeof(double) + sizeof(int32_t));
-    hipLaunchKernelGGL(k_pcg_persist, dim3(g->p_G), dim3(64 * (g->p_C + 1)), lds, hs, pp);
+    hipLaunchKernelGGL(k_pcg_persist, dim3(g->p_G), dim3(64 * g->p_C), lds, hs, pp);
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     g->step_fused = pa.fuse != 0;

@@ -16,8 +16,10 @@
 //   R ← exp([x_ω]) R (kornia 0.7 angle_axis_to_rotation_matrix), t += x_t (model.py:744-748).
 //
 // MI355X design.
-//  * Every residual row-triple is a "term" (data: 4 anchored nodes, ARAP edge: 2, motion: 1) whose
-//    3x6 Jacobian blocks are written to a scratch array once per GN iteration (k_terms).
+//  * Every residual row-triple is a "term" (data: 4 anchored nodes, ARAP edge: 2, motion: 1). Once per GN
+//    iteration k_terms writes each term's compact record (kRec doubles: the per-anchor vectors and the
+//    term's shared scalars, not its four 3x6 Jacobian blocks); the assembly expands a record into the
+//    blocks it needs with the same arithmetic, so A and b are the bits the blocks themselves gave.
 //  * JᵀJ lives as 6x6 f64 blocks in BSR over the node adjacency (diagonal, edges, co-anchored
 //    pairs). Per solve, each block gets a sorted list of the (term, p, q) products that land on it,
 //    so assembly is a deterministic gather: one wave per block, lane = block entry (k_blocks); the
@@ -75,7 +77,7 @@ struct GnDev {
   int32_t *anc = nullptr, *edges = nullptr;
   // terms
   int32_t* term_node = nullptr;  // T*4, -1 = unused entry
-  double* J = nullptr;           // T*4*18
+  double* J = nullptr;           // T·kRec term records (k_terms)
   double* res = nullptr;         // T*3
   int64_t T_cap = 0;
   // pattern + contribution lists
@@ -553,30 +555,79 @@ struct DataCoef {
   double lf, ld, la, lm, fx, fy, cx, cy;
 };
 
-__device__ void data_jacobian(const GnDev& g, const DataCoef& dc, int64_t m, int k, const double p[3], double zinv,
-                              double* __restrict__ J) {
+// Compact term records (kRec doubles per term at J + t·kRec; 160 B against the 576 B of four 3x6 blocks):
+//   data  : [v_k w_k] for anchors k = 0..3 (v_k = w_k R_k(x - g_k)) at 4k, then [fx/z fy/z mfx mfy] at 16
+//   ARAP  : [d0 d1 d2 s] at 0 (node i: d = R_i(g_j - g_i), s = la·w_e), node j's diagonal -s at 4
+//   motion: the three diagonal entries at 0
+// term_block() expands (record, slot) into the 3x6 block with the arithmetic the blocks were written with,
+// operation for operation, so the assembled A and b are the same bits.
+constexpr int kRec = 20;
+
+// slot k of data term m: its anchor's [v w]; slot 0 also the term's shared scalars
+__device__ __forceinline__ void data_record(const GnDev& g, const DataCoef& dc, int64_t m, int k, const double p[3],
+                                            double zinv, double* __restrict__ rec) {
   int a = g.anc[m * 4 + k];
   double w = g.wts[m * 4 + k];
   const double* R = g.R + 9 * (int64_t)a;
   const double* gn = g.nodes + 3 * (int64_t)a;
   double d0 = g.src[3 * m] - gn[0], d1 = g.src[3 * m + 1] - gn[1], d2 = g.src[3 * m + 2] - gn[2];
-  double v0 = w * (R[0] * d0 + R[1] * d1 + R[2] * d2);
-  double v1 = w * (R[3] * d0 + R[4] * d1 + R[5] * d2);
-  double v2 = w * (R[6] * d0 + R[7] * d1 + R[8] * d2);
-  // S = -[v]x
-  const double S[9] = {0.0, v2, -v1, -v2, 0.0, v0, v1, -v0, 0.0};
-  double fxdz = dc.fx * zinv, fydz = dc.fy * zinv;
-  double mfx = -(dc.fx * p[0] * zinv) * zinv;
-  double mfy = -(dc.fy * p[1] * zinv) * zinv;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    J[0 + j] = dc.lf * fxdz * S[0 + j] + mfx * S[6 + j] + dc.ld * S[0 + j];
-    J[6 + j] = dc.lf * fydz * S[3 + j] + mfy * S[6 + j] + dc.ld * S[3 + j];
-    J[12 + j] = dc.ld * S[6 + j];
+  double2* o = reinterpret_cast<double2*>(rec + 4 * k);
+  o[0] = make_double2(w * (R[0] * d0 + R[1] * d1 + R[2] * d2), w * (R[3] * d0 + R[4] * d1 + R[5] * d2));
+  o[1] = make_double2(w * (R[6] * d0 + R[7] * d1 + R[8] * d2), w);
+  if (k == 0) {
+    double2* tl = reinterpret_cast<double2*>(rec + 16);
+    tl[0] = make_double2(dc.fx * zinv, dc.fy * zinv);
+    tl[1] = make_double2(-(dc.fx * p[0] * zinv) * zinv, -(dc.fy * p[1] * zinv) * zinv);
   }
-  J[3] = dc.lf * w * fxdz + dc.ld * w; J[4] = 0.0; J[5] = dc.lf * w * mfx;
-  J[9] = 0.0; J[10] = dc.lf * w * fydz + dc.ld * w; J[11] = dc.lf * w * mfy;
-  J[15] = 0.0; J[16] = 0.0; J[17] = dc.ld * w;
+}
+
+enum TermKind { kData = 0, kEdge = 1, kMotion = 2 };
+__device__ __forceinline__ int term_kind(const GnDev& g, int64_t t) {
+  return t < g.M ? kData : (t < g.M + (int64_t)g.N * g.NB ? kEdge : kMotion);
+}
+
+// the 3x6 block of `slot` from the record's words x = rec[4·slot .. +3] and (data) tail = rec[16 .. 19]
+__device__ __forceinline__ void term_block(int kind, int slot, const double x[4], const double tail[4],
+                                           const DataCoef& dc, double J[18]) {
+#pragma unroll
+  for (int c = 0; c < 18; ++c) J[c] = 0.0;
+  if (kind == kData) {
+    const double v0 = x[0], v1 = x[1], v2 = x[2], w = x[3];
+    const double fxdz = tail[0], fydz = tail[1], mfx = tail[2], mfy = tail[3];
+    // S = -[v]x
+    const double S[9] = {0.0, v2, -v1, -v2, 0.0, v0, v1, -v0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      J[0 + j] = dc.lf * fxdz * S[0 + j] + mfx * S[6 + j] + dc.ld * S[0 + j];
+      J[6 + j] = dc.lf * fydz * S[3 + j] + mfy * S[6 + j] + dc.ld * S[3 + j];
+      J[12 + j] = dc.ld * S[6 + j];
+    }
+    J[3] = dc.lf * w * fxdz + dc.ld * w; J[5] = dc.lf * w * mfx;
+    J[10] = dc.lf * w * fydz + dc.ld * w; J[11] = dc.lf * w * mfy;
+    J[17] = dc.ld * w;
+  } else if (kind == kEdge && slot == 0) {   // node i: [-s[d]x | s I]
+    const double d0 = x[0], d1 = x[1], d2 = x[2], s = x[3];
+    J[1] = s * d2; J[2] = -s * d1; J[3] = s;
+    J[6] = -s * d2; J[8] = s * d0; J[10] = s;
+    J[12] = s * d1; J[13] = -s * d0; J[17] = s;
+  } else if (kind == kEdge) {                 // node j: [0 | -s I]
+    J[3] = x[0]; J[10] = x[0]; J[17] = x[0];
+  } else {
+    J[3] = x[0]; J[10] = x[1]; J[17] = x[2];
+  }
+}
+
+// the record words of (t, slot): two 16-B loads, plus two for a data term's tail
+__device__ __forceinline__ void load_record(const GnDev& g, int64_t t, int slot, int kind, double x[4], double tail[4]) {
+  const double2* r = reinterpret_cast<const double2*>(g.J + t * kRec);
+  const double2 a = r[2 * slot], b = r[2 * slot + 1];
+  x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+  if (kind == kData) {
+    const double2 c = r[8], d = r[9];
+    tail[0] = c.x; tail[1] = c.y; tail[2] = d.x; tail[3] = d.y;
+  } else {
+    tail[0] = tail[1] = tail[2] = tail[3] = 0.0;
+  }
 }
 
 // Anchor k's summand of the deformed point of match m: w_k (R_k (x - g_k) + g_k + t_k) (ED_warp, geometry.py:9-25)
@@ -592,11 +643,10 @@ __device__ __forceinline__ void anchor_term(const GnDev& g, int64_t m, int k, do
   c[2] = w * ((R[6] * d0 + R[7] * d1 + R[8] * d2) + gn[2] + tt[2]);
 }
 
-// Four threads per term (t = id/4, slot k = id%4): slot k writes the 3x6 Jacobian block of the
-// term's k-th node; slot 0 also writes the residual triple and the loss partials. Data slots each
-// recompute the deformed point (identical bits) so the four anchor Jacobians run in parallel.
-// Terms outside this rank's share (data matches outside [m0,m1), regularisers when !add_reg) are
-// written as exact zeros so the fixed contribution lists stay valid.
+// Four threads per term (t = id/4, slot k = id%4): slot k writes its node's words of the term record
+// (kRec above); slot 0 also writes the residual triple and the loss partials. Terms outside this rank's
+// share (data matches outside [m0,m1), regularisers when !add_reg) get all-zero records (exact zero
+// blocks) so the fixed contribution lists stay valid.
 __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, int m1, int add_reg) {
   const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t t = id >> 2;
@@ -605,7 +655,7 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
   double l2[3] = {0.0, 0.0, 0.0};
   double bad = 0.0;
   if (t < g.T) {
-    double* J = g.J + t * 72 + 18 * k;
+    double* rec = g.J + t * kRec;
     if (t < g.M) {
       if (t >= m0 && t < m1) {
         // deformed point: slot k computes its anchor's summand, the four slots (adjacent lanes of one wave, all
@@ -623,7 +673,7 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
 #pragma unroll
           for (int d = 0; d < 3; ++d) p[d] += __shfl(c[d], base + kk, 64);
         double zinv = 1.0 / (p[2] + 1e-7);
-        data_jacobian(g, dc, t, k, p, zinv, J);
+        data_record(g, dc, t, k, p, zinv, rec);
         if (k == 0) {
           r[0] = dc.lf * (dc.fx * p[0] * zinv + dc.cx - tpx) + dc.ld * (p[0] - tg0);
           r[1] = dc.lf * (dc.fy * p[1] * zinv + dc.cy - tpy) + dc.ld * (p[1] - tg1);
@@ -631,8 +681,9 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
           l2[0] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
         }
       } else {
-#pragma unroll
-        for (int c = 0; c < 18; ++c) J[c] = 0.0;
+        double2* o = reinterpret_cast<double2*>(rec + 4 * k);
+        o[0] = o[1] = make_double2(0.0, 0.0);
+        if (k == 0) reinterpret_cast<double2*>(rec + 16)[0] = reinterpret_cast<double2*>(rec + 16)[1] = make_double2(0.0, 0.0);
       }
     } else if (t < g.M + (int64_t)g.N * g.NB) {
       const int64_t e = t - g.M;
@@ -654,38 +705,35 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
             r[0] = s * (d0 + gi[0] + ti[0] - (gj[0] + tj[0]));
             r[1] = s * (d1 + gi[1] + ti[1] - (gj[1] + tj[1]));
             r[2] = s * (d2 + gi[2] + ti[2] - (gj[2] + tj[2]));
-            // node i: [-s[d]x | s I]
-            const double Ji[18] = {0.0, s * d2, -s * d1, s, 0, 0, -s * d2, 0.0, s * d0, 0, s, 0, s * d1, -s * d0, 0.0, 0, 0, s};
-#pragma unroll
-            for (int c = 0; c < 18; ++c) J[c] = Ji[c];
+            double2* o = reinterpret_cast<double2*>(rec);   // node i's [d s]
+            o[0] = make_double2(d0, d1);
+            o[1] = make_double2(d2, s);
             l2[1] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
-          } else {  // node j: [0 | -s I]
-#pragma unroll
-            for (int c = 0; c < 18; ++c) J[c] = 0.0;
-            J[3] = -s; J[10] = -s; J[17] = -s;
+          } else {  // node j's diagonal
+            rec[4] = -s;
           }
-        } else {
-#pragma unroll
-          for (int c = 0; c < 18; ++c) J[c] = 0.0;
+        } else if (k == 0) {
+          reinterpret_cast<double2*>(rec)[0] = reinterpret_cast<double2*>(rec)[1] = make_double2(0.0, 0.0);
+          rec[4] = 0.0;
         }
       }
     } else if (k == 0) {
       const int i = (int)(t - g.M - (int64_t)g.N * g.NB);
-#pragma unroll
-      for (int c = 0; c < 18; ++c) J[c] = 0.0;
+      double J3 = 0.0, J10 = 0.0, J17 = 0.0;
       if (add_reg && g.prm.mode == OFX_GN_ARAP) {
         // DeformNet.arap "flow" rows of the valid nodes (model.py:1766-1784): the Jacobian entry on
         // t_c is the residual itself, as the reference writes it
         const double c = dc.lf * g.conf[i];
         for (int q = 0; q < 3; ++q) r[q] = c * (g.t[3 * i + q] + g.nodes[3 * i + q] - g.tpos[3 * i + q]);
-        J[3] = r[0]; J[10] = r[1]; J[17] = r[2];
+        J3 = r[0]; J10 = r[1]; J17 = r[2];
         l2[0] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
       } else if (add_reg) {
         double c = dc.lm * g.conf[i];
         for (int q = 0; q < 3; ++q) r[q] = c * (g.t[3 * i + q] + g.nodes[3 * i + q] - g.tpos[3 * i + q]);
-        J[3] = c; J[10] = c; J[17] = c;
+        J3 = c; J10 = c; J17 = c;
         l2[2] = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
       }
+      rec[0] = J3; rec[1] = J10; rec[2] = J17;
     }
     if (k == 0) {
       g.res[3 * t] = r[0]; g.res[3 * t + 1] = r[1]; g.res[3 * t + 2] = r[2];
@@ -700,53 +748,9 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
   }
 }
 
-// JᵀJ blocks: 16 lanes per block, 4 blocks per wave; lane q takes list entries q, q+16, ... of its
-// block, loads both 3x6 Jacobian blocks of the entry whole (16-B accesses) and accumulates the full
-// 6x6 product; 16-lane DPP sums (fixed pairing) finish the block and lane 0 of the group stores it.
-// Deterministic; forward declared helpers live in the PCG section.
-__device__ __forceinline__ void blocks_body(const GnDev& g, double* __restrict__ A, int64_t wg, double lm) {
-  const int64_t s = wg * (kBlk / 16) + (threadIdx.x >> 4);
-  const int q = threadIdx.x & 15;
-  double acc[36];
-#pragma unroll
-  for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-  if (s < g.nnzb) {
-    const int b = g.blk_off[s], e = g.blk_off[s + 1];
-    // the next entry's code is loaded one iteration ahead: one dependent memory trip per entry
-    int code_next = b + q < e ? g.blk_list[b + q] : 0;
-    for (int k = b + q; k < e; k += 16) {
-      const int code = code_next;
-      code_next = k + 16 < e ? g.blk_list[k + 16] : 0;
-      const int64_t t = code >> 4;
-      const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * ((code >> 2) & 3));
-      const double2* Jq = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code & 3));
-      double P[18], Q[18];
-#pragma unroll
-      for (int u = 0; u < 9; ++u) {
-        const double2 x = Jp[u], y = Jq[u];
-        P[2 * u] = x.x; P[2 * u + 1] = x.y; Q[2 * u] = y.x; Q[2 * u + 1] = y.y;
-      }
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) acc[6 * c + j] += P[c] * Q[j] + P[6 + c] * Q[6 + j] + P[12 + c] * Q[12 + j];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) acc[k] = row16_sum(acc[k]);
-  if (s < g.nnzb && q == 0) {
-    if (lm != 0.0 && g.blk_row[s] == g.col[s])   // LM damping of the diagonal blocks (model.py:641-662)
-#pragma unroll
-      for (int r = 0; r < 6; ++r) acc[7 * r] += lm;
-    double2* out = reinterpret_cast<double2*>(A + 36 * s);
-#pragma unroll
-    for (int k = 0; k < 18; ++k) out[k] = make_double2(acc[2 * k], acc[2 * k + 1]);
-  }
-}
-
 // b = -Jᵀr: one wave per node, entry-parallel (below). WG 0 also reduces the loss partials into the
 // rhs tail.
-__device__ __forceinline__ void rhs_body(const GnDev& g, double* __restrict__ rhs, int wg) {
+__device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, double* __restrict__ rhs, int wg) {
   if (wg == 0 && threadIdx.x < 64) {   // the loss partials of k_terms, 4 streams in one pass, fixed order
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     for (int i = threadIdx.x; i < g.nwg_terms; i += 64) {
@@ -781,11 +785,11 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, double* __restrict__ rh
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t t = code[j] >> 2;
-      const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code[j] & 3));
+      const int kind = term_kind(g, t);
       const double* rr = g.res + 3 * t;
-      double P[18];
-#pragma unroll
-      for (int u = 0; u < 9; ++u) { const double2 x = Jp[u]; P[2 * u] = x.x; P[2 * u + 1] = x.y; }
+      double x[4], tail[4], P[18];
+      load_record(g, t, code[j] & 3, kind, x, tail);
+      term_block(kind, code[j] & 3, x, tail, dc, P);
       const double r0 = rr[0], r1 = rr[1], r2 = rr[2];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
@@ -808,7 +812,8 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, double* __restrict__ rh
 // the chunk in list order. A block's cost is its share of the workgroup's entries, not its own list length
 // (the 16-lane form took ceil(len/16) dependent trips: ~6 for a busy node's diagonal block).
 constexpr int kCoop = 128;
-__device__ __forceinline__ void blocks_coop(const GnDev& g, double* __restrict__ A, int64_t wg, double lm) {
+__device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, double* __restrict__ A, int64_t wg,
+                                            double lm) {
   __shared__ double s_prod[36 * (kCoop + 1)];
   __shared__ int s_off[17];
   const int tid = threadIdx.x;
@@ -838,14 +843,14 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, double* __restrict__
       code_next = k + kCoop < E1 ? g.blk_list[k + kCoop] : 0;
       if (k < E1) {
         const int64_t t = code >> 4;
-        const double2* Jp = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * ((code >> 2) & 3));
-        const double2* Jq = reinterpret_cast<const double2*>(g.J + t * 72 + 18 * (code & 3));
-        double P[18], Q[18];
-#pragma unroll
-        for (int u = 0; u < 9; ++u) {
-          const double2 x = Jp[u], y = Jq[u];
-          P[2 * u] = x.x; P[2 * u + 1] = x.y; Q[2 * u] = y.x; Q[2 * u + 1] = y.y;
-        }
+        const int kind = term_kind(g, t), sp = (code >> 2) & 3, sq = code & 3;
+        double xp[4], xq[4], tail[4], P[18], Q[18];
+        load_record(g, t, sp, kind, xp, tail);
+        const double2* r = reinterpret_cast<const double2*>(g.J + t * kRec + 4 * sq);
+        const double2 a = r[0], b = r[1];
+        xq[0] = a.x; xq[1] = a.y; xq[2] = b.x; xq[3] = b.y;
+        term_block(kind, sp, xp, tail, dc, P);
+        term_block(kind, sq, xq, tail, dc, Q);
 #pragma unroll
         for (int c = 0; c < 6; ++c)
 #pragma unroll
@@ -878,25 +883,19 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, double* __restrict__
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
-__global__ __launch_bounds__(kBlk) void k_assemble(GnDev g, double* __restrict__ A, double* __restrict__ rhs, int nwb,
-                                                  double lm) {
+__global__ __launch_bounds__(kBlk) void k_assemble(GnDev g, DataCoef dc, double* __restrict__ A, double* __restrict__ rhs,
+                                                  int nwb, double lm) {
   const int nrw = (int)gridDim.x - nwb;
-  if ((int)blockIdx.x < nrw) rhs_body(g, rhs, blockIdx.x);
-#ifdef OFX_ASSEMBLE_LANES   // tuning: the 16-lanes-per-block form
-  else blocks_body(g, A, blockIdx.x - nrw, lm);
-#else
-  else blocks_coop(g, A, blockIdx.x - nrw, lm);
-#endif
+  if ((int)blockIdx.x < nrw) rhs_body(g, dc, rhs, blockIdx.x);
+  else blocks_coop(g, dc, A, blockIdx.x - nrw, lm);
 }
 #ifdef OFX_SPLIT_ASSEMBLE
-__global__ __launch_bounds__(kBlk) void k_assemble_blocks(GnDev g, double* __restrict__ A, double lm) {
-#ifdef OFX_ASSEMBLE_LANES
-  blocks_body(g, A, blockIdx.x, lm);
-#else
-  blocks_coop(g, A, blockIdx.x, lm);
-#endif
+__global__ __launch_bounds__(kBlk) void k_assemble_blocks(GnDev g, DataCoef dc, double* __restrict__ A, double lm) {
+  blocks_coop(g, dc, A, blockIdx.x, lm);
 }
-__global__ __launch_bounds__(kBlk) void k_assemble_rhs(GnDev g, double* __restrict__ rhs) { rhs_body(g, rhs, blockIdx.x); }
+__global__ __launch_bounds__(kBlk) void k_assemble_rhs(GnDev g, DataCoef dc, double* __restrict__ rhs) {
+  rhs_body(g, dc, rhs, blockIdx.x);
+}
 #endif
 
 // ---------------------------------------------------------------------------- PCG
@@ -2945,7 +2944,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     int64_t c = g->T + g->T / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->term_node, 4 * c * sizeof(int32_t)));
-    OFX_HIP(hipMalloc((void**)&g->J, 72 * c * sizeof(double)));
+    OFX_HIP(hipMalloc((void**)&g->J, kRec * c * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->res, 3 * c * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->node_list, 4 * c * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_list, 16 * c * sizeof(int32_t)));
@@ -3098,10 +3097,10 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   const double lm = add_reg ? lm_for_iter(g->prm.lm_factor, gn_iter) : 0.0;
   const int nwb = g->nnzb > 0 ? (int)grid_for(g->nnzb, kBlk / 16, 1 << 30) : 0;
 #ifdef OFX_SPLIT_ASSEMBLE   // tuning build: the two halves as separate kernels (rocprof times each)
-  if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, A, lm);
-  hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, rhs);
+  if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, dc, A, lm);
+  hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, rhs);
 #else
-  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, A, rhs, nwb, lm);
+  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, A, rhs, nwb, lm);
 #endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;

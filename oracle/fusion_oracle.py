@@ -1152,6 +1152,18 @@ def depth_2_pc(depth, intrin):
     return np.stack([(u - K[0, 2]) * d / K[0, 0], (v - K[1, 2]) * d / K[1, 1], d])
 
 
+def xyz_2_uv(pcd, intrin):
+    """NonRigidICP/model/geometry.py:30-41: pixel (u, v) of camera points, truncated toward zero by astype(int).
+    Under the reference's numpy 1.x value-based casting the f64 intrinsic scalars meet the f32 point arrays as
+    f32, so every step rounds to f32."""
+    K = np.asarray(intrin, np.float64)
+    f32 = np.float32
+    X, Y, Z = (np.asarray(pcd[:, q], f32) for q in range(3))
+    u = ((f32(K[0, 0]) * X) / Z + f32(K[0, 2])).astype(np.int64)
+    v = ((f32(K[1, 1]) * Y) / Z + f32(K[1, 2])).astype(np.int64)
+    return np.stack([u, v], -1)
+
+
 def target_point_cloud(depth, intrin):
     """registration_fusion.py:104-109 + map_pixel_to_pcd (:388-395): the f32 cloud of pixels with depth > 0
     (row-major) and the pixel -> point index map (int64, -1 where invalid)."""

@@ -389,8 +389,87 @@ def make_gn_chain(name, config, frames, n_matches=10000):
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
 
 
+MOOSE = "/root/reference/NonRigidICP/demo/moose6OK9_AttackTrotRM"   # read here only; the fixture travels
+
+
+def moose_inputs():
+    """The reference's real demo pair (NonRigidICP/config.yaml: src = depth/cam1_0015.png, tgt = cam1_0009.png,
+    cam1intr.txt, Lepard landmarks landmark/moose_match_pred.npz; loaded as NonRigidICP/main.py:35-48 does).
+    -> (src_mm, tgt_mm uint16 (500, 512), K 3x3, uv_src, uv_tgt (455, 2) int64)."""
+    from PIL import Image
+    src_mm = np.array(Image.open(os.path.join(MOOSE, "depth/cam1_0015.png")))
+    tgt_mm = np.array(Image.open(os.path.join(MOOSE, "depth/cam1_0009.png")))
+    assert src_mm.dtype == np.uint16 and tgt_mm.dtype == np.uint16
+    K = np.loadtxt(os.path.join(MOOSE, "cam1intr.txt"))
+    lm = np.load(os.path.join(MOOSE, "landmark/moose_match_pred.npz"), allow_pickle=False)
+    ldmk_src = lm["src_pcd"][0][lm["match"][:, 1]]
+    ldmk_tgt = lm["tgt_pcd"][0][lm["match"][:, 2]]
+    return src_mm, tgt_mm, K, fo.xyz_2_uv(ldmk_src, K), fo.xyz_2_uv(ldmk_tgt, K)
+
+
+MOOSE_COVERAGE = 0.09          # NonRigidICP/model/geometry.py:123 (node_coverage, metres)
+MOOSE_MAX_TRIANGLE = 0.04      # geometry.py:117
+
+
+def moose_problem(src_mm, tgt_mm, K, uv_src, uv_tgt, nodes):
+    """The landmark GN problem on the §8 path's conventions: depth in metres as f32(mm) / f32(1000)
+    (backproject_depth's ushort branch), both clouds by depth_2_pc + map_pixel_to_pcd (registration_fusion.py:
+    104-109, 388-395: f64 from the f32 depth, then f32), landmark pixels looked up as registration.py:76-84 does
+    (pairs whose source or target pixel has no depth dropped), skinned by WarpField.skin (k-NN, node coverage)
+    keeping the valid ones. -> dict(src, tgt, anchors, weights, keep)."""
+    f32 = np.float32
+    ds, dt = src_mm.astype(f32) / f32(1000.0), tgt_mm.astype(f32) / f32(1000.0)
+    spc, smap = fo.target_point_cloud(ds, K)
+    tpc, tmap = fo.target_point_cloud(dt, K)
+    H, W = ds.shape
+    inb = ((uv_src[:, 0] >= 0) & (uv_src[:, 0] < W) & (uv_src[:, 1] >= 0) & (uv_src[:, 1] < H)
+           & (uv_tgt[:, 0] >= 0) & (uv_tgt[:, 0] < W) & (uv_tgt[:, 1] >= 0) & (uv_tgt[:, 1] < H))
+    assert inb.all()
+    s_id = smap[uv_src[:, 1], uv_src[:, 0]]
+    t_id = tmap[uv_tgt[:, 1], uv_tgt[:, 0]]
+    ok = (s_id > -1) & (t_id > -1)
+    src, tgt = spc[s_id[ok]], tpc[t_id[ok]]
+    a, w, v = fo.skin(src, nodes, MOOSE_COVERAGE)
+    keep = np.nonzero(ok)[0][v]
+    return dict(src=src[v], tgt=tgt[v], anchors=a[v], weights=w[v], keep=keep.astype(np.int32))
+
+
+def make_moose():
+    """moose.npz — the reference's real inputs through the hot path: the depth pair + intrinsics + the landmark
+    pixels (inputs), the SURVEY §8(d) depth-mesh graph of the source frame by the reference's compiled C++ with the
+    demo's coverage / triangle size, the landmark GN problem (moose_problem) and its DeformNet.optimize solve by
+    the dense f64 oracle (data rows: λ_depth = 1, λ_flow = 0 — 3-D landmark residuals, as landmark_cost; ARAP;
+    no node-motion targets), and a 128³ volume around the source cloud for the warped integrate. Parity of these
+    outputs against the reference itself is unpinned (its Python cannot run here)."""
+    src_mm, tgt_mm, K, uv_src, uv_tgt = moose_inputs()
+    cam = S.Intrinsics(float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]), src_mm.shape[1],
+                       src_mm.shape[0])
+    depth_m = src_mm.astype(np.float32) / np.float32(1000.0)
+    nodes, edges, ew = csrc_depth_graph(depth_m, cam, MOOSE_COVERAGE, max_triangle_distance=MOOSE_MAX_TRIANGLE)
+    pb = moose_problem(src_mm, tgt_mm, K, uv_src, uv_tgt, nodes)
+    N = nodes.shape[0]
+    intr = cam.as_vec()
+    res = fo.gn_optimize(nodes, edges, ew, nodes.copy(), np.zeros(N, np.float32), pb["src"], pb["anchors"],
+                         pb["weights"], pb["tgt"], intr)
+    ci = res["convergence_info"]
+    spc, _ = fo.target_point_cloud(depth_m, K)
+    lo, hi = spc.min(0), spc.max(0)
+    vs = np.float32(np.ceil((hi - lo).max() * 1.2 / 128 * 1000) / 1000)       # whole mm
+    origin = ((lo + hi) / 2 - vs * 64).astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "moose.npz"), src_mm=src_mm, tgt_mm=tgt_mm, K=K, uv_src=uv_src,
+                        uv_tgt=uv_tgt, nodes=nodes, edges=edges, edge_weights=ew, node_coverage=MOOSE_COVERAGE,
+                        max_triangle_distance=MOOSE_MAX_TRIANGLE, **pb, R=res["node_rotations"],
+                        t=res["node_translations"], valid=res["valid_solve"], loss_total=np.array(ci["total"]),
+                        origin=origin, voxel_size=vs, dims=np.array([128, 128, 128]))
+    print(f"moose: {N} nodes, {pb['src'].shape[0]} of {uv_src.shape[0]} landmarks, loss {ci['total'][0]:.6g} -> "
+          f"{ci['total'][-1]:.6g} in {len(ci['total'])} steps, volume origin {origin} voxel {vs}")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn", "gn1k", "gn2k", "gn4k"]
+    which = sys.argv[1:] or ["skin", "frontend", "anchors", "graph", "integrate", "gn", "gn1k", "gn2k", "gn4k",
+                             "moose"]
+    if "moose" in which:
+        make_moose()
     if "gn2k" in which:
         make_gn_chain("gn_2k", 3, (10, 11))
     if "gn4k" in which:

@@ -9,8 +9,8 @@ reference's dense LU), from committed fixtures made by tests/golden/make_golden.
   loaded from frame 10's device result) and inline; transforms within 1e-5, the per-step loss log within 1e-6
   relative.
 * gn_4k.npz — BASELINE config 4's graph (~4k nodes), frame 10.
-* Both PCG forms — one persistent launch per GN step (k_pcg_persist, the default) and one launch per iteration
-  (k_pcg_iter, OFX_PCG_PERSIST=0) — meet the same bars on gn_2k, and the persistent solve is bitwise repeatable.
+* Both PCG forms — one launch per iteration (k_pcg_iter, the default) and the opt-in persistent launch per GN step
+  (k_pcg_persist, OFX_PCG_PERSIST=1) — meet the same bars on gn_2k, and the persistent solve is bitwise repeatable.
 * The device graph builder (synthetic.depth_graph: EDGraph.from_mesh on the depth mesh) reproduces the fixture's
   graph (the bench's graph) exactly.
 """

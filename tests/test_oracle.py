@@ -469,3 +469,28 @@ def test_oracle_libstdcxx_heap_order():
         fo._heap_push(h, (v, np.float32(d)))
     order = [fo._heap_pop(h)[0] for _ in range(6)]
     assert order[:2] in ([2, 5], [5, 2]) and sorted(order[2:]) == [0, 1, 3, 4]
+
+
+# --------------------------------------------------------------------- the reference's real moose demo inputs
+def test_moose_fixture_regresses_the_oracle(golden_dir):
+    """tests/golden/moose.npz (the NonRigidICP demo pair + landmarks, tests/golden/make_golden.py moose): the
+    landmark problem rebuilt by the oracle from the fixture's raw inputs, and its dense f64 GN solve, reproduce the
+    committed outputs; xyz_2_uv's f32 rounding (numpy 1.x value-based casting) on a known answer."""
+    import sys
+    sys.path.insert(0, golden_dir)
+    import make_golden as mg
+    g = _load(golden_dir, "moose.npz")
+    assert g["src_mm"].shape == (500, 512) and g["uv_src"].shape == (455, 2)
+    pb = mg.moose_problem(g["src_mm"], g["tgt_mm"], g["K"], g["uv_src"], g["uv_tgt"], g["nodes"])
+    for k in ("src", "tgt", "anchors", "weights", "keep"):
+        np.testing.assert_array_equal(pb[k], g[k])
+    N = g["nodes"].shape[0]
+    K = g["K"]
+    res = fo.gn_optimize(g["nodes"], g["edges"], g["edge_weights"], g["nodes"].copy(), np.zeros(N, np.float32),
+                         pb["src"], pb["anchors"], pb["weights"], pb["tgt"],
+                         np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]]))
+    np.testing.assert_allclose(res["node_rotations"], g["R"], atol=1e-9)
+    np.testing.assert_allclose(res["node_translations"], g["t"], atol=1e-9)
+    # 443.677·0.5 + 256 = 477.8 -> 477, 443.677·(-0.25) + 250 = 139.1 -> 139 (truncation)
+    uv = fo.xyz_2_uv(np.array([[0.5, -0.25, 1.0], [0.0, 0.0, 2.0]], np.float32), K)
+    np.testing.assert_array_equal(uv, [[477, 139], [256, 250]])

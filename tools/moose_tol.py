@@ -1,0 +1,20 @@
+"""Moose landmark GN: transform / loss error against the dense f64 oracle fixture at several PCG tolerances."""
+import os
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from occlusionfusion_amd import GaussNewtonSolver  # noqa: E402
+
+g = np.load("tests/golden/moose.npz", allow_pickle=False)
+N = g["nodes"].shape[0]
+K = g["K"]
+for tol in (1e-6, 1e-7, 1e-8, 1e-10):
+    s = GaussNewtonSolver(N, 1000, pcg_tol=tol)
+    out = s.optimize(g["nodes"], g["edges"], g["edge_weights"], g["nodes"], np.zeros(N, np.float32), g["src"],
+                     g["anchors"], g["weights"], g["tgt"], np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]]))
+    dr = np.abs(out["node_rotations"].cpu().numpy() - g["R"]).max()
+    dt = np.abs(out["node_translations"].cpu().numpy() - g["t"]).max()
+    lr = np.abs(np.array(out["convergence_info"]["total"]) / g["loss_total"] - 1).max()
+    print(f"tol {tol:g}: dR {dr:.3g} dt {dt:.3g} loss rel {lr:.3g} pcg {out['convergence_info']['pcg_iterations']}",
+          flush=True)

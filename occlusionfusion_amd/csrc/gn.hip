@@ -95,7 +95,11 @@ struct GnDev {
   int pat_N = 0;                 // N and block count of the pattern currently set in `map`
   int64_t pat_nnzb = 0;
   int64_t ne_cap = 0;            // capacity of edges / ew
+  // contribution lists of the UPPER blocks only (col >= row, indexed u = up_of[slot]): A is exactly symmetric —
+  // the lower block (j, i)'s products are the upper block's with the factors commuted, summed in the same order —
+  // so the assembly computes each upper block once and also stores its transpose at up_tr[u]
   int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr, *blk_tmp = nullptr;
+  int32_t *up_of = nullptr, *up_slot = nullptr, *up_tr = nullptr;   // slot -> u (+ total at [nnzb]), u -> slot, transpose
   int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr, *node_tmp = nullptr;
   int64_t nnzb = 0, nnzb_cap = 0;
   // state
@@ -511,7 +515,7 @@ __global__ void k_pair_count(GnDev g) {
     if (n[p] < 0) continue;
     atomicAdd(&g.node_cnt[n[p]], 1);
     for (int q = 0; q < 4; ++q)
-      if (n[q] >= 0) atomicAdd(&g.blk_cnt[g.map[(int64_t)n[p] * g.N + n[q]] - 1], 1);
+      if (n[q] >= n[p]) atomicAdd(&g.blk_cnt[g.up_of[g.map[(int64_t)n[p] * g.N + n[q]] - 1]], 1);
   }
 }
 
@@ -525,12 +529,27 @@ __global__ void k_pair_scatter(GnDev g) {
     int pos = g.node_off[n[p]] + atomicAdd(&g.node_cnt[n[p]], 1);
     g.node_list[pos] = (int32_t)(t * 4 + p);
     for (int q = 0; q < 4; ++q) {
-      if (n[q] < 0) continue;
-      int s = g.map[(int64_t)n[p] * g.N + n[q]] - 1;
-      int pb = g.blk_off[s] + atomicAdd(&g.blk_cnt[s], 1);
+      if (n[q] < n[p]) continue;   // upper blocks only (n[p] >= 0 here)
+      const int u = g.up_of[g.map[(int64_t)n[p] * g.N + n[q]] - 1];
+      int pb = g.blk_off[u] + atomicAdd(&g.blk_cnt[u], 1);
       g.blk_list[pb] = (int32_t)(t * 16 + p * 4 + q);
     }
   }
+}
+
+// upper-block flags (scanned into up_of) and, after the scan, the upper list with each block's transpose slot
+__global__ __launch_bounds__(256) void k_up_flags(GnDev g, int32_t* __restrict__ flag) {
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s < g.nnzb) flag[s] = g.col[s] >= g.blk_row[s] ? 1 : 0;
+}
+__global__ __launch_bounds__(256) void k_up_list(GnDev g) {
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s >= g.nnzb) return;
+  const int r = g.blk_row[s], c = g.col[s];
+  if (c < r) return;
+  const int u = g.up_of[s];
+  g.up_slot[u] = (int32_t)s;
+  g.up_tr[u] = g.map[(int64_t)c * g.N + r] - 1;
 }
 
 // Deterministic ordering of each segment (values are unique codes): one wave per segment, every
@@ -817,20 +836,28 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
   __shared__ double s_prod[36 * (kCoop + 1)];
   __shared__ int s_off[17];
   const int tid = threadIdx.x;
-  const int64_t sb = wg * (kBlk / 16);
-  const int nb = (int)min<int64_t>(kBlk / 16, g.nnzb - sb);
-  if (tid <= kBlk / 16) s_off[tid] = g.blk_off[sb + min(tid, nb)];
-  __syncthreads();
-  const int E0 = s_off[0], E1 = s_off[nb];
+  const int64_t sb = wg * (kBlk / 16);   // upper blocks u in [sb, sb + 16); past the upper count up_slot is -1 and
+                                         // the lists are empty (blk_off there = the total)
   constexpr int kPairs = (kBlk / 16) * 36;
   constexpr int kU = (kPairs + kBlk - 1) / kBlk;
-  double acc[kU];
-  int pb[kU], po[kU], lo[kU], hi[kU];
+  // first trip: the 17 list offsets and every pair's output slots (consumed at the end, in flight all along)
+  if (tid <= kBlk / 16) s_off[tid] = g.blk_off[min<int64_t>(sb + tid, g.nnzb)];
+  int pb[kU], po[kU], os[kU], ot[kU];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int p = tid + kBlk * u;
-    pb[u] = p / 36; po[u] = p % 36;
-    const bool ok = p < kPairs && pb[u] < nb;
+    pb[u] = p < kPairs ? p / 36 : kBlk / 16 - 1; po[u] = p % 36;
+    os[u] = g.up_slot[sb + pb[u]];
+    ot[u] = g.up_tr[sb + pb[u]];
+  }
+  __syncthreads();
+  const int E0 = s_off[0], E1 = s_off[kBlk / 16];
+  if (E0 == E1) return;   // no upper block here (uniform over the workgroup)
+  double acc[kU];
+  int lo[kU], hi[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const bool ok = tid + kBlk * u < kPairs;
     lo[u] = ok ? s_off[pb[u]] : 0;
     hi[u] = ok ? s_off[pb[u] + 1] : 0;
     acc[u] = 0.0;
@@ -864,7 +891,25 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
       const int a = max(lo[u], c0), b = min(hi[u], c0 + kCoop);
       const double* sp = s_prod + po[u] * (kCoop + 1) - c0;
       double x = acc[u];
-      for (int e = a; e < b; ++e) x += sp[e];
+      // eight LDS reads in flight, then the eight adds in list order (a one-read-per-add loop waited out the LDS
+      // latency per entry: a busy diagonal block's outputs cost ~90 serial round trips per chunk)
+      int e = a;
+      for (; e + 8 <= b; e += 8) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = sp[e + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x += v[k];
+      }
+      if (e + 4 <= b) {
+        double v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = sp[e + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x += v[k];
+        e += 4;
+      }
+      for (; e < b; ++e) x += sp[e];
       acc[u] = x;
     }
     __syncthreads();
@@ -872,18 +917,19 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int p = tid + kBlk * u;
-    if (p >= kPairs || pb[u] >= nb) continue;
-    const int64_t s = sb + pb[u];
+    if (p >= kPairs || os[u] < 0) continue;
+    const int64_t s = os[u], st = ot[u];
     double v = acc[u];
     // LM damping of the diagonal blocks (model.py:641-662)
-    if (lm != 0.0 && po[u] % 7 == 0 && g.blk_row[s] == g.col[s]) v += lm;
+    if (lm != 0.0 && po[u] % 7 == 0 && s == st) v += lm;
     A[36 * s + po[u]] = v;
+    if (st != s) A[36 * st + 6 * (po[u] % 6) + po[u] / 6] = v;   // the lower block: the transpose
   }
 }
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
-__global__ __launch_bounds__(kBlk) void k_assemble(GnDev g, DataCoef dc, double* __restrict__ A, double* __restrict__ rhs,
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(4))) void k_assemble(GnDev g, DataCoef dc, double* __restrict__ A, double* __restrict__ rhs,
                                                   int nwb, double lm) {
   const int nrw = (int)gridDim.x - nwb;
   if ((int)blockIdx.x < nrw) rhs_body(g, dc, rhs, blockIdx.x);
@@ -2290,7 +2336,7 @@ static void free_all(Gn* g) {
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
-                  g->p_wg_cl, g->p_mgr, g->p_gran, g->p_abort};
+                  g->p_wg_cl, g->p_mgr, g->p_gran, g->p_abort, g->up_of, g->up_slot, g->up_tr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -3037,7 +3083,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   }
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
     for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->blk_off,
-                    (void**)&g->blk_cnt})
+                    (void**)&g->blk_cnt, (void**)&g->up_of, (void**)&g->up_slot, (void**)&g->up_tr})
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     g->nnzb_cap = (int64_t)nnz + nnz / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->col, g->nnzb_cap * sizeof(int32_t)));
@@ -3045,13 +3091,22 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
     OFX_HIP(hipMalloc((void**)&g->A_own, g->nnzb_cap * 36 * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->blk_off, (g->nnzb_cap + 1) * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->blk_cnt, (g->nnzb_cap + 1) * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->up_of, (g->nnzb_cap + 1) * sizeof(int32_t)));
+    OFX_HIP(hipMalloc((void**)&g->up_slot, (g->nnzb_cap + 32) * sizeof(int32_t)));   // + a workgroup's overhang
+    OFX_HIP(hipMalloc((void**)&g->up_tr, (g->nnzb_cap + 32) * sizeof(int32_t)));
   }
   g->nnzb = nnz;
   hipLaunchKernelGGL(k_row_assign, dim3(N), dim3(256), 0, hs, N, g->map, g->row_ptr, g->col, g->blk_row);
   hipLaunchKernelGGL(k_wave_list, dim3(grid_for((int64_t)(N / kCS) * kWL, 256, 1 << 30)), dim3(256), 0, hs, *g);
   g->pat_N = N;
   g->pat_nnzb = nnz;
-  // contribution lists (sorted -> deterministic assembly order)
+  // upper blocks: slot -> u by a scan of the flags (blk_cnt as scratch), u -> slot and transpose
+  OFX_HIP(hipMemsetAsync(g->up_slot, 0xFF, (size_t)(nnz + 32) * sizeof(int32_t), hs));   // -1: no upper block
+  hipLaunchKernelGGL(k_up_flags, dim3(grid_for(nnz, 256, 1 << 30)), dim3(256), 0, hs, *g, g->blk_cnt);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->up_of, (int32_t*)nullptr);
+  hipLaunchKernelGGL(k_up_list, dim3(grid_for(nnz, 256, 1 << 30)), dim3(256), 0, hs, *g);
+  // contribution lists (sorted -> deterministic assembly order); blocks indexed by u (the entries past the upper
+  // count stay empty)
   OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
   OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_pair_count, dim3(gT), dim3(256), 0, hs, *g);
@@ -3095,7 +3150,9 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   // the LM damping λ_k I (model.py:418-419,641-662) is added by the rank that adds the regularisers, so a
   // sum over ranks carries it once
   const double lm = add_reg ? lm_for_iter(g->prm.lm_factor, gn_iter) : 0.0;
-  const int nwb = g->nnzb > 0 ? (int)grid_for(g->nnzb, kBlk / 16, 1 << 30) : 0;
+  // upper blocks: (nnzb + diagonal blocks) / 2 <= (nnzb + rows) / 2 (the pattern is symmetric); workgroups past
+  // the device-side count return at once
+  const int nwb = g->nnzb > 0 ? (int)grid_for((g->nnzb + g->N) / 2 + 1, kBlk / 16, 1 << 30) : 0;
 #ifdef OFX_SPLIT_ASSEMBLE   // tuning build: the two halves as separate kernels (rocprof times each)
   if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, dc, A, lm);
   hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, rhs);

@@ -85,7 +85,9 @@ struct GnDev {
   int2* wl = nullptr;            // per PCG wave: its first kWL blocks (CSR order) as (col, slot); (-1, 0) = none
   int max_deg = 0;               // longest block row of the pattern
   int max_wave = 0;              // most blocks of one PCG wave (kCS rows)
-  int32_t* stopw = nullptr;      // per PCG wave and lane: 1 once the current solve has converged
+  int32_t* stopw = nullptr;      // per PCG wave and lane: the epoch of the last converged (or stopped) PCG solve
+  int32_t ep = 0;                // epoch of the current PCG solve (one per GN step, increasing per handle)
+  int32_t* arrive = nullptr;     // workgroups of the converging launch that have finished (reset by the last)
   uint64_t* stamps = nullptr;    // tuning builds (-DOFX_STAMPS): per iteration < 64 and wave, 8 clock stamps
   int32_t* blk_row = nullptr;    // block -> row (clears the slot map's pattern at the next setup)
   float* d_gnodes = nullptr;      // device copy of the graph the row order was built for (optimistic check)
@@ -133,7 +135,7 @@ struct GnDev {
   bool step_fused = false;                // this step's k_step work was done by the PCG
   int n_prev = 0;                 // valid entries of the ring for the current step
   int warm_now = 0;               // this step starts from the projected x0
-  int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED] mirrored by the kernels
+  int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED, H_ALLDONE] written by the kernels
   int32_t* hflags = nullptr;      // its device address (system-scope stores: no copy kernel per poll)
   hipEvent_t poll_ev = nullptr;   // recorded after each chunk of PCG launches
   double host_enqueue_us = 0.0;   // tuning build: host time spent enqueuing PCG iterations
@@ -181,12 +183,26 @@ struct Gn : GnDev {
   uint32_t p_epoch = 0;
   std::vector<int32_t> h_wg_cl;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
+  // two-stream GN loop (ofx_gn_solve): GN step i on ps[i & 1], so step i + 1 starts beside step i's drained PCG
+  // launches instead of behind them; the caller's stream is ordered after both at the next entry (fence_side)
+  int pipe_env = 0;                  // OFX_GN_PIPE=1: two streams (2: one internal stream, 3: high priority; tuning)
+  hipStream_t ps[2] = {nullptr, nullptr};
+  hipEvent_t ps_ev[2] = {nullptr, nullptr}, ev_cs = nullptr, ev_fin = nullptr, ev_step = nullptr;
+  bool pipe_dirty = false;
+  int32_t ep_next = 1;
 };
 
 // Order stream hs after everything the prefetch worker enqueued on the handle's side stream (call after
 // prep_wait: the worker has finished enqueuing). Every entry point that touches the handle's buffers on a
 // caller stream does this first, whether or not the prefetched setup is used.
 static int fence_side(Gn* g, hipStream_t hs) {
+  if (g->pipe_dirty) {   // the two-stream GN loop's streams (the last step's drained launches)
+    for (int k = 0; k < 2; ++k) {
+      OFX_HIP(hipEventRecord(g->ps_ev[k], g->ps[k]));
+      OFX_HIP(hipStreamWaitEvent(hs, g->ps_ev[k], 0));
+    }
+    g->pipe_dirty = false;
+  }
   if (!g->side || !g->side_dirty) return OFX_OK;
   OFX_HIP(hipEventRecord(g->ev_side, g->side));
   OFX_HIP(hipStreamWaitEvent(hs, g->ev_side, 0));
@@ -195,6 +211,10 @@ static int fence_side(Gn* g, hipStream_t hs) {
 }
 // the same for host reads of device buffers (synchronous copies do not order after a non-blocking stream)
 static int sync_side(Gn* g) {
+  if (g->pipe_dirty) {
+    for (int k = 0; k < 2; ++k) OFX_HIP(hipStreamSynchronize(g->ps[k]));
+    g->pipe_dirty = false;
+  }
   if (!g->side || !g->side_dirty) return OFX_OK;
   OFX_HIP(hipStreamSynchronize(g->side));
   g->side_dirty = false;
@@ -204,7 +224,10 @@ static int sync_side(Gn* g) {
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
 enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
-enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_COUNT = 4 };
+// host-mapped flags: H_DONE / H_ALLDONE hold the epoch (GnDev::ep) of the last converged PCG solve — H_DONE from
+// the converging launch's lead lane, H_ALLDONE once every workgroup of that launch has finished its writes;
+// H_STOPPED the epoch of the solve whose GN step stopped the loop (0: running). k_upload clears them per setup.
+enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_ALLDONE = 3, H_COUNT = 4 };
 __device__ __forceinline__ void host_flag(const int32_t* hf, int k, int v) {
   __hip_atomic_store(const_cast<int32_t*>(hf) + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1179,7 +1202,6 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
-    host_flag(g.hflags, H_DONE, 0);
   }
   const int lane = threadIdx.x;
   const int base = blockIdx.x * kCS;
@@ -1288,7 +1310,6 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
   if (g.flags[F_STOPPED]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {   // PCG bookkeeping of this GN step (also in k_pcg_prep)
     g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
-    host_flag(g.hflags, H_DONE, 0);
   }
   const int np = g.n_prev;
   const int64_t stride = 6 * (int64_t)g.N;
@@ -1392,7 +1413,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restr
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");   // keep the loads above the exit test (one trip with the flag)
   if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
-    g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
     return;
   }
   double p[kProjP];
@@ -1480,7 +1501,7 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");
   if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
-    g.stopw[(int64_t)blockIdx.x * 64 + lane] = 1;
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
     return;
   }
   const double b = own ? bo : 0.0;
@@ -1489,8 +1510,7 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
   const double w = pick6(n, q);
   if (own) s_v[6 * r + q] = w;
   __syncthreads();
-  double d[4] = {0.0, 0.0, 0.0, 0.0};
-  g.stopw[(int64_t)blockIdx.x * 64 + lane] = 0;
+  double d[4] = {0.0, 0.0, 0.0, 0.0};   // (the stop words hold an older epoch: this solve's launches run)
   if (own) {
     const double m = apply_mrow(mr, s_v);
     v[V_W] = w;
@@ -1551,6 +1571,8 @@ struct PcgIt {
   const double* tail;           // rhs + 6N: [loss² total, data, arap, motion, nonfinite]
   double stop_loss_diff;
   int32_t fuse, gn_iter, N, mode, n_iter_log, warm;
+  int32_t ep;                   // this solve's epoch (stop words, H_DONE / H_ALLDONE)
+  int32_t* arrive;
 };
 static PcgIt pcg_args(const Gn* g) {
   PcgIt a;
@@ -1561,6 +1583,7 @@ static PcgIt pcg_args(const Gn* g) {
   a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol;
   a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff;
   a.fuse = 0; a.gn_iter = 0; a.N = g->N; a.mode = g->prm.mode; a.n_iter_log = 64; a.warm = g->prm.pcg_warm;
+  a.ep = g->ep; a.arrive = g->arrive;
   return a;
 }
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
@@ -1603,7 +1626,7 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
     g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
     if (stop) {
       g.flags[F_STOPPED] = 1;
-      host_flag(g.hflags, H_STOPPED, 1);
+      host_flag(g.hflags, H_STOPPED, g.ep);
     } else {
       if (acc < g.n_iter_log) {
         sa.loss_log[4 * acc + 0] = loss;
@@ -1656,7 +1679,6 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
   const int nw = g.nwg_row;
-  (void)nw;   // read by the OFX_STAMPS tuning build
   const double* __restrict__ mc = par ? g.m1 : g.m0;
   double* __restrict__ mn = par ? g.m0 : g.m1;
   const int ns = g.nw_pad;
@@ -1674,7 +1696,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     bl0 = g.wl[(int64_t)wv * kWL + 64 * hw + lane];
     if (!kW2) bl1 = g.wl[(int64_t)wv * kWL + 64 + lane];
   }
-  const int stop = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
+  const int stop_ep = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
   const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
@@ -1716,7 +1738,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
-  if (stop) return;
+  if (stop_ep >= g.ep) return;     // this solve has converged (or stopped): a drained launch
 #ifdef OFX_STAMPS
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
 #endif
@@ -1768,14 +1790,22 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   if (conv || !isfinite(alpha) || !(alpha > 0.0)) {   // converged, or breakdown (A SPD => alpha > 0): keep x
     if (!w0) return;
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
-    g.stopw[(int64_t)wv * 64 + lane] = 1;
+    g.stopw[(int64_t)wv * 64 + lane] = g.ep;
     const bool ill = !conv && !isfinite(alpha);
     if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
     if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
       if (ill) g.flags[F_ILL] = 1;
       host_flag(g.hflags, H_PCG_IT, cnt);
-      __hip_atomic_store(g.hflags + H_DONE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
+      __hip_atomic_store(g.hflags + H_DONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
+    }
+    // every workgroup's writes of this launch released (device scope), then counted: the last one tells the host,
+    // which may then start the next GN step on another stream beside this chunk's remaining (drained) launches
+    __threadfence();
+    if (lane == 0 && atomicAdd(g.arrive, 1) == nw - 1) {
+      __threadfence();
+      __hip_atomic_store(g.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g.hflags + H_ALLDONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return;
   }
@@ -2152,7 +2182,7 @@ __global__ __launch_bounds__(64 * kPersistMaxC) void k_pcg_persist(PcgPersist P)
         g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
         if (ill) g.flags[F_ILL] = 1;
         host_flag(g.hflags, H_PCG_IT, it);
-        __hip_atomic_store(g.hflags + H_DONE, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(g.hflags + H_DONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       if (lead) g.flags[F_PCG_CNT] = it;
       break;
@@ -2236,7 +2266,7 @@ __global__ __launch_bounds__(256) void k_step(GnDev g, const double* __restrict_
       g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
       if (stop) {
         g.flags[F_STOPPED] = 1;
-        host_flag(g.hflags, H_STOPPED, 1);
+        host_flag(g.hflags, H_STOPPED, g.ep);
       } else {
         if (acc < n_iter_log) {
           g.loss_log[4 * acc + 0] = loss;
@@ -2336,7 +2366,7 @@ static void free_all(Gn* g) {
                   g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
-                  g->p_wg_cl, g->p_mgr, g->p_gran, g->p_abort, g->up_of, g->up_slot, g->up_tr};
+                  g->p_wg_cl, g->p_mgr, g->p_gran, g->p_abort, g->up_of, g->up_slot, g->up_tr, g->arrive};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -2440,6 +2470,7 @@ static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
+  g->ep = g->ep_next++;   // this solve's epoch (read by the launches below through their GnDev / PcgIt copies)
   g->warm_now = 0;
   if (g->prm.pcg_warm && gn_iter > 0) {   // k_step of the previous steps filled the ring
     g->n_prev = gn_iter < kProj ? gn_iter : kProj;
@@ -2518,7 +2549,6 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (g->timing) g->ev.emplace_back(e0, e1);
     return OFX_OK;
   }
-  hf[H_DONE] = 0;   // the previous step's converged launch has run (we saw it); prep also clears it
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
@@ -2536,7 +2566,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipEventRecord(g->poll_ev, hs));
     bool ran = false;
-    for (int spin = 0; !hf[H_DONE] && !hf[H_STOPPED]; ++spin) {
+    // converged = every workgroup of the converging launch is done (H_ALLDONE), so the caller may start the next
+    // GN step on any stream
+    // (a stop decided by an earlier solve: this one's launches end at their stop words, nothing to wait for; a stop
+    // decided by this solve's converging launch: wait until all its workgroups are done, like a convergence)
+    for (int spin = 0; hf[H_ALLDONE] < g->ep && !(hf[H_STOPPED] != 0 && hf[H_STOPPED] < g->ep); ++spin) {
       if ((spin & 63) == 63) {
         const hipError_t q = hipEventQuery(g->poll_ev);
         if (q == hipSuccess) { ran = true; break; }
@@ -2544,7 +2578,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       }
     }
     if (hf[H_STOPPED]) break;
-    if (hf[H_DONE]) {
+    if (hf[H_ALLDONE] >= g->ep) {
       (*g->last_pcg)[gn_iter & 63] = hf[H_PCG_IT];
       g->step_fused = pa.fuse != 0;
       break;
@@ -2612,9 +2646,12 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     return OFX_ERR_RANGE;
   }
   Gn* g = new Gn();
-  {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster
+  {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster; OFX_GN_PIPE=0 keeps the
+      // GN loop on the caller's stream
     const char* e = getenv("OFX_PCG_W1");
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
+    const char* pp = getenv("OFX_GN_PIPE");
+    g->pipe_env = pp ? atoi(pp) : 0;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
@@ -2640,8 +2677,11 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
   ALLOC(g->p_wg_cl, N / kCS + 2); ALLOC(g->p_mgr, 2 * 6 * N * 2); ALLOC(g->p_gran, 2 * kPersistMaxG * 8); ALLOC(g->p_abort, 1);
+  ALLOC(g->arrive, 1);
 #undef ALLOC
   if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess ||   // pattern entries are cleared per setup
+      hipMemset(g->arrive, 0, sizeof(int32_t)) != hipSuccess ||
+      hipMemset(g->stopw, 0, (size_t)(N / kCS) * 64 * sizeof(int32_t)) != hipSuccess ||   // epoch 0: none converged
       hipMemset(g->p_gran, 0, (size_t)2 * kPersistMaxG * 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(g->p_mgr, 0, (size_t)2 * 6 * N * 2 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(g->p_abort, 0, sizeof(int32_t)) != hipSuccess) {
@@ -2786,6 +2826,12 @@ int ofx_gn_destroy(void* handle) {
     g->worker.join();
   }
   (void)hipDeviceSynchronize();
+  for (int k = 0; k < 2; ++k) {
+    if (g->ps[k]) (void)hipStreamDestroy(g->ps[k]);
+    if (g->ps_ev[k]) (void)hipEventDestroy(g->ps_ev[k]);
+  }
+  for (hipEvent_t e : {g->ev_cs, g->ev_fin, g->ev_step})
+    if (e) (void)hipEventDestroy(e);
   if (g->side) (void)hipStreamDestroy(g->side);
   if (g->ev_in) (void)hipEventDestroy(g->ev_in);
   if (g->ev_prep) (void)hipEventDestroy(g->ev_prep);
@@ -2820,8 +2866,12 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
     OFX_HIP(hipEventCreateWithFlags(&g->ev_side, hipEventDisableTiming));
   }
   OFX_HIP(hipGetDevice(&g->prep_dev));
-  // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve)
-  // comes before the prefetched setup
+  // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve, its
+  // two-stream GN loop's tails) comes before the prefetched setup
+  if (g->pipe_dirty) {
+    const int fs = fence_side(g, as_stream(s));
+    if (fs) return fs;
+  }
   OFX_HIP(hipEventRecord(g->ev_in, as_stream(s)));
   g->prep_pb = *pb;
   g->prep_pb.prev_rot = nullptr;    // the pose is loaded by the solve (k_pose)
@@ -3222,16 +3272,69 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     st = gn_setup(g, pb, prm, nullptr, s);
     if (st) return st;
   }
+  if (const char* pp = getenv("OFX_GN_PIPE")) g->pipe_env = atoi(pp);   // (read per solve: in-process A/B)
+  const bool pipe = g->pipe_env && !g->p_on && g->n_comp == 0 && prm->num_iter > 0;
+  if (!pipe) {
+    for (int it = 0; it < prm->num_iter; ++it) {
+      st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, s);
+      if (st) return st;
+      st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
+      if (st) return st;
+      // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
+      // decision: a stop costs at most one extra (no-op) linearisation instead of a sync per step
+      if (((const volatile int32_t*)g->host_flags)[H_STOPPED]) break;
+    }
+    return ofx_gn_finish(handle, res, s);
+  }
+  // Two streams: GN step i runs on ps[i & 1]. The host returns from a step's PCG once every workgroup of its
+  // converging launch has finished (H_ALLDONE), so the next step, enqueued on the other stream, starts right
+  // away instead of behind this chunk's remaining launches, which end after their stop-word load (epoch-tagged
+  // stop words: a new solve's writes never re-arm an old solve's launches). The last solve runs k_finish on the
+  // other stream too; the caller's stream waits for that, and for the leftovers at its next use of the handle.
+  hipStream_t cs = as_stream(s);
+  if (!g->ps[0]) {
+    int lo = 0, hi = 0;
+    OFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    for (int k = 0; k < 2; ++k) {
+      if (g->pipe_env == 3)   // tuning: high-priority streams
+        OFX_HIP(hipStreamCreateWithPriority(&g->ps[k], hipStreamNonBlocking, hi));
+      else
+        OFX_HIP(hipStreamCreateWithFlags(&g->ps[k], hipStreamNonBlocking));
+      OFX_HIP(hipEventCreateWithFlags(&g->ps_ev[k], hipEventDisableTiming));
+    }
+    OFX_HIP(hipEventCreateWithFlags(&g->ev_cs, hipEventDisableTiming));
+    OFX_HIP(hipEventCreateWithFlags(&g->ev_fin, hipEventDisableTiming));
+    OFX_HIP(hipEventCreateWithFlags(&g->ev_step, hipEventDisableTiming));
+  }
+  OFX_HIP(hipEventRecord(g->ev_cs, cs));   // the setup / pose above, the caller's inputs
+  for (int k = 0; k < 2; ++k) OFX_HIP(hipStreamWaitEvent(g->ps[k], g->ev_cs, 0));
+  int last = 0;
+  const int np = g->pipe_env == 2 ? 1 : 2;   // tuning: 2 = one internal stream for every step
   for (int it = 0; it < prm->num_iter; ++it) {
-    st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, s);
+    hipStream_t x = g->ps[it % np];
+    last = it;
+    st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, (ofx_stream_t)x);
     if (st) return st;
-    st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
+    st = gn_pcg(g, it, g->A_own, g->rhs_own, x);
     if (st) return st;
-    // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
-    // decision: a stop costs at most one extra (no-op) linearisation instead of a sync per step
+    if (!g->step_fused) {   // not converged within pcg_max_iter (or stopped): k_step here, the next stream waits
+      double* xsave = g->prm.pcg_warm ? g->xh + (int64_t)(it % kProj) * 6 * g->N : nullptr;
+      hipLaunchKernelGGL(k_step, dim3(grid_for(g->N, 256)), dim3(256), 0, x, *g, (const double*)g->rhs_own, 64,
+                         g->prm.pcg_max_iter, it, xsave);
+      OFX_LAUNCH_CHECK();
+      OFX_HIP(hipEventRecord(g->ev_step, x));
+      OFX_HIP(hipStreamWaitEvent(g->ps[(it + 1) % np], g->ev_step, 0));
+    }
     if (((const volatile int32_t*)g->host_flags)[H_STOPPED]) break;
   }
-  return ofx_gn_finish(handle, res, s);
+  hipStream_t f = g->ps[(last + 1) % np];   // beside the last solve's drained launches (after k_step's event if any)
+  hipLaunchKernelGGL(k_finish, dim3(grid_for(g->N > 4 * prm->num_iter ? g->N : 4 * prm->num_iter, 256)), dim3(256), 0,
+                     f, *g, res->rot, res->trans, res->status, res->loss_log, (int)prm->num_iter);
+  OFX_LAUNCH_CHECK();
+  OFX_HIP(hipEventRecord(g->ev_fin, f));
+  OFX_HIP(hipStreamWaitEvent(cs, g->ev_fin, 0));
+  g->pipe_dirty = true;   // (set only now: the loop's own entry fences must not wait for the other stream)
+  return OFX_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,57 @@
+"""Tuning (not product): in-process A/B of environment switches read per solve (e.g. OFX_GN_PIPE), alternating frame by
+frame on the bench's config-3 sequence, so that run-level spread (whole processes land at ~5.0 or ~5.3 us per PCG
+launch) cancels. Prints mean ms per frame (solve + integrate, stream events) per setting.
+
+    python tools/ab_inproc.py OFX_GN_PIPE 0 1 [--frames 120]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("var")
+    ap.add_argument("values", nargs="+")
+    ap.add_argument("--frames", type=int, default=120)
+    ap.add_argument("--config", type=int, default=3)
+    a = ap.parse_args()
+    from occlusionfusion_amd import synthetic as S
+    from occlusionfusion_amd.pipeline import FusionPipeline
+    dev = torch.device("cuda", 0)
+    cfg = S.BASELINE_CONFIGS[a.config]
+    seq = S.config_sequence(a.config, device=dev)
+    D = cfg["dims"]
+    pipe = FusionPipeline(seq, cfg["origin"], cfg["voxel"], (D, D, D), device=dev)
+    total = a.frames + 4
+    frames = [pipe.prepare(t) for t in range(total + 1)]
+    torch.cuda.synchronize()
+    pipe.integrate_source(frames[0])
+    times = {v: [] for v in a.values}
+    marks = []
+    for t in range(1, total):
+        v = a.values[t % len(a.values)]
+        os.environ[a.var] = v
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        pipe.solve(frames[t], frames[t + 1])
+        pipe.integrate(frames[t], t)
+        e1.record()
+        if t > 4:
+            marks.append((v, e0, e1))
+    pipe.solver.drain()
+    torch.cuda.synchronize()
+    for v, e0, e1 in marks:
+        times[v].append(e0.elapsed_time(e1))
+    out = {v: {"ms_per_frame": float(np.mean(x)), "median": float(np.median(x)), "n": len(x)} for v, x in times.items()}
+    print(json.dumps({"var": a.var, "results": out}))
+
+
+if __name__ == "__main__":
+    main()

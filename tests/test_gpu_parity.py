@@ -435,6 +435,48 @@ def test_gn_stop_with_unconverged_pcg_keeps_the_stopping_step(cuda, golden_dir):
     assert torch.equal(a["node_translations"], b["node_translations"])
 
 
+@pytest.mark.parametrize("case", ["converged", "stop_unconverged"])
+def test_gn_two_stream_loop_is_bitwise_the_single_stream(cuda, golden_dir, monkeypatch, case):
+    """OFX_GN_PIPE=1 runs GN step i on internal stream i & 1 (the next step starts beside the previous step's drained
+    PCG launches: epoch-tagged stop words, H_ALLDONE); same arithmetic, so the same bits — also through k_step on
+    its own launch (PCG capped) and an early stop."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    kw = dict(pcg_max_iter=2, stop_loss_diff=-1.0) if case == "stop_unconverged" else {}
+    outs = []
+    for pipe in ("0", "1", "0", "1"):      # alternating on one handle: the caller stream is fenced after the loop
+        monkeypatch.setenv("OFX_GN_PIPE", pipe)
+        outs.append(GaussNewtonSolver(len(g["nodes"]), 1000, **kw).optimize(*_gn_inputs(g)))
+    s = GaussNewtonSolver(len(g["nodes"]), 1000, **kw)
+    for pipe in ("1", "0", "1"):
+        monkeypatch.setenv("OFX_GN_PIPE", pipe)
+        outs.append(s.optimize(*_gn_inputs(g)))
+    for o in outs[1:]:
+        assert o["convergence_info"]["gn_iterations"] == outs[0]["convergence_info"]["gn_iterations"]
+        assert torch.equal(o["node_rotations"], outs[0]["node_rotations"])
+        assert torch.equal(o["node_translations"], outs[0]["node_translations"])
+    if case == "converged":
+        assert np.abs(outs[1]["node_translations"].cpu().numpy() - g["t"]).max() < 1e-5
+
+
+def test_gn_duplicate_anchors_match_dense_oracle(cuda, golden_dir):
+    """Terms whose anchor list repeats a node (the JᵀJ assembly computes upper blocks only and mirrors them; a
+    repeated node puts two (p, q) products of one term into one block): within 1e-5 of the dense oracle."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    anc = g["anchors"].copy()
+    w = g["weights"].copy()
+    anc[::3, 1] = anc[::3, 0]                 # every third match: anchors [a, a, c, d]
+    anc[1::7, 3] = anc[1::7, 2]               # some: [a, b, c, c]
+    args = (g["nodes"], g["edges"], g["edge_weights"], g["tpos"], g["conf"], g["src"], anc, w, g["tgt"], g["intr"])
+    ref = fo.gn_optimize(*args)
+    out = GaussNewtonSolver(len(g["nodes"]), 1000).optimize(*args)
+    assert out["valid_solve"] == ref["valid_solve"] == 1
+    np.testing.assert_allclose(out["node_rotations"].cpu().numpy(), ref["node_rotations"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(out["node_translations"].cpu().numpy(), ref["node_translations"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(out["convergence_info"]["total"], ref["convergence_info"]["total"], rtol=1e-6)
+
+
 def test_gn_solver_reuse_across_graph_change(cuda, golden_dir):
     """A solver handle reused on a different graph of the same size (the row order is kept optimistically
     and checked on the device) gives exactly what a fresh handle gives."""

@@ -385,6 +385,56 @@ def dense_gn_terms(rows, N6, threads):
     return t_mm, t_lu, rate / 1e9
 
 
+def cpu_config1_full(dev, threads):
+    """configs 1-2 run fully on the CPU. BASELINE config 1 (128³ @8 mm, ~200 nodes, 320x224, 10k
+    matches) with the oracle port, unsampled: the source frame fused (untimed) and the volume's skin cached (as
+    WarpField.skin_tsdf caches it, untimed); then warped frame 1, the whole frame timed: the
+    matches' skin (oracle k-NN), the 10-step dense float64 GN solve (oracle gn_optimize: dense J, JᵀJ, LU) and the
+    warp + integrate of all 2.1M voxels (oracle/cpu_ref.c, OpenMP)."""
+    from occlusionfusion_amd import synthetic as S
+    from oracle import cpu_ref
+    from oracle import fusion_oracle as fo
+    c = S.BASELINE_CONFIGS[1]
+    seq = S.config_sequence(1, device=dev)     # the graph: SURVEY §8(d) depth-mesh graph (pinned to the csrc)
+    D = c["dims"]
+    dims = (D, D, D)
+    origin = np.asarray(c["origin"], np.float32)
+    vs = np.float32(c["voxel"])
+    world = fo.world_points(origin, np.array(dims), float(vs))
+    V = world.shape[0]
+    intr = seq.cam.as_vec()
+    nodes = seq.nodes
+    cpu_ref.set_threads(threads)
+    an_v, w_v, ok_v = fo.skin(world, nodes, seq.node_coverage)
+    im0 = seq.frame(0)
+    tsdf, weight, color = np.ones(V, np.float32), np.zeros(V, np.float32), np.zeros(V, np.float32)
+    vox = np.arange(V, dtype=np.int64)
+    cpu_ref.integrate(dims, origin, vs, vox, fo.depth_of(im0), fo.pack_color(im0), intr, tsdf, weight, color)
+    R = T = None
+    per = []
+    for t in (1,):
+        im = seq.frame(t)
+        t0 = time.perf_counter()
+        src, tgt, tpos, conf = seq.solver_inputs(t, 10000)
+        a_, w_, v_ = fo.skin(src, nodes, seq.node_coverage)
+        t1 = time.perf_counter()
+        res = fo.gn_optimize(nodes, seq.edges, seq.edge_weights, tpos, conf, src[v_], a_[v_], w_[v_], tgt[v_], intr,
+                             prev_rot=R, prev_trans=T)
+        R, T = res["node_rotations"], res["node_translations"]
+        t2 = time.perf_counter()
+        cpu_ref.integrate(dims, origin, vs, vox, fo.depth_of(im), fo.pack_color(im), intr, tsdf, weight, color,
+                          warp=True, anchors=an_v, weights=w_v, valid=ok_v.astype(np.uint8), R=R.reshape(-1, 9),
+                          T=T, nodes=nodes)
+        t3 = time.perf_counter()
+        per.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2, len(res["convergence_info"]["total"])))
+    sec = float(np.mean([x[0] for x in per]))
+    return {"value": 1.0 / sec, "unit": "frames/s", "cores": threads, "kind": "port", "s_per_frame": sec,
+            "s_skin_matches": float(np.mean([x[1] for x in per])), "s_gn": float(np.mean([x[2] for x in per])),
+            "s_warp_integrate": float(np.mean([x[3] for x in per])), "gn_steps": [x[4] for x in per],
+            "sample": f"BASELINE config 1 unsampled: {D}^3 voxels ({V}), {nodes.shape[0]} nodes, 10k matches, warped "
+                      f"frame 1 timed whole (match skin + 10-step dense f64 GN + warp/integrate of every voxel)"}
+
+
 def cpu_baseline(pipe, fi, t, a):
     """The oracle port on the host cores, on a bounded sample of the same frame (kind "port": the reference
     Python cannot run here or travel; oracle/ restates it line for line):
@@ -473,6 +523,10 @@ def cpu_baseline(pipe, fi, t, a):
                                           f"LU of {N6}² ({dt_lu:.1f} s, scaled from at most 6000²)"}
     except Exception as e:  # the reported baseline must not break the bench line
         out["single_thread"] = {"error": repr(e)}
+    try:
+        out["config1_full"] = cpu_config1_full(pipe.device, threads)
+    except Exception as e:
+        out["config1_full"] = {"error": repr(e)}
     return out
 
 

@@ -190,6 +190,13 @@ struct Gn : GnDev {
   hipEvent_t ps_ev[2] = {nullptr, nullptr}, ev_cs = nullptr, ev_fin = nullptr, ev_step = nullptr;
   bool pipe_dirty = false;
   int32_t ep_next = 1;
+#ifdef OFX_STAMPS   // tuning build: stream idle between a PCG chunk's last launch and the next GN step's first kernel
+  std::chrono::steady_clock::time_point t_seen{};   // host saw the step's convergence
+  double react_us = 0.0, prologue_us = 0.0;         // -> k_terms enqueued; -> the first PCG chunk launch enqueued
+  int64_t react_n = 0;
+  hipEvent_t gap_end = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> gap_ev;
+#endif
 };
 
 // Order stream hs after everything the prefetch worker enqueued on the handle's side stream (call after
@@ -374,6 +381,7 @@ __global__ __launch_bounds__(256) void k_upload(GnDev g, Upload u) {
   }
   if (i < F_COUNT) g.flags[i] = 0;
   if (i < H_COUNT) host_flag(g.hflags, (int)i, 0);
+  if (i == 0) *g.arrive = 0;   // the converging launch's workgroup count (reset by its last arrival; cleared per setup too)
   if (i < S_COUNT) g.scal[i] = 0.0;
   if (i < 3 * kMaxLog) g.stat[i] = 0.0;
   if (i < 2 * (kMaxLog + 1)) g.step_state[i] = 0.0;
@@ -2555,6 +2563,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
 #ifdef OFX_STAMPS
     const auto h0 = std::chrono::steady_clock::now();
+    if (it == 0 && gn_iter > 0 && g->t_seen.time_since_epoch().count())
+      g->prologue_us += std::chrono::duration<double, std::micro>(h0 - g->t_seen).count();
 #endif
     for (int k = 0; k < n; ++k, ++it)
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, pa, it & 1);
@@ -2579,6 +2589,9 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     if (hf[H_STOPPED]) break;
     if (hf[H_ALLDONE] >= g->ep) {
+#ifdef OFX_STAMPS
+      g->t_seen = std::chrono::steady_clock::now();
+#endif
       (*g->last_pcg)[gn_iter & 63] = hf[H_PCG_IT];
       g->step_fused = pa.fuse != 0;
       break;
@@ -2588,6 +2601,12 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   }
   g->n_iter_launches += it;
   if (g->timing) g->ev.emplace_back(e0, e1);
+#ifdef OFX_STAMPS
+  if (getenv("OFX_GAP_EVENTS")) {
+    OFX_HIP(hipEventCreate(&g->gap_end));
+    OFX_HIP(hipEventRecord(g->gap_end, hs));
+  }
+#endif
   return OFX_OK;
 }
 
@@ -2801,6 +2820,28 @@ int ofx_gn_host_enqueue(void* handle, double* us, int64_t* n) {
   Gn* g = (Gn*)handle;
   *us = g->host_enqueue_us; *n = g->host_enqueued;
   g->host_enqueue_us = 0.0; g->host_enqueued = 0;
+  return OFX_OK;
+}
+int ofx_gn_gaps(void* handle, double* ms, int64_t* n) {   // sum of the recorded step-boundary gaps (then cleared)
+  Gn* g = (Gn*)handle;
+  double t = 0.0;
+  for (auto& e : g->gap_ev) {
+    float x = 0.f;
+    OFX_HIP(hipEventSynchronize(e.second));
+    OFX_HIP(hipEventElapsedTime(&x, e.first, e.second));
+    t += x;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  *ms = t;
+  *n = (int64_t)g->gap_ev.size();
+  g->gap_ev.clear();
+  if (getenv("OFX_GAP_VERBOSE"))
+    fprintf(stderr, "host: convergence seen -> k_terms enqueued %.2f us, -> first chunk launch %.2f us (n %lld)\n",
+            g->react_us / (double)(g->react_n ? g->react_n : 1), g->prologue_us / (double)(g->react_n ? g->react_n : 1),
+            (long long)g->react_n);
+  g->react_us = g->prologue_us = 0.0;
+  g->react_n = 0;
   return OFX_OK;
 }
 int ofx_gn_stamps(void* handle, uint64_t* out, int64_t n) {
@@ -3192,11 +3233,30 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   hipStream_t hs = as_stream(s);
   const int fs = fence_side(g, hs);
   if (fs) return fs;
+#ifdef OFX_STAMPS
+  if (g->gap_end && gn_iter == 0) {   // the previous solve's last step: a frame boundary, not a GN-step one
+    (void)hipEventDestroy(g->gap_end);
+    g->gap_end = nullptr;
+  }
+  if (g->gap_end) {
+    hipEvent_t e;
+    OFX_HIP(hipEventCreate(&e));
+    OFX_HIP(hipEventRecord(e, hs));
+    g->gap_ev.emplace_back(g->gap_end, e);
+    g->gap_end = nullptr;
+  }
+#endif
   DataCoef dc;
   dc.lf = sqrt(g->prm.lambda_flow); dc.ld = sqrt(g->prm.lambda_depth);
   dc.la = sqrt(g->prm.lambda_arap); dc.lm = sqrt(g->prm.lambda_motion);
   dc.fx = g->fx; dc.fy = g->fy; dc.cx = g->cx; dc.cy = g->cy;
   hipLaunchKernelGGL(k_terms, dim3(g->nwg_terms), dim3(kBlk), 0, hs, *g, dc, m0, m1, add_reg);
+#ifdef OFX_STAMPS
+  if (gn_iter > 0 && g->t_seen.time_since_epoch().count()) {
+    g->react_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g->t_seen).count();
+    ++g->react_n;
+  }
+#endif
   // the LM damping λ_k I (model.py:418-419,641-662) is added by the rank that adds the regularisers, so a
   // sum over ranks carries it once
   const double lm = add_reg ? lm_for_iter(g->prm.lm_factor, gn_iter) : 0.0;

@@ -185,6 +185,7 @@ struct Gn : GnDev {
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   // two-stream GN loop (ofx_gn_solve): GN step i on ps[i & 1], so step i + 1 starts beside step i's drained PCG
   // launches instead of behind them; the caller's stream is ordered after both at the next entry (fence_side)
+  bool pipe_active = false;          // ofx_gn_solve is running its two-stream loop (the PCG signals H_ALLDONE)
   int pipe_env = 0;                  // OFX_GN_PIPE=1: two streams (2: one internal stream, 3: high priority; tuning)
   hipStream_t ps[2] = {nullptr, nullptr};
   hipEvent_t ps_ev[2] = {nullptr, nullptr}, ev_cs = nullptr, ev_fin = nullptr, ev_step = nullptr;
@@ -1580,7 +1581,7 @@ struct PcgIt {
   double stop_loss_diff;
   int32_t fuse, gn_iter, N, mode, n_iter_log, warm;
   int32_t ep;                   // this solve's epoch (stop words, H_DONE / H_ALLDONE)
-  int32_t* arrive;
+  int32_t* arrive;              // two-stream GN loop: the workgroup count behind H_ALLDONE (nullptr: not counted)
 };
 static PcgIt pcg_args(const Gn* g) {
   PcgIt a;
@@ -1591,7 +1592,7 @@ static PcgIt pcg_args(const Gn* g) {
   a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol;
   a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff;
   a.fuse = 0; a.gn_iter = 0; a.N = g->N; a.mode = g->prm.mode; a.n_iter_log = 64; a.warm = g->prm.pcg_warm;
-  a.ep = g->ep; a.arrive = g->arrive;
+  a.ep = g->ep; a.arrive = g->pipe_active ? g->arrive : nullptr;
   return a;
 }
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
@@ -1807,8 +1808,11 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
       host_flag(g.hflags, H_PCG_IT, cnt);
       __hip_atomic_store(g.hflags + H_DONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
     }
-    // every workgroup's writes of this launch released (device scope), then counted: the last one tells the host,
-    // which may then start the next GN step on another stream beside this chunk's remaining (drained) launches
+    // two-stream GN loop only (g.arrive set): every workgroup's writes of this launch released (device scope: an L2
+    // write-back per workgroup), then counted: the last one tells the host, which may then start the next GN step on
+    // another stream beside this chunk's remaining (drained) launches. On the one-stream path the next step's kernels
+    // follow this launch on the same stream and the lead's H_DONE suffices.
+    if (!g.arrive) return;
     __threadfence();
     if (lane == 0 && atomicAdd(g.arrive, 1) == nw - 1) {
       __threadfence();
@@ -2576,11 +2580,13 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipEventRecord(g->poll_ev, hs));
     bool ran = false;
-    // converged = every workgroup of the converging launch is done (H_ALLDONE), so the caller may start the next
-    // GN step on any stream
-    // (a stop decided by an earlier solve: this one's launches end at their stop words, nothing to wait for; a stop
-    // decided by this solve's converging launch: wait until all its workgroups are done, like a convergence)
-    for (int spin = 0; hf[H_ALLDONE] < g->ep && !(hf[H_STOPPED] != 0 && hf[H_STOPPED] < g->ep); ++spin) {
+    // converged: one stream — the converging launch's lead lane stored H_DONE (the next step's kernels follow it on
+    // the stream); two streams — every workgroup of that launch is done (H_ALLDONE), so the next step may start on
+    // the other stream. A stop decided by an earlier solve: this one's launches end at their stop words, nothing to
+    // wait for; a stop decided by this solve's converging launch: one stream — stop now; two streams — wait for
+    // H_ALLDONE, like a convergence
+    const int wf = g->pipe_active ? H_ALLDONE : H_DONE;
+    for (int spin = 0; hf[wf] < g->ep && !(hf[H_STOPPED] != 0 && (!g->pipe_active || hf[H_STOPPED] < g->ep)); ++spin) {
       if ((spin & 63) == 63) {
         const hipError_t q = hipEventQuery(g->poll_ev);
         if (q == hipSuccess) { ran = true; break; }
@@ -2588,7 +2594,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       }
     }
     if (hf[H_STOPPED]) break;
-    if (hf[H_ALLDONE] >= g->ep) {
+    if (hf[wf] >= g->ep) {
 #ifdef OFX_STAMPS
       g->t_seen = std::chrono::steady_clock::now();
 #endif
@@ -3368,6 +3374,11 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   }
   OFX_HIP(hipEventRecord(g->ev_cs, cs));   // the setup / pose above, the caller's inputs
   for (int k = 0; k < 2; ++k) OFX_HIP(hipStreamWaitEvent(g->ps[k], g->ev_cs, 0));
+  struct PipeActive {   // the PCG launches of this loop count their workgroups out (H_ALLDONE); off on every return
+    Gn* g;
+    ~PipeActive() { g->pipe_active = false; }
+  } pipe_guard{g};
+  g->pipe_active = true;
   int last = 0;
   const int np = g->pipe_env == 2 ? 1 : 2;   // tuning: 2 = one internal stream for every step
   for (int it = 0; it < prm->num_iter; ++it) {

@@ -137,6 +137,8 @@ struct GnDev {
   int warm_now = 0;               // this step starts from the projected x0
   int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED, H_ALLDONE] written by the kernels
   int32_t* hflags = nullptr;      // its device address (system-scope stores: no copy kernel per poll)
+  int32_t* setup_stat = nullptr;  // pinned, mapped: the setup's one host read [nnz, max row, max wave, abort, graph diff]
+  int32_t* d_setup_stat = nullptr;
   hipEvent_t poll_ev = nullptr;   // recorded after each chunk of PCG launches
   double host_enqueue_us = 0.0;   // tuning build: host time spent enqueuing PCG iterations
   int64_t host_enqueued = 0;
@@ -197,6 +199,8 @@ struct Gn : GnDev {
   int64_t react_n = 0;
   hipEvent_t gap_end = nullptr;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gap_ev;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> entry_ev;   // solve entry -> pose done (the prefetched setup's wait)
+  double prep_wait_us = 0.0;
 #endif
 };
 
@@ -537,6 +541,16 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
       mrow[j] = slot + 1;
       ++slot;
     }
+}
+
+// the setup's host-read scalars into host-mapped memory in one kernel (five small D2H copies through pageable
+// memory cost ~15-20 us each on the frame-boundary critical path)
+__global__ void k_setup_status(const int32_t* __restrict__ row_ptr, int N, const int32_t* __restrict__ row_cnt,
+                               const int32_t* __restrict__ p_abort, const int32_t* __restrict__ gdiff, int32_t* out) {
+  if (threadIdx.x != 0) return;
+  const int32_t v[5] = {row_ptr[N], row_cnt[N], row_cnt[N + 1], *p_abort, gdiff ? *gdiff : 0};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) __hip_atomic_store(out + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_pair_count(GnDev g) {
@@ -2382,6 +2396,7 @@ static void free_all(Gn* g) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
+  if (g->setup_stat) (void)hipHostFree(g->setup_stat);
   if (g->poll_ev) (void)hipEventDestroy(g->poll_ev);
 }
 
@@ -2732,6 +2747,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   }
   if (hipHostMalloc((void**)&g->host_flags, H_COUNT * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess ||
+      hipHostMalloc((void**)&g->setup_stat, 8 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&g->d_setup_stat, g->setup_stat, 0) != hipSuccess ||
       hipEventCreateWithFlags(&g->poll_ev, hipEventDisableTiming) != hipSuccess) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
@@ -2842,6 +2859,20 @@ int ofx_gn_gaps(void* handle, double* ms, int64_t* n) {   // sum of the recorded
   *ms = t;
   *n = (int64_t)g->gap_ev.size();
   g->gap_ev.clear();
+  double te = 0.0;
+  for (auto& e : g->entry_ev) {
+    float x = 0.f;
+    OFX_HIP(hipEventSynchronize(e.second));
+    OFX_HIP(hipEventElapsedTime(&x, e.first, e.second));
+    te += x;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (getenv("OFX_GAP_VERBOSE") && !g->entry_ev.empty())
+    fprintf(stderr, "solve entry -> setup waited + pose done: %.1f us per solve (%zu); host prep_wait %.1f us per solve\n",
+            1e3 * te / g->entry_ev.size(), g->entry_ev.size(), g->prep_wait_us / g->entry_ev.size());
+  g->entry_ev.clear();
+  g->prep_wait_us = 0.0;
   if (getenv("OFX_GAP_VERBOSE"))
     fprintf(stderr, "host: convergence seen -> k_terms enqueued %.2f us, -> first chunk launch %.2f us (n %lld)\n",
             g->react_us / (double)(g->react_n ? g->react_n : 1), g->prologue_us / (double)(g->react_n ? g->react_n : 1),
@@ -3127,14 +3158,18 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N);
   hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
-  int32_t nnz = 0, lens[2] = {0, 0}, gdiff = 0, aborted = 0;
-  std::vector<int32_t> hrp(N + 1);   // row pointers: the persistent PCG's cluster -> workgroup partition
-  OFX_HIP(hipMemcpyAsync(&nnz, g->row_ptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-  OFX_HIP(hipMemcpyAsync(lens, g->row_cnt + N, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-  OFX_HIP(hipMemcpyAsync(hrp.data(), g->row_ptr, (N + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-  OFX_HIP(hipMemcpyAsync(&aborted, g->p_abort, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-  if (optimistic) OFX_HIP(hipMemcpyAsync(&gdiff, g->d_gdiff, sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  std::vector<int32_t> hrp;   // row pointers: the persistent PCG's cluster -> workgroup partition (if it may run)
+  hipLaunchKernelGGL(k_setup_status, dim3(1), dim3(64), 0, hs, (const int32_t*)g->row_ptr, N,
+                     (const int32_t*)g->row_cnt, (const int32_t*)g->p_abort,
+                     (const int32_t*)(optimistic ? g->d_gdiff : nullptr), g->d_setup_stat);
+  OFX_LAUNCH_CHECK();
+  if (!g->p_disabled) {
+    hrp.resize(N + 1);
+    OFX_HIP(hipMemcpyAsync(hrp.data(), g->row_ptr, (N + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
+  }
   OFX_HIP(hipStreamSynchronize(hs));
+  const volatile int32_t* ss = g->setup_stat;
+  const int32_t nnz = ss[0], lens[2] = {ss[1], ss[2]}, aborted = ss[3], gdiff = ss[4];
   if (aborted) {   // a persistent solve timed out earlier (it marked itself ill-posed): per-iteration launches from now on
     g->p_disabled = true;
     OFX_HIP(hipMemsetAsync(g->p_abort, 0, sizeof(int32_t), hs));
@@ -3148,8 +3183,10 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   }
   g->max_deg = lens[0];
   g->max_wave = lens[1];
-  {   // persistent PCG: consecutive clusters (one wave each) packed into workgroups of <= p_C clusters whose A blocks
-      // fit the LDS budget; enabled when every row fits three lane passes and all workgroups can be resident
+  g->p_on = false;
+  if (!hrp.empty()) {   // persistent PCG: consecutive clusters (one wave each) packed into workgroups of <= p_C
+                        // clusters whose A blocks fit the LDS budget; enabled when every row fits three lane passes
+                        // and all workgroups can be resident
     const int nc = N / kCS;
     const int budget = kPersistLds / (int)(36 * sizeof(double) + sizeof(int32_t));
     g->h_wg_cl.assign(1, 0);
@@ -3316,7 +3353,18 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
                  ofx_stream_t s) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && pb && prm && res, "null handle/problem/params/result");
+#ifdef OFX_STAMPS
+  hipEvent_t ev_entry = nullptr;
+  if (getenv("OFX_GAP_EVENTS")) {
+    OFX_HIP(hipEventCreate(&ev_entry));
+    OFX_HIP(hipEventRecord(ev_entry, as_stream(s)));
+  }
+  const auto tw0 = std::chrono::steady_clock::now();
+#endif
   prep_wait(g);
+#ifdef OFX_STAMPS
+  g->prep_wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
+#endif
   // a setup prefetched for exactly this problem (ofx_gn_prepare): wait for it on the caller's stream and load
   // the pose; otherwise (none, another problem, or it failed) set up here
   const bool use = g->prepared && g->prep_status == OFX_OK && same_problem(g->prep_pb, *pb) &&
@@ -3338,6 +3386,14 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     st = gn_setup(g, pb, prm, nullptr, s);
     if (st) return st;
   }
+#ifdef OFX_STAMPS
+  if (ev_entry) {
+    hipEvent_t e;
+    OFX_HIP(hipEventCreate(&e));
+    OFX_HIP(hipEventRecord(e, as_stream(s)));
+    g->entry_ev.emplace_back(ev_entry, e);
+  }
+#endif
   if (const char* pp = getenv("OFX_GN_PIPE")) g->pipe_env = atoi(pp);   // (read per solve: in-process A/B)
   const bool pipe = g->pipe_env && !g->p_on && g->n_comp == 0 && prm->num_iter > 0;
   if (!pipe) {

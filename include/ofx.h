@@ -466,6 +466,12 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* 
  * or a prefetch that failed, falls back to the inline setup. The problem's buffers must stay allocated and
  * unchanged until that solve. */
 int ofx_gn_prepare(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params, ofx_stream_t s);
+/* ofx_gn_prepare, started later: the prefetch's host thread waits until the next ofx_gn_solve on `trigger`
+ * (another handle) has queued the first kernels of GN step `gn_step`, or returns, or ofx_gn_prepare_wait /
+ * ofx_gn_solve / ofx_gn_destroy on this handle needs it. The setup's kernels then overlap that solve's last steps
+ * instead of following them. The ordering on `s` is taken now, as for ofx_gn_prepare. */
+int ofx_gn_prepare_after(void* handle, const ofx_gn_problem* prob, const ofx_gn_params* params, ofx_stream_t s,
+                         void* trigger, int32_t gn_step);
 /* Wait (host) until a prefetch on this handle has been enqueued, and order stream `s` after it: a
  * synchronisation of `s` afterwards covers the prefetched setup. */
 int ofx_gn_prepare_wait(void* handle, ofx_stream_t s);

@@ -111,6 +111,7 @@ _SIGS = {
     "ofx_gn_finish": [P, P, P],
     "ofx_gn_solve": [P, P, P, P, P],
     "ofx_gn_prepare": [P, P, P, P],
+    "ofx_gn_prepare_after": [P, P, P, P, P, c_int32],
     "ofx_gn_prepare_wait": [P, P],
     "ofx_gn_prefetch_stats": [P, P, P],
     "ofx_gn_share_history": [P, P],

@@ -168,6 +168,12 @@ struct Gn : GnDev {
   std::mutex mu;
   std::condition_variable cv;
   bool job = false, quit = false;   // guarded by mu: a prefetch is queued / running; shut down
+  // guarded by mu: a queued prefetch waits for its trigger (ofx_gn_prepare_after) — another handle's solve
+  // reaching a GN step, that solve returning, or a wait on this handle
+  bool gate = false;
+  Gn* pf_peer = nullptr;            // (trigger side) the handle whose gated prefetch this handle's next solve opens
+  int pf_step = 0;                  // ... at the start of this GN step (or on return)
+  Gn* pf_trigger = nullptr;         // (prefetch side) the handle holding this one as pf_peer
   int prep_dev = 0;
   int prep_status = 0;
   bool prepared = false;            // the setup of prep_pb / prep_prm is (being) enqueued on `side`
@@ -2634,16 +2640,46 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
 static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, int64_t* nnz_blocks, ofx_stream_t s);
 
 // the prefetch worker of this handle has finished enqueuing the queued setup (its status is in prep_status)
+static void open_gate(Gn* g) {
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->gate) return;
+    g->gate = false;
+  }
+  g->cv.notify_all();
+}
+
 static void prep_wait(Gn* g) {
   if (!g->worker.joinable()) return;
+  open_gate(g);   // a gated prefetch not triggered yet starts now
   std::unique_lock<std::mutex> lk(g->mu);
   g->cv.wait(lk, [g] { return !g->job; });
+}
+
+// Unlink a gated prefetch's trigger pair (either side): at destroy, and when a new prefetch replaces the link.
+static void pf_unlink(Gn* g) {
+  if (g->pf_peer) {
+    g->pf_peer->pf_trigger = nullptr;
+    g->pf_peer = nullptr;
+  }
+  if (g->pf_trigger) {
+    g->pf_trigger->pf_peer = nullptr;
+    g->pf_trigger = nullptr;
+  }
+}
+
+// The solve on `g` reached GN step `it` (or returns: it < 0): start the prefetch it gates.
+static void pf_fire(Gn* g, int it) {
+  Gn* p = g->pf_peer;
+  if (!p || (it >= 0 && it < g->pf_step)) return;
+  pf_unlink(g);
+  open_gate(p);
 }
 
 static void prep_worker(Gn* g) {
   std::unique_lock<std::mutex> lk(g->mu);
   for (;;) {
-    g->cv.wait(lk, [g] { return g->job || g->quit; });
+    g->cv.wait(lk, [g] { return (g->job && !g->gate) || g->quit; });
     if (g->quit) return;
     lk.unlock();
     int r = (hipSetDevice(g->prep_dev) == hipSuccess && hipStreamWaitEvent(g->side, g->ev_in, 0) == hipSuccess)
@@ -2894,6 +2930,8 @@ int ofx_gn_stamps(void* handle, uint64_t* out, int64_t n) {
 int ofx_gn_destroy(void* handle) {
   if (!handle) return OFX_OK;
   Gn* g = (Gn*)handle;
+  if (g->pf_peer) pf_fire(g, -1);   // a prefetch this handle would have started: start it now
+  pf_unlink(g);
   prep_wait(g);
   if (g->worker.joinable()) {
     {
@@ -2931,10 +2969,14 @@ int ofx_gn_setup(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
   return gn_setup(g, pb, prm, nnz_blocks, s);
 }
 
-int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* prm, ofx_stream_t s) {
-  Gn* g = (Gn*)handle;
+}  // extern "C"
+
+static int prepare_impl(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, ofx_stream_t s, Gn* trigger,
+                        int step) {
   OFX_CHECK_ARG(g && pb && prm, "null handle/problem/params");
+  OFX_CHECK_ARG(trigger != g, "a prefetch cannot be triggered by its own handle");
   prep_wait(g);
+  pf_unlink(g);
   g->prepared = false;
   g->prep_status = OFX_OK;
   if (!g->side) {
@@ -2958,12 +3000,32 @@ int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* 
   g->prepared = true;
   g->side_dirty = true;
   if (!g->worker.joinable()) g->worker = std::thread(prep_worker, g);
+  if (trigger) {   // the trigger's next solve opens the gate (pf_fire); it gates one prefetch at a time
+    if (trigger->pf_peer) pf_fire(trigger, -1);
+    pf_unlink(trigger);
+    trigger->pf_peer = g;
+    trigger->pf_step = step;
+    g->pf_trigger = trigger;
+  }
   {
     std::lock_guard<std::mutex> lk(g->mu);
+    g->gate = trigger != nullptr;
     g->job = true;
   }
   g->cv.notify_all();
   return OFX_OK;
+}
+
+extern "C" {
+
+int ofx_gn_prepare(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* prm, ofx_stream_t s) {
+  return prepare_impl((Gn*)handle, pb, prm, s, nullptr, 0);
+}
+
+int ofx_gn_prepare_after(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* prm, ofx_stream_t s,
+                         void* trigger, int32_t gn_step) {
+  OFX_CHECK_ARG(trigger, "null trigger handle");
+  return prepare_impl((Gn*)handle, pb, prm, s, (Gn*)trigger, gn_step);
 }
 
 int ofx_gn_share_history(void* handle, void* other) {
@@ -3353,6 +3415,10 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
                  ofx_stream_t s) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && pb && prm && res, "null handle/problem/params/result");
+  struct PfReturn {   // a gated prefetch (ofx_gn_prepare_after) not started by a GN step starts on every return
+    Gn* g;
+    ~PfReturn() { pf_fire(g, -1); }
+  } pf_guard{g};
 #ifdef OFX_STAMPS
   hipEvent_t ev_entry = nullptr;
   if (getenv("OFX_GAP_EVENTS")) {
@@ -3400,6 +3466,7 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     for (int it = 0; it < prm->num_iter; ++it) {
       st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, s);
       if (st) return st;
+      pf_fire(g, it);   // (after this step's first kernels are queued)
       st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
       if (st) return st;
       // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
@@ -3442,6 +3509,7 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     last = it;
     st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, (ofx_stream_t)x);
     if (st) return st;
+    pf_fire(g, it);
     st = gn_pcg(g, it, g->A_own, g->rhs_own, x);
     if (st) return st;
     if (!g->step_fused) {   // not converged within pcg_max_iter (or stopped): k_step here, the next stream waits

@@ -252,13 +252,20 @@ def _(state, handle, nodes, edges, edge_weights, tpos, conf, src, anchors, weigh
 @_op("gn_prepare", mutates_args=("state",))
 def gn_prepare(state: Tensor, handle: int, nodes: Tensor, edges: Tensor, edge_weights: Tensor, tpos: Tensor,
                conf: Tensor, src: Tensor, anchors: Tensor, weights: Tensor, tgt: Tensor, target_px: Optional[Tensor],
-               target_py: Optional[Tensor], intr: List[float], fparams: List[float], iparams: List[int]) -> None:
+               target_py: Optional[Tensor], intr: List[float], fparams: List[float], iparams: List[int],
+               trigger: int = 0, trigger_step: int = 0) -> None:
     """ofx_gn_prepare: prefetch the setup of the next gn_solve on this handle (host thread + the handle's own
     stream, ordered after the current stream's work); returns at once. The tensors must stay alive and
-    unchanged until that solve."""
+    unchanged until that solve. trigger != 0 (ofx_gn_prepare_after): the setup starts when the next gn_solve on
+    handle `trigger` reaches GN step trigger_step (or returns)."""
     pb = _gn_problem(nodes, edges, edge_weights, tpos, conf, src, anchors, weights, tgt, target_px, target_py,
                      None, None, intr)
-    call("ofx_gn_prepare", _lib.c_void_p(handle), byref(pb), byref(_gn_params(fparams, iparams)), _stream(nodes))
+    prm = _gn_params(fparams, iparams)
+    if trigger:
+        call("ofx_gn_prepare_after", _lib.c_void_p(handle), byref(pb), byref(prm), _stream(nodes),
+             _lib.c_void_p(trigger), int(trigger_step))
+    else:
+        call("ofx_gn_prepare", _lib.c_void_p(handle), byref(pb), byref(prm), _stream(nodes))
 
 
 @gn_prepare.register_fake

@@ -52,6 +52,9 @@ class GaussNewtonSolver:
         self._cur = 0                   # slot of the next optimize()
         self._pending = [None, None]    # a prefetched problem's tensors, alive until its solve
         self._side = None               # torch stream that orders a prefetch before the current solve
+        # GN steps of the current solve a prefetch overlaps: its setup starts when the solve begins step
+        # num_iter - prefetch_lead (ofx_gn_prepare_after); 0 = when the solve's host loop returns
+        self.prefetch_lead = 1
         self._h, self._state = self._slots[0]   # the last solve's slot (info / stats / stopped / arap / distributed)
 
     def _new_slot(self):
@@ -218,23 +221,32 @@ class GaussNewtonSolver:
                                      q.get("target_px"), q.get("target_py"), None, None, keep=False)
             before = torch.cuda.Event()
             before.record()
+            lead = int(self.prefetch_lead)
+            if lead > 0:   # queued now, started by this solve at GN step num_iter - lead (or when it returns)
+                self._prefetch(pa, before, h, int(self.params["num_iter"]) - lead, fp, ip)
         out = torch.ops.ofx.gn_solve(st, h.value, *args, fp, ip)
         self._pending[cur] = None
         self._h, self._state = h, st
         if prefetch is not None:
-            nxt = 1 - cur
-            if len(self._slots) < 2:
-                self._slots.append(self._new_slot())
-                call("ofx_gn_share_history", self._slots[1][0], self._slots[0][0])
-            if self._side is None:
-                self._side = torch.cuda.Stream(self.device)
-            h1, st1 = self._slots[nxt]
-            with torch.cuda.stream(self._side):
-                self._side.wait_event(before)
-                torch.ops.ofx.gn_prepare(st1, h1.value, *pa[:11], pa[13], fp, ip)
-            self._pending[nxt] = pa
-            self._cur = nxt
+            if lead <= 0:
+                self._prefetch(pa, before, None, 0, fp, ip)
+            self._cur = 1 - cur
         return self._pack(out, sync)
+
+    def _prefetch(self, pa, before, trigger, step, fp, ip):
+        """Queue the next problem's setup on the other slot, ordered after `before` (torch.ops.ofx.gn_prepare)."""
+        nxt = 1 - self._cur
+        if len(self._slots) < 2:
+            self._slots.append(self._new_slot())
+            call("ofx_gn_share_history", self._slots[1][0], self._slots[0][0])
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        h1, st1 = self._slots[nxt]
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(before)
+            torch.ops.ofx.gn_prepare(st1, h1.value, *pa[:11], pa[13], fp, ip, trigger.value if trigger else 0,
+                                     max(step, 0))
+        self._pending[nxt] = pa
 
     def arap(self, graph_nodes, source_node_position, target_node_position, valid_nodes_mask, original_graph_nodes,
              graph_edges, graph_edges_weights, graph_clusters, R_current, t_current, sync=True, pcg_tol=1e-10):

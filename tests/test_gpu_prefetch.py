@@ -1,7 +1,8 @@
 """GPU: the prefetched solver setup (ofx_gn_prepare / GaussNewtonSolver.optimize(prefetch=) — frame t+1's
 upload and JᵀJ pattern built on the other solver slot while frame t solves) gives bit for bit the transforms
-and the fused volume of the inline setup, over chained frames; a prefetch for a different problem is
-discarded and set up inline."""
+and the fused volume of the inline setup, over chained frames, whether the setup starts when the previous solve
+returns or during its last GN steps (ofx_gn_prepare_after); a prefetch for a different problem is discarded and set
+up inline; a gated prefetch whose trigger never solves still runs."""
 import pytest
 import torch
 
@@ -20,8 +21,9 @@ def make_pipe(cuda, config=1):
     return pipe, frames
 
 
-def run(cuda, prefetch):
+def run(cuda, prefetch, lead=1):
     pipe, frames = make_pipe(cuda)
+    pipe.solver.prefetch_lead = lead
     out = []
     for t in range(1, 6):
         res = pipe.solve(frames[t], frames[t + 1] if prefetch else None)
@@ -32,9 +34,10 @@ def run(cuda, prefetch):
     return pipe, out
 
 
-def test_prefetched_setup_equals_inline(cuda):
+@pytest.mark.parametrize("lead", [0, 1, 3, 10])
+def test_prefetched_setup_equals_inline(cuda, lead):
     p0, ref = run(cuda, False)
-    p1, got = run(cuda, True)
+    p1, got = run(cuda, True, lead)
     used, missed = p1.solver.prefetch_stats()
     assert (used, missed) == (4, 0)          # frames 2..5 used the setup prefetched during the previous frame
     assert p0.solver.prefetch_stats() == (0, 0)
@@ -89,4 +92,34 @@ def test_discarded_larger_prefetch_is_ordered_before_the_inline_setup(cuda):
         ref.solve(rframes[t])
     torch.cuda.synchronize()
     assert pipe.solver.prefetch_stats() == (1, 1)
+    assert torch.equal(pipe.prev_rot, ref.prev_rot) and torch.equal(pipe.prev_trans, ref.prev_trans)
+
+
+@pytest.mark.parametrize("destroy_trigger", [False, True])
+def test_gated_prefetch_without_its_trigger_solve(cuda, destroy_trigger):
+    """ofx_gn_prepare_after with a trigger handle that never solves: the prefetch starts when the solve that uses it
+    waits for it, or when the trigger handle is destroyed, and gives the inline result."""
+    from occlusionfusion_amd import _lib
+    pipe, frames = make_pipe(cuda)
+    ref, _ = make_pipe(cuda)
+    s = pipe.solver
+    pipe.solve(frames[1])
+    ref.solve(frames[1])
+    trig, _ = s._new_slot()
+    q = pipe.problem(frames[2])
+    pa, _, _ = s._problem(q["graph_nodes"], q["graph_edges"], q["graph_edges_weights"], q["target_node_position"],
+                          q["node_confidence"], q["source_points"], q["anchors"], q["weights"], q["target_points"],
+                          pipe.intr, None, None, None, None, keep=False)
+    before = torch.cuda.Event()
+    before.record()
+    s._prefetch(pa, before, trig, 0, *s._plist())
+    s._cur = 1 - s._cur
+    if destroy_trigger:
+        _lib.lib.ofx_gn_destroy(trig)
+    pipe.solve(frames[2])
+    ref.solve(frames[2])
+    torch.cuda.synchronize()
+    if not destroy_trigger:
+        _lib.lib.ofx_gn_destroy(trig)
+    assert s.prefetch_stats() == (1, 0)
     assert torch.equal(pipe.prev_rot, ref.prev_rot) and torch.equal(pipe.prev_trans, ref.prev_trans)

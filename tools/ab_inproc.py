@@ -3,6 +3,12 @@ frame on the bench's config-3 sequence, so that run-level spread (whole processe
 launch) cancels. Prints mean ms per frame (solve + integrate, stream events) per setting.
 
     python tools/ab_inproc.py OFX_GN_PIPE 0 1 [--frames 120]
+    python tools/ab_inproc.py prefetch_lead 0 1 2 --block 8   # a solver attribute, switched every 8 frames
+
+--block B: switch every B frames and leave the first frame of each block out (a setting that acts across the
+frame boundary, such as when the next frame's prefetched setup starts, then counts only against itself).
+--sweep R: instead, run the same frames once per setting, R rounds (settings in turn); also reports the mean per-frame
+difference to the first setting over identical frames.
 """
 import argparse
 import json
@@ -21,6 +27,8 @@ def main():
     ap.add_argument("values", nargs="+")
     ap.add_argument("--frames", type=int, default=120)
     ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--block", type=int, default=1)
+    ap.add_argument("--sweep", type=int, default=0)
     a = ap.parse_args()
     from occlusionfusion_amd import synthetic as S
     from occlusionfusion_amd.pipeline import FusionPipeline
@@ -35,15 +43,49 @@ def main():
     pipe.integrate_source(frames[0])
     times = {v: [] for v in a.values}
     marks = []
+
+    def setv(v):
+        if a.var == "prefetch_lead":
+            pipe.solver.prefetch_lead = int(v)
+        else:
+            os.environ[a.var] = v
+
+    if a.sweep:
+        per = {v: [] for v in a.values}
+        tg = 0   # the volume's frame counter keeps increasing over the repeated frames
+        for r in range(a.sweep):
+            for v in a.values:
+                setv(v)
+                pipe.prev_rot = pipe.prev_trans = None   # the same solves each run: frame 1 from the rest pose
+                ev = []
+                for t in range(1, total):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    pipe.solve(frames[t], frames[t + 1])
+                    tg += 1
+                    pipe.integrate(frames[t], tg)
+                    e1.record()
+                    ev.append((e0, e1))
+                pipe.solver.drain()
+                torch.cuda.synchronize()
+                per[v].append(np.array([e0.elapsed_time(e1) for e0, e1 in ev[4:]]))
+        base = np.stack(per[a.values[0]])
+        out = {}
+        for v in a.values:
+            x = np.stack(per[v])
+            out[v] = {"ms_per_frame": float(x.mean()), "run_means": [float(q) for q in x.mean(1)],
+                      "paired_diff_ms": float((x - base).mean()), "n": int(x.size)}
+        print(json.dumps({"var": a.var, "sweep": a.sweep, "results": out}))
+        return
     for t in range(1, total):
-        v = a.values[t % len(a.values)]
-        os.environ[a.var] = v
+        v = a.values[(t // a.block) % len(a.values)]
+        setv(v)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         pipe.solve(frames[t], frames[t + 1])
         pipe.integrate(frames[t], t)
         e1.record()
-        if t > 4:
+        if t > 4 and (a.block == 1 or t % a.block != 0):
             marks.append((v, e0, e1))
     pipe.solver.drain()
     torch.cuda.synchronize()

@@ -72,7 +72,10 @@ class FusionPipeline:
                     weights=fi.weights, target_points=fi.tgt)
 
     def solve(self, fi, next_fi=None):
-        """GN solve of frame fi; next_fi: the next frame, whose solver setup is prefetched concurrently."""
+        """GN solve of frame fi; next_fi: the next frame, whose solver setup is prefetched concurrently. Frame fi's
+        depth/colour unpacking for its integrate is enqueued first (TSDFVolume.stage), so the host work between the
+        solve's return and the integrate launch is only the integrate's own."""
+        self.vol.stage(fi.im)
         out = self.solver.optimize(self.nodes_t, self.edges_t, self.ew_t, fi.tpos, fi.conf, fi.src, fi.anchors,
                                    fi.weights, fi.tgt, self.intr, prev_rot=self.prev_rot, prev_trans=self.prev_trans,
                                    sync=False, prefetch=None if next_fi is None else self.problem(next_fi))

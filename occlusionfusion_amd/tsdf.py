@@ -144,17 +144,34 @@ class TSDFVolume:
         c.height, c.width = int(self.depth_t.shape[0]), int(self.depth_t.shape[1])
         return c
 
-    def update(self, im, frame_id):
-        """tsdf.py:545-572: unpack the (6,H,W) frame; depth = im[-1]; colour folded on device."""
+    def _unpack(self, im):
+        """(depth, packed colour) device tensors of a (6,H,W) frame; the colour packing is enqueued here."""
         im_t = im if isinstance(im, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(im, dtype=np.float32))
         im_t = im_t.to(self.device, torch.float32, non_blocking=True)
         assert im_t.dim() == 3 and im_t.shape[0] >= 4, f"Input not correct: expected (6,H,W), got {tuple(im_t.shape)}"
-        self.im = im
-        self.depth_t = im_t[-1].contiguous()
-        H, W = self.depth_t.shape
-        self.color_t = torch.empty((H, W), dtype=torch.float32, device=self.device)
+        depth = im_t[-1].contiguous()
+        H, W = depth.shape
+        color = torch.empty((H, W), dtype=torch.float32, device=self.device)
         rgb = im_t[:3].contiguous()
-        call("ofx_pack_color", ptr(rgb), H, W, ptr(self.color_t), stream_ptr())
+        call("ofx_pack_color", ptr(rgb), H, W, ptr(color), stream_ptr())
+        return depth, color
+
+    def stage(self, im):
+        """Unpack the frame that the next update(im, ...) will take, now: its device work (the colour packing) is
+        enqueued at this point of the stream and update() only adopts the result. A frame loop stages frame t
+        before frame t's solve, so the host work between the solve's return and the integrate launch shrinks (the
+        GPU waits for it there)."""
+        self._staged = (im,) + self._unpack(im)
+
+    def update(self, im, frame_id):
+        """tsdf.py:545-572: unpack the (6,H,W) frame; depth = im[-1]; colour folded on device."""
+        st = getattr(self, "_staged", None)
+        self._staged = None
+        if st is not None and st[0] is im:
+            self.depth_t, self.color_t = st[1], st[2]
+        else:
+            self.depth_t, self.color_t = self._unpack(im)
+        self.im = im
         if hasattr(self, "frame_id"):
             skip = _opt(self.fopt, "skip_rate", 1)
             assert self.frame_id + skip == frame_id, \
@@ -176,19 +193,20 @@ class TSDFVolume:
         self.integrate_device(obs_weight)
 
     def integrate_device(self, obs_weight=1., count_updates=False):
-        """Integrate the current (already updated) frame through torch.ops.ofx.integrate; no host sync."""
+        """Integrate the current (already updated) frame through torch.ops.ofx.integrate (the warped palette path:
+        its library call directly); no host sync."""
         src = _opt(self.fopt, "source_frame", 0)
         color = self.color_b if self.with_color else None
         color_im = self.color_t if self.with_color else None
         nu = self.n_updated if count_updates else None
         d = self.desc
-        geo = ([int(v) for v in d.dim], [self.brick_x0, self.brick_x1], [float(v) for v in d.origin],
-               float(d.voxel_size), float(d.trunc_margin), int(d.semantics),
-               [float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1]), float(self.cam_intr[0, 2]),
-                float(self.cam_intr[1, 2])], float(obs_weight))
+        geo = lambda: ([int(v) for v in d.dim], [self.brick_x0, self.brick_x1], [float(v) for v in d.origin],
+                       float(d.voxel_size), float(d.trunc_margin), int(d.semantics),
+                       [float(self.cam_intr[0, 0]), float(self.cam_intr[1, 1]), float(self.cam_intr[0, 2]),
+                        float(self.cam_intr[1, 2])], float(obs_weight))
         if self.frame_id == src:
             ob = self.owned_bricks
-            torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo,
+            torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo(),
                                     None, 0, 1, ob, 0 if ob is None else int(ob.shape[0]), None, None, None, None, None)
             return
         if self.warpfield is None:
@@ -196,7 +214,13 @@ class TSDFVolume:
         cache = self.warpfield.skin_tsdf_cache()
         nodes = self.warpfield.packed_nodes()
         pal = self.use_palette and cache.pal_n is not None
-        torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo,
+        if pal:   # the frame loop's path: the library call of torch.ops.ofx.integrate's palette branch, made directly
+            call("ofx_integrate_palette", byref(d), byref(self.camera()), ptr(self.depth_t), ptr(color_im), ptr(nodes),
+                 self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
+                 ptr(cache.weights), ptr(cache.pal_ids), ptr(cache.pal_n), ptr(cache.local), float(obs_weight),
+                 ptr(self.tsdf_b), ptr(self.weight_b), ptr(color), ptr(nu), stream_ptr())
+            return
+        torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo(),
                                 nodes, self.warpfield.num_nodes, cache.k, cache.brick_list, cache.n_list,
                                 cache.anchors, cache.weights, cache.pal_ids if pal else None,
                                 cache.pal_n if pal else None, cache.local if pal else None)

@@ -288,10 +288,16 @@ class WarpField:
         self._packed = None
 
     def packed_nodes(self):
+        """(N,16) f32 device rows [R | t | g] of the current transforms (ofx_pack_nodes), repacked into one buffer
+        kept across frames (stream-ordered after the previous frame's readers)."""
         if self._packed is None:
-            self._packed = torch.empty((self.num_nodes, 16), dtype=torch.float32, device=self.device)
-            call("ofx_pack_nodes", ptr(self.R_t), ptr(self.T_t), ptr(self.nodes_t), self.num_nodes, ptr(self._packed),
+            buf = getattr(self, "_packed_buf", None)
+            if buf is None or buf.shape[0] != self.num_nodes or buf.device != self.R_t.device:
+                buf = torch.empty((self.num_nodes, 16), dtype=torch.float32, device=self.device)
+                self._packed_buf = buf
+            call("ofx_pack_nodes", ptr(self.R_t), ptr(self.T_t), ptr(self.nodes_t), self.num_nodes, ptr(buf),
                  stream_ptr())
+            self._packed = buf
         return self._packed
 
     def update_transformations(self, nnrt_data):

@@ -882,7 +882,11 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
 // free writes); then each (block, output) pair — 576 per workgroup, up to 3 per thread — adds its entries of
 // the chunk in list order. A block's cost is its share of the workgroup's entries, not its own list length
 // (the 16-lane form took ceil(len/16) dependent trips: ~6 for a busy node's diagonal block).
-constexpr int kCoop = 128;
+#ifndef OFX_KCOOP
+#define OFX_KCOOP 128   // (tuning builds: -DOFX_KCOOP=n, n <= kBlk)
+#endif
+constexpr int kCoop = OFX_KCOOP;
+static_assert(kCoop <= kBlk, "one entry per thread per chunk");
 __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, double* __restrict__ A, int64_t wg,
                                             double lm) {
   __shared__ double s_prod[36 * (kCoop + 1)];

@@ -4,6 +4,8 @@ restatement of the GN linearisation) for warm-start strategies:
   proj4     Galerkin projection on the last 4 GN-step solutions (the product's warm start)
   krylov    x0 = sum_i p_i (p_i·b)/(p_i·A_old p_i) over the previous step's PCG directions
   both      krylov directions + last 4 solutions, Galerkin with the new A (small dense solve)
+  prev1     x0 = the previous step's solution (no projection: no global reduction before the PCG)
+  extrap    x0 = 2 x_{k-1} - x_{k-2} (linear extrapolation, likewise reduction-free)
 """
 import math
 import os
@@ -160,6 +162,10 @@ def run(prob, mode, N):
         x0 = np.zeros(6 * N)
         if mode == "proj4" and hist:
             x0 = galerkin(A, b, np.stack(hist[-4:], 1))
+        elif mode == "prev1" and hist:
+            x0 = hist[-1].copy()
+        elif mode == "extrap" and hist:
+            x0 = (2 * hist[-1] - hist[-2]) if len(hist) > 1 else hist[-1].copy()
         elif mode == "krylov" and P:
             x0 = kry_init(b, P, PAP, 400)
         elif mode == "both" and hist:
@@ -178,7 +184,8 @@ if __name__ == "__main__":
     seq = S.SyntheticSequence.build(2000, seed=3)
     prob = Problem(seq, int(sys.argv[1]) if len(sys.argv) > 1 else 12)
     N = seq.nodes.shape[0]
-    for mode in (() if len(sys.argv) > 2 else ("cold", "proj4", "krylov", "both")):
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ("cold", "proj4", "krylov", "both")
+    for mode in modes:
         its = run(prob, mode, N)
         print(mode, sum(its), its, flush=True)
 

@@ -16,6 +16,7 @@ cd $R
 grep '"metric"' gpurun_out/bench_rocprof.log | tail -1 > gpurun_out/${TAG}_bench_under_rocprof.json
 python tools/kstats.py gpurun_out/prof_final/run_results.db --csv gpurun_out/${TAG}_bench_kernel_stats.csv > gpurun_out/kstats.txt
 head -16 gpurun_out/kstats.txt
+rm -rf gpurun_out/prof_final
 timeout -k 10 900 python bench.py > gpurun_out/bench_full.log 2>&1
 tail -1 gpurun_out/bench_full.log > gpurun_out/${TAG}_bench.json
 cat gpurun_out/${TAG}_bench.json

@@ -1699,12 +1699,18 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
 // two), stages only its half of the inverse's column groups and applies that half (split-K); the scalar
 // work, row sums and recurrences run in both waves (identical bits), wave 0 alone stores. Two LDS barriers
 // (products, M⁻¹ halves), no memory release.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+// kEarly: trip 1 issues the wave list and the stop word first, and waits only for those two before the stop test and
+// trip 2's issue (the rest of trip 1 lands under trip 2's flight; the scalars and the M⁻¹ apply wait for their own
+// loads, which retire in issue order), instead of waiting for all of trip 1. The lane's row of the cluster inverse
+// (its wave's column half) then comes to registers by plain loads (the wave's 48 row lanes read 768 contiguous bytes
+// per column group): a pending LDS-DMA would make the compiler wait for everything (vmcnt(0)) at the first use of
+// any load.
+template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kEarly = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   constexpr int kNH = kW2 ? 2 : 1;
   __shared__ double s_v[kNH][kCD];
-  __shared__ float4 s_m[kCD * kCD / 4];
+  __shared__ float4 s_m[kEarly ? 1 : kCD * kCD / 4];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   __shared__ double s_half[kW2 ? 64 : 1];
   const int lane = threadIdx.x & 63;
@@ -1733,6 +1739,13 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
+  if (kEarly) asm volatile("" ::: "memory");   // the list and stop word leave first
+  constexpr int kMR = kEarly ? kCD / 4 / kNH : 1;   // the lane's inverse row: float4 column groups of its wave's half
+  float4 mreg[kMR];
+  if (kEarly)
+#pragma unroll
+    for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
+  auto inverse_dma = [&]() {
   if (kW2) {   // wave h: column groups [6h, 6h + 6) = float4 [288h, 288h + 288), 5 DMA instructions; the last
               // one is moved back to end at the half's end (it rewrites 32 of the wave's own float4 with the
               // same bits), so no wave's DMA touches the other wave's half
@@ -1748,6 +1761,8 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     for (int k = 0; k < kMS; ++k)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + k * 64 + lane), reinterpret_cast<void*>(s_m + k * 64), 16, 0, 0);
   }
+  };
+  if (!kEarly) inverse_dma();
   double v[V_N];
   load_rec(g.st, o, v);
   const double m = mc[o];
@@ -1770,7 +1785,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
+  if (!kEarly) __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
   if (stop_ep >= g.ep) return;     // this solve has converged (or stopped): a drained launch
 #ifdef OFX_STAMPS
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
@@ -1914,7 +1929,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int kk = 0; kk < kCD / 8; ++kk) {
         const int k = (kCD / 8) * hw + kk;
-        const float4 t = mrow[k * kCD];
+        const float4 t = kEarly ? mreg[kk % kMR] : mrow[k * kCD];
         a[0] = fma((double)t.x, s_v[hw][4 * k], a[0]);
         a[1] = fma((double)t.y, s_v[hw][4 * k + 1], a[1]);
         a[2] = fma((double)t.z, s_v[hw][4 * k + 2], a[2]);
@@ -1931,7 +1946,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     double a[4] = {0.0, 0.0, 0.0, 0.0};   // four independent FMA chains
 #pragma unroll
     for (int k = 0; k < kCD / 4; ++k) {
-      const float4 t = mrow[k * kCD];
+      const float4 t = kEarly ? mreg[k % kMR] : mrow[k * kCD];
       a[0] = fma((double)t.x, s_v[0][4 * k], a[0]);
       a[1] = fma((double)t.y, s_v[0][4 * k + 1], a[1]);
       a[2] = fma((double)t.z, s_v[0][4 * k + 2], a[2]);
@@ -2487,22 +2502,27 @@ static int pcg_ku_for(int waves) {
 }
 
 using PcgKernel = void (*)(PcgIt, int);
-template <int KU>
-static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
+template <int KU, bool E>
+static void pcg_pick_e(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU == 3) {
     if (wave && w2) {
-      first = k_pcg_iter<true, true, 3, true>;
-      rest = k_pcg_iter<true, false, 3, true>;
+      first = k_pcg_iter<true, true, 3, true, E>;
+      rest = k_pcg_iter<true, false, 3, true, E>;
       return;
     }
   }
   if (wave) {
-    first = k_pcg_iter<true, true, KU>;
-    rest = k_pcg_iter<true, false, KU>;
+    first = k_pcg_iter<true, true, KU, false, E>;
+    rest = k_pcg_iter<true, false, KU, false, E>;
   } else {
-    first = k_pcg_iter<false, true, KU>;
-    rest = k_pcg_iter<false, false, KU>;
+    first = k_pcg_iter<false, true, KU, false, E>;
+    rest = k_pcg_iter<false, false, KU, false, E>;
   }
+}
+template <int KU>
+static void pcg_pick(bool wave, bool w2, bool early, PcgKernel& first, PcgKernel& rest) {
+  if (early) pcg_pick_e<KU, true>(wave, w2, first, rest);
+  else pcg_pick_e<KU, false>(wave, w2, first, rest);
 }
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
@@ -2546,11 +2566,15 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku == 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
+  // early stop test / trip-2 issue (kEarly, the default; OFX_PCG_EARLY=0: the all-of-trip-1 wait with the inverse by
+  // LDS-DMA; read per solve: in-process A/B)
+  const char* ee = getenv("OFX_PCG_EARLY");
+  const bool early = !(ee && ee[0] == '0');
   switch (g->pcg_ku) {
-    case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
-    case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
-    case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
-    default: pcg_pick<17>(wave, w2, iter0, iter); break;
+    case 3: pcg_pick<3>(wave, w2, early, iter0, iter); break;
+    case 4: pcg_pick<4>(wave, w2, early, iter0, iter); break;
+    case 8: pcg_pick<8>(wave, w2, early, iter0, iter); break;
+    default: pcg_pick<17>(wave, w2, early, iter0, iter); break;
   }
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host

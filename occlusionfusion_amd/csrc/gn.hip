@@ -1233,9 +1233,6 @@ __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const dou
 __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __restrict__ A,
                                                  const double* __restrict__ rhs, int invert) {
   if (g.flags[F_STOPPED]) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
-  }
   const int lane = threadIdx.x;
   const int base = blockIdx.x * kCS;
   const int ti = lane / kCS, tj = lane % kCS;
@@ -1292,6 +1289,8 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
     for (int c = 0; c < 3; ++c)   // (j, j+1) with j even share a float4
       *reinterpret_cast<float2*>(g.Mcl + mcl_idx(blockIdx.x, 6 * ti + r, 6 * tj + 2 * c)) =
           make_float2(m[r][2 * c], m[r][2 * c + 1]);
+  // PCG bookkeeping of this GN step (as k_pcg_proj: after the workgroup's loads)
+  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
   if (g.warm_now) return;
   // cold start: u = M⁻¹ b with the stored (f32) operator; the 8 lanes of a block row sum in fixed order
   double bj[6], u[6];
@@ -1341,9 +1340,6 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
   const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];   // issued with the stop flag: one trip
   if (g.flags[F_STOPPED]) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {   // PCG bookkeeping of this GN step (also in k_pcg_prep)
-    g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0;
-  }
   const int np = g.n_prev;
   const int64_t stride = 6 * (int64_t)g.N;
   double n[kProj][6];
@@ -1420,6 +1416,9 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
   if (lane == 0)
 #pragma unroll
     for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nwg_row + blockIdx.x] = v[k];
+  // PCG bookkeeping of this GN step (also in k_pcg_prep), stored last: on gfx9 vmcnt counts stores too, so stores
+  // ahead of the loads made workgroup 0's first wait a vmcnt(0) that also waited for their acks
+  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
 }
 
 // Galerkin warm start, pass 2: every wave re-derives G and f from the partials (fixed order,
@@ -1705,7 +1704,7 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
 // (its wave's column half) then comes to registers by plain loads (the wave's 48 row lanes read 768 contiguous bytes
 // per column group): a pending LDS-DMA would make the compiler wait for everything (vmcnt(0)) at the first use of
 // any load.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kEarly = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+template <bool kWave, bool kFirst, int kU, bool kW2 = false, int kEarly = 0>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   constexpr int kNH = kW2 ? 2 : 1;
@@ -1735,11 +1734,13 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     bl0 = g.wl[(int64_t)wv * kWL + 64 * hw + lane];
     if (!kW2) bl1 = g.wl[(int64_t)wv * kWL + 64 + lane];
   }
-  const int stop_ep = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
+  int stop_ep = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
   const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
   if (kEarly) asm volatile("" ::: "memory");   // the list and stop word leave first
+  constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
+  double2 ab[kNB][18], xb[kNB][3];
   constexpr int kMR = kEarly ? kCD / 4 / kNH : 1;   // the lane's inverse row: float4 column groups of its wave's half
   float4 mreg[kMR];
   if (kEarly)
@@ -1786,24 +1787,32 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
   if (!kEarly) __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
+  // kEarly >= 2: the wave's stop words are equal (every lane stores the same epoch), and so are the scalars below: taken
+  // as wave-uniform values the exits are scalar branches, so the main path's waits are not merged with the exit paths'
+  // (a divergent exit left a vmcnt(0) at the join in front of the products)
+  if (kEarly >= 2) stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
   if (stop_ep >= g.ep) return;     // this solve has converged (or stopped): a drained launch
 #ifdef OFX_STAMPS
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
 #endif
   OFX_STAMP(1)
   // ---- trip 2: A blocks and gathered m (issued first; the scalar work below overlaps their flight)
-  constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
-  double2 ab[kNB][18], xb[kNB][3];
   if (kWave)
 #pragma unroll
     for (int j = 0; j < kNB; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked later)
       const int2 e = j ? bl1 : bl0;
       const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e.y);
       const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
+      if (kEarly >= 2) {   // the gathered m row first: the products of the first block rows start before the block's tail lands
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
+        asm volatile("" ::: "memory");
+      }
 #pragma unroll
       for (int k = 0; k < 18; ++k) ab[j][k] = blk[k];
+      if (kEarly < 2)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
+        for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
   // ---- scalars from the partials (trip-1 data)
@@ -1826,7 +1835,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const double tol = g.prm.pcg_tol;
   const bool lead = wv == 0 && lane == 0 && hw == 0;
   const bool w0 = hw == 0;   // the wave that stores (kW2: both compute the same bits)
-  if (kFirst && lead) g.scal[S_BB] = bb;
+  if (kFirst && lead && kEarly < 2) g.scal[S_BB] = bb;   // (kEarly >= 2: with the lead's other stores, last)
   double beta = 0.0, alpha;
   if (kFirst) {
     alpha = gam / del;
@@ -1835,7 +1844,10 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     alpha = gam / (del - beta * gam * ralpha_prev);
   }
   const bool conv = rr <= tol * tol * bb || gam == 0.0;
-  if (conv || !isfinite(alpha) || !(alpha > 0.0)) {   // converged, or breakdown (A SPD => alpha > 0): keep x
+  int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
+  if (kEarly >= 2) leave = __builtin_amdgcn_readfirstlane(leave);
+  if (leave) {   // converged, or breakdown (A SPD => alpha > 0): keep x
+    if (kFirst && lead && kEarly >= 2) g.scal[S_BB] = bb;
     if (!w0) return;
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
     g.stopw[(int64_t)wv * 64 + lane] = g.ep;
@@ -1860,7 +1872,13 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     }
     return;
   }
-  if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
+  // the lead's scalar stores (read by the next launch only): kEarly issues them last — on gfx9 vmcnt counts stores too,
+  // so stores issued here made the lead wave's first wait on trip 2 a vmcnt(0) that also waited for their acks
+  auto lead_stores = [&]() {
+    if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
+    if (kFirst && lead && kEarly >= 2) g.scal[S_BB] = bb;
+  };
+  if (kEarly < 2) lead_stores();
   OFX_STAMP(2)
   // ---- n = A m (own component)
   double nc;
@@ -1959,6 +1977,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
+  if (kEarly >= 2) lead_stores();
   OFX_STAMP(7)
 }
 
@@ -2502,7 +2521,7 @@ static int pcg_ku_for(int waves) {
 }
 
 using PcgKernel = void (*)(PcgIt, int);
-template <int KU, bool E>
+template <int KU, int E>
 static void pcg_pick_e(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU == 3) {
     if (wave && w2) {
@@ -2520,9 +2539,10 @@ static void pcg_pick_e(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   }
 }
 template <int KU>
-static void pcg_pick(bool wave, bool w2, bool early, PcgKernel& first, PcgKernel& rest) {
-  if (early) pcg_pick_e<KU, true>(wave, w2, first, rest);
-  else pcg_pick_e<KU, false>(wave, w2, first, rest);
+static void pcg_pick(bool wave, bool w2, int early, PcgKernel& first, PcgKernel& rest) {
+  if (early == 2) pcg_pick_e<KU, 2>(wave, w2, first, rest);
+  else if (early == 1) pcg_pick_e<KU, 1>(wave, w2, first, rest);
+  else pcg_pick_e<KU, 0>(wave, w2, first, rest);
 }
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
@@ -2566,10 +2586,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku == 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
-  // early stop test / trip-2 issue (kEarly, the default; OFX_PCG_EARLY=0: the all-of-trip-1 wait with the inverse by
-  // LDS-DMA; read per solve: in-process A/B)
+  // early stop test / trip-2 issue (kEarly; OFX_PCG_EARLY=0: the all-of-trip-1 wait with the inverse by LDS-DMA, 1: the
+  // early trip-2 issue alone, 2 (default): + gathered rows first, the lead's stores last and scalar exit branches; read
+  // per solve: in-process A/B)
   const char* ee = getenv("OFX_PCG_EARLY");
-  const bool early = !(ee && ee[0] == '0');
+  const int early = (ee && ee[0] >= '0' && ee[0] <= '2') ? ee[0] - '0' : 2;
   switch (g->pcg_ku) {
     case 3: pcg_pick<3>(wave, w2, early, iter0, iter); break;
     case 4: pcg_pick<4>(wave, w2, early, iter0, iter); break;

@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--voxel", type=float, default=None)
     p.add_argument("--nodes", type=int, default=None)
     p.add_argument("--matches", type=int, default=10000)
+    p.add_argument("--scene-rank", type=int, default=None,
+                   help="config 5: run this rank's independent scene (default: the process's own rank)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                    help="set up each frame's solve inline instead of prefetching it during the previous frame")
@@ -169,7 +171,8 @@ def main():
     D = a.dims
     origin = cfg["origin"] if (a.dims, a.voxel) == (cfg["dims"], cfg["voxel"]) else \
         (-D * a.voxel / 2, -D * a.voxel / 2, 0.5)
-    seq = S.config_sequence(a.config, a.nodes, rank=rank if a.mode == "replicas" else 0, device=dev)
+    scene_rank = (a.scene_rank if a.scene_rank is not None else rank) if a.mode == "replicas" else 0
+    seq = S.config_sequence(a.config, a.nodes, rank=scene_rank, device=dev)
     scene_seed = int(seq.seed)
     sharded = a.mode == "shard" and world > 1
     shard = (rank, world, "hash") if sharded else None   # spatial-hash brick buckets (sharding.hash_owner)
@@ -306,7 +309,7 @@ def main():
                    "solve": (a.solve if sharded else "local"), "dims": D, "voxel_size_m": a.voxel,
                    "nodes": int(seq.nodes.shape[0]), "matches": a.matches,
                    "parallelism": f"{a.mode}{world}" + (f"-{a.solve}" if sharded else ""),
-                   "setup_prefetch": prefetch},
+                   "setup_prefetch": prefetch, "scene_seed": scene_seed},
         "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * float(np.mean(t_int)),
                          "allreduce": 1e3 * t_ar, "pcg_iters_per_frame": float(np.mean(pcg)),
                          "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid)),

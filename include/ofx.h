@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define OFX_ABI_VERSION 1
+#define OFX_ABI_VERSION 2
 
 typedef void* ofx_stream_t; /* hipStream_t; NULL = legacy default stream */
 
@@ -367,6 +367,10 @@ typedef struct ofx_gn_params {
   int32_t precond_every;     /* the cluster preconditioner is rebuilt on GN steps gn_iter % precond_every == 0
                                 (0 or 1: every step) and reused by the warm-started steps in between; it only
                                 shapes convergence, the stop test is unchanged */
+  double pcg_err_tol;        /* error-based stop (> 0): the inner solve also runs until its estimated solution
+                                error sqrt(r^T M^-1 r) / theta <= pcg_err_tol, theta = the smallest Ritz value of
+                                the preconditioned operator's Lanczos tridiagonal (from below, within a factor
+                                sqrt 2); 0: the relative residual alone. Both stop at a relative residual of 1e-12 */
 } ofx_gn_params;
 
 /* OFX_GN_ARAP restates DeformNet.arap (model/model.py:1639-1986), the graph-update solve for nodes
@@ -409,7 +413,7 @@ typedef struct ofx_gn_result {
 int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle);
 /* Profiling hook: returns (and resets) the device time of the PCG iteration loops recorded since the
  * last call (hipEvents on the solve stream; synchronises on them), the number of PCG launches (k_pcg_iter
- * launches, or one k_pcg_persist launch per GN step) and of timed solves; `enable` switches recording for the
+ * launches) and of timed solves; `enable` switches recording for the
  * following steps. */
 int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_launches, int64_t* n_solves);
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
@@ -419,13 +423,10 @@ int ofx_gn_info(void* handle, int64_t* info);
  * 384 clusters (default) or 1 (environment OFX_PCG_W1 set to anything but "" / "0" at create; tuning and A/B
  * only); larger problems always run one wave per cluster. */
 int ofx_gn_pcg_waves(void* handle, int32_t* waves);
-/* PCG form of the last setup: form (host int32[3]) = [1 if each GN step's PCG is ONE persistent launch
- * (k_pcg_persist: A blocks in LDS, state in registers, m and the dot-product partials handed between workgroups)
- * else 0 (one k_pcg_iter launch per iteration), workgroups of the persistent launch, clusters per workgroup].
- * Persistent when selected (environment OFX_PCG_PERSIST=1 at create) unless a workgroup's blocks exceed its LDS, a
- * cluster has more than 128 blocks or a row more than 20, more than min(128, CUs) workgroups would be needed,
- * pcg_max_iter >= 4096, or an earlier persistent solve of the handle timed out (it then reported valid_solve = 0). */
-int ofx_gn_pcg_form(void* handle, int32_t* form);
+/* 1 if the last ofx_gn_step's GN update was taken by its converging PCG launch (its stop flag, ofx_gn_stopped, is
+ * then already visible to the host when ofx_gn_step returns); 0 if k_step runs as its own launch (the PCG hit
+ * pcg_max_iter, or the arap null-space projection runs first): the flag is written asynchronously. */
+int ofx_gn_step_fused(void* handle, int32_t* fused);
 /* The solve's stop flag as the host sees it (host-mapped, no synchronisation): 1 once a GN step's loss rule
  * (model.py:726-732) or an ill-posed solve stopped it. The device writes it asynchronously: a stepped multi-rank
  * loop reads it only after synchronising the stream behind ofx_gn_step(i), so that every rank leaves after the

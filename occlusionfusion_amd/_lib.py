@@ -30,7 +30,8 @@ class GnParams(ctypes.Structure):
     _fields_ = [("num_iter", c_int32), ("use_edge_weighting", c_int32), ("pcg_max_iter", c_int32), ("pcg_warm", c_int32),
                 ("lambda_flow", c_double), ("lambda_depth", c_double), ("lambda_arap", c_double),
                 ("lambda_motion", c_double), ("lm_factor", c_double), ("stop_loss_diff", c_double),
-                ("pcg_tol", c_double), ("mode", c_int32), ("precond_every", c_int32)]
+                ("pcg_tol", c_double), ("mode", c_int32), ("precond_every", c_int32),
+                ("pcg_err_tol", c_double)]
 
 
 class GnProblem(ctypes.Structure):
@@ -101,7 +102,7 @@ _SIGS = {
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
     "ofx_gn_pcg_waves": [P, P],
-    "ofx_gn_pcg_form": [P, P],
+    "ofx_gn_step_fused": [P, P],
     "ofx_gn_stopped": [P, P],
     "ofx_gn_stats": [P, P, c_int32],
     "ofx_gn_row_order": [P, P, c_int32],

@@ -87,7 +87,6 @@ struct GnDev {
   int max_wave = 0;              // most blocks of one PCG wave (kCS rows)
   int32_t* stopw = nullptr;      // per PCG wave and lane: the epoch of the last converged (or stopped) PCG solve
   int32_t ep = 0;                // epoch of the current PCG solve (one per GN step, increasing per handle)
-  int32_t* arrive = nullptr;     // workgroups of the converging launch that have finished (reset by the last)
   uint64_t* stamps = nullptr;    // tuning builds (-DOFX_STAMPS): per iteration < 64 and wave, 8 clock stamps
   int32_t* blk_row = nullptr;    // block -> row (clears the slot map's pattern at the next setup)
   float* d_gnodes = nullptr;      // device copy of the graph the row order was built for (optimistic check)
@@ -97,9 +96,10 @@ struct GnDev {
   int pat_N = 0;                 // N and block count of the pattern currently set in `map`
   int64_t pat_nnzb = 0;
   int64_t ne_cap = 0;            // capacity of edges / ew
-  // contribution lists of the UPPER blocks only (col >= row, indexed u = up_of[slot]): A is exactly symmetric —
-  // the lower block (j, i)'s products are the upper block's with the factors commuted, summed in the same order —
-  // so the assembly computes each upper block once and also stores its transpose at up_tr[u]
+  // contribution lists of the UPPER blocks only (col >= row, indexed u = up_of[slot]): the assembly computes each
+  // upper block once and also stores its transpose at up_tr[u], so A is exactly symmetric. (A separate gather of the
+  // lower block (j, i) would sum the same products in the same order only when no node repeats within a term; with
+  // a repeated anchor its last bits could differ from the transpose.)
   int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr, *blk_tmp = nullptr;
   int32_t *up_of = nullptr, *up_slot = nullptr, *up_tr = nullptr;   // slot -> u (+ total at [nnzb]), u -> slot, transpose
   int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr, *node_tmp = nullptr;
@@ -111,7 +111,8 @@ struct GnDev {
   const double* Aop = nullptr;    // PCG operator (the damped A of the current step)
   double *st = nullptr;          // PCG recurrence state, 6N records of 8 (see the PCG layout note)
   double *m0 = nullptr, *m1 = nullptr;   // double-buffered m = M⁻¹w (gathered by the SpMV)
-  double *pcg_alpha = nullptr, *pcg_gamma = nullptr;
+  double *pcg_alpha = nullptr, *pcg_gamma = nullptr;   // [-, -, 1/x of parity 0, 1] (+ alpha: [4 + par] = thr)
+  double2* sturm = nullptr;       // error-based PCG stop (k_pcg_iter): 64 shifted LDLᵀ pivots + counts
   int64_t pcg_cap = 0;
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
@@ -135,7 +136,7 @@ struct GnDev {
   bool step_fused = false;                // this step's k_step work was done by the PCG
   int n_prev = 0;                 // valid entries of the ring for the current step
   int warm_now = 0;               // this step starts from the projected x0
-  int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED, H_ALLDONE] written by the kernels
+  int32_t* host_flags = nullptr;  // pinned, mapped: [H_DONE, H_PCG_IT, H_STOPPED] written by the kernels
   int32_t* hflags = nullptr;      // its device address (system-scope stores: no copy kernel per poll)
   int32_t* setup_stat = nullptr;  // pinned, mapped: the setup's one host read [nnz, max row, max wave, abort, graph diff]
   int32_t* d_setup_stat = nullptr;
@@ -146,11 +147,6 @@ struct GnDev {
   // optional timing of the PCG iteration loop (hipEvents on the caller's stream)
   bool timing = false;
   int64_t n_iter_launches = 0;
-  // persistent PCG (k_pcg_persist): cluster -> workgroup partition, m double buffer, partial granules, abort word
-  int32_t* p_wg_cl = nullptr;
-  unsigned long long* p_mgr = nullptr;
-  unsigned long long* p_gran = nullptr;
-  int32_t* p_abort = nullptr;
 };
 static_assert(std::is_trivially_copyable<GnDev>::value, "kernel argument");
 
@@ -185,19 +181,7 @@ struct Gn : GnDev {
   // its last kernels (row assignment, contribution lists, ...) have run, and they write this handle's buffers
   bool side_dirty = false;
   hipEvent_t ev_side = nullptr;
-  // persistent PCG: enabled for this setup, workgroups, clusters per workgroup, A blocks of the largest workgroup
-  bool p_on = false, p_disabled = false;
-  int p_G = 0, p_C = 4, p_lds_blocks = 0, p_cus = 0;
-  uint32_t p_epoch = 0;
-  std::vector<int32_t> h_wg_cl;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
-  // two-stream GN loop (ofx_gn_solve): GN step i on ps[i & 1], so step i + 1 starts beside step i's drained PCG
-  // launches instead of behind them; the caller's stream is ordered after both at the next entry (fence_side)
-  bool pipe_active = false;          // ofx_gn_solve is running its two-stream loop (the PCG signals H_ALLDONE)
-  int pipe_env = 0;                  // OFX_GN_PIPE=1: two streams (2: one internal stream, 3: high priority; tuning)
-  hipStream_t ps[2] = {nullptr, nullptr};
-  hipEvent_t ps_ev[2] = {nullptr, nullptr}, ev_cs = nullptr, ev_fin = nullptr, ev_step = nullptr;
-  bool pipe_dirty = false;
   int32_t ep_next = 1;
 #ifdef OFX_STAMPS   // tuning build: stream idle between a PCG chunk's last launch and the next GN step's first kernel
   std::chrono::steady_clock::time_point t_seen{};   // host saw the step's convergence
@@ -214,13 +198,6 @@ struct Gn : GnDev {
 // prep_wait: the worker has finished enqueuing). Every entry point that touches the handle's buffers on a
 // caller stream does this first, whether or not the prefetched setup is used.
 static int fence_side(Gn* g, hipStream_t hs) {
-  if (g->pipe_dirty) {   // the two-stream GN loop's streams (the last step's drained launches)
-    for (int k = 0; k < 2; ++k) {
-      OFX_HIP(hipEventRecord(g->ps_ev[k], g->ps[k]));
-      OFX_HIP(hipStreamWaitEvent(hs, g->ps_ev[k], 0));
-    }
-    g->pipe_dirty = false;
-  }
   if (!g->side || !g->side_dirty) return OFX_OK;
   OFX_HIP(hipEventRecord(g->ev_side, g->side));
   OFX_HIP(hipStreamWaitEvent(hs, g->ev_side, 0));
@@ -229,10 +206,6 @@ static int fence_side(Gn* g, hipStream_t hs) {
 }
 // the same for host reads of device buffers (synchronous copies do not order after a non-blocking stream)
 static int sync_side(Gn* g) {
-  if (g->pipe_dirty) {
-    for (int k = 0; k < 2; ++k) OFX_HIP(hipStreamSynchronize(g->ps[k]));
-    g->pipe_dirty = false;
-  }
   if (!g->side || !g->side_dirty) return OFX_OK;
   OFX_HIP(hipStreamSynchronize(g->side));
   g->side_dirty = false;
@@ -242,14 +215,15 @@ static int sync_side(Gn* g) {
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
        F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
 enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
-// host-mapped flags: H_DONE / H_ALLDONE hold the epoch (GnDev::ep) of the last converged PCG solve — H_DONE from
-// the converging launch's lead lane, H_ALLDONE once every workgroup of that launch has finished its writes;
+// host-mapped flags: H_DONE holds the epoch (GnDev::ep) of the last converged PCG solve (from the converging launch's
+// lead lane);
 // H_STOPPED the epoch of the solve whose GN step stopped the loop (0: running). k_upload clears them per setup.
-enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_ALLDONE = 3, H_COUNT = 4 };
+enum { H_DONE = 0, H_PCG_IT = 1, H_STOPPED = 2, H_COUNT = 3 };
 __device__ __forceinline__ void host_flag(const int32_t* hf, int k, int v) {
   __hip_atomic_store(const_cast<int32_t*>(hf) + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 constexpr int kMaxLog = 64;   // per-GN-step statistics slots
+constexpr int32_t kEpochWrap = 1 << 30;   // GnDev::ep restarts at 1 from a setup once it reaches this (a solve adds <= 64)
 
 // ---------------------------------------------------------------------------- reductions
 template <int CTL>
@@ -392,7 +366,6 @@ __global__ __launch_bounds__(256) void k_upload(GnDev g, Upload u) {
   }
   if (i < F_COUNT) g.flags[i] = 0;
   if (i < H_COUNT) host_flag(g.hflags, (int)i, 0);
-  if (i == 0) *g.arrive = 0;   // the converging launch's workgroup count (reset by its last arrival; cleared per setup too)
   if (i < S_COUNT) g.scal[i] = 0.0;
   if (i < 3 * kMaxLog) g.stat[i] = 0.0;
   if (i < 2 * (kMaxLog + 1)) g.step_state[i] = 0.0;
@@ -552,11 +525,11 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
 // the setup's host-read scalars into host-mapped memory in one kernel (five small D2H copies through pageable
 // memory cost ~15-20 us each on the frame-boundary critical path)
 __global__ void k_setup_status(const int32_t* __restrict__ row_ptr, int N, const int32_t* __restrict__ row_cnt,
-                               const int32_t* __restrict__ p_abort, const int32_t* __restrict__ gdiff, int32_t* out) {
+                               const int32_t* __restrict__ gdiff, int32_t* out) {
   if (threadIdx.x != 0) return;
-  const int32_t v[5] = {row_ptr[N], row_cnt[N], row_cnt[N + 1], *p_abort, gdiff ? *gdiff : 0};
+  const int32_t v[4] = {row_ptr[N], row_cnt[N], row_cnt[N + 1], gdiff ? *gdiff : 0};
 #pragma unroll
-  for (int k = 0; k < 5; ++k) __hip_atomic_store(out + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int k = 0; k < 4; ++k) __hip_atomic_store(out + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_pair_count(GnDev g) {
@@ -1595,16 +1568,16 @@ struct PcgIt {
   const int2* wl;
   double *m0, *m1, *st, *part_p, *part_b, *pcg_alpha, *pcg_gamma, *scal;
   int32_t *flags, *hflags, *stopw;
+  double2* sturm;               // error-based stop: per lead lane s the LDLᵀ pivot of T_k - σ_s I and its negative count
   uint64_t* stamps;
   int32_t nwg_row, nw_pad;
-  struct { double pcg_tol; } prm;
+  struct { double pcg_tol, pcg_err_tol; } prm;
   // fused GN step (fuse = 0: k_step runs as its own launch)
   const StepArgs* sa;
   const double* tail;           // rhs + 6N: [loss² total, data, arap, motion, nonfinite]
   double stop_loss_diff;
   int32_t fuse, gn_iter, N, mode, n_iter_log, warm;
-  int32_t ep;                   // this solve's epoch (stop words, H_DONE / H_ALLDONE)
-  int32_t* arrive;              // two-stream GN loop: the workgroup count behind H_ALLDONE (nullptr: not counted)
+  int32_t ep;                   // this solve's epoch (stop words, H_DONE)
 };
 static PcgIt pcg_args(const Gn* g) {
   PcgIt a;
@@ -1612,10 +1585,11 @@ static PcgIt pcg_args(const Gn* g) {
   a.m0 = g->m0; a.m1 = g->m1; a.st = g->st; a.part_p = g->part_p; a.part_b = g->part_b;
   a.pcg_alpha = g->pcg_alpha; a.pcg_gamma = g->pcg_gamma; a.scal = g->scal;
   a.flags = g->flags; a.hflags = g->hflags; a.stopw = g->stopw; a.stamps = g->stamps;
-  a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol;
+  a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol; a.prm.pcg_err_tol = g->prm.pcg_err_tol;
+  a.sturm = g->sturm;
   a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff;
   a.fuse = 0; a.gn_iter = 0; a.N = g->N; a.mode = g->prm.mode; a.n_iter_log = 64; a.warm = g->prm.pcg_warm;
-  a.ep = g->ep; a.arrive = g->pipe_active ? g->arrive : nullptr;
+  a.ep = g->ep;
   return a;
 }
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
@@ -1708,7 +1682,7 @@ template <bool kWave, bool kFirst, int kU, bool kW2 = false, int kEarly = 0>   /
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
   constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   constexpr int kNH = kW2 ? 2 : 1;
-  __shared__ double s_v[kNH][kCD];
+  __shared__ __attribute__((aligned(16))) double s_v[kNH][kCD];
   __shared__ float4 s_m[kEarly ? 1 : kCD * kCD / 4];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   __shared__ double s_half[kW2 ? 64 : 1];
@@ -1782,6 +1756,8 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const int cnt = g.flags[F_PCG_CNT];
   const double rgam_prev = kFirst ? 1.0 : g.pcg_gamma[2 + (par ^ 1)];     // 1/γ, 1/α of the previous iteration
   const double ralpha_prev = kFirst ? 1.0 : g.pcg_alpha[2 + (par ^ 1)];
+  const double thr_prev = kFirst ? 0.0 : g.pcg_alpha[4 + (par ^ 1)];       // error-based stop: bound on γ (below)
+  const double2 sd = g.sturm[lane];   // (every wave loads it: no load behind a branch; the lead wave uses it)
   const double bb_stored = g.scal[S_BB];
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
@@ -1843,7 +1819,12 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     beta = gam * rgam_prev;
     alpha = gam / (del - beta * gam * ralpha_prev);
   }
-  const bool conv = rr <= tol * tol * bb || gam == 0.0;
+  // Stop: the relative residual ‖r‖ <= tol·‖b‖ AND (pcg_err_tol > 0) the error estimate √γ / θ̂ <= pcg_err_tol, or
+  // the relative residual at the f64 floor (1e-12). γ = rᵀM⁻¹r = ‖z‖²_M (z = M⁻¹r), so the error e = (M⁻¹A)⁻¹z has
+  // ‖e‖_M <= √γ / λ_min(M⁻¹A); θ̂ is the previous iteration's estimate of λ_min(M⁻¹A) from below, kept by the lead
+  // wave (sturm_step). The residual alone cannot see the error of an ill-conditioned system (real data: DESIGN §6).
+  const double etol = g.prm.pcg_err_tol;
+  const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam <= thr_prev)) || gam == 0.0 || rr <= 1e-24 * bb;
   int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
   if (kEarly >= 2) leave = __builtin_amdgcn_readfirstlane(leave);
   if (leave) {   // converged, or breakdown (A SPD => alpha > 0): keep x
@@ -1859,23 +1840,37 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
       host_flag(g.hflags, H_PCG_IT, cnt);
       __hip_atomic_store(g.hflags + H_DONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
     }
-    // two-stream GN loop only (g.arrive set): every workgroup's writes of this launch released (device scope: an L2
-    // write-back per workgroup), then counted: the last one tells the host, which may then start the next GN step on
-    // another stream beside this chunk's remaining (drained) launches. On the one-stream path the next step's kernels
-    // follow this launch on the same stream and the lead's H_DONE suffices.
-    if (!g.arrive) return;
-    __threadfence();
-    if (lane == 0 && atomicAdd(g.arrive, 1) == nw - 1) {
-      __threadfence();
-      __hip_atomic_store(g.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g.hflags + H_ALLDONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
     return;
   }
   // the lead's scalar stores (read by the next launch only): kEarly issues them last — on gfx9 vmcnt counts stores too,
   // so stores issued here made the lead wave's first wait on trip 2 a vmcnt(0) that also waited for their acks
+  // the Lanczos tridiagonal of the preconditioned operator grows by one row per iteration: T_kk = 1/α_k + β_{k-1}/α_{k-1},
+  // T_{k,k-1}² = β_{k-1}/α_{k-1}² (β_{k-1} = γ_k/γ_{k-1}); its smallest eigenvalue (Ritz value) θ_k decreases towards
+  // λ_min(M⁻¹A). Lane s of the lead wave keeps the LDLᵀ pivot d_k(σ_s) = T_kk - σ_s - T²_{k,k-1}/d_{k-1}(σ_s) of
+  // T_k - σ_s I for the shift σ_s = 2^(-s/2) and the count of negative pivots, which is the number of Ritz values
+  // below σ_s (Sylvester's inertia; the bisection count of LAPACK's dstebz): O(1) per iteration. θ̂ = the largest
+  // σ_s with no Ritz value below it (θ_k / √2 < θ̂ <= θ_k; 1 if θ_k >= 1; 0 below 2^-31.5), thr = (pcg_err_tol·θ̂)².
+  double2 sd_new = sd;
+  double thr_new = 0.0;
+  if (wv == 0 && hw == 0 && etol > 0.0) {   // (workgroup-uniform)
+    const double rca = 1.0 / alpha;
+    const double diag = kFirst ? rca : rca + beta * ralpha_prev;
+    const double e2 = kFirst ? 0.0 : beta * ralpha_prev * ralpha_prev;
+    const double sig = ldexp((lane & 1) ? 0.70710678118654752440 : 1.0, -(lane >> 1));
+    double d = (diag - sig) - (kFirst ? 0.0 : e2 / sd.x);
+    if (fabs(d) < 1e-300) d = -1e-300;        // an exact zero pivot counts as negative (dstebz's pivmin)
+    const double c = (kFirst ? 0.0 : sd.y) + (d < 0.0 ? 1.0 : 0.0);
+    sd_new = make_double2(d, c);
+    const uint64_t free_ = __ballot(c == 0.0);   // the shifts with no Ritz value below them: a suffix of the lanes
+    const double th = free_ ? ldexp(((__ffsll((unsigned long long)free_) - 1) & 1) ? 0.70710678118654752440 : 1.0,
+                                    -((__ffsll((unsigned long long)free_) - 1) >> 1))
+                            : 0.0;
+    thr_new = (etol * th) * (etol * th);
+  }
   auto lead_stores = [&]() {
     if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
+    if (lead) g.pcg_alpha[4 + par] = thr_new;
+    if (wv == 0 && hw == 0 && etol > 0.0) g.sturm[lane] = sd_new;
     if (kFirst && lead && kEarly >= 2) g.scal[S_BB] = bb;
   };
   if (kEarly < 2) lead_stores();
@@ -1909,10 +1904,19 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     const int len = b1 - b0;
     const double* sp = s_prod + (b0 - wb0) * 6 + qc;
     double a = 0.0;
+    if (kEarly >= 3) {   // every read in flight before the first add (one LDS round trip instead of five)
+      double tv[kRowMax];
 #pragma unroll
-    for (int k = 0; k < kRowMax; ++k) {
-      const double t = sp[6 * k];
-      a += k < len ? t : 0.0;
+      for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kRowMax; ++k) {
+        const double t = sp[6 * k];
+        a += k < len ? t : 0.0;
+      }
     }
     nc = a;
   } else {
@@ -1944,14 +1948,27 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     if (own) {
       const float4* mrow = s_m + (6 * r + q);
       double a[4] = {0.0, 0.0, 0.0, 0.0};
+      double2 vv[kCD / 4];   // kEarly >= 3: the half's 24 entries of w by 12 broadcast reads, all in flight at once
+      if (kEarly >= 3) {
+#pragma unroll
+        for (int kk = 0; kk < kCD / 8; ++kk) {
+          const int k = (kCD / 8) * hw + kk;
+          vv[2 * kk] = *reinterpret_cast<const double2*>(&s_v[hw][4 * k]);
+          vv[2 * kk + 1] = *reinterpret_cast<const double2*>(&s_v[hw][4 * k + 2]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int kk = 0; kk < kCD / 8; ++kk) {
         const int k = (kCD / 8) * hw + kk;
         const float4 t = kEarly ? mreg[kk % kMR] : mrow[k * kCD];
-        a[0] = fma((double)t.x, s_v[hw][4 * k], a[0]);
-        a[1] = fma((double)t.y, s_v[hw][4 * k + 1], a[1]);
-        a[2] = fma((double)t.z, s_v[hw][4 * k + 2], a[2]);
-        a[3] = fma((double)t.w, s_v[hw][4 * k + 3], a[3]);
+        const double v0 = kEarly >= 3 ? vv[2 * kk].x : s_v[hw][4 * k], v1 = kEarly >= 3 ? vv[2 * kk].y : s_v[hw][4 * k + 1];
+        const double v2 = kEarly >= 3 ? vv[2 * kk + 1].x : s_v[hw][4 * k + 2];
+        const double v3 = kEarly >= 3 ? vv[2 * kk + 1].y : s_v[hw][4 * k + 3];
+        a[0] = fma((double)t.x, v0, a[0]);
+        a[1] = fma((double)t.y, v1, a[1]);
+        a[2] = fma((double)t.z, v2, a[2]);
+        a[3] = fma((double)t.w, v3, a[3]);
       }
       hsum = (a[0] + a[1]) + (a[2] + a[3]);
     }
@@ -1979,332 +1996,6 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
   if (kEarly >= 2) lead_stores();
   OFX_STAMP(7)
-}
-
-// ---------------------------------------------------------------------------- persistent PCG
-// The same pipelined PCG as k_pcg_iter, as ONE launch per solve (GN step) instead of one per iteration. Why: a
-// launch re-reads the iteration's whole working set (A blocks, cluster inverses, state: ~11 MB at 2k nodes) from
-// beyond L2 and pays the kernel boundary; a bare launch that only reads 44 KB per workgroup already takes ~4.5 us
-// back to back on this part (tools/sync_micro.hip), the iteration kernel 5.1 us. Here every workgroup keeps its
-// clusters' A blocks in LDS, its rows' recurrence state and cluster-inverse rows in registers for the whole solve,
-// and only m (48 doubles per cluster) and the three dot-product partials (per workgroup) cross workgroups:
-//  * workgroup = up to kPersistMaxC waves (one cluster each; at most one wave per SIMD, so the kernel has the
-//    whole register file: a fifth, polling wave capped it at 256 VGPRs and spilled); G <= 128 workgroups (two
-//    producers per lane in the partial sweep), all co-resident (host: G <= CUs, one workgroup's LDS per CU);
-//  * SpMV as the iteration kernel's wave-list form: lane l multiplies the cluster's blocks l and l + 64 (balanced
-//    whatever the row lengths), the products meet in LDS and each row sums its blocks in CSR order; the cluster's
-//    A blocks sit in LDS element-major (element e of block s at e·nb + s), so every read is one contiguous,
-//    bank-conflict-free wave access;
-//  * hand-offs carry their own flag (MI355X_MICROARCH.md, visibility, R2 granules): every double travels as two
-//    8-byte granules {tag | 32-bit half}, each written by one sc1 store and read by sc1 loads until the tag matches.
-//    m_{it+1} (per row component) is published as soon as M⁻¹ has produced it, the workgroup's partials of
-//    iteration it + 1 (its clusters summed in order) right after;
-//  * iteration it: every wave gathers m_it of its blocks' columns (spinning on the granules of just those rows) and
-//    multiplies from LDS; wave 0 then sweeps every workgroup's partials (published with the m granules, so the
-//    global reduction overlaps the neighbour hop and the SpMV); one barrier hands the scalars to every wave;
-//  * m and the partials are double-buffered by iteration parity: a producer writes iteration it + 2 only after it
-//    has seen every workgroup's partials of it + 1, which each consumer publishes after it has read iteration it;
-//  * tags = (launch epoch << 12) | iteration: no per-launch memset, stale granules never match;
-//  * scalars: every workgroup sums the G partials in the same fixed order, so all of them take the same
-//    convergence / breakdown / cap decision at the same iteration and leave the loop together; the converging
-//    iteration takes the GN step (fused_step) for the workgroup's rows;
-//  * every spin is bounded: a timeout marks the solve ill-posed (valid_solve = 0), records the epoch in abort_word
-//    (the host then stays on the per-iteration launches) and the waits of the other workgroups time out in turn.
-// Deterministic: fixed-order sums everywhere (not bit-identical to k_pcg_iter, whose partial tree differs).
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-constexpr int kPersistMaxC = 4;         // compute waves (clusters) per workgroup, + 1 poll wave
-constexpr int kPersistRowMax = kRowMax; // longest block row (row sums over the products in LDS)
-constexpr int kPersistMaxG = 128;
-constexpr unsigned kPersistSpin = 1u << 20;   // polls before a wait gives up (~1 s)
-constexpr int kPersistLds = 126 * 1024;       // dynamic LDS budget per workgroup: A blocks + their columns
-
-struct PcgPersist {
-  PcgIt b;                  // the iteration kernel's arguments: operator, state, flags, fused GN step
-  const int32_t* wg_cl;     // per workgroup its first cluster (G + 1 entries)
-  unsigned long long* mgr;  // [2][6N][2] m granules of iteration it >= 1 at parity it & 1
-  unsigned long long* gran; // [2][G][8] partial granules
-  int32_t* abort_word;      // epoch of a launch that timed out
-  int32_t G, max_it, lds_blocks, C;
-  uint32_t epoch;
-};
-
-__device__ __forceinline__ uint32_t persist_tag(uint32_t epoch, int it) { return (epoch << 12) | (uint32_t)it; }
-__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long* p) {
-  return __hip_atomic_load((gu64*)const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_gran(unsigned long long* p, uint32_t tag, uint32_t v) {
-  __hip_atomic_store((gu64*)p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_gran_double(unsigned long long* p, uint32_t tag, double v) {
-  const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
-  st_gran(p, tag, (uint32_t)bits);
-  st_gran(p + 1, tag, (uint32_t)(bits >> 32));
-}
-__device__ __forceinline__ double gran_double(unsigned long long lo, unsigned long long hi) {
-  return __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
-}
-__device__ __forceinline__ bool gran_tag_is(unsigned long long lo, unsigned long long hi, uint32_t tag) {
-  return (uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag;
-}
-__device__ __forceinline__ bool persist_give_up(const PcgPersist& P, unsigned spins) {
-  return spins > kPersistSpin ||
-         ((spins & 255) == 255 &&
-          __hip_atomic_load(P.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int32_t)P.epoch);
-}
-
-#ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every workgroup for the first 64 iterations
-#define OFX_PSTAMP(cond, k)                                                                                     \
-  if ((cond) && lane == 0 && g.stamps && it < 64)                                                              \
-    g.stamps[((int64_t)it * g.nwg_row + wg) * 8 + (k)] = __builtin_amdgcn_s_memtime();
-#else
-#define OFX_PSTAMP(cond, k)
-#endif
-__global__ __launch_bounds__(64 * kPersistMaxC) void k_pcg_persist(PcgPersist P) {
-  extern __shared__ double s_A[];                 // the workgroup's A blocks (CSR order), then their columns
-  __shared__ double s_v[kPersistMaxC][kCD];
-  __shared__ double s_sc[4];                      // gamma, delta, r.r of the iteration; |b|^2
-  __shared__ double s_part[kPersistMaxC][3];
-  __shared__ double s_prod[kPersistMaxC][(kWL + kRowMax) * 6];   // block products, slot-major
-  __shared__ int s_cb[kPersistMaxC + 1];          // the clusters' first blocks (workgroup-relative)
-  __shared__ int s_abort;
-  const PcgIt& g = P.b;
-  const int wg = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  if (g.flags[F_STOPPED]) return;                 // the solve already stopped: this GN step is a no-op (uniform)
-  const int c0 = P.wg_cl[wg], c1 = P.wg_cl[wg + 1], ncl = c1 - c0;
-  const bool poller = w == 0;                     // compute wave 0 also sweeps the partials (after its SpMV)
-  const bool act = w < ncl;
-  const int cl = c0 + (act ? w : 0);
-  const int r = lane / kSL, q = lane % kSL, row = cl * kRW + r;
-  const bool own = q < 6;
-  const int qc = own ? q : 5;
-  const int64_t o = 6 * (int64_t)row + qc;
-  const int64_t n6 = 6 * (int64_t)g.N;
-  const int bw = g.row_ptr[c0 * kRW];
-  const int nblk = g.row_ptr[c1 * kRW] - bw;
-  int* s_col = reinterpret_cast<int*>(s_A + 36 * (size_t)P.lds_blocks);
-  if (tid <= ncl) s_cb[tid] = g.row_ptr[(c0 + tid) * kRW] - bw;
-  __syncthreads();
-  {   // stage the workgroup's A blocks (element-major per cluster) and columns (earlier launches wrote them)
-    const double* src = g.Aop + 36 * (int64_t)bw;
-    for (int i = tid; i < nblk * 36; i += blockDim.x) {
-      const int b = i / 36, e = i - 36 * b;
-      int j = 0;
-#pragma unroll
-      for (int k = 1; k < kPersistMaxC; ++k) j += (k < ncl && b >= s_cb[k]) ? 1 : 0;
-      const int nb = s_cb[j + 1] - s_cb[j];
-      s_A[36 * s_cb[j] + e * nb + (b - s_cb[j])] = src[i];
-    }
-    for (int i = tid; i < nblk; i += blockDim.x) s_col[i] = g.col[bw + i];
-  }
-  const int cb = s_cb[act ? w : 0], cnb = s_cb[act ? w + 1 : 1] - cb;   // this wave's cluster: first block, blocks
-  const int b0 = g.row_ptr[row] - bw - cb, b1 = g.row_ptr[row + 1] - bw - cb;   // the row's blocks, cluster-relative
-  double v[V_N];
-  load_rec(g.st, o, v);
-  double mown = g.m0[o];                          // the own row's m of the current iteration (k_pcg_w0 wrote m_0)
-  float4 mr[kCD / 4];                             // this lane's row of its cluster inverse, for the whole solve
-  {
-    const float4* p = reinterpret_cast<const float4*>(g.Mcl + mcl_idx(cl, 6 * r + qc, 0));
-#pragma unroll
-    for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k * kCD];
-  }
-  if (w == 0) {   // iteration 0's scalars and |b|^2 from k_pcg_w0's per-cluster partials, fixed order
-    const int nc = g.nwg_row, ns = g.nw_pad;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = lane; i < nc; i += 64) {
-      a[0] += g.part_p[i]; a[1] += g.part_p[ns + i]; a[2] += g.part_p[2 * ns + i]; a[3] += g.part_b[i];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = wave_sum(a[k]);
-    if (lane == 0) { s_sc[0] = a[0]; s_sc[1] = a[1]; s_sc[2] = a[2]; s_sc[3] = a[3]; s_abort = 0; }
-  }
-  __syncthreads();
-  const double bb = s_sc[3];
-  const double tol = g.prm.pcg_tol;
-  const bool lead = wg == 0 && tid == 0;
-  if (lead) g.scal[S_BB] = bb;
-  double rgam = 1.0, ralpha = 1.0;
-  for (int it = 0;; ++it) {
-    const uint32_t tag = persist_tag(P.epoch, it);
-    OFX_PSTAMP(w == 0, 0)
-    double nc = 0.0;
-    if (act) {   // ---- n = A m_it (own component): the cluster's blocks lane and lane + 64, products via LDS
-      double xm[2][6];
-      bool okb[2];
-      int64_t c6[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int sl = lane + 64 * k;
-        okb[k] = sl < cnb;
-        c6[k] = 6 * (int64_t)s_col[cb + (okb[k] ? sl : 0)];
-      }
-      if (it == 0) {   // m_0: written by k_pcg_w0 (an earlier launch)
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-          for (int j = 0; j < 6; ++j) xm[k][j] = g.m0[c6[k] + j];
-      } else {         // m_it: the producers' granules, spun on until all carry this iteration's tag
-        const unsigned long long* mg = P.mgr + (size_t)(it & 1) * n6 * 2;
-        for (unsigned spins = 0;; ++spins) {
-          bool ok = true;
-#pragma unroll
-          for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-              const unsigned long long lo = ld_gran(mg + 2 * (c6[k] + j)), hi = ld_gran(mg + 2 * (c6[k] + j) + 1);
-              ok &= !okb[k] || gran_tag_is(lo, hi, tag);
-              xm[k][j] = gran_double(lo, hi);
-            }
-          if (__all(ok)) break;
-          if (persist_give_up(P, spins)) {
-            if (lane == 0) s_abort = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      OFX_PSTAMP(w == 0, 1)
-      const double* sa = s_A + 36 * (size_t)cb;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int sl = lane + 64 * k;
-        const int slc = okb[k] ? sl : 0;
-        double a[36];
-#pragma unroll
-        for (int e = 0; e < 36; ++e) a[e] = sa[e * cnb + slc];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const double t = fma(a[6 * i + 5], xm[k][5], fma(a[6 * i + 4], xm[k][4], fma(a[6 * i + 3], xm[k][3],
-                           fma(a[6 * i + 2], xm[k][2], fma(a[6 * i + 1], xm[k][1], a[6 * i] * xm[k][0])))));
-          s_prod[w][sl * 6 + i] = okb[k] ? t : 0.0;
-        }
-      }
-      wave_lds_sync();
-      {   // row sums in CSR order (rows of at most kRowMax blocks; masked reads inside the padded array)
-        const int len = b1 - b0;
-        const double* sp = s_prod[w] + b0 * 6 + qc;
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < kRowMax; ++k) {
-          const double t = sp[6 * k];
-          acc += k < len ? t : 0.0;
-        }
-        nc = acc;
-      }
-      OFX_PSTAMP(w == 0, 2)
-    }
-    if (poller && it > 0) {   // ---- meanwhile: the partials of iteration it from every workgroup, fixed order
-      const unsigned long long* gs = P.gran + (size_t)(it & 1) * P.G * 8;
-      double a[3] = {0.0, 0.0, 0.0};
-      for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
-        double sx[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int p = lane + 64 * u;
-          const int pc = p < P.G ? p : 0;
-          unsigned long long x[6];
-#pragma unroll
-          for (int k = 0; k < 6; ++k) x[k] = ld_gran(gs + (size_t)pc * 8 + k);
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            ok &= p >= P.G || gran_tag_is(x[2 * k], x[2 * k + 1], tag);
-            sx[k] += p < P.G ? gran_double(x[2 * k], x[2 * k + 1]) : 0.0;
-          }
-        }
-        if (__all(ok)) { a[0] = sx[0]; a[1] = sx[1]; a[2] = sx[2]; break; }
-        if (persist_give_up(P, spins)) {
-          if (lane == 0) s_abort = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) a[k] = wave_sum(a[k]);
-      if (lane == 0) { s_sc[0] = a[0]; s_sc[1] = a[1]; s_sc[2] = a[2]; }
-      OFX_PSTAMP(true, 3)
-    }
-    __syncthreads();   // the scalars (and any timeout) reach every wave
-    OFX_PSTAMP(w == 0, 4)
-    if (s_abort) {     // a wait timed out: this solve is invalid (the host falls back for the next ones)
-      if (tid == 0) __hip_atomic_store(P.abort_word, (int32_t)P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lead) g.flags[F_ILL] = 1;
-      return;
-    }
-    const double gam = s_sc[0], del = s_sc[1], rr = s_sc[2];
-    // ---- scalars (identical in every workgroup) and the stop decision
-    double beta = 0.0, alpha;
-    if (it == 0) {
-      alpha = gam / del;
-    } else {
-      beta = gam * rgam;
-      alpha = gam / (del - beta * gam * ralpha);
-    }
-    const bool conv = rr <= tol * tol * bb || gam == 0.0;
-    const bool brk = !isfinite(alpha) || !(alpha > 0.0);
-    if (conv || brk || it >= P.max_it) {
-      const bool ill = !conv && brk && !isfinite(alpha);
-      const bool done = conv || brk;
-      if (act) {
-        if (own) g.st[V_N * o + V_X] = v[V_X];
-        if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, cl, lane, r, q, own, o, row, v[V_X], ill, it, bb);
-      }
-      if (lead && !g.flags[F_STOPPED] && (done || g.fuse)) {
-        g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = it; g.flags[F_PCG_TOTAL] += it;
-        if (ill) g.flags[F_ILL] = 1;
-        host_flag(g.hflags, H_PCG_IT, it);
-        __hip_atomic_store(g.hflags + H_DONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      if (lead) g.flags[F_PCG_CNT] = it;
-      break;
-    }
-    rgam = 1.0 / gam;
-    ralpha = 1.0 / alpha;
-    // ---- recurrences (own components), m_{it+1} = M⁻¹ w_new (cluster-local, LDS), published at once
-    const uint32_t tag1 = persist_tag(P.epoch, it + 1);
-    if (act) {
-      double d[3] = {0.0, 0.0, 0.0};
-      const double zz = fma(beta, v[V_Z], nc);
-      const double qq = fma(beta, v[V_Q], mown);
-      const double sv = fma(beta, v[V_S], v[V_W]);
-      const double p = fma(beta, v[V_P], v[V_U]);
-      const double rn = fma(-alpha, sv, v[V_R]);
-      const double un = fma(-alpha, qq, v[V_U]);
-      const double w2 = fma(-alpha, zz, v[V_W]);
-      v[V_X] = fma(alpha, p, v[V_X]); v[V_R] = rn; v[V_U] = un; v[V_Z] = zz; v[V_Q] = qq; v[V_S] = sv; v[V_P] = p;
-      v[V_W] = w2;
-      if (own) {
-        s_v[w][6 * r + q] = w2;
-        d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
-      }
-      wave_lds_sync();
-      if (own) {
-        double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < kCD / 4; ++k) {
-          a4[0] = fma((double)mr[k].x, s_v[w][4 * k], a4[0]);
-          a4[1] = fma((double)mr[k].y, s_v[w][4 * k + 1], a4[1]);
-          a4[2] = fma((double)mr[k].z, s_v[w][4 * k + 2], a4[2]);
-          a4[3] = fma((double)mr[k].w, s_v[w][4 * k + 3], a4[3]);
-        }
-        mown = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-        st_gran_double(P.mgr + ((size_t)((it + 1) & 1) * n6 + o) * 2, tag1, mown);
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
-      if (lane == 0) { s_part[w][0] = d[0]; s_part[w][1] = d[1]; s_part[w][2] = d[2]; }
-      OFX_PSTAMP(w == 0, 5)
-    }
-    __syncthreads();   // the clusters' partials -> compute wave 0 publishes the workgroup's before it gathers again
-    OFX_PSTAMP(w == 0, 6)
-    if (w == 0 && lane < 3) {
-      double sum = 0.0;
-      for (int c = 0; c < ncl; ++c) sum += s_part[c][lane];
-      st_gran_double(P.gran + ((size_t)((it + 1) & 1) * P.G + wg) * 8 + 2 * lane, tag1, sum);
-    }
-    // the partial stores leave before the other waves' next gather loads fill this CU's memory queue
-    __syncthreads();
-    OFX_PSTAMP(w == 0, 7)
-  }
 }
 
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
@@ -2433,10 +2124,10 @@ static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->stopw, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
-                  g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma,
+                  g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma, g->sturm,
                   g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
-                  g->p_wg_cl, g->p_mgr, g->p_gran, g->p_abort, g->up_of, g->up_slot, g->up_tr, g->arrive};
+                  g->up_of, g->up_slot, g->up_tr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -2540,7 +2231,8 @@ static void pcg_pick_e(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
 }
 template <int KU>
 static void pcg_pick(bool wave, bool w2, int early, PcgKernel& first, PcgKernel& rest) {
-  if (early == 2) pcg_pick_e<KU, 2>(wave, w2, first, rest);
+  if (early == 3) pcg_pick_e<KU, 3>(wave, w2, first, rest);
+  else if (early == 2) pcg_pick_e<KU, 2>(wave, w2, first, rest);
   else if (early == 1) pcg_pick_e<KU, 1>(wave, w2, first, rest);
   else pcg_pick_e<KU, 0>(wave, w2, first, rest);
 }
@@ -2590,7 +2282,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // early trip-2 issue alone, 2 (default): + gathered rows first, the lead's stores last and scalar exit branches; read
   // per solve: in-process A/B)
   const char* ee = getenv("OFX_PCG_EARLY");
-  const int early = (ee && ee[0] >= '0' && ee[0] <= '2') ? ee[0] - '0' : 2;
+  const int early = (ee && ee[0] >= '0' && ee[0] <= '3') ? ee[0] - '0' : 2;
   switch (g->pcg_ku) {
     case 3: pcg_pick<3>(wave, w2, early, iter0, iter); break;
     case 4: pcg_pick<4>(wave, w2, early, iter0, iter); break;
@@ -2611,26 +2303,6 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   pa.gn_iter = gn_iter;
   pa.tail = rhs + 6 * (int64_t)g->N;
   g->step_fused = false;
-  if (g->p_on) {   // the whole solve in one launch (k_pcg_persist); no host polling, nothing drains
-    PcgPersist pp;
-    pp.b = pa;
-    pp.wg_cl = g->p_wg_cl; pp.mgr = g->p_mgr; pp.gran = g->p_gran; pp.abort_word = g->p_abort;
-    pp.G = g->p_G; pp.max_it = max_it; pp.lds_blocks = g->p_lds_blocks; pp.C = g->p_C;
-    if (++g->p_epoch >= (1u << 20)) {   // tag space wrapped: clear the granules once
-      OFX_HIP(hipMemsetAsync(g->p_gran, 0, (size_t)2 * kPersistMaxG * 8 * sizeof(unsigned long long), hs));
-      OFX_HIP(hipMemsetAsync(g->p_mgr, 0, (size_t)2 * 6 * g->max_pad * 2 * sizeof(unsigned long long), hs));
-      g->p_epoch = 1;
-    }
-    pp.epoch = g->p_epoch;
-    const size_t lds = (size_t)g->p_lds_blocks * (36 * sizeof(double) + sizeof(int32_t));
-    hipLaunchKernelGGL(k_pcg_persist, dim3(g->p_G), dim3(64 * g->p_C), lds, hs, pp);
-    OFX_LAUNCH_CHECK();
-    if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
-    g->step_fused = pa.fuse != 0;
-    g->n_iter_launches += 1;
-    if (g->timing) g->ev.emplace_back(e0, e1);
-    return OFX_OK;
-  }
   int chunk = lp > 0 ? lp + 4 : 64;
   int it = 0;
   while (it < max_it) {
@@ -2650,13 +2322,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipEventRecord(g->poll_ev, hs));
     bool ran = false;
-    // converged: one stream — the converging launch's lead lane stored H_DONE (the next step's kernels follow it on
-    // the stream); two streams — every workgroup of that launch is done (H_ALLDONE), so the next step may start on
-    // the other stream. A stop decided by an earlier solve: this one's launches end at their stop words, nothing to
-    // wait for; a stop decided by this solve's converging launch: one stream — stop now; two streams — wait for
-    // H_ALLDONE, like a convergence
-    const int wf = g->pipe_active ? H_ALLDONE : H_DONE;
-    for (int spin = 0; hf[wf] < g->ep && !(hf[H_STOPPED] != 0 && (!g->pipe_active || hf[H_STOPPED] < g->ep)); ++spin) {
+    // converged: the converging launch's lead lane stored H_DONE (the next step's kernels follow it on the stream);
+    // stopped (by an earlier solve: this one's launches end at their stop words; by this solve's converging launch):
+    // nothing to wait for
+    for (int spin = 0; hf[H_DONE] < g->ep && !hf[H_STOPPED]; ++spin) {
       if ((spin & 63) == 63) {
         const hipError_t q = hipEventQuery(g->poll_ev);
         if (q == hipSuccess) { ran = true; break; }
@@ -2664,7 +2333,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       }
     }
     if (hf[H_STOPPED]) break;
-    if (hf[wf] >= g->ep) {
+    if (hf[H_DONE] >= g->ep) {
 #ifdef OFX_STAMPS
       g->t_seen = std::chrono::steady_clock::now();
 #endif
@@ -2755,7 +2424,7 @@ static bool same_params(const ofx_gn_params& a, const ofx_gn_params& b) {
          a.pcg_max_iter == b.pcg_max_iter && a.pcg_warm == b.pcg_warm && a.lambda_flow == b.lambda_flow &&
          a.lambda_depth == b.lambda_depth && a.lambda_arap == b.lambda_arap && a.lambda_motion == b.lambda_motion &&
          a.lm_factor == b.lm_factor && a.stop_loss_diff == b.stop_loss_diff && a.pcg_tol == b.pcg_tol &&
-         a.mode == b.mode && a.precond_every == b.precond_every;
+         a.mode == b.mode && a.precond_every == b.precond_every && a.pcg_err_tol == b.pcg_err_tol;
 }
 
 }  // namespace ofx
@@ -2771,12 +2440,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     return OFX_ERR_RANGE;
   }
   Gn* g = new Gn();
-  {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster; OFX_GN_PIPE=0 keeps the
-      // GN loop on the caller's stream
+  {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster
     const char* e = getenv("OFX_PCG_W1");
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
-    const char* pp = getenv("OFX_GN_PIPE");
-    g->pipe_env = pp ? atoi(pp) : 0;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
@@ -2799,36 +2465,13 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   const int64_t max_ns = 128 * 17;   // nw_pad bound: 2·64·17 >= max_pad / kCS waves
   static_assert(2 * 64 * 17 * kCS >= 2 * kMaxNodes + kCS, "partial stream width");
   ALLOC(g->part_p, (6 * max_ns > kProjP * max_row_wg ? 6 * max_ns : kProjP * max_row_wg)); ALLOC(g->part_b, max_ns);
+  ALLOC(g->sturm, 64);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
-  ALLOC(g->p_wg_cl, N / kCS + 2); ALLOC(g->p_mgr, 2 * 6 * N * 2); ALLOC(g->p_gran, 2 * kPersistMaxG * 8); ALLOC(g->p_abort, 1);
-  ALLOC(g->arrive, 1);
 #undef ALLOC
   if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess ||   // pattern entries are cleared per setup
-      hipMemset(g->arrive, 0, sizeof(int32_t)) != hipSuccess ||
-      hipMemset(g->stopw, 0, (size_t)(N / kCS) * 64 * sizeof(int32_t)) != hipSuccess ||   // epoch 0: none converged
-      hipMemset(g->p_gran, 0, (size_t)2 * kPersistMaxG * 8 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(g->p_mgr, 0, (size_t)2 * 6 * N * 2 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(g->p_abort, 0, sizeof(int32_t)) != hipSuccess) {
+      hipMemset(g->stopw, 0, (size_t)(N / kCS) * 64 * sizeof(int32_t)) != hipSuccess) {   // epoch 0: none converged
     free_all(g); delete g; set_error("hipMemset failed"); return OFX_ERR_HIP;
-  }
-  {   // persistent PCG: CU count (all workgroups must be resident), dynamic LDS beyond the default 64 KB;
-      // OFX_PCG_PERSIST=1 selects it (default: the per-iteration launches), OFX_PCG_PERSIST_C=<1..4> sets the
-      // clusters per workgroup
-    int dev = 0;
-    const char* e = getenv("OFX_PCG_PERSIST");
-    g->p_disabled = !(e && strcmp(e, "1") == 0);
-    if (const char* c = getenv("OFX_PCG_PERSIST_C")) {
-      const int v = atoi(c);
-      if (v >= 1 && v <= kPersistMaxC) g->p_C = v;
-    }
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&g->p_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_pcg_persist, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kPersistLds) != hipSuccess) {
-      g->p_disabled = true;
-      (void)hipGetLastError();
-    }
   }
   if (hipHostMalloc((void**)&g->host_flags, H_COUNT * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&g->hflags, g->host_flags, 0) != hipSuccess ||
@@ -2885,20 +2528,17 @@ int ofx_gn_stopped(void* handle, int32_t* stopped) {
   return OFX_OK;
 }
 
+int ofx_gn_step_fused(void* handle, int32_t* fused) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g && fused, "null handle/fused");
+  *fused = g->step_fused ? 1 : 0;
+  return OFX_OK;
+}
+
 int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && waves, "null handle/waves");
   *waves = (g->pcg_w2 && g->pcg_ku == 3) ? 2 : 1;   // the last setup's form (two only up to 384 clusters)
-  return OFX_OK;
-}
-
-int ofx_gn_pcg_form(void* handle, int32_t* form) {
-  Gn* g = (Gn*)handle;
-  if (g) prep_wait(g);   // a prefetch thread of this handle has finished
-  OFX_CHECK_ARG(g && form, "null handle/form");
-  form[0] = g->p_on ? 1 : 0;
-  form[1] = g->p_on ? g->p_G : 0;
-  form[2] = g->p_C;
   return OFX_OK;
 }
 
@@ -2991,12 +2631,6 @@ int ofx_gn_destroy(void* handle) {
     g->worker.join();
   }
   (void)hipDeviceSynchronize();
-  for (int k = 0; k < 2; ++k) {
-    if (g->ps[k]) (void)hipStreamDestroy(g->ps[k]);
-    if (g->ps_ev[k]) (void)hipEventDestroy(g->ps_ev[k]);
-  }
-  for (hipEvent_t e : {g->ev_cs, g->ev_fin, g->ev_step})
-    if (e) (void)hipEventDestroy(e);
   if (g->side) (void)hipStreamDestroy(g->side);
   if (g->ev_in) (void)hipEventDestroy(g->ev_in);
   if (g->ev_prep) (void)hipEventDestroy(g->ev_prep);
@@ -3035,12 +2669,8 @@ static int prepare_impl(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* pr
     OFX_HIP(hipEventCreateWithFlags(&g->ev_side, hipEventDisableTiming));
   }
   OFX_HIP(hipGetDevice(&g->prep_dev));
-  // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve, its
-  // two-stream GN loop's tails) comes before the prefetched setup
-  if (g->pipe_dirty) {
-    const int fs = fence_side(g, as_stream(s));
-    if (fs) return fs;
-  }
+  // everything enqueued on the caller's stream so far (the problem's producers, this handle's last solve) comes
+  // before the prefetched setup
   OFX_HIP(hipEventRecord(g->ev_in, as_stream(s)));
   g->prep_pb = *pb;
   g->prep_pb.prev_rot = nullptr;    // the pose is loaded by the solve (k_pose)
@@ -3210,10 +2840,10 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->N = N; g->N_real = N0; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
   g->T = (int64_t)M + (int64_t)N * NB + N;
-  if (4 > g->pcg_cap) {   // [alpha, gamma] of both parities + their reciprocals
+  if (6 > g->pcg_cap) {   // [-, -, 1/alpha | 1/gamma of both parities, thr of both parities (alpha only)]
     if (g->pcg_alpha) OFX_HIP(hipFree(g->pcg_alpha));
     if (g->pcg_gamma) OFX_HIP(hipFree(g->pcg_gamma));
-    g->pcg_cap = 4;
+    g->pcg_cap = 6;
     OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
     OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
   }
@@ -3259,6 +2889,11 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
       n = v > n ? v : n;
     u.n = n;
   }
+  if (g->ep_next >= kEpochWrap) {   // PCG epochs restart before int32 overflow: stop words cleared on this stream (after
+                                     // every earlier launch of the handle); k_upload clears the host flags
+    OFX_HIP(hipMemsetAsync(g->stopw, 0, (size_t)(g->max_pad / kCS) * 64 * sizeof(int32_t), hs));
+    g->ep_next = 1;
+  }
   hipLaunchKernelGGL(k_upload, dim3(grid_for(u.n, 256, 1 << 30)), dim3(256), 0, hs, *g, u);
   OFX_LAUNCH_CHECK();
   // terms -> block pattern
@@ -3269,22 +2904,13 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N);
   hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
-  std::vector<int32_t> hrp;   // row pointers: the persistent PCG's cluster -> workgroup partition (if it may run)
   hipLaunchKernelGGL(k_setup_status, dim3(1), dim3(64), 0, hs, (const int32_t*)g->row_ptr, N,
-                     (const int32_t*)g->row_cnt, (const int32_t*)g->p_abort,
+                     (const int32_t*)g->row_cnt,
                      (const int32_t*)(optimistic ? g->d_gdiff : nullptr), g->d_setup_stat);
   OFX_LAUNCH_CHECK();
-  if (!g->p_disabled) {
-    hrp.resize(N + 1);
-    OFX_HIP(hipMemcpyAsync(hrp.data(), g->row_ptr, (N + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, hs));
-  }
   OFX_HIP(hipStreamSynchronize(hs));
   const volatile int32_t* ss = g->setup_stat;
-  const int32_t nnz = ss[0], lens[2] = {ss[1], ss[2]}, aborted = ss[3], gdiff = ss[4];
-  if (aborted) {   // a persistent solve timed out earlier (it marked itself ill-posed): per-iteration launches from now on
-    g->p_disabled = true;
-    OFX_HIP(hipMemsetAsync(g->p_abort, 0, sizeof(int32_t), hs));
-  }
+  const int32_t nnz = ss[0], lens[2] = {ss[1], ss[2]}, gdiff = ss[3];
   if (gdiff) {   // the graph changed: clear the slot map marked with the stale order and start over
     OFX_HIP(hipMemsetAsync(g->map, 0, (size_t)g->max_pad * g->max_pad * sizeof(int32_t), hs));
     g->pat_N = 0;
@@ -3294,38 +2920,6 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   }
   g->max_deg = lens[0];
   g->max_wave = lens[1];
-  g->p_on = false;
-  if (!hrp.empty()) {   // persistent PCG: consecutive clusters (one wave each) packed into workgroups of <= p_C
-                        // clusters whose A blocks fit the LDS budget; enabled when every row fits three lane passes
-                        // and all workgroups can be resident
-    const int nc = N / kCS;
-    const int budget = kPersistLds / (int)(36 * sizeof(double) + sizeof(int32_t));
-    g->h_wg_cl.assign(1, 0);
-    int cur = 0, n_in = 0, maxb = 0;
-    bool fits = true;
-    for (int c = 0; c < nc; ++c) {
-      const int bc = hrp[(c + 1) * kCS] - hrp[c * kCS];
-      fits = fits && bc <= budget;
-      if (n_in == g->p_C || (n_in > 0 && cur + bc > budget)) {
-        g->h_wg_cl.push_back(c);
-        maxb = cur > maxb ? cur : maxb;
-        cur = 0;
-        n_in = 0;
-      }
-      cur += bc;
-      ++n_in;
-    }
-    g->h_wg_cl.push_back(nc);
-    maxb = cur > maxb ? cur : maxb;
-    g->p_G = (int)g->h_wg_cl.size() - 1;
-    g->p_lds_blocks = maxb;
-    const int cap = g->p_cus < kPersistMaxG ? g->p_cus : kPersistMaxG;
-    g->p_on = !g->p_disabled && fits && nc > 0 && g->max_deg <= kPersistRowMax && g->max_wave <= kWL && g->p_G <= cap &&
-              prm->pcg_max_iter < 4096;
-    if (g->p_on)
-      OFX_HIP(hipMemcpyAsync(g->p_wg_cl, g->h_wg_cl.data(), g->h_wg_cl.size() * sizeof(int32_t),
-                             hipMemcpyHostToDevice, hs));
-  }
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
     for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->blk_off,
                     (void**)&g->blk_cnt, (void**)&g->up_of, (void**)&g->up_slot, (void**)&g->up_tr})
@@ -3509,76 +3103,17 @@ int ofx_gn_solve(void* handle, const ofx_gn_problem* pb, const ofx_gn_params* pr
     g->entry_ev.emplace_back(ev_entry, e);
   }
 #endif
-  if (const char* pp = getenv("OFX_GN_PIPE")) g->pipe_env = atoi(pp);   // (read per solve: in-process A/B)
-  const bool pipe = g->pipe_env && !g->p_on && g->n_comp == 0 && prm->num_iter > 0;
-  if (!pipe) {
-    for (int it = 0; it < prm->num_iter; ++it) {
-      st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, s);
-      if (st) return st;
-      pf_fire(g, it);   // (after this step's first kernels are queued)
-      st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
-      if (st) return st;
-      // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
-      // decision: a stop costs at most one extra (no-op) linearisation instead of a sync per step
-      if (((const volatile int32_t*)g->host_flags)[H_STOPPED]) break;
-    }
-    return ofx_gn_finish(handle, res, s);
-  }
-  // Two streams: GN step i runs on ps[i & 1]. The host returns from a step's PCG once every workgroup of its
-  // converging launch has finished (H_ALLDONE), so the next step, enqueued on the other stream, starts right
-  // away instead of behind this chunk's remaining launches, which end after their stop-word load (epoch-tagged
-  // stop words: a new solve's writes never re-arm an old solve's launches). The last solve runs k_finish on the
-  // other stream too; the caller's stream waits for that, and for the leftovers at its next use of the handle.
-  hipStream_t cs = as_stream(s);
-  if (!g->ps[0]) {
-    int lo = 0, hi = 0;
-    OFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    for (int k = 0; k < 2; ++k) {
-      if (g->pipe_env == 3)   // tuning: high-priority streams
-        OFX_HIP(hipStreamCreateWithPriority(&g->ps[k], hipStreamNonBlocking, hi));
-      else
-        OFX_HIP(hipStreamCreateWithFlags(&g->ps[k], hipStreamNonBlocking));
-      OFX_HIP(hipEventCreateWithFlags(&g->ps_ev[k], hipEventDisableTiming));
-    }
-    OFX_HIP(hipEventCreateWithFlags(&g->ev_cs, hipEventDisableTiming));
-    OFX_HIP(hipEventCreateWithFlags(&g->ev_fin, hipEventDisableTiming));
-    OFX_HIP(hipEventCreateWithFlags(&g->ev_step, hipEventDisableTiming));
-  }
-  OFX_HIP(hipEventRecord(g->ev_cs, cs));   // the setup / pose above, the caller's inputs
-  for (int k = 0; k < 2; ++k) OFX_HIP(hipStreamWaitEvent(g->ps[k], g->ev_cs, 0));
-  struct PipeActive {   // the PCG launches of this loop count their workgroups out (H_ALLDONE); off on every return
-    Gn* g;
-    ~PipeActive() { g->pipe_active = false; }
-  } pipe_guard{g};
-  g->pipe_active = true;
-  int last = 0;
-  const int np = g->pipe_env == 2 ? 1 : 2;   // tuning: 2 = one internal stream for every step
   for (int it = 0; it < prm->num_iter; ++it) {
-    hipStream_t x = g->ps[it % np];
-    last = it;
-    st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, (ofx_stream_t)x);
+    st = ofx_gn_linearize(handle, it, 0, g->M, 1, g->A_own, g->rhs_own, s);
     if (st) return st;
-    pf_fire(g, it);
-    st = gn_pcg(g, it, g->A_own, g->rhs_own, x);
+    pf_fire(g, it);   // (after this step's first kernels are queued)
+    st = ofx_gn_step(handle, it, g->A_own, g->rhs_own, s);
     if (st) return st;
-    if (!g->step_fused) {   // not converged within pcg_max_iter (or stopped): k_step here, the next stream waits
-      double* xsave = g->prm.pcg_warm ? g->xh + (int64_t)(it % kProj) * 6 * g->N : nullptr;
-      hipLaunchKernelGGL(k_step, dim3(grid_for(g->N, 256)), dim3(256), 0, x, *g, (const double*)g->rhs_own, 64,
-                         g->prm.pcg_max_iter, it, xsave);
-      OFX_LAUNCH_CHECK();
-      OFX_HIP(hipEventRecord(g->ev_step, x));
-      OFX_HIP(hipStreamWaitEvent(g->ps[(it + 1) % np], g->ev_step, 0));
-    }
+    // host_flags was refreshed by this step's PCG poll, i.e. after the previous step's stop
+    // decision: a stop costs at most one extra (no-op) linearisation instead of a sync per step
     if (((const volatile int32_t*)g->host_flags)[H_STOPPED]) break;
   }
-  hipStream_t f = g->ps[(last + 1) % np];   // beside the last solve's drained launches (after k_step's event if any)
-  hipLaunchKernelGGL(k_finish, dim3(grid_for(g->N > 4 * prm->num_iter ? g->N : 4 * prm->num_iter, 256)), dim3(256), 0,
-                     f, *g, res->rot, res->trans, res->status, res->loss_log, (int)prm->num_iter);
-  OFX_LAUNCH_CHECK();
-  OFX_HIP(hipEventRecord(g->ev_fin, f));
-  OFX_HIP(hipStreamWaitEvent(cs, g->ev_fin, 0));
-  g->pipe_dirty = true;   // (set only now: the loop's own entry fences must not wait for the other stream)
-  return OFX_OK;
+  return ofx_gn_finish(handle, res, s);
 }
 
 }  // extern "C"

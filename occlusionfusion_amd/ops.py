@@ -204,11 +204,11 @@ def _gn_problem(nodes, edges, edge_weights, tpos, conf, src, anchors, weights, t
 
 
 def _gn_params(fparams, iparams):
-    """fparams = [lambda_flow, lambda_depth, lambda_arap, lambda_motion, lm_factor, stop_loss_diff, pcg_tol];
-    iparams = [num_iter, use_edge_weighting, pcg_max_iter, pcg_warm, mode, precond_every]."""
+    """fparams = [lambda_flow, lambda_depth, lambda_arap, lambda_motion, lm_factor, stop_loss_diff, pcg_tol,
+    pcg_err_tol]; iparams = [num_iter, use_edge_weighting, pcg_max_iter, pcg_warm, mode, precond_every]."""
     p = _lib.GnParams()
     (p.lambda_flow, p.lambda_depth, p.lambda_arap, p.lambda_motion, p.lm_factor, p.stop_loss_diff,
-     p.pcg_tol) = (float(v) for v in fparams)
+     p.pcg_tol, p.pcg_err_tol) = (float(v) for v in fparams)
     p.num_iter, p.use_edge_weighting, p.pcg_max_iter, p.pcg_warm, p.mode, p.precond_every = (int(v) for v in iparams)
     return p
 

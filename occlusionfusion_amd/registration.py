@@ -24,8 +24,8 @@ from ._lib import call, byref
 from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
-                   lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=1000, pcg_tol=1e-6,
-                   pcg_warm=True, precond_every=10)
+                   lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=2000, pcg_tol=1e-6,
+                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5)
 MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
 
 
@@ -118,12 +118,12 @@ class GaussNewtonSolver:
         call("ofx_gn_pcg_waves", self._h, byref(w))
         return w.value
 
-    def pcg_form(self):
-        """(persistent, workgroups, clusters per workgroup) of the last setup's PCG: persistent = one k_pcg_persist
-        launch per GN step, else one k_pcg_iter launch per iteration (include/ofx.h ofx_gn_pcg_form)."""
-        f = (ctypes.c_int32 * 3)()
-        call("ofx_gn_pcg_form", self._h, f)
-        return bool(f[0]), int(f[1]), int(f[2])
+    def step_fused(self):
+        """True if the last GN step's update was taken by its converging PCG launch (include/ofx.h
+        ofx_gn_step_fused): its stop flag is then already visible to the host."""
+        f = ctypes.c_int32()
+        call("ofx_gn_step_fused", self._h, byref(f))
+        return bool(f.value)
 
     def row_order(self):
         """PCG row -> node of the last setup (-1: padding row); the order of rhs / the state rows."""
@@ -143,7 +143,8 @@ class GaussNewtonSolver:
         """GN parameters as the ofx::gn_* operators take them (ops._gn_params)."""
         q = self.params
         fp = [float(q["lambda_flow"]), float(q["lambda_depth"]), float(q["lambda_arap"]), float(q["lambda_motion"]),
-              float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"] if pcg_tol is None else pcg_tol)]
+              float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"] if pcg_tol is None else pcg_tol),
+              float(q.get("pcg_err_tol", 0.0))]
         ip = [int(q["num_iter"]), int(bool(q["use_edge_weighting"])), int(q["pcg_max_iter"]), int(bool(q["pcg_warm"])),
               int(mode), int(q.get("precond_every", 1))]
         return fp, ip
@@ -320,11 +321,13 @@ class GaussNewtonSolver:
                 e1.record()
                 timer.append((e0, e1))
             torch.ops.ofx.gn_step(self._state, h, it, A, rhs)
-            # The stop decision of step `it` is identical on every rank (identical all-reduced systems), but the host
-            # flag that carries it is written asynchronously when the step is not fused into the converging PCG
-            # launch (k_step after pcg_max_iter launches): read it only after the step has run, so that every rank
-            # leaves the loop after the same step and the collectives stay matched.
-            torch.cuda.current_stream(self.device).synchronize()
+            # The stop decision of step `it` is identical on every rank (identical all-reduced systems). A step fused
+            # into its converging PCG launch stored the stop flag before the convergence flag the host already saw;
+            # otherwise (k_step as its own launch, after pcg_max_iter launches) the flag is written asynchronously:
+            # read it only after the step has run, so that every rank leaves the loop after the same step and the
+            # collectives stay matched.
+            if not self.step_fused():
+                torch.cuda.current_stream(self.device).synchronize()
             if self.stopped():
                 break
         out = torch.ops.ofx.gn_finish(self._state, h, N, int(self.params["num_iter"]))

@@ -22,12 +22,15 @@
                         chained from the first, ~2k nodes of the SURVEY §8(d) depth-mesh graph built by the
                         reference's C++, 10k matches) by the f64 oracle with a sparse JᵀJ + dense LU.
   gn_4k.npz           — the same at config 4's graph (~4k nodes, frame 10).
+  gn_c5r1.npz,        — BASELINE config 5 (one independent 512³ scene per GPU): the scenes of ranks 1 and 7
+  gn_c5r7.npz           (synthetic.config_scene(5, r): their own sphere, occluder and motion phase), frame 10, the
+                        same solve at their own ~2k-node depth-mesh graphs.
   frontend_csrc.npz   — backproject_depth_float / _ushort and compute_mesh_from_depth outputs of the
                         REFERENCE's compiled C++ (csrc/cpu/image_proc.cpp:351-545) on a synthetic frame,
                         incl. max-distance thresholds that tie exactly with triangle edge lengths; plus the
                         oracle's depth_2_pc target cloud (geometry.py:44-59) of the same frame.
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [which ...]  (e.g. gn5)
 """
 import os
 import sys
@@ -360,17 +363,18 @@ def _frame_problem(seq, t, n_matches=10000):
     return dict(src=src[v], tgt=tgt[v], tpos=tpos, conf=conf, anchors=a[v], weights=w[v])
 
 
-def make_gn_chain(name, config, frames, n_matches=10000):
+def make_gn_chain(name, config, frames, n_matches=10000, rank=0):
     """gn_2k.npz / gn_4k.npz — DeformNet.optimize (model.py:222-859) at the headline sizes by the f64 oracle
     (gn_optimize_sparse: the dense restatement's rows with a sparse JᵀJ, then the reference's dense LU), on
     BASELINE config `config`'s occluded non-rigid frames with its SURVEY §8(d) depth-mesh graph (the reference's
     compiled C++). frames = (t0, t1, ...): t0 starts from the identity, every later frame from the previous
-    frame's oracle result (the frame loop's prev_rot / prev_trans)."""
+    frame's oracle result (the frame loop's prev_rot / prev_trans). Config 5: `rank`'s independent scene
+    (synthetic.config_scene)."""
     import time
-    seq = config_sequence_cpu(config)
+    seq = config_sequence_cpu(config, rank)
     intr = seq.cam.as_vec()
     out = dict(nodes=seq.nodes, edges=seq.edges, edge_weights=seq.edge_weights, node_coverage=seq.node_coverage,
-               intr=intr, config=config, frames=np.array(frames, np.int32), seed=seq.seed)
+               intr=intr, config=config, frames=np.array(frames, np.int32), seed=seq.seed, rank=rank)
     R = T = None
     for q, t in enumerate(frames):
         pb = _frame_problem(seq, t, n_matches)
@@ -474,6 +478,9 @@ if __name__ == "__main__":
         make_gn_chain("gn_2k", 3, (10, 11))
     if "gn4k" in which:
         make_gn_chain("gn_4k", 4, (10,))
+    if "gn5" in which:   # BASELINE config 5: rank 1's and rank 7's independent scenes (one GPU each)
+        make_gn_chain("gn_c5r1", 5, (10,), rank=1)
+        make_gn_chain("gn_c5r7", 5, (10,), rank=7)
     if "gn1k" in which:
         make_gn_1k()
     if "skin" in which:

@@ -104,3 +104,56 @@ def test_c_oracle_matches_numpy_oracle(golden_dir):
     np.testing.assert_array_equal(t, g["tsdf1"])
     np.testing.assert_array_equal(w, g["weight1"])
     np.testing.assert_array_equal(c, g["color1"])
+
+
+def test_error_stop_shift_counts_bracket_the_smallest_ritz_value():
+    """The error-based PCG stop (gn.hip k_pcg_iter, sturm_step) keeps, per lead lane s, the LDLᵀ pivot of T_k - σ_s I
+    (σ_s = 2^(-s/2)) of the CG Lanczos tridiagonal T_k (T_kk = 1/α_k + β_{k-1}/α_{k-1}, T²_{k,k-1} = β_{k-1}/α²_{k-1})
+    and counts the negative pivots = Ritz values below σ_s (Sylvester). Restated here with the kernel's O(1)-per-
+    iteration recurrence on a real CG run: θ̂ = the largest shift with count 0 brackets the smallest Ritz value,
+    θ/√2 < θ̂ <= θ, at every iteration."""
+    from scipy.linalg import eigvalsh_tridiagonal
+    rng = np.random.default_rng(0)
+    n = 300
+    Q = np.linalg.qr(rng.normal(size=(n, n)))[0]
+    lam = np.concatenate([np.geomspace(3e-4, 0.05, 40), rng.uniform(0.05, 2.0, n - 40)])
+    A = (Q * lam) @ Q.T
+    b = rng.normal(size=n)
+    sig = np.array([2.0 ** (-s / 2) for s in range(64)])
+    d = np.zeros(64)
+    cnt = np.zeros(64)
+    x, r = np.zeros(n), b.copy()
+    p, gam = r.copy(), r @ r
+    alphas, betas = [], []
+    for k in range(120):
+        q = A @ p
+        alpha = gam / (p @ q)
+        if k == 0:
+            diag, e2 = 1.0 / alpha, 0.0
+        else:
+            diag = 1.0 / alpha + betas[-1] / alphas[-1]
+            e2 = betas[-1] / alphas[-1] ** 2
+        dn = (diag - sig) - (e2 / d if k else 0.0)
+        dn = np.where(np.abs(dn) < 1e-300, -1e-300, dn)
+        cnt = cnt + (dn < 0)
+        d = dn
+        alphas.append(alpha)
+        x += alpha * p
+        r -= alpha * q
+        g2 = r @ r
+        betas.append(g2 / gam)
+        p = r + betas[-1] * p
+        gam = g2
+        # exact smallest Ritz value of T_k
+        m = len(alphas)
+        dd = [1.0 / alphas[0]] + [1.0 / alphas[j] + betas[j - 1] / alphas[j - 1] for j in range(1, m)]
+        ee = [np.sqrt(betas[j]) / alphas[j] for j in range(m - 1)]
+        theta = eigvalsh_tridiagonal(np.array(dd), np.array(ee), select="i", select_range=(0, 0))[0]
+        free = np.nonzero(cnt == 0)[0]
+        th_hat = sig[free[0]] if len(free) else 0.0
+        assert np.all(cnt[:-1] >= cnt[1:])                       # counts fall with the shift: a suffix is free
+        if theta < 1.0:
+            assert theta / np.sqrt(2) < th_hat <= theta * (1 + 1e-9), (k, theta, th_hat)
+        else:
+            assert th_hat == 1.0
+    assert th_hat < 1e-3                                         # the run found the small end of the spectrum

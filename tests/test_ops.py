@@ -27,7 +27,7 @@ def test_fake_kernels():
         st = torch.zeros(1, dtype=torch.int32)
         args = [nodes, torch.empty(37, 8, dtype=torch.int32), torch.empty(37, 8), nodes, torch.empty(37),
                 pts, a, w, pts, None, None, None, None, [525.0, 525.0, 319.5, 223.5]]
-        fp, ip = [0.0, 1.0, 0.5, 1.0, 1e-7, 1.0, 1e-6], [10, 0, 1000, 1, 0, 10]
+        fp, ip = [0.0, 1.0, 0.5, 1.0, 1e-7, 1.0, 1e-6, 1e-5], [10, 0, 1000, 1, 0, 10]
         R, T, status, loss = torch.ops.ofx.gn_solve(st, 0, *args, fp, ip)
         assert (R.shape, T.shape, status.dtype, loss.shape, loss.dtype) == \
             ((37, 3, 3), (37, 3), torch.int32, (10, 4), torch.float64)

@@ -47,6 +47,7 @@
 #include <type_traits>
 #include <utility>
 #include <cstdlib>
+#include <cstdio>
 #include <vector>
 
 #include "ofx_common.h"
@@ -157,7 +158,11 @@ struct Gn : GnDev {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // timing events of the PCG loops
   // converged PCG iteration count of the previous solve, per GN step (sizes the first chunk of launches);
   // shared by the solver slots of one frame loop (ofx_gn_share_history)
-  std::shared_ptr<std::array<int, 64>> last_pcg = std::make_shared<std::array<int, 64>>();
+  struct PcgHist {                  // per GN step the converged counts of the last 4 solves (ring), newest at n % 4
+    int c[64][4] = {};
+    int n[64] = {};
+  };
+  std::shared_ptr<PcgHist> last_pcg = std::make_shared<PcgHist>();
   // prefetched setup (ofx_gn_prepare): the next problem's setup runs on a host thread, on the handle's own
   // stream, while the caller's stream still works on the current problem (of another handle)
   std::thread worker;               // persistent (created by the first prefetch): no per-frame thread start
@@ -442,6 +447,7 @@ __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restr
 // Per PCG wave (kCS consecutive rows = one contiguous CSR range) the (col, slot) of its first kWL
 // blocks, so the iteration reads its gather addresses without the row_ptr -> col chain
 constexpr int kWL = 128;
+constexpr int kRowMax = 20;   // longest block row of the wave-list SpMV forms (k_pcg_iter, k_pcg_w0)
 __global__ __launch_bounds__(256) void k_wave_max(int nwave, const int32_t* __restrict__ row_ptr, int32_t* __restrict__ out) {
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w < nwave) atomicMax(out, row_ptr[(w + 1) * kCS] - row_ptr[w * kCS]);
@@ -1061,6 +1067,15 @@ __device__ __forceinline__ void load_streams2(const double* __restrict__ p, int 
       t[k][u] = i < nw ? *reinterpret_cast<const double2*>(p + (int64_t)k * stride + i) : make_double2(0.0, 0.0);
     }
 }
+// the same, unconditionally: streams padded to a stride of 128·U entries with zero tails
+template <int K, int U>
+__device__ __forceinline__ void load_streams2_padded(const double* __restrict__ p, int stride, double2 t[K][U]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[k][u] = *reinterpret_cast<const double2*>(p + (int64_t)k * stride + 2 * (lane + 64 * u));
+}
 template <int K, int U>
 __device__ __forceinline__ void reduce_streams2(const double* __restrict__ p, int nw, int stride, double2 t[K][U],
                                                 double out[K]) {
@@ -1187,12 +1202,20 @@ __device__ __forceinline__ void load_mrow(const GnDev& g, int64_t o, float4 mr[k
   for (int k = 0; k < kCD / 4; ++k) mr[k] = p[k * kCD];
 }
 // (M⁻¹ v)_(r,c) with v the wave's cluster vector staged in LDS (s_v[6 r' + c'], f64)
+// (s_v 16-B aligned: the 48 entries come as 24 broadcast reads in two batches of 12 in flight, not 12 dependent rounds)
 __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const double* s_v) {
+  double2 vv[kCD / 2];
+  const double2* sv2 = reinterpret_cast<const double2*>(s_v);
+#pragma unroll
+  for (int k = 0; k < kCD / 4; ++k) vv[k] = sv2[k];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = kCD / 4; k < kCD / 2; ++k) vv[k] = sv2[k];
   double a = 0.0;
 #pragma unroll
   for (int k = 0; k < kCD / 4; ++k)
-    a += (((double)mr[k].x * s_v[4 * k] + (double)mr[k].y * s_v[4 * k + 1]) +
-          ((double)mr[k].z * s_v[4 * k + 2] + (double)mr[k].w * s_v[4 * k + 3]));
+    a += (((double)mr[k].x * vv[2 * k].x + (double)mr[k].y * vv[2 * k].y) +
+          ((double)mr[k].z * vv[2 * k + 1].x + (double)mr[k].w * vv[2 * k + 1].y));
   return a;
 }
 
@@ -1308,7 +1331,101 @@ __device__ __forceinline__ void proj_accumulate(const double bk[36], const doubl
   }
 }
 
-__global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restrict__ rhs) {
+// kWave: the SpMVs in k_pcg_iter's wave-list form (as k_pcg_w0): the wave's (col, slot) list, row bounds, the own
+// rows' b and history values leave in the first trip with the stop flag; the second trip is every block of the wave
+// (lane l: blocks l and l + 64) with the kProj history rows it multiplies; the products meet in LDS and each row sums
+// its blocks in CSR order. (The row form's first trip is row_ptr, then col, then blocks + gathers.)
+template <bool kWave>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs) {
+  if constexpr (kWave) {
+    __shared__ double s_prod[kProj][(kWL + kRowMax) * 6];
+    const int lane = threadIdx.x;
+    const int wv = blockIdx.x;
+    const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
+    const int qc = q < 6 ? q : 5;
+    const int64_t oc = 6 * (int64_t)row + qc;
+    const int64_t stride = 6 * (int64_t)g.N;
+    int2 bl[2];
+    bl[0] = g.wl[(int64_t)wv * kWL + lane];
+    bl[1] = g.wl[(int64_t)wv * kWL + 64 + lane];
+    const int wb0 = g.row_ptr[wv * kRW];
+    const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];
+    const double b = rhs[oc];
+    double xo[kProj];
+#pragma unroll
+    for (int j = 0; j < kProj; ++j) xo[j] = g.xh[j * stride + oc];
+    const int stopped = g.flags[F_STOPPED];
+    asm volatile("" ::: "memory");   // the loads above leave with the stop flag (one trip)
+    if (stopped) return;
+    const int np = g.n_prev;
+    double2 ab[2][18], xb[2][kProj][3];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {   // unconditional (padding entries read block 0 / row 0, masked below)
+      const int64_t cc = 6 * (int64_t)(bl[jj].x >= 0 ? bl[jj].x : 0);
+#pragma unroll
+      for (int h = 0; h < kProj; ++h)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xb[jj][h][k] = reinterpret_cast<const double2*>(g.xh + h * stride + cc)[k];
+      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)bl[jj].y);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) ab[jj][k] = blk[k];
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const bool ok = bl[jj].x >= 0;
+#pragma unroll
+      for (int h = 0; h < kProj; ++h) {
+        double x[6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { x[2 * k] = xb[jj][h][k].x; x[2 * k + 1] = xb[jj][h][k].y; }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double2 b01 = ab[jj][3 * i], b23 = ab[jj][3 * i + 1], b45 = ab[jj][3 * i + 2];
+          const double t = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+          s_prod[h][(jj * 64 + lane) * 6 + i] = (ok && h < np) ? t : 0.0;
+        }
+      }
+    }
+    wave_lds_sync();
+    const int len = rb1 - rb0;
+    double t[kProj];
+#pragma unroll
+    for (int h = 0; h < kProj; ++h) {   // per history vector: its kRowMax reads in flight, then the adds in CSR order
+      const double* sp = s_prod[h] + (rb0 - wb0) * 6 + qc;
+      double tv[kRowMax];
+#pragma unroll
+      for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+      __builtin_amdgcn_sched_barrier(0);
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
+      t[h] = a;
+    }
+    double v[kProjP];
+#pragma unroll
+    for (int k = 0; k < kProjP; ++k) v[k] = 0.0;
+    if (q < 6) {
+      double x[kProj];
+#pragma unroll
+      for (int j = 0; j < kProj; ++j) {
+        x[j] = j < np ? xo[j] : 0.0;
+        if (j < np) g.th[j * stride + oc] = t[j];
+      }
+#pragma unroll
+      for (int j = 0; j < kProj; ++j) {
+#pragma unroll
+        for (int i = 0; i <= j; ++i) v[tri(i, j)] = x[i] * t[j];
+        v[kProj * (kProj + 1) / 2 + j] = x[j] * b;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kProjP; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nw_pad + blockIdx.x] = v[k];
+    if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
+    return;
+  }
   const int lane = threadIdx.x;
   const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];   // issued with the stop flag: one trip
@@ -1388,7 +1505,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
   for (int k = 0; k < kProjP; ++k) v[k] = wave_sum(v[k]);
   if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nwg_row + blockIdx.x] = v[k];
+    for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nw_pad + blockIdx.x] = v[k];
   // PCG bookkeeping of this GN step (also in k_pcg_prep), stored last: on gfx9 vmcnt counts stores too, so stores
   // ahead of the loads made workgroup 0's first wait a vmcnt(0) that also waited for their acks
   if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
@@ -1398,8 +1515,11 @@ __global__ __launch_bounds__(64) void k_pcg_proj(GnDev g, const double* __restri
 // identical bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get
 // c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0 (cluster, via LDS),
 // z = q = s = p = w = 0, u0 -> m1.
-__global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restrict__ rhs) {
-  __shared__ double s_v[kCD];
+// The projection partials are read as KU pairs per lane and stream at the iteration streams' padded stride nw_pad =
+// 128·KU (zero beyond the wave count: cleared at setup): unconditional loads, no per-load branches.
+template <int KU>
+__global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) {   // (not __restrict__: see k_pcg_w0)
+  __shared__ __attribute__((aligned(16))) double s_v[kCD];
   const int lane = threadIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const int np = g.n_prev;
@@ -1413,8 +1533,8 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restr
   double xo[kProj], to[kProj];
 #pragma unroll
   for (int j = 0; j < kProj; ++j) { xo[j] = g.xh[j * stride + oc]; to[j] = g.th[j * stride + oc]; }
-  double pt[kProjP][8];
-  load_streams<kProjP, 8>(g.part_p, g.nwg_row, pt);
+  double2 pt[kProjP][KU];
+  load_streams2_padded<kProjP, KU>(g.part_p, g.nw_pad, pt);
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");   // keep the loads above the exit test (one trip with the flag)
   if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
@@ -1422,7 +1542,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restr
     return;
   }
   double p[kProjP];
-  reduce_streams<kProjP, 8>(g.part_p, g.nwg_row, pt, p);
+  reduce_streams2<kProjP, KU>(g.part_p, g.nw_pad, g.nw_pad, pt, p);
   // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
   double L[kProj][kProj], y[kProj], c[kProj];
   bool use[kProj];
@@ -1489,20 +1609,31 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* __restr
 
 // w0 = A u0 (u0 gathered from m1), m0 = M⁻¹ w0 (cluster, via LDS); per-wave partials
 // (γ0 = r·u, δ0 = w·u, r·r) -> parity 0, b·b -> part_b.
-__global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict__ rhs) {
-  __shared__ double s_v[kCD];
+// kWave: the SpMV in k_pcg_iter's wave-list form — the wave's (col, slot) list leaves in the first trip with the state
+// and the stop flag, so the blocks and gathers are the second (the row form needs row_ptr -> col -> blocks: three);
+// lane l multiplies the wave's blocks l and l + 64, the products meet in LDS, each row sums its blocks in CSR order.
+template <bool kWave>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_w0(GnDev g, const double* rhs) {   // (rhs not __restrict__: a restrict load sinks past the exit test)
+  __shared__ __attribute__((aligned(16))) double s_v[kCD];
+  __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   const int lane = threadIdx.x;
+  const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const bool own = q < 6;
+  const int qc = own ? q : 5;
   const int64_t o = 6 * (int64_t)row + q;
-  const int64_t oc = 6 * (int64_t)row + (own ? q : 5);   // every lane loads (clamped)
-  // row bounds, own state, M⁻¹ row and b issued with the stop flag: one trip
+  const int64_t oc = 6 * (int64_t)row + qc;   // every lane loads (clamped)
+  // (wave list,) row bounds, own state, M⁻¹ row and b issued with the stop flag: one trip
+  int2 bl[2] = {make_int2(-1, 0), make_int2(-1, 0)};
+  if (kWave) { bl[0] = g.wl[(int64_t)wv * kWL + lane]; bl[1] = g.wl[(int64_t)wv * kWL + 64 + lane]; }
+  const int wb0 = g.row_ptr[wv * kRW];
   const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];
+  const double bo = rhs[oc];
   float4 mr[kCD / 4];
   double v[V_N];
   load_mrow(g, oc, mr);
   load_rec(g.st, oc, v);
-  const double bo = rhs[oc];
+  const double w_old = v[V_W];   // unused, but kept live to the end (see the end of the kernel)
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");
   if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
@@ -1510,9 +1641,46 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
     return;
   }
   const double b = own ? bo : 0.0;
-  double n[6];
-  row_spmv_2(g, rb0, rb1, q, g.m1, n);
-  const double w = pick6(n, q);
+  double w;
+  if (kWave) {
+    double2 ab[2][18], xb[2][3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked below)
+      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)bl[j].y);
+      const double2* vc = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)(bl[j].x >= 0 ? bl[j].x : 0));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
+#pragma unroll
+      for (int k = 0; k < 18; ++k) ab[j][k] = blk[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = bl[j].x >= 0;
+      double x[6];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { x[2 * k] = xb[j][k].x; x[2 * k + 1] = xb[j][k].y; }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double2 b01 = ab[j][3 * i], b23 = ab[j][3 * i + 1], b45 = ab[j][3 * i + 2];
+        const double t = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+        s_prod[(j * 64 + lane) * 6 + i] = ok ? t : 0.0;
+      }
+    }
+    wave_lds_sync();
+    const int len = rb1 - rb0;
+    const double* sp = s_prod + (rb0 - wb0) * 6 + qc;
+    double tv[kRowMax];
+#pragma unroll
+    for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
+    w = a;
+  } else {
+    double n[6];
+    row_spmv_2(g, rb0, rb1, q, g.m1, n);
+    w = pick6(n, q);
+  }
   if (own) s_v[6 * r + q] = w;
   __syncthreads();
   double d[4] = {0.0, 0.0, 0.0, 0.0};   // (the stop words hold an older epoch: this solve's launches run)
@@ -1536,6 +1704,9 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
       for (int k = 0; k < 6; ++k) g.part_p[k * ns + i] = 0.0;
       g.part_b[i] = 0.0;
     }
+  // the loaded (dead) w register stays allocated to here: otherwise the compiler reuses it for a temporary of the
+  // SpMV's issue and waits for its load first (a vmcnt that held trip 2 behind nearly all of trip 1)
+  asm volatile("" ::"v"(w_old));
 }
 
 // One PCG iteration; par = parity of the iteration (iteration i has par = i & 1), kFirst only for
@@ -1552,7 +1723,6 @@ __global__ __launch_bounds__(64) void k_pcg_w0(GnDev g, const double* __restrict
 // stop word: a converged (or broken-down) launch copies its wave's partials (rr = 0 on breakdown)
 // into the next parity and sets the stop words, so later launches of the chunk end after trip 1.
 // kWave = false: plain CSR rows (waves of more than kWL blocks or rows longer than kRowMax).
-constexpr int kRowMax = 20;
 // The iteration kernel's arguments: only what it reads (a ~200-B kernarg instead of the whole Gn:
 // the host enqueues ~1000 of these per frame, so per-launch host work is on the critical path).
 // What the converging PCG launch needs to also take the GN step (k_step's work, fused): fixed pointers in
@@ -2250,12 +2420,21 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // proj2 applies the stored M⁻¹) only damp A's diagonal
   const int every = g->prm.precond_every > 1 ? g->prm.precond_every : 1;
   const int invert = (!g->warm_now || gn_iter % every == 0) ? 1 : 0;
+  // wave-list SpMV forms (k_pcg_proj, k_pcg_w0, k_pcg_iter) when every wave's blocks fit the list and every row kRowMax
+  const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
   if (invert) hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
   if (g->warm_now) {
-    hipLaunchKernelGGL(k_pcg_proj, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
-    hipLaunchKernelGGL(k_pcg_proj2, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    switch (g->pcg_ku) {
+      case 3: hipLaunchKernelGGL(k_pcg_proj2<3>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      case 4: hipLaunchKernelGGL(k_pcg_proj2<4>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      case 8: hipLaunchKernelGGL(k_pcg_proj2<8>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      default: hipLaunchKernelGGL(k_pcg_proj2<17>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+    }
   }
-  hipLaunchKernelGGL(k_pcg_w0, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+  if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+  else hipLaunchKernelGGL(k_pcg_w0<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
   OFX_LAUNCH_CHECK();
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g->timing) {
@@ -2268,14 +2447,25 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // covers the previous frame's count for this GN step plus a small margin. (A hipGraph replay of
   // parity-pair chunks was measured: no gain over plain launches for this kernel.)
   const int max_it = g->prm.pcg_max_iter;
-  const int lp = (*g->last_pcg)[gn_iter & 63];
+  Gn::PcgHist& ph = *g->last_pcg;
+  const int hk = gn_iter & 63;
+  const int lp = ph.n[hk] > 0 ? ph.c[hk][(ph.n[hk] - 1) & 3] : 0;   // the previous solve's count for this GN step
+  // Chunk rule (OFX_PCG_CHUNK="mode,window,topup,lookahead", read per solve for in-process A/B): mode 0 — the first
+  // chunk covers the previous solve's count + 4, a chunk that runs out is followed by 8 more, the poll event sits at
+  // each chunk's end; mode 1 — the first chunk is the smallest count of the last `window` solves (an under-estimate),
+  // top-ups of `topup`, and the poll event sits `lookahead` launches before each chunk's end, so the host enqueues the
+  // next chunk while the GPU still has launches queued.
+  int c_mode = 0, c_win = 3, c_top = 4, c_look = 3;
+  if (const char* ce = getenv("OFX_PCG_CHUNK")) sscanf(ce, "%d,%d,%d,%d", &c_mode, &c_win, &c_top, &c_look);
+  c_win = c_win < 1 ? 1 : (c_win > 4 ? 4 : c_win);
+  c_top = c_top < 1 ? 1 : c_top;
+  c_look = c_look < 0 ? 0 : c_look;
   const dim3 grid(g->nwg_row), block(64);
   // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width kU for the cluster count (pcg_ku_for);
   // two waves per cluster only up to 384 clusters (kU = 3): config 4's 490 clusters ran 5.38 us per launch
   // with one wave and kU = 4, 5.58 with two; kU = 8: 5.66 vs 5.91; kU = 17: 6.35 vs 6.93 (A/B, 1278.9
   // iterations per frame; one wave per cluster and kU = 17 was the round-1 form for > 384 clusters: 95 vs 111
   // frames/s)
-  const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku == 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
   // early stop test / trip-2 issue (kEarly; OFX_PCG_EARLY=0: the all-of-trip-1 wait with the inverse by LDS-DMA, 1: the
@@ -2304,23 +2494,31 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   pa.tail = rhs + 6 * (int64_t)g->N;
   g->step_fused = false;
   int chunk = lp > 0 ? lp + 4 : 64;
+  if (c_mode == 1 && ph.n[hk] > 0) {
+    int mn = 1 << 30;
+    for (int q = 0; q < c_win && q < ph.n[hk]; ++q) mn = std::min(mn, ph.c[hk][(ph.n[hk] - 1 - q) & 3]);
+    chunk = mn + 1 > 1 ? mn + 1 : 1;   // launch i tests the state after i iterations: count + 1 launches
+  }
   int it = 0;
   while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
+    const int mark = (c_mode == 1 && n > c_look) ? n - c_look : n;   // the poll event after this chunk's launch `mark`
 #ifdef OFX_STAMPS
     const auto h0 = std::chrono::steady_clock::now();
     if (it == 0 && gn_iter > 0 && g->t_seen.time_since_epoch().count())
       g->prologue_us += std::chrono::duration<double, std::micro>(h0 - g->t_seen).count();
 #endif
-    for (int k = 0; k < n; ++k, ++it)
+    for (int k = 0; k < n; ++k, ++it) {
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, pa, it & 1);
+      if (k + 1 == mark && mark < n) OFX_HIP(hipEventRecord(g->poll_ev, hs));
+    }
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
     g->host_enqueued += n;
 #endif
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
-    OFX_HIP(hipEventRecord(g->poll_ev, hs));
+    if (mark == n) OFX_HIP(hipEventRecord(g->poll_ev, hs));
     bool ran = false;
     // converged: the converging launch's lead lane stored H_DONE (the next step's kernels follow it on the stream);
     // stopped (by an earlier solve: this one's launches end at their stop words; by this solve's converging launch):
@@ -2337,12 +2535,13 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
 #ifdef OFX_STAMPS
       g->t_seen = std::chrono::steady_clock::now();
 #endif
-      (*g->last_pcg)[gn_iter & 63] = hf[H_PCG_IT];
+      ph.c[hk][ph.n[hk] & 3] = hf[H_PCG_IT];
+      ++ph.n[hk];
       g->step_fused = pa.fuse != 0;
       break;
     }
-    (void)ran;   // the chunk ran out without convergence: next chunk
-    chunk = 8;
+    (void)ran;   // the chunk ran out (mode 1: reached its poll mark) without convergence: next chunk
+    chunk = c_mode == 1 ? c_top : 8;
   }
   g->n_iter_launches += it;
   if (g->timing) g->ev.emplace_back(e0, e1);
@@ -2464,7 +2663,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   const int64_t max_ns = 128 * 17;   // nw_pad bound: 2·64·17 >= max_pad / kCS waves
   static_assert(2 * 64 * 17 * kCS >= 2 * kMaxNodes + kCS, "partial stream width");
-  ALLOC(g->part_p, (6 * max_ns > kProjP * max_row_wg ? 6 * max_ns : kProjP * max_row_wg)); ALLOC(g->part_b, max_ns);
+  static_assert(kProjP >= 6, "part_p: kProjP projection streams / 6 iteration streams, stride nw_pad");
+  (void)max_row_wg;
+  ALLOC(g->part_p, kProjP * max_ns); ALLOC(g->part_b, max_ns);
   ALLOC(g->sturm, 64);
   ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
@@ -2850,6 +3051,9 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->nwg_row = N / kRW;
   g->pcg_ku = pcg_ku_for(g->nwg_row);
   g->nw_pad = 128 * g->pcg_ku;
+  // every partial stream is read unconditionally up to nw_pad: the tails must be zero (the kernels write only the
+  // entries of their own waves; k_pcg_w0 re-zeroes the iteration streams' tails, nothing writes the others')
+  OFX_HIP(hipMemsetAsync(g->part_p, 0, (size_t)kProjP * g->nw_pad * sizeof(double), hs));
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T

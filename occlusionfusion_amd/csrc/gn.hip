@@ -800,6 +800,7 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
 
 // b = -Jᵀr: one wave per node, entry-parallel (below). WG 0 also reduces the loss partials into the
 // rhs tail.
+template <int NPW>   // nodes per wave (processed one after the other)
 __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, double* __restrict__ rhs, int wg) {
   if (wg == 0 && threadIdx.x < 64) {   // the loss partials of k_terms, 4 streams in one pass, fixed order
     double a[4] = {0.0, 0.0, 0.0, 0.0};
@@ -815,9 +816,11 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
       tail[0] = a[0]; tail[1] = a[1]; tail[2] = a[2]; tail[3] = a[3];
     }
   }
-  const int n = wg * (kBlk / 64) + (threadIdx.x >> 6);
-  if (n >= g.N) return;
   const int lane = threadIdx.x & 63;
+#pragma unroll 1
+  for (int nn = 0; nn < NPW; ++nn) {
+  const int n = (wg * (kBlk / 64) + (threadIdx.x >> 6)) * NPW + nn;
+  if (n >= g.N) return;
   // one wave per node, one list entry per lane (two per lane per pass: a busy node's ~90 terms in one
   // pass of two dependent trips — code, then J + r — where 10 slots took ~10 serial passes); every load
   // unconditional (clamped index, masked value) so no branch splits a trip; fixed-order wave sums
@@ -853,6 +856,7 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
   if (lane == 0)
 #pragma unroll
     for (int c = 0; c < 6; ++c) rhs[6 * (int64_t)n + c] = -v[c];
+  }
 }
 
 // JᵀJ blocks, workgroup-cooperative: the workgroup's 16 blocks own one contiguous range of the sorted
@@ -866,27 +870,28 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
 #endif
 constexpr int kCoop = OFX_KCOOP;
 static_assert(kCoop <= kBlk, "one entry per thread per chunk");
+template <int BPW>   // upper blocks per workgroup
 __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, double* __restrict__ A, int64_t wg,
                                             double lm) {
   __shared__ double s_prod[36 * (kCoop + 1)];
-  __shared__ int s_off[17];
+  __shared__ int s_off[BPW + 1];
   const int tid = threadIdx.x;
-  const int64_t sb = wg * (kBlk / 16);   // upper blocks u in [sb, sb + 16); past the upper count up_slot is -1 and
-                                         // the lists are empty (blk_off there = the total)
-  constexpr int kPairs = (kBlk / 16) * 36;
+  const int64_t sb = wg * BPW;   // upper blocks u in [sb, sb + BPW); past the upper count up_slot is -1 and
+                                 // the lists are empty (blk_off there = the total)
+  constexpr int kPairs = BPW * 36;
   constexpr int kU = (kPairs + kBlk - 1) / kBlk;
   // first trip: the 17 list offsets and every pair's output slots (consumed at the end, in flight all along)
-  if (tid <= kBlk / 16) s_off[tid] = g.blk_off[min<int64_t>(sb + tid, g.nnzb)];
+  if (tid <= BPW) s_off[tid] = g.blk_off[min<int64_t>(sb + tid, g.nnzb)];
   int pb[kU], po[kU], os[kU], ot[kU];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int p = tid + kBlk * u;
-    pb[u] = p < kPairs ? p / 36 : kBlk / 16 - 1; po[u] = p % 36;
+    pb[u] = p < kPairs ? p / 36 : BPW - 1; po[u] = p % 36;
     os[u] = g.up_slot[sb + pb[u]];
     ot[u] = g.up_tr[sb + pb[u]];
   }
   __syncthreads();
-  const int E0 = s_off[0], E1 = s_off[kBlk / 16];
+  const int E0 = s_off[0], E1 = s_off[BPW];
   if (E0 == E1) return;   // no upper block here (uniform over the workgroup)
   double acc[kU];
   int lo[kU], hi[kU];
@@ -964,18 +969,19 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
+template <int BPW, int NPW>
 __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(4))) void k_assemble(GnDev g, DataCoef dc, double* __restrict__ A, double* __restrict__ rhs,
                                                   int nwb, double lm) {
   const int nrw = (int)gridDim.x - nwb;
-  if ((int)blockIdx.x < nrw) rhs_body(g, dc, rhs, blockIdx.x);
-  else blocks_coop(g, dc, A, blockIdx.x - nrw, lm);
+  if ((int)blockIdx.x < nrw) rhs_body<NPW>(g, dc, rhs, blockIdx.x);
+  else blocks_coop<BPW>(g, dc, A, blockIdx.x - nrw, lm);
 }
 #ifdef OFX_SPLIT_ASSEMBLE
 __global__ __launch_bounds__(kBlk) void k_assemble_blocks(GnDev g, DataCoef dc, double* __restrict__ A, double lm) {
-  blocks_coop(g, dc, A, blockIdx.x, lm);
+  blocks_coop<16>(g, dc, A, blockIdx.x, lm);
 }
 __global__ __launch_bounds__(kBlk) void k_assemble_rhs(GnDev g, DataCoef dc, double* __restrict__ rhs) {
-  rhs_body(g, dc, rhs, blockIdx.x);
+  rhs_body<1>(g, dc, rhs, blockIdx.x);
 }
 #endif
 
@@ -3214,12 +3220,22 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   const double lm = add_reg ? lm_for_iter(g->prm.lm_factor, gn_iter) : 0.0;
   // upper blocks: (nnzb + diagonal blocks) / 2 <= (nnzb + rows) / 2 (the pattern is symmetric); workgroups past
   // the device-side count return at once
-  const int nwb = g->nnzb > 0 ? (int)grid_for((g->nnzb + g->N) / 2 + 1, kBlk / 16, 1 << 30) : 0;
+  // workgroup shape (OFX_ASM="blocks per workgroup,nodes per rhs wave", read per call for in-process A/B): all of
+  // the launch's workgroups reserve the blocks' LDS (4 per CU), so the count decides whether it runs in one round
+  int bpw = 16, npw = 1;
+  if (const char* e = getenv("OFX_ASM")) sscanf(e, "%d,%d", &bpw, &npw);
+  if (bpw != 32) bpw = 16;
+  if (npw != 2) npw = 1;
+  const int nwb = g->nnzb > 0 ? (int)grid_for((g->nnzb + g->N) / 2 + 1, bpw, 1 << 30) : 0;
+  const int nwr = (int)grid_for(g->N, (kBlk / 64) * npw);
+  using AsmKernel = void (*)(GnDev, DataCoef, double*, double*, int, double);
+  const AsmKernel kasm = bpw == 32 ? (npw == 2 ? k_assemble<32, 2> : k_assemble<32, 1>)
+                                   : (npw == 2 ? k_assemble<16, 2> : k_assemble<16, 1>);
 #ifdef OFX_SPLIT_ASSEMBLE   // tuning build: the two halves as separate kernels (rocprof times each)
   if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, dc, A, lm);
   hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, rhs);
 #else
-  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, A, rhs, nwb, lm);
+  hipLaunchKernelGGL(kasm, dim3(nwb + nwr), dim3(kBlk), 0, hs, *g, dc, A, rhs, nwb, lm);
 #endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;

@@ -800,7 +800,6 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
 
 // b = -Jᵀr: one wave per node, entry-parallel (below). WG 0 also reduces the loss partials into the
 // rhs tail.
-template <int NPW>   // nodes per wave (processed one after the other)
 __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, double* __restrict__ rhs, int wg) {
   if (wg == 0 && threadIdx.x < 64) {   // the loss partials of k_terms, 4 streams in one pass, fixed order
     double a[4] = {0.0, 0.0, 0.0, 0.0};
@@ -816,11 +815,9 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
       tail[0] = a[0]; tail[1] = a[1]; tail[2] = a[2]; tail[3] = a[3];
     }
   }
-  const int lane = threadIdx.x & 63;
-#pragma unroll 1
-  for (int nn = 0; nn < NPW; ++nn) {
-  const int n = (wg * (kBlk / 64) + (threadIdx.x >> 6)) * NPW + nn;
+  const int n = wg * (kBlk / 64) + (threadIdx.x >> 6);
   if (n >= g.N) return;
+  const int lane = threadIdx.x & 63;
   // one wave per node, one list entry per lane (two per lane per pass: a busy node's ~90 terms in one
   // pass of two dependent trips — code, then J + r — where 10 slots took ~10 serial passes); every load
   // unconditional (clamped index, masked value) so no branch splits a trip; fixed-order wave sums
@@ -856,7 +853,6 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
   if (lane == 0)
 #pragma unroll
     for (int c = 0; c < 6; ++c) rhs[6 * (int64_t)n + c] = -v[c];
-  }
 }
 
 // JᵀJ blocks, workgroup-cooperative: the workgroup's 16 blocks own one contiguous range of the sorted
@@ -870,28 +866,27 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
 #endif
 constexpr int kCoop = OFX_KCOOP;
 static_assert(kCoop <= kBlk, "one entry per thread per chunk");
-template <int BPW>   // upper blocks per workgroup
 __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, double* __restrict__ A, int64_t wg,
                                             double lm) {
   __shared__ double s_prod[36 * (kCoop + 1)];
-  __shared__ int s_off[BPW + 1];
+  __shared__ int s_off[17];
   const int tid = threadIdx.x;
-  const int64_t sb = wg * BPW;   // upper blocks u in [sb, sb + BPW); past the upper count up_slot is -1 and
-                                 // the lists are empty (blk_off there = the total)
-  constexpr int kPairs = BPW * 36;
+  const int64_t sb = wg * (kBlk / 16);   // upper blocks u in [sb, sb + 16); past the upper count up_slot is -1 and
+                                         // the lists are empty (blk_off there = the total)
+  constexpr int kPairs = (kBlk / 16) * 36;
   constexpr int kU = (kPairs + kBlk - 1) / kBlk;
   // first trip: the 17 list offsets and every pair's output slots (consumed at the end, in flight all along)
-  if (tid <= BPW) s_off[tid] = g.blk_off[min<int64_t>(sb + tid, g.nnzb)];
+  if (tid <= kBlk / 16) s_off[tid] = g.blk_off[min<int64_t>(sb + tid, g.nnzb)];
   int pb[kU], po[kU], os[kU], ot[kU];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
     const int p = tid + kBlk * u;
-    pb[u] = p < kPairs ? p / 36 : BPW - 1; po[u] = p % 36;
+    pb[u] = p < kPairs ? p / 36 : kBlk / 16 - 1; po[u] = p % 36;
     os[u] = g.up_slot[sb + pb[u]];
     ot[u] = g.up_tr[sb + pb[u]];
   }
   __syncthreads();
-  const int E0 = s_off[0], E1 = s_off[BPW];
+  const int E0 = s_off[0], E1 = s_off[kBlk / 16];
   if (E0 == E1) return;   // no upper block here (uniform over the workgroup)
   double acc[kU];
   int lo[kU], hi[kU];
@@ -969,19 +964,18 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
-template <int BPW, int NPW>
 __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(4))) void k_assemble(GnDev g, DataCoef dc, double* __restrict__ A, double* __restrict__ rhs,
                                                   int nwb, double lm) {
   const int nrw = (int)gridDim.x - nwb;
-  if ((int)blockIdx.x < nrw) rhs_body<NPW>(g, dc, rhs, blockIdx.x);
-  else blocks_coop<BPW>(g, dc, A, blockIdx.x - nrw, lm);
+  if ((int)blockIdx.x < nrw) rhs_body(g, dc, rhs, blockIdx.x);
+  else blocks_coop(g, dc, A, blockIdx.x - nrw, lm);
 }
 #ifdef OFX_SPLIT_ASSEMBLE
 __global__ __launch_bounds__(kBlk) void k_assemble_blocks(GnDev g, DataCoef dc, double* __restrict__ A, double lm) {
-  blocks_coop<16>(g, dc, A, blockIdx.x, lm);
+  blocks_coop(g, dc, A, blockIdx.x, lm);
 }
 __global__ __launch_bounds__(kBlk) void k_assemble_rhs(GnDev g, DataCoef dc, double* __restrict__ rhs) {
-  rhs_body<1>(g, dc, rhs, blockIdx.x);
+  rhs_body(g, dc, rhs, blockIdx.x);
 }
 #endif
 
@@ -1848,18 +1842,17 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
 // two), stages only its half of the inverse's column groups and applies that half (split-K); the scalar
 // work, row sums and recurrences run in both waves (identical bits), wave 0 alone stores. Two LDS barriers
 // (products, M⁻¹ halves), no memory release.
-// kEarly: trip 1 issues the wave list and the stop word first, and waits only for those two before the stop test and
-// trip 2's issue (the rest of trip 1 lands under trip 2's flight; the scalars and the M⁻¹ apply wait for their own
-// loads, which retire in issue order), instead of waiting for all of trip 1. The lane's row of the cluster inverse
-// (its wave's column half) then comes to registers by plain loads (the wave's 48 row lanes read 768 contiguous bytes
-// per column group): a pending LDS-DMA would make the compiler wait for everything (vmcnt(0)) at the first use of
-// any load.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false, int kEarly = 0>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+// Trip 1 issues the wave list and the stop word first, and waits only for those two before the stop test and trip 2's
+// issue (the rest of trip 1 lands under trip 2's flight; the scalars and the M⁻¹ apply wait for their own loads, which
+// retire in issue order), instead of waiting for all of trip 1. The lane's row of the cluster inverse (its wave's
+// column half) comes to registers by plain loads (the wave's 48 row lanes read 768 contiguous bytes per column group):
+// a pending LDS-DMA would make the compiler wait for everything (vmcnt(0)) at the first use of any load. (Round 3's
+// OFX_PCG_EARLY levels 0 / 1 — the all-of-trip-1 wait with the inverse by LDS-DMA, the early issue alone — and round 4's
+// level 3 (batched LDS reads) and write-through stores lost their A/Bs and are gone: DESIGN §6.)
+template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
-  constexpr int kMS = kCD * kCD / 4 / 64;   // LDS-DMA instructions for the cluster inverse (9)
   constexpr int kNH = kW2 ? 2 : 1;
   __shared__ __attribute__((aligned(16))) double s_v[kNH][kCD];
-  __shared__ float4 s_m[kEarly ? 1 : kCD * kCD / 4];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   __shared__ double s_half[kW2 ? 64 : 1];
   const int lane = threadIdx.x & 63;
@@ -1888,32 +1881,13 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const int wb0 = g.row_ptr[wv * kRW];
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
   const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
-  if (kEarly) asm volatile("" ::: "memory");   // the list and stop word leave first
+  asm volatile("" ::: "memory");   // the list and stop word leave first
   constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
   double2 ab[kNB][18], xb[kNB][3];
-  constexpr int kMR = kEarly ? kCD / 4 / kNH : 1;   // the lane's inverse row: float4 column groups of its wave's half
+  constexpr int kMR = kCD / 4 / kNH;   // the lane's inverse row: float4 column groups of its wave's half
   float4 mreg[kMR];
-  if (kEarly)
 #pragma unroll
-    for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
-  auto inverse_dma = [&]() {
-  if (kW2) {   // wave h: column groups [6h, 6h + 6) = float4 [288h, 288h + 288), 5 DMA instructions; the last
-              // one is moved back to end at the half's end (it rewrites 32 of the wave's own float4 with the
-              // same bits), so no wave's DMA touches the other wave's half
-    constexpr int kHalf = kCD * kCD / 8;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int f = kHalf * hw + min(k * 64, kHalf - 64);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + f + lane), reinterpret_cast<void*>(s_m + f),
-                                       16, 0, 0);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kMS; ++k)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Mw + k * 64 + lane), reinterpret_cast<void*>(s_m + k * 64), 16, 0, 0);
-  }
-  };
-  if (!kEarly) inverse_dma();
+  for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
   double v[V_N];
   load_rec(g.st, o, v);
   const double m = mc[o];
@@ -1938,11 +1912,10 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
-  if (!kEarly) __builtin_amdgcn_s_waitcnt(0);   // trip 1 (incl. the LDS-DMA) landed
-  // kEarly >= 2: the wave's stop words are equal (every lane stores the same epoch), and so are the scalars below: taken
+  // the wave's stop words are equal (every lane stores the same epoch), and so are the scalars below: taken
   // as wave-uniform values the exits are scalar branches, so the main path's waits are not merged with the exit paths'
   // (a divergent exit left a vmcnt(0) at the join in front of the products)
-  if (kEarly >= 2) stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
+  stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
   if (stop_ep >= g.ep) return;     // this solve has converged (or stopped): a drained launch
 #ifdef OFX_STAMPS
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
@@ -1955,16 +1928,12 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
       const int2 e = j ? bl1 : bl0;
       const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e.y);
       const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
-      if (kEarly >= 2) {   // the gathered m row first: the products of the first block rows start before the block's tail lands
+      // the gathered m row first: the products of the first block rows start before the block's tail lands
 #pragma unroll
-        for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
-        asm volatile("" ::: "memory");
-      }
+      for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int k = 0; k < 18; ++k) ab[j][k] = blk[k];
-      if (kEarly < 2)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
   // ---- scalars from the partials (trip-1 data)
@@ -1987,7 +1956,6 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const double tol = g.prm.pcg_tol;
   const bool lead = wv == 0 && lane == 0 && hw == 0;
   const bool w0 = hw == 0;   // the wave that stores (kW2: both compute the same bits)
-  if (kFirst && lead && kEarly < 2) g.scal[S_BB] = bb;   // (kEarly >= 2: with the lead's other stores, last)
   double beta = 0.0, alpha;
   if (kFirst) {
     alpha = gam / del;
@@ -2002,9 +1970,9 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const double etol = g.prm.pcg_err_tol;
   const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam <= thr_prev)) || gam == 0.0 || rr <= 1e-24 * bb;
   int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
-  if (kEarly >= 2) leave = __builtin_amdgcn_readfirstlane(leave);
+  leave = __builtin_amdgcn_readfirstlane(leave);
   if (leave) {   // converged, or breakdown (A SPD => alpha > 0): keep x
-    if (kFirst && lead && kEarly >= 2) g.scal[S_BB] = bb;
+    if (kFirst && lead) g.scal[S_BB] = bb;
     if (!w0) return;
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
     g.stopw[(int64_t)wv * 64 + lane] = g.ep;
@@ -2018,7 +1986,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     }
     return;
   }
-  // the lead's scalar stores (read by the next launch only): kEarly issues them last — on gfx9 vmcnt counts stores too,
+  // the lead's scalar stores (read by the next launch only) are issued last — on gfx9 vmcnt counts stores too,
   // so stores issued here made the lead wave's first wait on trip 2 a vmcnt(0) that also waited for their acks
   // the Lanczos tridiagonal of the preconditioned operator grows by one row per iteration: T_kk = 1/α_k + β_{k-1}/α_{k-1},
   // T_{k,k-1}² = β_{k-1}/α_{k-1}² (β_{k-1} = γ_k/γ_{k-1}); its smallest eigenvalue (Ritz value) θ_k decreases towards
@@ -2047,9 +2015,8 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
     if (lead) g.pcg_alpha[4 + par] = thr_new;
     if (wv == 0 && hw == 0 && etol > 0.0) g.sturm[lane] = sd_new;
-    if (kFirst && lead && kEarly >= 2) g.scal[S_BB] = bb;
+    if (kFirst && lead) g.scal[S_BB] = bb;
   };
-  if (kEarly < 2) lead_stores();
   OFX_STAMP(2)
   // ---- n = A m (own component)
   double nc;
@@ -2080,19 +2047,10 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     const int len = b1 - b0;
     const double* sp = s_prod + (b0 - wb0) * 6 + qc;
     double a = 0.0;
-    if (kEarly >= 3) {   // every read in flight before the first add (one LDS round trip instead of five)
-      double tv[kRowMax];
 #pragma unroll
-      for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
-    } else {
-#pragma unroll
-      for (int k = 0; k < kRowMax; ++k) {
-        const double t = sp[6 * k];
-        a += k < len ? t : 0.0;
-      }
+    for (int k = 0; k < kRowMax; ++k) {
+      const double t = sp[6 * k];
+      a += k < len ? t : 0.0;
     }
     nc = a;
   } else {
@@ -2122,29 +2080,15 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   if (kW2) {      // split-K: wave h applies column groups [6h, 6h + 6); wave 0 adds the halves (fixed order)
     double hsum = 0.0;
     if (own) {
-      const float4* mrow = s_m + (6 * r + q);
       double a[4] = {0.0, 0.0, 0.0, 0.0};
-      double2 vv[kCD / 4];   // kEarly >= 3: the half's 24 entries of w by 12 broadcast reads, all in flight at once
-      if (kEarly >= 3) {
-#pragma unroll
-        for (int kk = 0; kk < kCD / 8; ++kk) {
-          const int k = (kCD / 8) * hw + kk;
-          vv[2 * kk] = *reinterpret_cast<const double2*>(&s_v[hw][4 * k]);
-          vv[2 * kk + 1] = *reinterpret_cast<const double2*>(&s_v[hw][4 * k + 2]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
 #pragma unroll
       for (int kk = 0; kk < kCD / 8; ++kk) {
         const int k = (kCD / 8) * hw + kk;
-        const float4 t = kEarly ? mreg[kk % kMR] : mrow[k * kCD];
-        const double v0 = kEarly >= 3 ? vv[2 * kk].x : s_v[hw][4 * k], v1 = kEarly >= 3 ? vv[2 * kk].y : s_v[hw][4 * k + 1];
-        const double v2 = kEarly >= 3 ? vv[2 * kk + 1].x : s_v[hw][4 * k + 2];
-        const double v3 = kEarly >= 3 ? vv[2 * kk + 1].y : s_v[hw][4 * k + 3];
-        a[0] = fma((double)t.x, v0, a[0]);
-        a[1] = fma((double)t.y, v1, a[1]);
-        a[2] = fma((double)t.z, v2, a[2]);
-        a[3] = fma((double)t.w, v3, a[3]);
+        const float4 t = mreg[kk];
+        a[0] = fma((double)t.x, s_v[hw][4 * k], a[0]);
+        a[1] = fma((double)t.y, s_v[hw][4 * k + 1], a[1]);
+        a[2] = fma((double)t.z, s_v[hw][4 * k + 2], a[2]);
+        a[3] = fma((double)t.w, s_v[hw][4 * k + 3], a[3]);
       }
       hsum = (a[0] + a[1]) + (a[2] + a[3]);
     }
@@ -2152,12 +2096,11 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     if (w0 && own) mn[o] = hsum + s_half[lane];
-  } else if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (inverse rows staged in LDS)
-    const float4* mrow = s_m + (6 * r + q);
+  } else if (own) {      // m of the next iteration: M⁻¹ w_new, cluster-local (the lane's inverse row in registers)
     double a[4] = {0.0, 0.0, 0.0, 0.0};   // four independent FMA chains
 #pragma unroll
     for (int k = 0; k < kCD / 4; ++k) {
-      const float4 t = kEarly ? mreg[k % kMR] : mrow[k * kCD];
+      const float4 t = mreg[k];
       a[0] = fma((double)t.x, s_v[0][4 * k], a[0]);
       a[1] = fma((double)t.y, s_v[0][4 * k + 1], a[1]);
       a[2] = fma((double)t.z, s_v[0][4 * k + 2], a[2]);
@@ -2170,7 +2113,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
   if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
-  if (kEarly >= 2) lead_stores();
+  lead_stores();
   OFX_STAMP(7)
 }
 
@@ -2388,29 +2331,22 @@ static int pcg_ku_for(int waves) {
 }
 
 using PcgKernel = void (*)(PcgIt, int);
-template <int KU, int E>
-static void pcg_pick_e(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
+template <int KU>
+static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU == 3) {
     if (wave && w2) {
-      first = k_pcg_iter<true, true, 3, true, E>;
-      rest = k_pcg_iter<true, false, 3, true, E>;
+      first = k_pcg_iter<true, true, 3, true>;
+      rest = k_pcg_iter<true, false, 3, true>;
       return;
     }
   }
   if (wave) {
-    first = k_pcg_iter<true, true, KU, false, E>;
-    rest = k_pcg_iter<true, false, KU, false, E>;
+    first = k_pcg_iter<true, true, KU, false>;
+    rest = k_pcg_iter<true, false, KU, false>;
   } else {
-    first = k_pcg_iter<false, true, KU, false, E>;
-    rest = k_pcg_iter<false, false, KU, false, E>;
+    first = k_pcg_iter<false, true, KU, false>;
+    rest = k_pcg_iter<false, false, KU, false>;
   }
-}
-template <int KU>
-static void pcg_pick(bool wave, bool w2, int early, PcgKernel& first, PcgKernel& rest) {
-  if (early == 3) pcg_pick_e<KU, 3>(wave, w2, first, rest);
-  else if (early == 2) pcg_pick_e<KU, 2>(wave, w2, first, rest);
-  else if (early == 1) pcg_pick_e<KU, 1>(wave, w2, first, rest);
-  else pcg_pick_e<KU, 0>(wave, w2, first, rest);
 }
 
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
@@ -2456,16 +2392,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   Gn::PcgHist& ph = *g->last_pcg;
   const int hk = gn_iter & 63;
   const int lp = ph.n[hk] > 0 ? ph.c[hk][(ph.n[hk] - 1) & 3] : 0;   // the previous solve's count for this GN step
-  // Chunk rule (OFX_PCG_CHUNK="mode,window,topup,lookahead", read per solve for in-process A/B): mode 0 — the first
-  // chunk covers the previous solve's count + 4, a chunk that runs out is followed by 8 more, the poll event sits at
-  // each chunk's end; mode 1 — the first chunk is the smallest count of the last `window` solves (an under-estimate),
-  // top-ups of `topup`, and the poll event sits `lookahead` launches before each chunk's end, so the host enqueues the
-  // next chunk while the GPU still has launches queued.
-  int c_mode = 0, c_win = 3, c_top = 4, c_look = 3;
-  if (const char* ce = getenv("OFX_PCG_CHUNK")) sscanf(ce, "%d,%d,%d,%d", &c_mode, &c_win, &c_top, &c_look);
-  c_win = c_win < 1 ? 1 : (c_win > 4 ? 4 : c_win);
-  c_top = c_top < 1 ? 1 : c_top;
-  c_look = c_look < 0 ? 0 : c_look;
+  // Chunk rule (round 4, `profiles/r04_ab.json`): an under-estimate (the smallest of the last 3 counts) with top-ups of
+  // 3-4 launches and a poll event 3 launches ahead of each chunk's end cut the drained launches from ~100 to ~30-55 per
+  // frame but never the frame time (+0.02 ... +0.33 ms): the drains overlap the host's reaction to convergence, while
+  // every top-up risks an empty queue. The first chunk stays the previous count + 4, and 8 more when one runs out.
   const dim3 grid(g->nwg_row), block(64);
   // variants: wave-list SpMV (short rows) or CSR rows; partial-sum width kU for the cluster count (pcg_ku_for);
   // two waves per cluster only up to 384 clusters (kU = 3): config 4's 490 clusters ran 5.38 us per launch
@@ -2474,16 +2404,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // frames/s)
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku == 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
-  // early stop test / trip-2 issue (kEarly; OFX_PCG_EARLY=0: the all-of-trip-1 wait with the inverse by LDS-DMA, 1: the
-  // early trip-2 issue alone, 2 (default): + gathered rows first, the lead's stores last and scalar exit branches; read
-  // per solve: in-process A/B)
-  const char* ee = getenv("OFX_PCG_EARLY");
-  const int early = (ee && ee[0] >= '0' && ee[0] <= '3') ? ee[0] - '0' : 2;
   switch (g->pcg_ku) {
-    case 3: pcg_pick<3>(wave, w2, early, iter0, iter); break;
-    case 4: pcg_pick<4>(wave, w2, early, iter0, iter); break;
-    case 8: pcg_pick<8>(wave, w2, early, iter0, iter); break;
-    default: pcg_pick<17>(wave, w2, early, iter0, iter); break;
+    case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
+    case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
+    case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
+    default: pcg_pick<17>(wave, w2, iter0, iter); break;
   }
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
@@ -2500,15 +2425,9 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   pa.tail = rhs + 6 * (int64_t)g->N;
   g->step_fused = false;
   int chunk = lp > 0 ? lp + 4 : 64;
-  if (c_mode == 1 && ph.n[hk] > 0) {
-    int mn = 1 << 30;
-    for (int q = 0; q < c_win && q < ph.n[hk]; ++q) mn = std::min(mn, ph.c[hk][(ph.n[hk] - 1 - q) & 3]);
-    chunk = mn + 1 > 1 ? mn + 1 : 1;   // launch i tests the state after i iterations: count + 1 launches
-  }
   int it = 0;
   while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
-    const int mark = (c_mode == 1 && n > c_look) ? n - c_look : n;   // the poll event after this chunk's launch `mark`
 #ifdef OFX_STAMPS
     const auto h0 = std::chrono::steady_clock::now();
     if (it == 0 && gn_iter > 0 && g->t_seen.time_since_epoch().count())
@@ -2516,7 +2435,6 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
 #endif
     for (int k = 0; k < n; ++k, ++it) {
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, pa, it & 1);
-      if (k + 1 == mark && mark < n) OFX_HIP(hipEventRecord(g->poll_ev, hs));
     }
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
@@ -2524,7 +2442,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
 #endif
     OFX_LAUNCH_CHECK();
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
-    if (mark == n) OFX_HIP(hipEventRecord(g->poll_ev, hs));
+    OFX_HIP(hipEventRecord(g->poll_ev, hs));
     bool ran = false;
     // converged: the converging launch's lead lane stored H_DONE (the next step's kernels follow it on the stream);
     // stopped (by an earlier solve: this one's launches end at their stop words; by this solve's converging launch):
@@ -2546,8 +2464,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       g->step_fused = pa.fuse != 0;
       break;
     }
-    (void)ran;   // the chunk ran out (mode 1: reached its poll mark) without convergence: next chunk
-    chunk = c_mode == 1 ? c_top : 8;
+    (void)ran;   // the chunk ran out without convergence: next chunk
+    chunk = 8;
   }
   g->n_iter_launches += it;
   if (g->timing) g->ev.emplace_back(e0, e1);
@@ -3220,22 +3138,12 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   const double lm = add_reg ? lm_for_iter(g->prm.lm_factor, gn_iter) : 0.0;
   // upper blocks: (nnzb + diagonal blocks) / 2 <= (nnzb + rows) / 2 (the pattern is symmetric); workgroups past
   // the device-side count return at once
-  // workgroup shape (OFX_ASM="blocks per workgroup,nodes per rhs wave", read per call for in-process A/B): all of
-  // the launch's workgroups reserve the blocks' LDS (4 per CU), so the count decides whether it runs in one round
-  int bpw = 16, npw = 1;
-  if (const char* e = getenv("OFX_ASM")) sscanf(e, "%d,%d", &bpw, &npw);
-  if (bpw != 32) bpw = 16;
-  if (npw != 2) npw = 1;
-  const int nwb = g->nnzb > 0 ? (int)grid_for((g->nnzb + g->N) / 2 + 1, bpw, 1 << 30) : 0;
-  const int nwr = (int)grid_for(g->N, (kBlk / 64) * npw);
-  using AsmKernel = void (*)(GnDev, DataCoef, double*, double*, int, double);
-  const AsmKernel kasm = bpw == 32 ? (npw == 2 ? k_assemble<32, 2> : k_assemble<32, 1>)
-                                   : (npw == 2 ? k_assemble<16, 2> : k_assemble<16, 1>);
+  const int nwb = g->nnzb > 0 ? (int)grid_for((g->nnzb + g->N) / 2 + 1, kBlk / 16, 1 << 30) : 0;
 #ifdef OFX_SPLIT_ASSEMBLE   // tuning build: the two halves as separate kernels (rocprof times each)
   if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, dc, A, lm);
   hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, rhs);
 #else
-  hipLaunchKernelGGL(kasm, dim3(nwb + nwr), dim3(kBlk), 0, hs, *g, dc, A, rhs, nwb, lm);
+  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, A, rhs, nwb, lm);
 #endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;

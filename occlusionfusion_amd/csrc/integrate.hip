@@ -408,21 +408,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 // (pixel_of), SDF rounding certified cheaply (sdf_color_update), per-wave update counts by ballot;
 // bit-identical to k_integrate<1,1,0>. The kernel is VALU-bound: every per-wave instruction
 // is shared by two voxels.
-// TAB: separable warp tables. On the brick's voxel grid dx = x_i - g_x depends only on (node, i), dy on (node, j), dz
-// on (node, k), so every product of R(x - g) is a table entry per palette node and brick coordinate: TX[n][i] =
-// {R00·dx, R10·dx, R20·dx, g_z}, TY[n][j] = {R01·dy, R11·dy, R21·dy, t_z}, TZ[n][k] = {R02·dz, R12·dz, R22·dz, -},
-// GT[n] = {g_x, g_y, t_x, t_y}: built once per brick (one barrier), then per voxel and anchor the reference's sums
-// ((R·dx + R·dy) + R·dz, + g, + t, · w in ed_warp's order and rounding) from four LDS reads — the same bits, without
-// the subtractions and the nine products.
-template <bool COLOR, bool TAB = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAB ? 4 : 6))) void k_integrate_pal4(
+template <bool COLOR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_integrate_pal4(
     BrickGeom g, BrickDiv bd, CamD c, const float* __restrict__ depth, const float* __restrict__ color_im,
     const float4* __restrict__ nodes, int n_nodes, const int32_t* __restrict__ list,
     const ushort4* __restrict__ anchors, const float4* __restrict__ weights, const uint16_t* __restrict__ pal_ids,
     const int32_t* __restrict__ pal_n, const uchar4* __restrict__ local, double trunc, double itrunc, double obs,
     float* __restrict__ tsdf, float* __restrict__ weight, float* __restrict__ color, uint32_t* counter) {
   __shared__ float4 s_node[4 * kPal];
-  __shared__ float4 s_tab[TAB ? 3 * kPal * kBrick + kPal : 1];   // TX, TY, TZ (node-major, 8 per node), then GT
   __shared__ float s_xyz[3 * kBrick];   // vox2world of the brick's 8 x, y and z coordinates
   __shared__ uint32_t s_cnt[4];
   const int tid = threadIdx.x;
@@ -472,31 +465,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAB ? 4 : 6
                                                                : vox2world(g.oz, g.vs, k0 + o);
   }
   __syncthreads();
-  if (TAB && use_pal) {   // the brick's warp tables (entries e < 3·8·pn: axis, node, coordinate), then one barrier
-    for (int e = tid; e < 3 * kBrick * pn + pn; e += 256) {
-      if (e < 3 * kBrick * pn) {
-        const int ax = e / (kBrick * pn), r = e - ax * kBrick * pn, n = r >> 3, o = r & 7;
-        const float4 na = s_node[4 * n], nb = s_node[4 * n + 1], nc = s_node[4 * n + 2], nd = s_node[4 * n + 3];
-        float4 t;
-        if (ax == 0) {
-          const float d = s_xyz[o] - nb.z;
-          t = make_float4(na.x * d, na.y * d, nc.z * d, nd.y);
-        } else if (ax == 1) {
-          const float d = s_xyz[kBrick + o] - nb.w;
-          t = make_float4(na.z * d, na.w * d, nc.w * d, nd.z);
-        } else {
-          const float d = s_xyz[2 * kBrick + o] - nd.y;
-          t = make_float4(nb.x * d, nb.y * d, nd.x * d, 0.f);
-        }
-        s_tab[(ax * kPal + n) * kBrick + o] = t;
-      } else {
-        const int n = e - 3 * kBrick * pn;
-        const float4 nb = s_node[4 * n + 1], nc = s_node[4 * n + 2];
-        s_tab[3 * kPal * kBrick + n] = make_float4(nb.z, nb.w, nc.x, nc.y);
-      }
-    }
-    __syncthreads();
-  }
   const float y0 = s_xyz[kBrick + ((tid >> 3) & 7)], z0 = s_xyz[2 * kBrick + (tid & 7)];
   int pix[2];
   float zw[2];
@@ -507,26 +475,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAB ? 4 : 6
     if (!act[h]) continue;
     float px = s_xyz[(tid >> 6) + 4 * h], py = y0, pz = z0;
     const float w[4] = {ww[h].x, ww[h].y, ww[h].z, ww[h].w};
-    if (TAB && use_pal) {
-      const int ids[4] = {la[h].x, la[h].y, la[h].z, la[h].w};
-      const int oi = (tid >> 6) + 4 * h, oj = (tid >> 3) & 7, ok = tid & 7;
-      f2 axy = {0.f, 0.f};
-      float az = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 tx = s_tab[ids[q] * kBrick + oi], ty = s_tab[(kPal + ids[q]) * kBrick + oj];
-        const float4 tz = s_tab[(2 * kPal + ids[q]) * kBrick + ok], gt = s_tab[3 * kPal * kBrick + ids[q]];
-        f2 r = f2{tx.x, tx.y} + f2{ty.x, ty.y};
-        r = r + f2{tz.x, tz.y};
-        float rz = tx.z + ty.z;
-        rz = rz + tz.z;
-        const f2 yxy = ((r + f2{gt.x, gt.y}) + f2{gt.z, gt.w}) * w[q];
-        const float yz = ((rz + tx.w) + ty.w) * w[q];
-        if (q == 0) { axy = yxy; az = yz; }
-        else { axy = axy + yxy; az = az + yz; }
-      }
-      px = axy.x; py = axy.y; pz = az;
-    } else if (use_pal) {
+    if (use_pal) {
       const int ids[4] = {la[h].x, la[h].y, la[h].z, la[h].w};
       ed_warp(s_node, ids, w, 4, px, py, pz);
     } else {
@@ -942,21 +891,6 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
   OFX_CHECK_ARG(desc->semantics == OFX_SEM_CPU || desc->semantics == OFX_SEM_PYCUDA, "bad semantics %d", desc->semantics);
   IntTimer timer;
   if (desc->semantics == OFX_SEM_CPU && k == 4 && g.n_bricks * kBrickVox < (1ll << 31) && !getenv("OFX_INT_GENERIC")) {
-    const char* te = getenv("OFX_INT_TAB");   // separable warp tables (A/B; read per launch)
-    if (te && te[0] == '1') {
-      if (color)
-        OFX_TIMED_LAUNCH(timer, (k_integrate_pal4<true, true>), dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g,
-                         make_div(g), make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
-                         (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
-                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
-      else
-        OFX_TIMED_LAUNCH(timer, (k_integrate_pal4<false, true>), dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g,
-                         make_div(g), make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
-                         (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
-                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
-      OFX_LAUNCH_CHECK();
-      return OFX_OK;
-    }
     if (color)
       OFX_TIMED_LAUNCH(timer, k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,

@@ -4,6 +4,7 @@ launch) cancels. Prints mean ms per frame (solve + integrate, stream events) per
 
     python tools/ab_inproc.py OFX_GN_PIPE 0 1 [--frames 120]
     python tools/ab_inproc.py prefetch_lead 0 1 2 --block 8   # a solver attribute, switched every 8 frames
+    python tools/ab_inproc.py param:pcg_tol 1e-6 3e-6 --sweep 3   # a GN parameter
 
 --block B: switch every B frames and leave the first frame of each block out (a setting that acts across the
 frame boundary, such as when the next frame's prefetched setup starts, then counts only against itself).
@@ -47,21 +48,26 @@ def main():
     def setv(v):
         if a.var == "prefetch_lead":
             pipe.solver.prefetch_lead = int(v)
+        elif a.var.startswith("param:"):   # a GN parameter (e.g. param:pcg_tol); use --sweep (prefetches match params)
+            pipe.solver.params[a.var[6:]] = float(v)
         else:
             os.environ[a.var] = v
 
     if a.sweep:
         per = {v: [] for v in a.values}
+        launches = {v: [] for v in a.values}   # k_pcg_iter launches and PCG iterations per frame (whole run)
+        iters = {v: [] for v in a.values}
         tg = 0   # the volume's frame counter keeps increasing over the repeated frames
         for r in range(a.sweep):
             for v in a.values:
                 setv(v)
                 pipe.prev_rot = pipe.prev_trans = None   # the same solves each run: frame 1 from the rest pose
-                ev = []
+                ev, outs = [], []
+                pipe.solver.timing(True)
                 for t in range(1, total):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    pipe.solve(frames[t], frames[t + 1])
+                    outs.append(pipe.solve(frames[t], frames[t + 1]))
                     tg += 1
                     pipe.integrate(frames[t], tg)
                     e1.record()
@@ -69,12 +75,16 @@ def main():
                 pipe.solver.drain()
                 torch.cuda.synchronize()
                 per[v].append(np.array([e0.elapsed_time(e1) for e0, e1 in ev[4:]]))
+                _, nl, _ = pipe.solver.timing(False)
+                launches[v].append(nl / len(outs))
+                iters[v].append(float(np.mean([int(o["_status"][2].item()) for o in outs])))
         base = np.stack(per[a.values[0]])
         out = {}
         for v in a.values:
             x = np.stack(per[v])
             out[v] = {"ms_per_frame": float(x.mean()), "run_means": [float(q) for q in x.mean(1)],
-                      "paired_diff_ms": float((x - base).mean()), "n": int(x.size)}
+                      "paired_diff_ms": float((x - base).mean()), "n": int(x.size),
+                      "launches_per_frame": float(np.mean(launches[v])), "iters_per_frame": float(np.mean(iters[v]))}
         print(json.dumps({"var": a.var, "sweep": a.sweep, "results": out}))
         return
     for t in range(1, total):

@@ -1,9 +1,9 @@
 """Tuning study (not product): warped integrate kernel time under an environment switch read per launch, the settings
 interleaved launch by launch in one process on the bench scene (config 3 by default). Default switch OFX_INT_GENERIC
-(the generic k_integrate<1,1,0> against the specialised k_integrate_pal4, plus the source-frame pass); e.g.
-OFX_INT_TAB 0 1 (the palette kernel's separable warp tables).
+(the generic k_integrate<1,1,0> against the specialised k_integrate_pal4, plus the source-frame pass); any switch the
+integrate reads per launch (round 4: OFX_INT_TAB, separable warp tables, 113.9 vs 90.2 us: dropped).
 
-    python tools/int_ab.py [--config 3] [--var OFX_INT_TAB --vals 0 1] [--reps 40]
+    python tools/int_ab.py [--config 3] [--var OFX_INT_GENERIC --vals 1 0] [--reps 40]
 """
 import argparse
 import os

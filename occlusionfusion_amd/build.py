@@ -16,7 +16,10 @@ LIB = os.path.join(HERE, "libofx.so")
 OBJ = os.path.join(HERE, "_build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OFX_ARCH", "gfx950")
+# -amdgpu-kernarg-preload-count: the leading scalar / pointer kernel arguments arrive preloaded in SGPRs at wave launch
+# (no kernarg fetch ahead of a kernel's first loads; k_pcg_iter passes its trip-1 pointers that way: gn.hip)
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", "-munsafe-fp-atomics",
+         "-mllvm", "-amdgpu-kernarg-preload-count=16",
          "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
 
 

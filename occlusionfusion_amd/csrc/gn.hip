@@ -1849,8 +1849,14 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
 // a pending LDS-DMA would make the compiler wait for everything (vmcnt(0)) at the first use of any load. (Round 3's
 // OFX_PCG_EARLY levels 0 / 1 — the all-of-trip-1 wait with the inverse by LDS-DMA, the early issue alone — and round 4's
 // level 3 (batched LDS reads) and write-through stores lost their A/Bs and are gone: DESIGN §6.)
+// The first seven arguments are the pointers trip 1 loads through: scalar pointer arguments are preloaded into SGPRs at
+// wave launch (-amdgpu-kernarg-preload-count, build.py), so the first loads issue without waiting for a kernarg fetch
+// (tools/preload_micro.hip: 3.15 -> 2.88 us per dependent launch); a struct argument is never preloaded. mc / Pc are the
+// parity's m and partial streams.
 template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
-__global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(PcgIt g, int par) {
+__global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(
+    const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const float* Mcl,
+    const int32_t* row_ptr, PcgIt g, int par) {   // (not __restrict__: a restrict load sinks past the exit test)
   constexpr int kNH = kW2 ? 2 : 1;
   __shared__ __attribute__((aligned(16))) double s_v[kNH][kCD];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
@@ -1858,29 +1864,31 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const int lane = threadIdx.x & 63;
   const int hw = kW2 ? (int)(threadIdx.x >> 6) : 0;   // wave within the cluster's workgroup
   const int wv = blockIdx.x;
-  const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
-  const int nw = g.nwg_row;
-  const double* __restrict__ mc = par ? g.m1 : g.m0;
-  double* __restrict__ mn = par ? g.m0 : g.m1;
-  const int ns = g.nw_pad;
-  const double* Pc = g.part_p + 3 * (int64_t)ns * par;
-  double* Pn = g.part_p + 3 * (int64_t)ns * (par ^ 1);
-  const bool own = q < 6;
-  const int qc = own ? q : 5;
-  const int64_t o = 6 * (int64_t)row + qc;
-  // ---- trip 1 (block list first: trip 2 waits only for it)
+  // ---- trip 1: the block list and the stop word leave first, through preloaded pointers only (no kernarg wait)
 #ifdef OFX_STAMPS
   const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
   int2 bl0 = make_int2(-1, 0), bl1 = make_int2(-1, 0);
   if (kWave) {
-    bl0 = g.wl[(int64_t)wv * kWL + 64 * hw + lane];
-    if (!kW2) bl1 = g.wl[(int64_t)wv * kWL + 64 + lane];
+    bl0 = wl[(int64_t)wv * kWL + 64 * hw + lane];
+    if (!kW2) bl1 = wl[(int64_t)wv * kWL + 64 + lane];
   }
-  int stop_ep = g.stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
-  const int wb0 = g.row_ptr[wv * kRW];
-  const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];
-  const float4* Mw = reinterpret_cast<const float4*>(g.Mcl + (int64_t)wv * kCD * kCD);
+  int stop_ep = stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
+  // kernarg-derived scalars pass through an opaque copy ordered after these two loads (memory clobber): otherwise the
+  // compiler schedules an early use of them and with it a kernarg wait ahead of the list and stop-word loads
+  __builtin_amdgcn_sched_barrier(0);
+  int ns = g.nw_pad, par_ = par;
+  asm volatile("" : "+s"(ns), "+s"(par_) :: "memory");
+  const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
+  const int nw = g.nwg_row;
+  double* __restrict__ mn = par_ ? g.m0 : g.m1;
+  double* Pn = g.part_p + 3 * (int64_t)ns * (par_ ^ 1);
+  const bool own = q < 6;
+  const int qc = own ? q : 5;
+  const int64_t o = 6 * (int64_t)row + qc;
+  const int wb0 = row_ptr[wv * kRW];
+  const int b0 = row_ptr[row], b1 = row_ptr[row + 1];
+  const float4* Mw = reinterpret_cast<const float4*>(Mcl + (int64_t)wv * kCD * kCD);
   asm volatile("" ::: "memory");   // the list and stop word leave first
   constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
   double2 ab[kNB][18], xb[kNB][3];
@@ -1889,7 +1897,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
   double v[V_N];
-  load_rec(g.st, o, v);
+  load_rec(st, o, v);
   const double m = mc[o];
   double2 tp[3][kU];              // the streams are zero beyond nw up to ns = 128·kU: no masks
 #pragma unroll
@@ -1904,9 +1912,9 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
   for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * ns + wv];
   const int cnt = g.flags[F_PCG_CNT];
-  const double rgam_prev = kFirst ? 1.0 : g.pcg_gamma[2 + (par ^ 1)];     // 1/γ, 1/α of the previous iteration
-  const double ralpha_prev = kFirst ? 1.0 : g.pcg_alpha[2 + (par ^ 1)];
-  const double thr_prev = kFirst ? 0.0 : g.pcg_alpha[4 + (par ^ 1)];       // error-based stop: bound on γ (below)
+  const double rgam_prev = kFirst ? 1.0 : g.pcg_gamma[2 + (par_ ^ 1)];     // 1/γ, 1/α of the previous iteration
+  const double ralpha_prev = kFirst ? 1.0 : g.pcg_alpha[2 + (par_ ^ 1)];
+  const double thr_prev = kFirst ? 0.0 : g.pcg_alpha[4 + (par_ ^ 1)];       // error-based stop: bound on γ (below)
   const double2 sd = g.sturm[lane];   // (every wave loads it: no load behind a branch; the lead wave uses it)
   const double bb_stored = g.scal[S_BB];
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
@@ -2012,8 +2020,8 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     thr_new = (etol * th) * (etol * th);
   }
   auto lead_stores = [&]() {
-    if (lead) { g.pcg_alpha[2 + par] = 1.0 / alpha; g.pcg_gamma[2 + par] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
-    if (lead) g.pcg_alpha[4 + par] = thr_new;
+    if (lead) { g.pcg_alpha[2 + par_] = 1.0 / alpha; g.pcg_gamma[2 + par_] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
+    if (lead) g.pcg_alpha[4 + par_] = thr_new;
     if (wv == 0 && hw == 0 && etol > 0.0) g.sturm[lane] = sd_new;
     if (kFirst && lead) g.scal[S_BB] = bb;
   };
@@ -2070,7 +2078,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     const double w2 = fma(-alpha, zz, v[V_W]);
     if (own) {
       const double nv[V_N] = {fma(alpha, p, v[V_X]), rn, un, zz, qq, sv, p, w2};
-      if (w0) store_rec(g.st, o, nv);
+      if (w0) store_rec(g.st, o, nv);   // (g.st: the same buffer, written; st is the const view)
       s_v[hw][6 * r + q] = w2;
       d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
     }
@@ -2330,7 +2338,8 @@ static int pcg_ku_for(int waves) {
   return ku;
 }
 
-using PcgKernel = void (*)(PcgIt, int);
+using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const float*,
+                          const int32_t*, PcgIt, int);
 template <int KU>
 static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU == 3) {
@@ -2434,7 +2443,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       g->prologue_us += std::chrono::duration<double, std::micro>(h0 - g->t_seen).count();
 #endif
     for (int k = 0; k < n; ++k, ++it) {
-      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, pa, it & 1);
+      const int par = it & 1;
+      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, (const int2*)g->wl, (const int32_t*)g->stopw,
+                         (const double*)(g->part_p + 3 * (int64_t)g->nw_pad * par), (const double*)g->st,
+                         (const double*)(par ? g->m1 : g->m0), (const float*)g->Mcl, (const int32_t*)g->row_ptr, pa, par);
     }
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();

@@ -42,7 +42,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
+PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
 
 from occlusionfusion_amd.synthetic import BASELINE_CONFIGS as CONFIGS  # noqa: E402  (configs 1-5)
 

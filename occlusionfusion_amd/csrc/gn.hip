@@ -2327,13 +2327,14 @@ static void order_rows(int N, int NB, const float* nodes, const int32_t* edges, 
 }
 
 // Partial pairs per lane and stream of k_pcg_iter for a cluster (wave) count: the streams are 2·64·kU wide, so
-// fewer loads and adds per lane for fewer clusters (3: <= 384, 4: <= 512, 8: <= 1024, 17: <= 2176 clusters).
-// OFX_PCG_KU=<3|4|8|17> forces one (A/B; it must still cover the count).
+// fewer loads and adds per lane for fewer clusters (2: <= 256, 3: <= 384, 4: <= 512, 8: <= 1024, 17: <= 2176
+// clusters; kU = 2 for config 3's 250 clusters: -0.031 ms per frame against 3, same frames, profiles/r04_ab.json).
+// OFX_PCG_KU=<2|3|4|8|17> forces one (A/B, read per setup; it must still cover the count).
 static int pcg_ku_for(int waves) {
-  int ku = waves <= 384 ? 3 : waves <= 512 ? 4 : waves <= 1024 ? 8 : 17;
+  int ku = waves <= 256 ? 2 : waves <= 384 ? 3 : waves <= 512 ? 4 : waves <= 1024 ? 8 : 17;
   if (const char* e = getenv("OFX_PCG_KU")) {
     const int f = atoi(e);
-    if ((f == 3 || f == 4 || f == 8 || f == 17) && 128 * f >= waves) ku = f;
+    if ((f == 2 || f == 3 || f == 4 || f == 8 || f == 17) && 128 * f >= waves) ku = f;
   }
   return ku;
 }
@@ -2342,10 +2343,10 @@ using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const dou
                           const int32_t*, PcgIt, int);
 template <int KU>
 static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
-  if constexpr (KU == 3) {
+  if constexpr (KU <= 3) {
     if (wave && w2) {
-      first = k_pcg_iter<true, true, 3, true>;
-      rest = k_pcg_iter<true, false, 3, true>;
+      first = k_pcg_iter<true, true, KU, true>;
+      rest = k_pcg_iter<true, false, KU, true>;
       return;
     }
   }
@@ -2378,6 +2379,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
     else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
     switch (g->pcg_ku) {
+      case 2: hipLaunchKernelGGL(k_pcg_proj2<2>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
       case 3: hipLaunchKernelGGL(k_pcg_proj2<3>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
       case 4: hipLaunchKernelGGL(k_pcg_proj2<4>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
       case 8: hipLaunchKernelGGL(k_pcg_proj2<8>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
@@ -2411,9 +2413,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // with one wave and kU = 4, 5.58 with two; kU = 8: 5.66 vs 5.91; kU = 17: 6.35 vs 6.93 (A/B, 1278.9
   // iterations per frame; one wave per cluster and kU = 17 was the round-1 form for > 384 clusters: 95 vs 111
   // frames/s)
-  const bool w2 = wave && g->pcg_w2 && g->pcg_ku == 3;
+  const bool w2 = wave && g->pcg_w2 && g->pcg_ku <= 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
   switch (g->pcg_ku) {
+    case 2: pcg_pick<2>(wave, w2, iter0, iter); break;
     case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
     case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
     case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
@@ -2675,7 +2678,7 @@ int ofx_gn_step_fused(void* handle, int32_t* fused) {
 int ofx_gn_pcg_waves(void* handle, int32_t* waves) {
   Gn* g = (Gn*)handle;
   OFX_CHECK_ARG(g && waves, "null handle/waves");
-  *waves = (g->pcg_w2 && g->pcg_ku == 3) ? 2 : 1;   // the last setup's form (two only up to 384 clusters)
+  *waves = (g->pcg_w2 && g->pcg_ku <= 3) ? 2 : 1;   // the last setup's form (two only up to 384 clusters)
   return OFX_OK;
 }
 

@@ -2437,6 +2437,20 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   pa.tail = rhs + 6 * (int64_t)g->N;
   g->step_fused = false;
   int chunk = lp > 0 ? lp + 4 : 64;
+  // Later GN steps: the previous frame's count for this step scaled by how this frame's step 0 compared with the
+  // previous frame's (the steps' counts move together frame to frame) + a margin (OFX_PCG_RATIO=<margin>, default 2;
+  // "off": the previous count + 4; read per solve, A/B). tools/chunk_sim.py on recorded counts: 89 -> 55 drained
+  // launches per frame at the same number of top-ups.
+  const char* re = getenv("OFX_PCG_RATIO");
+  const bool ratio_on = !(re && strcmp(re, "off") == 0);
+  const int ratio_margin = (re && ratio_on) ? atoi(re) : 2;
+  if (ratio_on && hk > 0 && lp > 0 && ph.n[0] >= 2) {
+    const int c0 = ph.c[0][(ph.n[0] - 1) & 3], c0p = ph.c[0][(ph.n[0] - 2) & 3];
+    if (c0 > 0 && c0p > 0) {
+      const double ratio = std::min(2.0, std::max(0.5, (double)c0 / (double)c0p));
+      chunk = std::max(4, (int)std::lround(lp * ratio) + ratio_margin);
+    }
+  }
   int it = 0;
   while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;

@@ -34,17 +34,22 @@ def main():
     counts = json.load(open(sys.argv[1]))["counts"]
     print(f"{len(counts)} frames, {np.mean([sum(c) for c in counts]):.1f} iterations per frame")
     prev = lambda f, k, C: C[f - 1][k]
-    replay(counts, lambda f, k, C: prev(f, k, C) + 4, name="product: previous frame's count + 4")
+    replay(counts, lambda f, k, C: prev(f, k, C) + 4, name="rounds 1-3: previous frame's count + 4")
     for m in (0, 2):
         replay(counts, lambda f, k, C, m=m: prev(f, k, C) + m, name=f"previous + {m}")
 
-    def ratio(f, k, C, m=0):
+    # the product rule since round 4 (gn.hip gn_pcg, OFX_PCG_RATIO): step 0 keeps previous + 4, later steps scale the
+    # previous frame's count by this frame's step-0 ratio (clamped to [0.5, 2]) + m
+    def ratio(f, k, C, m=0, upto=lambda k: 1):
         if k == 0:
-            return C[f - 1][0] + m
-        r = C[f][0] / max(1, C[f - 1][0])
+            return C[f - 1][0] + 4
+        j = upto(k)
+        r = min(2.0, max(0.5, sum(C[f][:j]) / max(1, sum(C[f - 1][:j]))))
         return int(round(C[f - 1][k] * r)) + m
     for m in (0, 2, 4):
-        replay(counts, lambda f, k, C, m=m: ratio(f, k, C, m), name=f"ratio of step 0 + {m}")
+        replay(counts, lambda f, k, C, m=m: ratio(f, k, C, m), name=f"product: ratio of step 0 + {m}")
+        replay(counts, lambda f, k, C, m=m: ratio(f, k, C, m, upto=lambda k: k),
+               name=f"ratio of steps 0..k-1 (cumulative) + {m}")
 
     def minlast(f, k, C, w=3, m=0):
         return min(C[g][k] for g in range(max(0, f - w), f)) + m

@@ -113,8 +113,10 @@ struct GnDev {
   double *st = nullptr;          // PCG recurrence state, 6N records of 8 (see the PCG layout note)
   double *m0 = nullptr, *m1 = nullptr;   // double-buffered m = M⁻¹w (gathered by the SpMV)
   double *pcg_alpha = nullptr, *pcg_gamma = nullptr;   // [-, -, 1/x of parity 0, 1] (+ alpha: [4 + par] = thr)
+  // pcg_alpha, pcg_gamma, scal, sturm and flags live in ONE allocation at fixed offsets (kSc*), so the PCG iteration
+  // reaches all of them through one preloaded pointer argument (no kernel-argument fetch ahead of their loads)
+  double* pcs = nullptr;
   double2* sturm = nullptr;       // error-based PCG stop (k_pcg_iter): 64 shifted LDLᵀ pivots + counts
-  int64_t pcg_cap = 0;
   double *part_p = nullptr, *part_b = nullptr, *part_loss = nullptr;
   int32_t nwg_row = 0, nwg_node = 0, nwg_terms = 0;   // nwg_row: PCG row waves (= workgroups)
   int32_t nw_pad = 0;            // stride of the iteration partial streams: 128·pcg_ku, zero beyond nwg_row
@@ -188,6 +190,10 @@ struct Gn : GnDev {
   hipEvent_t ev_side = nullptr;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   int32_t ep_next = 1;
+  // the PCG iteration's constant launch arguments (struct PcgIt) in device memory, and the bytes last copied there
+  void* d_pcgit = nullptr;
+  alignas(16) unsigned char pcgit_last[512] = {};
+  bool pcgit_valid = false;
 #ifdef OFX_STAMPS   // tuning build: stream idle between a PCG chunk's last launch and the next GN step's first kernel
   std::chrono::steady_clock::time_point t_seen{};   // host saw the step's convergence
   double react_us = 0.0, prologue_us = 0.0;         // -> k_terms enqueued; -> the first PCG chunk launch enqueued
@@ -229,6 +235,10 @@ __device__ __forceinline__ void host_flag(const int32_t* hf, int k, int v) {
 }
 constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 constexpr int32_t kEpochWrap = 1 << 30;   // GnDev::ep restarts at 1 from a setup once it reaches this (a solve adds <= 64)
+
+// the scalar block (GnDev::pcs), in doubles: pcg_alpha [0, 6), pcg_gamma [6, 12), scal [12, 16), sturm (64 double2)
+// [16, 144), flags (int32) from 144, the PCG operator's address (written by k_pcg_w0 per solve) at 150
+constexpr int kScAlpha = 0, kScGamma = 6, kScScal = 12, kScSturm = 16, kScFlags = 144, kScAop = 150, kScSize = 152;
 
 // ---------------------------------------------------------------------------- reductions
 template <int CTL>
@@ -444,10 +454,17 @@ __global__ __launch_bounds__(256) void k_row_count(int N, const int32_t* __restr
   if (threadIdx.x == 0) cnt[i] = s[0];
 }
 
-// Per PCG wave (kCS consecutive rows = one contiguous CSR range) the (col, slot) of its first kWL
-// blocks, so the iteration reads its gather addresses without the row_ptr -> col chain
+// Per PCG wave (kCS consecutive rows = one contiguous CSR range) its first kWL blocks: the block's column (-1: none)
+// and, packed, the wave's first CSR block (19 bits; block k of the wave is that + k), the first block of lane k % 64's
+// row relative to it (8 bits) and the row's length (5 bits) — so the iteration reads its gather addresses without the
+// row_ptr -> col chain and needs no row_ptr (the packing holds whenever the wave-list forms run: <= kWL blocks per wave,
+// <= kRowMax per row, nnzb <= 16·rows < 2^19)
 constexpr int kWL = 128;
 constexpr int kRowMax = 20;   // longest block row of the wave-list SpMV forms (k_pcg_iter, k_pcg_w0)
+static_assert(kRowMax < 32 && kWL <= 255 && 16 * (2 * kMaxNodes + 8) < (1 << 19), "wave-list packing");
+__device__ __forceinline__ int wl_base(int2 e) { return e.y & 0x7FFFF; }
+__device__ __forceinline__ int wl_rel(int2 e) { return (e.y >> 19) & 0xFF; }
+__device__ __forceinline__ int wl_len(int2 e) { return (int)((uint32_t)e.y >> 27); }
 __global__ __launch_bounds__(256) void k_wave_max(int nwave, const int32_t* __restrict__ row_ptr, int32_t* __restrict__ out) {
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w < nwave) atomicMax(out, row_ptr[(w + 1) * kCS] - row_ptr[w * kCS]);
@@ -456,8 +473,12 @@ __global__ __launch_bounds__(256) void k_wave_list(GnDev g) {
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e >= (int64_t)(g.N / kCS) * kWL) return;
   const int w = (int)(e / kWL), k = (int)(e % kWL);
-  const int b = g.row_ptr[w * kCS] + k;
-  g.wl[e] = b < g.row_ptr[(w + 1) * kCS] ? make_int2(g.col[b], b) : make_int2(-1, 0);
+  const int wb = g.row_ptr[w * kCS], b = wb + k;
+  const int row = w * kCS + (k % 64) / (64 / kCS);
+  // (clamped: a wave or row too long for the wave-list forms is never run through them)
+  const uint32_t rel = (uint32_t)min(g.row_ptr[row] - wb, 0xFF), len = (uint32_t)min(g.row_ptr[row + 1] - g.row_ptr[row], 31);
+  const uint32_t y = ((uint32_t)wb & 0x7FFFFu) | (rel << 19) | (len << 27);
+  g.wl[e] = make_int2(b < g.row_ptr[(w + 1) * kCS] ? g.col[b] : -1, (int)y);
 }
 
 // exclusive scan of cnt[0..n) into off[0..n] (off[n] = total), single workgroup: contiguous chunk
@@ -698,7 +719,13 @@ __device__ __forceinline__ void anchor_term(const GnDev& g, int64_t m, int k, do
 // share (data matches outside [m0,m1), regularisers when !add_reg) get all-zero records (exact zero
 // blocks) so the fixed contribution lists stay valid.
 __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, int m1, int add_reg) {
-  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // every kernel-argument field in SGPRs up front, in one scalar trip (left to the compiler, each branch loaded its own
+  // fields after the branch: four dependent scalar trips ahead of the first vector load)
+  asm volatile("" :: "s"(g.J), "s"(g.anc), "s"(g.wts), "s"(g.R), "s"(g.nodes), "s"(g.src), "s"(g.t), "s"(g.tgt),
+               "s"(g.tpx), "s"(g.tpy), "s"(g.edges), "s"(g.ew), "s"(g.res), "s"(g.T), "s"(g.M), "s"(g.N), "s"(g.NB),
+               "s"(g.conf), "s"(g.tpos), "s"(g.prm.mode), "s"(g.part_loss), "s"(m0), "s"(m1), "s"(add_reg));
+  asm volatile("" :: "s"(dc.lf), "s"(dc.ld), "s"(dc.la), "s"(dc.lm), "s"(dc.fx), "s"(dc.fy), "s"(dc.cx), "s"(dc.cy));
+  const int64_t id = blockIdx.x * (int64_t)kBlk + threadIdx.x;
   const int64_t t = id >> 2;
   const int k = (int)(id & 3);
   double r[3] = {0.0, 0.0, 0.0};
@@ -965,8 +992,13 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
 // JᵀJ blocks and -Jᵀr in one launch: the rhs workgroups first (their per-node loops are the longest
 // chains), then nwb workgroups of blocks.
 __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(4))) void k_assemble(GnDev g, DataCoef dc, double* __restrict__ A, double* __restrict__ rhs,
-                                                  int nwb, double lm) {
-  const int nrw = (int)gridDim.x - nwb;
+                                                  int nrw, double lm) {
+  // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms; nrw, the rhs workgroup count, is an
+  // argument rather than gridDim.x - nwb: the grid size is one more scalar load)
+  asm volatile("" :: "s"(g.N), "s"(g.M), "s"(g.NB), "s"(g.node_list), "s"(g.node_off), "s"(g.nwg_terms),
+               "s"(g.part_loss), "s"(g.res), "s"(g.J), "s"(g.blk_list), "s"(g.blk_off), "s"(g.nnzb), "s"(g.up_slot),
+               "s"(g.up_tr), "s"(A), "s"(rhs), "s"(nrw), "s"(lm));
+  asm volatile("" :: "s"(dc.lf), "s"(dc.ld), "s"(dc.la), "s"(dc.lm), "s"(dc.fx), "s"(dc.fy), "s"(dc.cx), "s"(dc.cy));
   if ((int)blockIdx.x < nrw) rhs_body(g, dc, rhs, blockIdx.x);
   else blocks_coop(g, dc, A, blockIdx.x - nrw, lm);
 }
@@ -1337,6 +1369,9 @@ __device__ __forceinline__ void proj_accumulate(const double bk[36], const doubl
 // its blocks in CSR order. (The row form's first trip is row_ptr, then col, then blocks + gathers.)
 template <bool kWave>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs) {
+  // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
+  asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.col), "s"(g.xh), "s"(g.th), "s"(g.N), "s"(g.flags), "s"(g.n_prev),
+               "s"(g.Aop), "s"(g.part_p), "s"(g.nw_pad), "s"(rhs));
   if constexpr (kWave) {
     __shared__ double s_prod[kProj][(kWL + kRowMax) * 6];
     const int lane = threadIdx.x;
@@ -1366,7 +1401,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       for (int h = 0; h < kProj; ++h)
 #pragma unroll
         for (int k = 0; k < 3; ++k) xb[jj][h][k] = reinterpret_cast<const double2*>(g.xh + h * stride + cc)[k];
-      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)bl[jj].y);
+      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)(bl[jj].x >= 0 ? wl_base(bl[jj]) + 64 * jj + lane : 0));
 #pragma unroll
       for (int k = 0; k < 18; ++k) ab[jj][k] = blk[k];
     }
@@ -1520,6 +1555,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 template <int KU>
 __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) {   // (not __restrict__: see k_pcg_w0)
   __shared__ __attribute__((aligned(16))) double s_v[kCD];
+  // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
+  asm volatile("" :: "s"(g.n_prev), "s"(g.N), "s"(g.Mcl), "s"(g.xh), "s"(g.th), "s"(g.part_p), "s"(g.nw_pad),
+               "s"(g.flags), "s"(g.stopw), "s"(g.ep), "s"(g.st), "s"(g.m1), "s"(rhs));
   const int lane = threadIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
   const int np = g.n_prev;
@@ -1616,6 +1654,9 @@ template <bool kWave>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_w0(GnDev g, const double* rhs) {   // (rhs not __restrict__: a restrict load sinks past the exit test)
   __shared__ __attribute__((aligned(16))) double s_v[kCD];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
+  // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
+  asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.Mcl), "s"(g.st), "s"(g.flags), "s"(g.m0), "s"(g.m1), "s"(g.Aop),
+               "s"(g.part_p), "s"(g.part_b), "s"(g.nw_pad), "s"(g.nwg_row), "s"(g.ep), "s"(g.stopw), "s"(g.pcs), "s"(rhs));
   const int lane = threadIdx.x;
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
@@ -1636,17 +1677,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const double w_old = v[V_W];   // unused, but kept live to the end (see the end of the kernel)
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");
-  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
-    g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
-    return;
-  }
+  // this solve's stop words: the epoch if the solve already stopped (its iteration launches end after trip 1), else 0
+  // (a converging iteration sets them to the epoch), so the iteration's stop test needs no epoch; and the operator's
+  // address into the scalar block, where the iteration finds it through a preloaded pointer
+  g.stopw[(int64_t)blockIdx.x * 64 + lane] = stopped ? g.ep : 0;
+  if (blockIdx.x == 0 && lane == 0) reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(g.Aop);
+  if (stopped) return;
   const double b = own ? bo : 0.0;
   double w;
   if (kWave) {
     double2 ab[2][18], xb[2][3];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked below)
-      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)bl[j].y);
+      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)(bl[j].x >= 0 ? wl_base(bl[j]) + 64 * j + lane : 0));
       const double2* vc = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)(bl[j].x >= 0 ? bl[j].x : 0));
 #pragma unroll
       for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
@@ -1751,6 +1794,7 @@ struct PcgIt {
 };
 static PcgIt pcg_args(const Gn* g) {
   PcgIt a;
+  memset(&a, 0, sizeof(a));   // (padding too: the host compares copies bytewise)
   a.Aop = g->Aop; a.Mcl = g->Mcl; a.row_ptr = g->row_ptr; a.col = g->col; a.wl = g->wl;
   a.m0 = g->m0; a.m1 = g->m1; a.st = g->st; a.part_p = g->part_p; a.part_b = g->part_b;
   a.pcg_alpha = g->pcg_alpha; a.pcg_gamma = g->pcg_gamma; a.scal = g->scal;
@@ -1784,10 +1828,10 @@ __device__ __forceinline__ void kornia_exp(const double x[3], double Ri[9]) {
     Ri[0] = 1; Ri[1] = -a2; Ri[2] = a1; Ri[3] = a2; Ri[4] = 1; Ri[5] = -a0; Ri[6] = -a1; Ri[7] = a0; Ri[8] = 1;
   }
 }
-__device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int r, int q, bool own, int64_t o,
+__device__ __forceinline__ void fused_step(const PcgIt& g, int ep, int gn_iter, int wv, int lane, int r, int q, bool own, int64_t o,
                                            int row, double xv, bool ill, int cnt, double bb) {
   const StepArgs& sa = *g.sa;
-  const int gi = g.gn_iter;
+  const int gi = gn_iter;
   const double* tail = g.tail;
   const double loss = sqrt(tail[0] + tail[1] + tail[2]);
   const double prev = sa.step_state[2 * gi];
@@ -1802,7 +1846,7 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
     g.flags[F_RES_NONFINITE] = tail[3] != 0.0 ? 1 : 0;
     if (stop) {
       g.flags[F_STOPPED] = 1;
-      host_flag(g.hflags, H_STOPPED, g.ep);
+      host_flag(g.hflags, H_STOPPED, ep);
     } else {
       if (acc < g.n_iter_log) {
         sa.loss_log[4 * acc + 0] = loss;
@@ -1853,10 +1897,14 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int wv, int lane, int
 // wave launch (-amdgpu-kernarg-preload-count, build.py), so the first loads issue without waiting for a kernarg fetch
 // (tools/preload_micro.hip: 3.15 -> 2.88 us per dependent launch); a struct argument is never preloaded. mc / Pc are the
 // parity's m and partial streams.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kSc = true>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(
     const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const float* Mcl,
-    const int32_t* row_ptr, PcgIt g, int par) {   // (not __restrict__: a restrict load sinks past the exit test)
+    const double* sc, const PcgIt* __restrict__ gp, int par, int ep, int gn_iter) {   // (not __restrict__: a restrict load sinks past the exit test)
+  // the launch's constant arguments live in device memory (one copy per handle, rewritten when they change): a ~76-B
+  // kernel argument instead of ~290 B, which the host enqueues ~1 us faster per launch on some boxes
+  // (tools/enqueue_micro.hip); the solve's epoch and GN step come by value
+  const PcgIt& g = *gp;   // (read where used: a copy here made the compiler load it all ahead of trip 1)
   constexpr int kNH = kW2 ? 2 : 1;
   __shared__ __attribute__((aligned(16))) double s_v[kNH][kCD];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
@@ -1868,55 +1916,86 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #ifdef OFX_STAMPS
   const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
+  // the operator's address first (kSc: k_pcg_w0 wrote it into the scalar block; a vector load, retired by the time
+  // the stop word is, then made scalar), then the list and the stop word
+  uint2 aop_v = make_uint2(0, 0);
+  if (kSc) aop_v = reinterpret_cast<const uint2*>(sc)[kScAop];
   int2 bl0 = make_int2(-1, 0), bl1 = make_int2(-1, 0);
   if (kWave) {
     bl0 = wl[(int64_t)wv * kWL + 64 * hw + lane];
     if (!kW2) bl1 = wl[(int64_t)wv * kWL + 64 + lane];
   }
   int stop_ep = stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
-  // kernarg-derived scalars pass through an opaque copy ordered after these two loads (memory clobber): otherwise the
-  // compiler schedules an early use of them and with it a kernarg wait ahead of the list and stop-word loads
-  __builtin_amdgcn_sched_barrier(0);
-  int ns = g.nw_pad, par_ = par;
-  asm volatile("" : "+s"(ns), "+s"(par_) :: "memory");
+  asm volatile("" ::: "memory");   // the list and stop word leave first
+  // The rest of trip 1 needs no kernel-argument fetch either, so it leaves right behind them: the partial streams'
+  // stride is 128·kU (= nw_pad), the step scalars come from the scalar block sc (both parities, selected once par has
+  // arrived), the inverse row, state and m through their own pointers. Consumption order (loads retire in issue
+  // order): the partials and scalars for the step scalars, then the own state and m for the recurrences, the inverse
+  // row last (the M⁻¹ apply).
+  constexpr int kNs = 128 * kU;
+  // kernel-argument values (one scalar trip), pinned with the A pointer and the tolerances (left to the compiler, those
+  // were loaded after the exit test: trip 2's block loads waited for a second scalar trip). The A pointer goes through
+  // the asm as an integer and comes back as a global-address-space pointer (an opaque generic pointer would be loaded
+  // through with flat loads, which the compiler waits for with vmcnt(0)). kSc: after trip 1's issue (under its flight);
+  // !kSc (A/B: the round-4 form): before the rest of trip 1, whose addresses then come from the kernel arguments.
+  int ns = 0, par_ = 0;
+  uint64_t aop_bits = 0;
+  double tol_s = 0.0, etol_s = 0.0;
+  auto pin = [&](int) {
+    __builtin_amdgcn_sched_barrier(0);
+    ns = g.nw_pad; par_ = par;
+    if (!kSc) aop_bits = reinterpret_cast<uint64_t>(g.Aop);
+    tol_s = g.prm.pcg_tol; etol_s = g.prm.pcg_err_tol;
+    asm volatile("" : "+s"(ns), "+s"(par_), "+s"(aop_bits), "+s"(tol_s), "+s"(etol_s) :: "memory");
+  };
+  if (!kSc) pin(0);
+  const int64_t sstr = kSc ? (int64_t)kNs : (int64_t)ns;
+  const double* scx = kSc ? sc : g.pcg_alpha;   // (pcg_alpha is the scalar block's start)
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
-  const int nw = g.nwg_row;
-  double* __restrict__ mn = par_ ? g.m0 : g.m1;
-  double* Pn = g.part_p + 3 * (int64_t)ns * (par_ ^ 1);
   const bool own = q < 6;
   const int qc = own ? q : 5;
   const int64_t o = 6 * (int64_t)row + qc;
-  const int wb0 = row_ptr[wv * kRW];
-  const int b0 = row_ptr[row], b1 = row_ptr[row + 1];
-  const float4* Mw = reinterpret_cast<const float4*>(Mcl + (int64_t)wv * kCD * kCD);
-  asm volatile("" ::: "memory");   // the list and stop word leave first
-  constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
-  double2 ab[kNB][18], xb[kNB][3];
-  constexpr int kMR = kCD / 4 / kNH;   // the lane's inverse row: float4 column groups of its wave's half
-  float4 mreg[kMR];
-#pragma unroll
-  for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
-  double v[V_N];
-  load_rec(st, o, v);
-  const double m = mc[o];
   double2 tp[3][kU];              // the streams are zero beyond nw up to ns = 128·kU: no masks
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int u = 0; u < kU; ++u) tp[k][u] = *reinterpret_cast<const double2*>(Pc + (int64_t)k * ns + 2 * (lane + 64 * u));
-  double tb[kFirst ? 2 * kU : 1];
-  if (kFirst)
-#pragma unroll
-    for (int u = 0; u < 2 * kU; ++u) tb[u] = g.part_b[lane + 64 * u];
+    for (int u = 0; u < kU; ++u) tp[k][u] = *reinterpret_cast<const double2*>(Pc + k * sstr + 2 * (lane + 64 * u));
   double own_p[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * ns + wv];
-  const int cnt = g.flags[F_PCG_CNT];
-  const double rgam_prev = kFirst ? 1.0 : g.pcg_gamma[2 + (par_ ^ 1)];     // 1/γ, 1/α of the previous iteration
-  const double ralpha_prev = kFirst ? 1.0 : g.pcg_alpha[2 + (par_ ^ 1)];
-  const double thr_prev = kFirst ? 0.0 : g.pcg_alpha[4 + (par_ ^ 1)];       // error-based stop: bound on γ (below)
-  const double2 sd = g.sturm[lane];   // (every wave loads it: no load behind a branch; the lead wave uses it)
-  const double bb_stored = g.scal[S_BB];
+  for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * sstr + wv];
+  const int cnt = reinterpret_cast<const int32_t*>(scx + kScFlags)[F_PCG_CNT];
+  const double2 ra = *reinterpret_cast<const double2*>(scx + kScAlpha + 2);   // 1/α of parities 0, 1
+  const double2 rt = *reinterpret_cast<const double2*>(scx + kScAlpha + 4);   // the error-stop bound of parities 0, 1
+  const double2 rg = *reinterpret_cast<const double2*>(scx + kScGamma + 2);   // 1/γ of parities 0, 1
+  const double2 sd = reinterpret_cast<const double2*>(scx + kScSturm)[lane];   // (every wave loads it: the lead uses it)
+  const double bb_stored = scx[kScScal + S_BB];
+  asm volatile("" ::: "memory");
+  constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
+  double2 ab[kNB][18], xb[kNB][3];
+  constexpr int kMR = kCD / 4 / kNH;   // the lane's inverse row: float4 column groups of its wave's half
+  float4 mreg[kMR];
+  double v[V_N];
+  load_rec(st, o, v);
+  const double m = mc[o];
+  asm volatile("" ::: "memory");
+  const float4* Mw = reinterpret_cast<const float4*>(Mcl + (int64_t)wv * kCD * kCD);
+#pragma unroll
+  for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
+  const int nw = g.nwg_row;   // (tuning builds' stamps only)
+  // the rows' bounds: packed in the wave list, or (CSR form) from row_ptr
+  int wb0 = 0, b0 = 0, b1 = 0;
+  if (kWave) {
+    wb0 = wl_base(bl0);
+    b0 = wb0 + wl_rel(bl0);
+    b1 = b0 + wl_len(bl0);
+  } else {
+    b0 = g.row_ptr[row];
+    b1 = g.row_ptr[row + 1];
+  }
+  // the operator (kSc: from the scalar block, made scalar; !kSc: pinned above with the kernel arguments)
+  if (kSc) aop_bits = ((uint64_t)__builtin_amdgcn_readfirstlane(aop_v.y) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(aop_v.x);
+  const __attribute__((address_space(1))) double* Aop =
+      reinterpret_cast<const __attribute__((address_space(1))) double*>(aop_bits);
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
@@ -1924,7 +2003,9 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // as wave-uniform values the exits are scalar branches, so the main path's waits are not merged with the exit paths'
   // (a divergent exit left a vmcnt(0) at the join in front of the products)
   stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
-  if (stop_ep >= g.ep) return;     // this solve has converged (or stopped): a drained launch
+  // this solve has converged (or stopped): a drained launch. (k_pcg_w0 reset the stop words to 0 for this solve; the
+  // epoch comparison of the !kSc form needs the kernel arguments first.)
+  if (kSc ? stop_ep != 0 : stop_ep >= ep) return;
 #ifdef OFX_STAMPS
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
 #endif
@@ -1934,16 +2015,29 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int j = 0; j < kNB; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked later)
       const int2 e = j ? bl1 : bl0;
-      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)e.y);
+      typedef double gd2 __attribute__((ext_vector_type(2)));   // (a plain vector type: loads through address space 1)
+      const __attribute__((address_space(1))) gd2* blk = reinterpret_cast<const __attribute__((address_space(1))) gd2*>(
+          Aop + 36 * (int64_t)(e.x >= 0 ? wb0 + (kW2 ? 64 * hw + lane : 64 * j + lane) : 0));
       const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
       // the gathered m row first: the products of the first block rows start before the block's tail lands
 #pragma unroll
       for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
       asm volatile("" ::: "memory");
 #pragma unroll
-      for (int k = 0; k < 18; ++k) ab[j][k] = blk[k];
+      for (int k = 0; k < 18; ++k) { const gd2 t = blk[k]; ab[j][k] = make_double2(t.x, t.y); }
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
+  __builtin_amdgcn_sched_barrier(0);   // ... and no scalar arithmetic above its issue (it would wait for the partials)
+  if (kSc) pin(0);
+  double* __restrict__ mn = par_ ? g.m0 : g.m1;
+  double* Pn = g.part_p + 3 * (int64_t)ns * (par_ ^ 1);
+  double tb[kFirst ? 2 * kU : 1];   // the first iteration's |b|² partials (kernel-argument pointer: once per solve)
+  if (kFirst)
+#pragma unroll
+    for (int u = 0; u < 2 * kU; ++u) tb[u] = g.part_b[lane + 64 * u];
+  const double rgam_prev = kFirst ? 1.0 : ((par_ ^ 1) ? rg.y : rg.x);     // 1/γ, 1/α of the previous iteration
+  const double ralpha_prev = kFirst ? 1.0 : ((par_ ^ 1) ? ra.y : ra.x);
+  const double thr_prev = kFirst ? 0.0 : ((par_ ^ 1) ? rt.y : rt.x);       // error-based stop: bound on γ (below)
   // ---- scalars from the partials (trip-1 data)
   double pa[3];
 #pragma unroll
@@ -1961,7 +2055,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     bb = wave_sum(t);
   }
   const double gam = pa[0], del = pa[1], rr = pa[2];
-  const double tol = g.prm.pcg_tol;
+  const double tol = tol_s;
   const bool lead = wv == 0 && lane == 0 && hw == 0;
   const bool w0 = hw == 0;   // the wave that stores (kW2: both compute the same bits)
   double beta = 0.0, alpha;
@@ -1975,7 +2069,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // the relative residual at the f64 floor (1e-12). γ = rᵀM⁻¹r = ‖z‖²_M (z = M⁻¹r), so the error e = (M⁻¹A)⁻¹z has
   // ‖e‖_M <= √γ / λ_min(M⁻¹A); θ̂ is the previous iteration's estimate of λ_min(M⁻¹A) from below, kept by the lead
   // wave (sturm_step). The residual alone cannot see the error of an ill-conditioned system (real data: DESIGN §6).
-  const double etol = g.prm.pcg_err_tol;
+  const double etol = etol_s;
   const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam <= thr_prev)) || gam == 0.0 || rr <= 1e-24 * bb;
   int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
   leave = __builtin_amdgcn_readfirstlane(leave);
@@ -1983,14 +2077,14 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     if (kFirst && lead) g.scal[S_BB] = bb;
     if (!w0) return;
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
-    g.stopw[(int64_t)wv * 64 + lane] = g.ep;
+    g.stopw[(int64_t)wv * 64 + lane] = ep;
     const bool ill = !conv && !isfinite(alpha);
-    if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
+    if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, ep, gn_iter, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
     if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
       g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
       if (ill) g.flags[F_ILL] = 1;
       host_flag(g.hflags, H_PCG_IT, cnt);
-      __hip_atomic_store(g.hflags + H_DONE, g.ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
+      __hip_atomic_store(g.hflags + H_DONE, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // after the count
     }
     return;
   }
@@ -2251,8 +2345,8 @@ static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->stopw, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
-                  g->st, g->m0, g->m1, g->pcg_alpha, g->pcg_gamma, g->sturm,
-                  g->part_p, g->part_b, g->part_loss, g->scal, g->flags,
+                  g->st, g->m0, g->m1, g->pcs,
+                  g->part_p, g->part_b, g->part_loss,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
                   g->up_of, g->up_slot, g->up_tr};
   for (void* p : ptrs)
@@ -2260,6 +2354,7 @@ static void free_all(Gn* g) {
   if (g->host_flags) (void)hipHostFree(g->host_flags);
   if (g->setup_stat) (void)hipHostFree(g->setup_stat);
   if (g->poll_ev) (void)hipEventDestroy(g->poll_ev);
+  if (g->d_pcgit) (void)hipFree(g->d_pcgit);
 }
 
 // Row order for the cluster preconditioner (host, from the ED graph). Clusters: the lowest
@@ -2340,13 +2435,15 @@ static int pcg_ku_for(int waves) {
 }
 
 using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const float*,
-                          const int32_t*, PcgIt, int);
+                          const double*, const PcgIt*, int, int, int);
 template <int KU>
 static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU <= 3) {
     if (wave && w2) {
-      first = k_pcg_iter<true, true, KU, true>;
-      rest = k_pcg_iter<true, false, KU, true>;
+      const char* e = getenv("OFX_PCG_SC");   // A/B only (read per solve): 0 = the round-4 kernel-argument form
+      const bool sc = !(e && atoi(e) == 0);
+      first = sc ? k_pcg_iter<true, true, KU, true> : k_pcg_iter<true, true, KU, true, false>;
+      rest = sc ? k_pcg_iter<true, false, KU, true> : k_pcg_iter<true, false, KU, true, false>;
       return;
     }
   }
@@ -2433,8 +2530,16 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   PcgIt pa = pcg_args(g);
   // the converging launch also takes the GN step (not when arap's null-space projection must run first)
   pa.fuse = g->n_comp == 0 ? 1 : 0;
-  pa.gn_iter = gn_iter;
   pa.tail = rhs + 6 * (int64_t)g->N;
+  pa.ep = 0;   // (the epoch and the GN step go by value with each launch)
+  // the device copy of the constant arguments: rewritten only when they change (a setup, another A / rhs)
+  static_assert(sizeof(PcgIt) <= sizeof(g->pcgit_last), "PcgIt staging");
+  if (!g->pcgit_valid || memcmp(&pa, g->pcgit_last, sizeof(PcgIt)) != 0) {
+    OFX_HIP(hipMemcpyAsync(g->d_pcgit, &pa, sizeof(PcgIt), hipMemcpyHostToDevice, hs));   // (pageable: staged at the call)
+    memcpy(g->pcgit_last, &pa, sizeof(PcgIt));
+    g->pcgit_valid = true;
+  }
+  const PcgIt* gp = static_cast<const PcgIt*>(g->d_pcgit);
   g->step_fused = false;
   int chunk = lp > 0 ? lp + 4 : 64;
   // Later GN steps: the previous frame's count for this step scaled by how this frame's step 0 compared with the
@@ -2463,7 +2568,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       const int par = it & 1;
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, (const int2*)g->wl, (const int32_t*)g->stopw,
                          (const double*)(g->part_p + 3 * (int64_t)g->nw_pad * par), (const double*)g->st,
-                         (const double*)(par ? g->m1 : g->m0), (const float*)g->Mcl, (const int32_t*)g->row_ptr, pa, par);
+                         (const double*)(par ? g->m1 : g->m0), (const float*)g->Mcl, (const double*)g->pcs, gp, par, g->ep,
+                         gn_iter);
     }
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
@@ -2619,10 +2725,16 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   static_assert(kProjP >= 6, "part_p: kProjP projection streams / 6 iteration streams, stride nw_pad");
   (void)max_row_wg;
   ALLOC(g->part_p, kProjP * max_ns); ALLOC(g->part_b, max_ns);
-  ALLOC(g->sturm, 64);
-  ALLOC(g->scal, S_COUNT); ALLOC(g->flags, F_COUNT);
+  static_assert(S_COUNT <= kScSturm - kScScal && 2 * kScFlags + F_COUNT <= 2 * kScAop && kScAop < kScSize,
+                "scalar block layout");
+  ALLOC(g->pcs, kScSize);
+  g->pcg_alpha = g->pcs + kScAlpha; g->pcg_gamma = g->pcs + kScGamma; g->scal = g->pcs + kScScal;
+  g->sturm = reinterpret_cast<double2*>(g->pcs + kScSturm); g->flags = reinterpret_cast<int32_t*>(g->pcs + kScFlags);
   ALLOC(g->loss_log, 4 * 64); ALLOC(g->stat, 3 * kMaxLog); ALLOC(g->step_state, 2 * (kMaxLog + 1)); ALLOC(g->rhs_own, 6 * N + 4);
 #undef ALLOC
+  if (hipMalloc(&g->d_pcgit, sizeof(g->pcgit_last)) != hipSuccess) {
+    free_all(g); delete g; set_error("hipMalloc failed"); return OFX_ERR_ALLOC;
+  }
   if (hipMemset(g->map, 0, (size_t)N * N * sizeof(int32_t)) != hipSuccess ||   // pattern entries are cleared per setup
       hipMemset(g->stopw, 0, (size_t)(N / kCS) * 64 * sizeof(int32_t)) != hipSuccess) {   // epoch 0: none converged
     free_all(g); delete g; set_error("hipMemset failed"); return OFX_ERR_HIP;
@@ -2994,13 +3106,6 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->N = N; g->N_real = N0; g->M = M; g->NB = NB; g->prm = *prm;
   g->fx = pb->fx; g->fy = pb->fy; g->cx = pb->cx; g->cy = pb->cy;
   g->T = (int64_t)M + (int64_t)N * NB + N;
-  if (6 > g->pcg_cap) {   // [-, -, 1/alpha | 1/gamma of both parities, thr of both parities (alpha only)]
-    if (g->pcg_alpha) OFX_HIP(hipFree(g->pcg_alpha));
-    if (g->pcg_gamma) OFX_HIP(hipFree(g->pcg_gamma));
-    g->pcg_cap = 6;
-    OFX_HIP(hipMalloc((void**)&g->pcg_alpha, g->pcg_cap * sizeof(double)));
-    OFX_HIP(hipMalloc((void**)&g->pcg_gamma, g->pcg_cap * sizeof(double)));
-  }
   g->nwg_row = N / kRW;
   g->pcg_ku = pcg_ku_for(g->nwg_row);
   g->nw_pad = 128 * g->pcg_ku;
@@ -3172,7 +3277,8 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, dc, A, lm);
   hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, rhs);
 #else
-  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, A, rhs, nwb, lm);
+  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, A, rhs,
+                     (int)grid_for(g->N, kBlk / 64), lm);
 #endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;

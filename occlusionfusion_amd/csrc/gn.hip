@@ -237,8 +237,12 @@ constexpr int kMaxLog = 64;   // per-GN-step statistics slots
 constexpr int32_t kEpochWrap = 1 << 30;   // GnDev::ep restarts at 1 from a setup once it reaches this (a solve adds <= 64)
 
 // the scalar block (GnDev::pcs), in doubles: pcg_alpha [0, 6), pcg_gamma [6, 12), scal [12, 16), sturm (64 double2)
-// [16, 144), flags (int32) from 144, the PCG operator's address (written by k_pcg_w0 per solve) at 150
-constexpr int kScAlpha = 0, kScGamma = 6, kScScal = 12, kScSturm = 16, kScFlags = 144, kScAop = 150, kScSize = 152;
+// [16, 144), flags (int32) from 144; written by k_pcg_w0 per solve: the PCG operator's address at 150, the stop tolerances
+// (pcg_tol, pcg_err_tol) at 152, 153, the cluster inverses' address at 154, m0 / m1's at 156 / 157. The iteration gets
+// the block's address with its parity in bit 3 (the block is 256-B aligned), so it needs no kernel-argument fetch for
+// any of them.
+constexpr int kScAlpha = 0, kScGamma = 6, kScScal = 12, kScSturm = 16, kScFlags = 144, kScAop = 150, kScTol = 152,
+              kScMcl = 154, kScM = 156, kScSize = 160;
 
 // ---------------------------------------------------------------------------- reductions
 template <int CTL>
@@ -1656,7 +1660,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
   asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.Mcl), "s"(g.st), "s"(g.flags), "s"(g.m0), "s"(g.m1), "s"(g.Aop),
-               "s"(g.part_p), "s"(g.part_b), "s"(g.nw_pad), "s"(g.nwg_row), "s"(g.ep), "s"(g.stopw), "s"(g.pcs), "s"(rhs));
+               "s"(g.part_p), "s"(g.part_b), "s"(g.nw_pad), "s"(g.nwg_row), "s"(g.ep), "s"(g.stopw), "s"(g.pcs), "s"(rhs),
+               "s"(g.prm.pcg_tol), "s"(g.prm.pcg_err_tol), "s"(g.Mcl));
   const int lane = threadIdx.x;
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
@@ -1681,7 +1686,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // (a converging iteration sets them to the epoch), so the iteration's stop test needs no epoch; and the operator's
   // address into the scalar block, where the iteration finds it through a preloaded pointer
   g.stopw[(int64_t)blockIdx.x * 64 + lane] = stopped ? g.ep : 0;
-  if (blockIdx.x == 0 && lane == 0) reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(g.Aop);
+  if (blockIdx.x == 0 && lane == 0) {
+    reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(g.Aop);
+    g.pcs[kScTol] = g.prm.pcg_tol;
+    g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
+    reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = reinterpret_cast<uint64_t>(g.Mcl);
+    reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
+    reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
+  }
   if (stopped) return;
   const double b = own ? bo : 0.0;
   double w;
@@ -1886,40 +1898,46 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int ep, int gn_iter, 
 // two), stages only its half of the inverse's column groups and applies that half (split-K); the scalar
 // work, row sums and recurrences run in both waves (identical bits), wave 0 alone stores. Two LDS barriers
 // (products, M⁻¹ halves), no memory release.
-// Trip 1 issues the wave list and the stop word first, and waits only for those two before the stop test and trip 2's
-// issue (the rest of trip 1 lands under trip 2's flight; the scalars and the M⁻¹ apply wait for their own loads, which
-// retire in issue order), instead of waiting for all of trip 1. The lane's row of the cluster inverse (its wave's
-// column half) comes to registers by plain loads (the wave's 48 row lanes read 768 contiguous bytes per column group):
-// a pending LDS-DMA would make the compiler wait for everything (vmcnt(0)) at the first use of any load. (Round 3's
-// OFX_PCG_EARLY levels 0 / 1 — the all-of-trip-1 wait with the inverse by LDS-DMA, the early issue alone — and round 4's
-// level 3 (batched LDS reads) and write-through stores lost their A/Bs and are gone: DESIGN §6.)
-// The first seven arguments are the pointers trip 1 loads through: scalar pointer arguments are preloaded into SGPRs at
-// wave launch (-amdgpu-kernarg-preload-count, build.py), so the first loads issue without waiting for a kernarg fetch
-// (tools/preload_micro.hip: 3.15 -> 2.88 us per dependent launch); a struct argument is never preloaded. mc / Pc are the
-// parity's m and partial streams.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kSc = true>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+// Trip 1 issues the wave list and the stop word first, and waits only for the stop word before the stop test and trip
+// 2's issue (the rest of trip 1 lands under trip 2's flight; the scalars and the M⁻¹ apply wait for their own loads,
+// which retire in issue order). The lane's row of the cluster inverse (its wave's column half) comes to registers by
+// plain loads (the wave's 48 row lanes read 768 contiguous bytes per column group): a pending LDS-DMA would make the
+// compiler wait for everything (vmcnt(0)) at the first use of any load. (Round 3's OFX_PCG_EARLY levels 0 / 1 — the
+// all-of-trip-1 wait with the inverse by LDS-DMA, the early issue alone — and round 4's level 3 (batched LDS reads) and
+// write-through stores lost their A/Bs and are gone: DESIGN §6.)
+// No kernel-argument fetch on the main path (late round 4): the first seven arguments are pointers, preloaded
+// into SGPRs at wave launch (-amdgpu-kernarg-preload-count, build.py; a struct argument is never preloaded); everything
+// else the iteration reads comes through them — the step scalars, tolerances and the operator / inverse / new-m addresses
+// from the scalar block sc (GnDev::pcs, k_pcg_w0 writes the addresses and tolerances per solve), whose address carries
+// the parity in bit 3; the rows' bounds from the wave list; the other parity's partial streams beside Pc. The stop words
+// are reset by k_pcg_w0 per solve, so the stop test needs no epoch. The rest of the launch's arguments (rare paths:
+// the converging launch's bookkeeping and fused GN step, the CSR form) live in device memory (gp, one copy per handle,
+// rewritten when they change): a 76-B kernel argument instead of ~290 B, which the host enqueues faster. In-process A/B
+// against the same kernel with its scalars and addresses through the kernel arguments: -0.27 / -0.28 ms per frame.
+// mc / Pc are the parity's m and partial streams.
+template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(
-    const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const float* Mcl,
-    const double* sc, const PcgIt* __restrict__ gp, int par, int ep, int gn_iter) {   // (not __restrict__: a restrict load sinks past the exit test)
-  // the launch's constant arguments live in device memory (one copy per handle, rewritten when they change): a ~76-B
-  // kernel argument instead of ~290 B, which the host enqueues ~1 us faster per launch on some boxes
-  // (tools/enqueue_micro.hip); the solve's epoch and GN step come by value
+    const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const double* sc,
+    const PcgIt* __restrict__ gp, int par, int ep, int gn_iter) {   // (not __restrict__: a restrict load sinks past the exit test)
   const PcgIt& g = *gp;   // (read where used: a copy here made the compiler load it all ahead of trip 1)
+  (void)par;              // (the parity comes with sc; par stays in the signature for tools and traces)
   constexpr int kNH = kW2 ? 2 : 1;
+  constexpr int kNs = 128 * kU;   // the partial streams' stride (= nw_pad)
   __shared__ __attribute__((aligned(16))) double s_v[kNH][kCD];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
   __shared__ double s_half[kW2 ? 64 : 1];
   const int lane = threadIdx.x & 63;
   const int hw = kW2 ? (int)(threadIdx.x >> 6) : 0;   // wave within the cluster's workgroup
   const int wv = blockIdx.x;
-  // ---- trip 1: the block list and the stop word leave first, through preloaded pointers only (no kernarg wait)
 #ifdef OFX_STAMPS
   const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
-  // the operator's address first (kSc: k_pcg_w0 wrote it into the scalar block; a vector load, retired by the time
-  // the stop word is, then made scalar), then the list and the stop word
-  uint2 aop_v = make_uint2(0, 0);
-  if (kSc) aop_v = reinterpret_cast<const uint2*>(sc)[kScAop];
+  // ---- trip 1. The scalar block's addresses first (uniform: scalar loads), then the list and the stop word
+  const int par_ = (int)((reinterpret_cast<uintptr_t>(sc) >> 3) & 1);
+  const double* scb = sc - par_;
+  const uint2 aop_v = reinterpret_cast<const uint2*>(scb)[kScAop];
+  const uint2 mcl_v = reinterpret_cast<const uint2*>(scb)[kScMcl];
+  const uint2 mn_v = reinterpret_cast<const uint2*>(scb)[kScM + (par_ ^ 1)];   // the new m: the other parity's buffer
   int2 bl0 = make_int2(-1, 0), bl1 = make_int2(-1, 0);
   if (kWave) {
     bl0 = wl[(int64_t)wv * kWL + 64 * hw + lane];
@@ -1927,48 +1945,27 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   }
   int stop_ep = stopw[(int64_t)wv * 64 + lane];   // vector load: retires with trip 1
   asm volatile("" ::: "memory");   // the list and stop word leave first
-  // The rest of trip 1 needs no kernel-argument fetch either, so it leaves right behind them: the partial streams'
-  // stride is 128·kU (= nw_pad), the step scalars come from the scalar block sc (both parities, selected once par has
-  // arrived), the inverse row, state and m through their own pointers. Consumption order (loads retire in issue
-  // order): the partials and scalars for the step scalars, then the own state and m for the recurrences, the inverse
-  // row last (the M⁻¹ apply).
-  constexpr int kNs = 128 * kU;
-  // kernel-argument values (one scalar trip), pinned with the A pointer and the tolerances (left to the compiler, those
-  // were loaded after the exit test: trip 2's block loads waited for a second scalar trip). The A pointer goes through
-  // the asm as an integer and comes back as a global-address-space pointer (an opaque generic pointer would be loaded
-  // through with flat loads, which the compiler waits for with vmcnt(0)). kSc: after trip 1's issue (under its flight);
-  // !kSc (A/B: the round-4 form): before the rest of trip 1, whose addresses then come from the kernel arguments.
-  int ns = 0, par_ = 0;
-  uint64_t aop_bits = 0;
-  double tol_s = 0.0, etol_s = 0.0;
-  auto pin = [&](int) {
-    __builtin_amdgcn_sched_barrier(0);
-    ns = g.nw_pad; par_ = par;
-    if (!kSc) aop_bits = reinterpret_cast<uint64_t>(g.Aop);
-    tol_s = g.prm.pcg_tol; etol_s = g.prm.pcg_err_tol;
-    asm volatile("" : "+s"(ns), "+s"(par_), "+s"(aop_bits), "+s"(tol_s), "+s"(etol_s) :: "memory");
-  };
-  if (!kSc) pin(0);
-  const int64_t sstr = kSc ? (int64_t)kNs : (int64_t)ns;
-  const double* scx = kSc ? sc : g.pcg_alpha;   // (pcg_alpha is the scalar block's start)
+  // the rest of trip 1 in consumption order (loads retire in issue order): the partials and scalars for the step
+  // scalars, then the own state and m for the recurrences, the inverse row last (the M⁻¹ apply)
   const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
   const bool own = q < 6;
   const int qc = own ? q : 5;
   const int64_t o = 6 * (int64_t)row + qc;
-  double2 tp[3][kU];              // the streams are zero beyond nw up to ns = 128·kU: no masks
+  double2 tp[3][kU];              // the streams are zero beyond nw up to 128·kU: no masks
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int u = 0; u < kU; ++u) tp[k][u] = *reinterpret_cast<const double2*>(Pc + k * sstr + 2 * (lane + 64 * u));
+    for (int u = 0; u < kU; ++u) tp[k][u] = *reinterpret_cast<const double2*>(Pc + k * kNs + 2 * (lane + 64 * u));
   double own_p[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * sstr + wv];
-  const int cnt = reinterpret_cast<const int32_t*>(scx + kScFlags)[F_PCG_CNT];
-  const double2 ra = *reinterpret_cast<const double2*>(scx + kScAlpha + 2);   // 1/α of parities 0, 1
-  const double2 rt = *reinterpret_cast<const double2*>(scx + kScAlpha + 4);   // the error-stop bound of parities 0, 1
-  const double2 rg = *reinterpret_cast<const double2*>(scx + kScGamma + 2);   // 1/γ of parities 0, 1
-  const double2 sd = reinterpret_cast<const double2*>(scx + kScSturm)[lane];   // (every wave loads it: the lead uses it)
-  const double bb_stored = scx[kScScal + S_BB];
+  for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * kNs + wv];
+  const int cnt = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
+  const double2 ra = *reinterpret_cast<const double2*>(scb + kScAlpha + 2);   // 1/α of parities 0, 1
+  const double2 rt = *reinterpret_cast<const double2*>(scb + kScAlpha + 4);   // the error-stop bound of parities 0, 1
+  const double2 rg = *reinterpret_cast<const double2*>(scb + kScGamma + 2);   // 1/γ of parities 0, 1
+  const double2 sd = reinterpret_cast<const double2*>(scb + kScSturm)[lane];   // (every wave loads it: the lead uses it)
+  const double bb_stored = scb[kScScal + S_BB];
+  const double2 tols = *reinterpret_cast<const double2*>(scb + kScTol);       // pcg_tol, pcg_err_tol
   asm volatile("" ::: "memory");
   constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
   double2 ab[kNB][18], xb[kNB][3];
@@ -1978,10 +1975,24 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   load_rec(st, o, v);
   const double m = mc[o];
   asm volatile("" ::: "memory");
-  const float4* Mw = reinterpret_cast<const float4*>(Mcl + (int64_t)wv * kCD * kCD);
+  // An address from the scalar block is made scalar and turned back into a global-address-space pointer (a generic
+  // pointer would be read with flat loads, which the compiler waits for with vmcnt(0)).
+  auto addr = [](uint2 v2) -> uint64_t {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane(v2.y) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(v2.x);
+  };
+  {
+    typedef float gf4 __attribute__((ext_vector_type(4)));
+    const __attribute__((address_space(1))) gf4* Mw =
+        reinterpret_cast<const __attribute__((address_space(1))) gf4*>(addr(mcl_v)) + (int64_t)wv * kCD * kCD / 4;
 #pragma unroll
-  for (int kk = 0; kk < kMR; ++kk) mreg[kk] = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
-  const int nw = g.nwg_row;   // (tuning builds' stamps only)
+    for (int kk = 0; kk < kMR; ++kk) {
+      const gf4 t = Mw[(6 * r + qc) + (kMR * hw + kk) * kCD];
+      mreg[kk] = make_float4(t.x, t.y, t.z, t.w);
+    }
+  }
+#ifdef OFX_STAMPS
+  const int nw = g.nwg_row;
+#endif
   // the rows' bounds: packed in the wave list, or (CSR form) from row_ptr
   int wb0 = 0, b0 = 0, b1 = 0;
   if (kWave) {
@@ -1992,20 +2003,16 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     b0 = g.row_ptr[row];
     b1 = g.row_ptr[row + 1];
   }
-  // the operator (kSc: from the scalar block, made scalar; !kSc: pinned above with the kernel arguments)
-  if (kSc) aop_bits = ((uint64_t)__builtin_amdgcn_readfirstlane(aop_v.y) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(aop_v.x);
   const __attribute__((address_space(1))) double* Aop =
-      reinterpret_cast<const __attribute__((address_space(1))) double*>(aop_bits);
+      reinterpret_cast<const __attribute__((address_space(1))) double*>(addr(aop_v));
   // after convergence the rest of the chunk ends here. The empty asm with a memory clobber keeps
   // the trip-1 loads above the exit (otherwise they sink past it and the test would gate them).
   asm volatile("" ::: "memory");
-  // the wave's stop words are equal (every lane stores the same epoch), and so are the scalars below: taken
+  // the wave's stop words are equal (every lane stores the same value), and so are the scalars below: taken
   // as wave-uniform values the exits are scalar branches, so the main path's waits are not merged with the exit paths'
   // (a divergent exit left a vmcnt(0) at the join in front of the products)
   stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
-  // this solve has converged (or stopped): a drained launch. (k_pcg_w0 reset the stop words to 0 for this solve; the
-  // epoch comparison of the !kSc form needs the kernel arguments first.)
-  if (kSc ? stop_ep != 0 : stop_ep >= ep) return;
+  if (stop_ep != 0) return;     // this solve has converged (or stopped): a drained launch (k_pcg_w0 zeroed the words)
 #ifdef OFX_STAMPS
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8] = t_entry;
 #endif
@@ -2028,13 +2035,23 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
   __builtin_amdgcn_sched_barrier(0);   // ... and no scalar arithmetic above its issue (it would wait for the partials)
-  if (kSc) pin(0);
-  double* __restrict__ mn = par_ ? g.m0 : g.m1;
-  double* Pn = g.part_p + 3 * (int64_t)ns * (par_ ^ 1);
+  const double tol_s = tols.x, etol_s = tols.y;
+  // outputs, through the preloaded (const) views or the scalar block: the new m, the other parity's partial streams,
+  // the state, the stop words, the lead's scalars
+  __attribute__((address_space(1))) double* mn = reinterpret_cast<__attribute__((address_space(1))) double*>(addr(mn_v));
+  const int ns = kNs;
+  double* Pn = const_cast<double*>(Pc) + (par_ ? -3 : 3) * (int64_t)kNs;
+  double* stw = const_cast<double*>(st);
+  int32_t* stopw_w = const_cast<int32_t*>(stopw);
+  double* sc_w = const_cast<double*>(scb);
+  int32_t* flags_w = reinterpret_cast<int32_t*>(sc_w + kScFlags);
   double tb[kFirst ? 2 * kU : 1];   // the first iteration's |b|² partials (kernel-argument pointer: once per solve)
-  if (kFirst)
+  if (kFirst) {   // (a pointer read from memory is generic: back to the global address space, or flat loads)
+    const __attribute__((address_space(1))) double* pb =
+        reinterpret_cast<const __attribute__((address_space(1))) double*>(reinterpret_cast<uint64_t>(g.part_b));
 #pragma unroll
-    for (int u = 0; u < 2 * kU; ++u) tb[u] = g.part_b[lane + 64 * u];
+    for (int u = 0; u < 2 * kU; ++u) tb[u] = pb[lane + 64 * u];
+  }
   const double rgam_prev = kFirst ? 1.0 : ((par_ ^ 1) ? rg.y : rg.x);     // 1/γ, 1/α of the previous iteration
   const double ralpha_prev = kFirst ? 1.0 : ((par_ ^ 1) ? ra.y : ra.x);
   const double thr_prev = kFirst ? 0.0 : ((par_ ^ 1) ? rt.y : rt.x);       // error-based stop: bound on γ (below)
@@ -2074,10 +2091,10 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
   leave = __builtin_amdgcn_readfirstlane(leave);
   if (leave) {   // converged, or breakdown (A SPD => alpha > 0): keep x
-    if (kFirst && lead) g.scal[S_BB] = bb;
+    if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
     if (!w0) return;
     if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
-    g.stopw[(int64_t)wv * 64 + lane] = ep;
+    stopw_w[(int64_t)wv * 64 + lane] = ep;
     const bool ill = !conv && !isfinite(alpha);
     if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, ep, gn_iter, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
     if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {   // first launch to see it
@@ -2114,10 +2131,12 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     thr_new = (etol * th) * (etol * th);
   }
   auto lead_stores = [&]() {
-    if (lead) { g.pcg_alpha[2 + par_] = 1.0 / alpha; g.pcg_gamma[2 + par_] = 1.0 / gam; g.flags[F_PCG_CNT] = cnt + 1; }
-    if (lead) g.pcg_alpha[4 + par_] = thr_new;
-    if (wv == 0 && hw == 0 && etol > 0.0) g.sturm[lane] = sd_new;
-    if (kFirst && lead) g.scal[S_BB] = bb;
+    if (lead) {
+      sc_w[kScAlpha + 2 + par_] = 1.0 / alpha; sc_w[kScGamma + 2 + par_] = 1.0 / gam; flags_w[F_PCG_CNT] = cnt + 1;
+      sc_w[kScAlpha + 4 + par_] = thr_new;
+    }
+    if (wv == 0 && hw == 0 && etol > 0.0) reinterpret_cast<double2*>(sc_w + kScSturm)[lane] = sd_new;
+    if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
   };
   OFX_STAMP(2)
   // ---- n = A m (own component)
@@ -2172,7 +2191,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     const double w2 = fma(-alpha, zz, v[V_W]);
     if (own) {
       const double nv[V_N] = {fma(alpha, p, v[V_X]), rn, un, zz, qq, sv, p, w2};
-      if (w0) store_rec(g.st, o, nv);   // (g.st: the same buffer, written; st is the const view)
+      if (w0) store_rec(stw, o, nv);   // (the same buffer as st, written)
       s_v[hw][6 * r + q] = w2;
       d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
     }
@@ -2434,16 +2453,14 @@ static int pcg_ku_for(int waves) {
   return ku;
 }
 
-using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const float*,
-                          const double*, const PcgIt*, int, int, int);
+using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const double*,
+                          const PcgIt*, int, int, int);
 template <int KU>
 static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU <= 3) {
     if (wave && w2) {
-      const char* e = getenv("OFX_PCG_SC");   // A/B only (read per solve): 0 = the round-4 kernel-argument form
-      const bool sc = !(e && atoi(e) == 0);
-      first = sc ? k_pcg_iter<true, true, KU, true> : k_pcg_iter<true, true, KU, true, false>;
-      rest = sc ? k_pcg_iter<true, false, KU, true> : k_pcg_iter<true, false, KU, true, false>;
+      first = k_pcg_iter<true, true, KU, true>;
+      rest = k_pcg_iter<true, false, KU, true>;
       return;
     }
   }
@@ -2568,7 +2585,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       const int par = it & 1;
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, (const int2*)g->wl, (const int32_t*)g->stopw,
                          (const double*)(g->part_p + 3 * (int64_t)g->nw_pad * par), (const double*)g->st,
-                         (const double*)(par ? g->m1 : g->m0), (const float*)g->Mcl, (const double*)g->pcs, gp, par, g->ep,
+                         (const double*)(par ? g->m1 : g->m0), (const double*)g->pcs + par, gp, par, g->ep,
                          gn_iter);
     }
 #ifdef OFX_STAMPS

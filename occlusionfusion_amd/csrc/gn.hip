@@ -83,7 +83,9 @@ struct GnDev {
   int64_t T_cap = 0;
   // pattern + contribution lists
   int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;   // row_cnt[N]: max row length
-  int2* wl = nullptr;            // per PCG wave: its first kWL blocks (CSR order) as (col, slot); (-1, 0) = none
+  int2* wl = nullptr;            // per PCG wave: its first kWL blocks' columns and packed row bounds (k_wave_list)
+  double* Aw = nullptr;          // per PCG wave: its kWL blocks of the operator, [wave][18][kWL] 16-B words (k_pcg_w0)
+  int32_t pcg_aw = 1;            // k_pcg_iter reads A from Aw (OFX_PCG_AW=0: from the CSR copy; read per setup)
   int max_deg = 0;               // longest block row of the pattern
   int max_wave = 0;              // most blocks of one PCG wave (kCS rows)
   int32_t* stopw = nullptr;      // per PCG wave and lane: the epoch of the last converged (or stopped) PCG solve
@@ -264,10 +266,22 @@ __device__ __forceinline__ double read_lane(double x, int l) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
   return __hiloint2double(hi, lo);
 }
-// Full-wave sum, fixed order, uniform result. Call from wave-uniform control flow.
+// x from the lanes selected by a broadcast DPP control into the rows of row_mask (0 elsewhere)
+template <int CTL, int ROWS>
+__device__ __forceinline__ double dpp_bcast(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTL, ROWS, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// Full-wave sum, fixed order, uniform result. Call from wave-uniform control flow. After the 16-lane row sums r0..r3,
+// row_bcast:15 adds row 0 into row 1 and row 2 into row 3, row_bcast:31 adds row 1 into row 3, whose lane 63 then
+// holds (r3 + r2) + (r1 + r0) — bitwise the (r0 + r1) + (r2 + r3) of reading four lanes (f64 addition commutes
+// exactly), in 2 DPP adds and one lane read instead of 4 lane reads, 2 moves back to VGPRs and 3 adds.
 __device__ __forceinline__ double wave_sum(double x) {
   x = row16_sum(x);
-  return (read_lane(x, 0) + read_lane(x, 16)) + (read_lane(x, 32) + read_lane(x, 48));
+  x += dpp_bcast<0x142, 0xA>(x);   // row_bcast:15 into rows 1, 3
+  x += dpp_bcast<0x143, 0x8>(x);   // row_bcast:31 into row 3
+  return read_lane(x, 63);
 }
 // four block sums at once: fixed-order wave sums, then the kBlk/64 wave results combined in wave order
 __device__ __forceinline__ void block_sum4(double v[4]) {
@@ -1138,6 +1152,20 @@ __device__ __forceinline__ void reduce_streams2(const double* __restrict__ p, in
   for (int k = 0; k < K; ++k) out[k] = wave_sum(a[k]);
 }
 
+// a / b by the hardware reciprocal, two Newton steps and one quotient correction (≈ 6 dependent operations against the
+// ≈ 11 of IEEE division: div_scale, rcp, four fma, mul, fma, div_fmas, div_fixup); within an ulp of a / b for the finite,
+// normal operands the PCG's step scalars are (the PCG is not bit-pinned: it uses fused multiply-adds throughout), and
+// non-finite when b is 0 or non-finite, which the breakdown test catches
+__device__ __forceinline__ double div_nr(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  const double q = a * r;
+  return fma(r, fma(-b, q, a), q);
+}
+
 // n[c] without a dynamically indexed array (which the compiler would put in scratch): masked sum,
 // exact for finite n (x·1 + 0 terms); a non-finite component poisons the row, as it would anyway.
 __device__ __forceinline__ double pick6(const double n[6], int c) {
@@ -1661,7 +1689,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
   asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.Mcl), "s"(g.st), "s"(g.flags), "s"(g.m0), "s"(g.m1), "s"(g.Aop),
                "s"(g.part_p), "s"(g.part_b), "s"(g.nw_pad), "s"(g.nwg_row), "s"(g.ep), "s"(g.stopw), "s"(g.pcs), "s"(rhs),
-               "s"(g.prm.pcg_tol), "s"(g.prm.pcg_err_tol), "s"(g.Mcl));
+               "s"(g.prm.pcg_tol), "s"(g.prm.pcg_err_tol), "s"(g.Mcl), "s"(g.Aw), "s"(g.pcg_aw));
   const int lane = threadIdx.x;
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
@@ -1687,7 +1715,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // address into the scalar block, where the iteration finds it through a preloaded pointer
   g.stopw[(int64_t)blockIdx.x * 64 + lane] = stopped ? g.ep : 0;
   if (blockIdx.x == 0 && lane == 0) {
-    reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(g.Aop);
+    reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>((kWave && g.pcg_aw) ? g.Aw : g.Aop);
     g.pcs[kScTol] = g.prm.pcg_tol;
     g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
     reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = reinterpret_cast<uint64_t>(g.Mcl);
@@ -1697,8 +1725,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (stopped) return;
   const double b = own ? bo : 0.0;
   double w;
+  double2 ab[2][18];
   if (kWave) {
-    double2 ab[2][18], xb[2][3];
+    double2 xb[2][3];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked below)
       const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)(bl[j].x >= 0 ? wl_base(bl[j]) + 64 * j + lane : 0));
@@ -1761,6 +1790,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   // the loaded (dead) w register stays allocated to here: otherwise the compiler reuses it for a temporary of the
   // SpMV's issue and waits for its load first (a vmcnt that held trip 2 behind nearly all of trip 1)
+  // the wave's blocks into its padded copy for k_pcg_iter (kWave, pcg_aw): last, so no wait here is behind their acks
+  if (kWave && g.pcg_aw) {
+    double2* Aw = reinterpret_cast<double2*>(g.Aw) + (int64_t)wv * 18 * kWL;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = bl[j].x >= 0;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) Aw[k * kWL + 64 * j + lane] = ok ? ab[j][k] : make_double2(0.0, 0.0);
+    }
+  }
   asm volatile("" ::"v"(w_old));
 }
 
@@ -1819,10 +1858,18 @@ static PcgIt pcg_args(const Gn* g) {
   return a;
 }
 #ifdef OFX_STAMPS   // tuning build only: phase clock stamps of every wave of the first 64 iterations
-#define OFX_STAMP(k)                                                                                  \
+#define OFX_STAMP_AT(k)                                                                               \
   if (lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nw + wv) * 8 + (k)] = __builtin_amdgcn_s_memtime();
 #else
-#define OFX_STAMP(k)
+#define OFX_STAMP_AT(k)
+#endif
+#ifdef OFX_STAMPS_SCALARS   // (with OFX_STAMPS) the scalar phase split instead: 1 stop test, 2 trip 2 issued, 3 partials landed,
+                            // 4 wave sums, 5 division + leave test, 6 products' start, 7 end
+#define OFX_STAMP(k) if ((k) == 1 || (k) == 7) { OFX_STAMP_AT(k) }
+#define OFX_STAMPX(k) OFX_STAMP_AT(k)
+#else
+#define OFX_STAMP(k) OFX_STAMP_AT(k)
+#define OFX_STAMPX(k)
 #endif
 // k_step's work done by the converging PCG launch (every wave for its own rows; wave 0 lane 0 the
 // bookkeeping). Every wave derives the same decision from read-only inputs, as k_step's workgroups do.
@@ -1915,7 +1962,7 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int ep, int gn_iter, 
 // rewritten when they change): a 76-B kernel argument instead of ~290 B, which the host enqueues faster. In-process A/B
 // against the same kernel with its scalars and addresses through the kernel arguments: -0.27 / -0.28 ms per frame.
 // mc / Pc are the parity's m and partial streams.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kAw = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(
     const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const double* sc,
     const PcgIt* __restrict__ gp, int par, int ep, int gn_iter) {   // (not __restrict__: a restrict load sinks past the exit test)
@@ -2023,18 +2070,34 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     for (int j = 0; j < kNB; ++j) {   // unconditional loads (padding reads block 0 / m row 0, masked later)
       const int2 e = j ? bl1 : bl0;
       typedef double gd2 __attribute__((ext_vector_type(2)));   // (a plain vector type: loads through address space 1)
+      const int slot = kW2 ? 64 * hw + lane : 64 * j + lane;
       const __attribute__((address_space(1))) gd2* blk = reinterpret_cast<const __attribute__((address_space(1))) gd2*>(
-          Aop + 36 * (int64_t)(e.x >= 0 ? wb0 + (kW2 ? 64 * hw + lane : 64 * j + lane) : 0));
+          Aop + 36 * (int64_t)(e.x >= 0 ? wb0 + slot : 0));
+      // kAw: the wave's padded copy, 16-B word k of every slot contiguous (1 KB per load instruction, not 64 lines)
+      const __attribute__((address_space(1))) gd2* blw =
+          reinterpret_cast<const __attribute__((address_space(1))) gd2*>(Aop) + (int64_t)wv * 18 * kWL + slot;
       const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
       // the gathered m row first: the products of the first block rows start before the block's tail lands
 #pragma unroll
       for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
       asm volatile("" ::: "memory");
 #pragma unroll
-      for (int k = 0; k < 18; ++k) { const gd2 t = blk[k]; ab[j][k] = make_double2(t.x, t.y); }
+      for (int k = 0; k < 18; ++k) {
+        const gd2 t = kAw ? blw[k * kWL] : blk[k];
+        ab[j][k] = make_double2(t.x, t.y);
+      }
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
   __builtin_amdgcn_sched_barrier(0);   // ... and no scalar arithmetic above its issue (it would wait for the partials)
+  OFX_STAMPX(2)
+#ifdef OFX_STAMPS_SCALARS
+  {
+    double t_ = tp[2][kU - 1].y;   // (wait for the last partial here)
+    asm volatile("" : "+v"(t_) :: "memory");
+    tp[2][kU - 1].y = t_;
+  }
+  OFX_STAMPX(3)
+#endif
   const double tol_s = tols.x, etol_s = tols.y;
   // outputs, through the preloaded (const) views or the scalar block: the new m, the other parity's partial streams,
   // the state, the stop words, the lead's scalars
@@ -2064,6 +2127,10 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     for (int u = 0; u < kU; ++u) t += tp[k][u].x + tp[k][u].y;
     pa[k] = wave_sum(t);
   }
+#ifdef OFX_STAMPS_SCALARS
+  asm volatile("" : "+v"(pa[0]), "+v"(pa[1]), "+v"(pa[2]) :: "memory");
+  OFX_STAMPX(4)
+#endif
   double bb = bb_stored;
   if (kFirst) {
     double t = 0.0;
@@ -2077,10 +2144,10 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const bool w0 = hw == 0;   // the wave that stores (kW2: both compute the same bits)
   double beta = 0.0, alpha;
   if (kFirst) {
-    alpha = gam / del;
+    alpha = div_nr(gam, del);
   } else {
     beta = gam * rgam_prev;
-    alpha = gam / (del - beta * gam * ralpha_prev);
+    alpha = div_nr(gam, del - beta * gam * ralpha_prev);
   }
   // Stop: the relative residual ‖r‖ <= tol·‖b‖ AND (pcg_err_tol > 0) the error estimate √γ / θ̂ <= pcg_err_tol, or
   // the relative residual at the f64 floor (1e-12). γ = rᵀM⁻¹r = ‖z‖²_M (z = M⁻¹r), so the error e = (M⁻¹A)⁻¹z has
@@ -2090,6 +2157,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam <= thr_prev)) || gam == 0.0 || rr <= 1e-24 * bb;
   int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
   leave = __builtin_amdgcn_readfirstlane(leave);
+  OFX_STAMPX(5)
   if (leave) {   // converged, or breakdown (A SPD => alpha > 0): keep x
     if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
     if (!w0) return;
@@ -2139,6 +2207,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
   };
   OFX_STAMP(2)
+  OFX_STAMPX(6)
   // ---- n = A m (own component)
   double nc;
   if (kWave) {
@@ -2167,12 +2236,15 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     // masked; s_prod is padded so the reads past the wave's last block stay inside it)
     const int len = b1 - b0;
     const double* sp = s_prod + (b0 - wb0) * 6 + qc;
+    // every read in flight before the first add (left to the compiler, each pair of reads was waited for before the
+    // next pair issued: ten LDS round trips in a row)
+    double tv[kRowMax];
+#pragma unroll
+    for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+    __builtin_amdgcn_sched_barrier(0);
     double a = 0.0;
 #pragma unroll
-    for (int k = 0; k < kRowMax; ++k) {
-      const double t = sp[6 * k];
-      a += k < len ? t : 0.0;
-    }
+    for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
     nc = a;
   } else {
     double n[6];
@@ -2201,15 +2273,20 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   if (kW2) {      // split-K: wave h applies column groups [6h, 6h + 6); wave 0 adds the halves (fixed order)
     double hsum = 0.0;
     if (own) {
+      // the half's 24 values in flight before the first FMA (left to the compiler: five LDS round trips in a row)
+      double2 vv[kCD / 4];
+      const double2* sv2 = reinterpret_cast<const double2*>(&s_v[hw][4 * (kCD / 8) * hw]);
+#pragma unroll
+      for (int i = 0; i < kCD / 4; ++i) vv[i] = sv2[i];
+      __builtin_amdgcn_sched_barrier(0);
       double a[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < kCD / 8; ++kk) {
-        const int k = (kCD / 8) * hw + kk;
         const float4 t = mreg[kk];
-        a[0] = fma((double)t.x, s_v[hw][4 * k], a[0]);
-        a[1] = fma((double)t.y, s_v[hw][4 * k + 1], a[1]);
-        a[2] = fma((double)t.z, s_v[hw][4 * k + 2], a[2]);
-        a[3] = fma((double)t.w, s_v[hw][4 * k + 3], a[3]);
+        a[0] = fma((double)t.x, vv[2 * kk].x, a[0]);
+        a[1] = fma((double)t.y, vv[2 * kk].y, a[1]);
+        a[2] = fma((double)t.z, vv[2 * kk + 1].x, a[2]);
+        a[3] = fma((double)t.w, vv[2 * kk + 1].y, a[3]);
       }
       hsum = (a[0] + a[1]) + (a[2] + a[3]);
     }
@@ -2362,7 +2439,7 @@ static double lm_for_iter(double lm0, int gn_iter) {
 
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
-                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->stopw, g->blk_off, g->blk_cnt,
+                  g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->Aw, g->stopw, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcs,
                   g->part_p, g->part_b, g->part_loss,
@@ -2456,17 +2533,17 @@ static int pcg_ku_for(int waves) {
 using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const double*,
                           const PcgIt*, int, int, int);
 template <int KU>
-static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
+static void pcg_pick(bool wave, bool w2, bool aw, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU <= 3) {
     if (wave && w2) {
-      first = k_pcg_iter<true, true, KU, true>;
-      rest = k_pcg_iter<true, false, KU, true>;
+      first = aw ? k_pcg_iter<true, true, KU, true, true> : k_pcg_iter<true, true, KU, true>;
+      rest = aw ? k_pcg_iter<true, false, KU, true, true> : k_pcg_iter<true, false, KU, true>;
       return;
     }
   }
   if (wave) {
-    first = k_pcg_iter<true, true, KU, false>;
-    rest = k_pcg_iter<true, false, KU, false>;
+    first = aw ? k_pcg_iter<true, true, KU, false, true> : k_pcg_iter<true, true, KU, false>;
+    rest = aw ? k_pcg_iter<true, false, KU, false, true> : k_pcg_iter<true, false, KU, false>;
   } else {
     first = k_pcg_iter<false, true, KU, false>;
     rest = k_pcg_iter<false, false, KU, false>;
@@ -2530,11 +2607,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku <= 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
   switch (g->pcg_ku) {
-    case 2: pcg_pick<2>(wave, w2, iter0, iter); break;
-    case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
-    case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
-    case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
-    default: pcg_pick<17>(wave, w2, iter0, iter); break;
+    case 2: pcg_pick<2>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
+    case 3: pcg_pick<3>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
+    case 4: pcg_pick<4>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
+    case 8: pcg_pick<8>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
+    default: pcg_pick<17>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
   }
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
@@ -2735,7 +2812,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
   ALLOC(g->Mcl, 6 * N * kCD); ALLOC(g->st, V_N * 6 * N); ALLOC(g->m0, 6 * N); ALLOC(g->m1, 6 * N);
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N); ALLOC(g->step_args, 1);
-  ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes); ALLOC(g->wl, N / kCS * kWL); ALLOC(g->stopw, N / kCS * 64);
+  ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes); ALLOC(g->wl, N / kCS * kWL); ALLOC(g->Aw, N / kCS * kWL * 36);
+  ALLOC(g->stopw, N / kCS * 64);
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   const int64_t max_ns = 128 * 17;   // nw_pad bound: 2·64·17 >= max_pad / kCS waves
   static_assert(2 * 64 * 17 * kCS >= 2 * kMaxNodes + kCS, "partial stream width");
@@ -3126,6 +3204,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->nwg_row = N / kRW;
   g->pcg_ku = pcg_ku_for(g->nwg_row);
   g->nw_pad = 128 * g->pcg_ku;
+  if (const char* e = getenv("OFX_PCG_AW")) g->pcg_aw = atoi(e) ? 1 : 0;   // (A/B)
   // every partial stream is read unconditionally up to nw_pad: the tails must be zero (the kernels write only the
   // entries of their own waves; k_pcg_w0 re-zeroes the iteration streams' tails, nothing writes the others')
   OFX_HIP(hipMemsetAsync(g->part_p, 0, (size_t)kProjP * g->nw_pad * sizeof(double), hs));

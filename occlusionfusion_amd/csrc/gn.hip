@@ -2081,10 +2081,21 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
       asm volatile("" ::: "memory");
+      if (kAw) {
+        // padding slots read the half's first slot (lines its own lane fetches anyway: no extra bytes; their products
+        // are masked) — an exec-masked load would make the compiler's waits at the join conservative
+        const __attribute__((address_space(1))) gd2* b = e.x >= 0 ? blw : blw - slot + (kW2 ? 64 * hw : 64 * j);
 #pragma unroll
-      for (int k = 0; k < 18; ++k) {
-        const gd2 t = kAw ? blw[k * kWL] : blk[k];
-        ab[j][k] = make_double2(t.x, t.y);
+        for (int k = 0; k < 18; ++k) {
+          const gd2 t = b[k * kWL];
+          ab[j][k] = make_double2(t.x, t.y);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 18; ++k) {
+          const gd2 t = blk[k];
+          ab[j][k] = make_double2(t.x, t.y);
+        }
       }
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 
 struct Big {
   double* p[28];
@@ -37,8 +38,12 @@ int main() {
   hipEventCreate(&e1);
   Big big{};
   big.a = 1;
-  const int N = 2000, grid = 250, block = 128;
-  for (long long cyc : {0LL, 5000LL, 7500LL}) {   // s_memtime ticks at ~100 MHz on gfx950? (reported, see below)
+  const int N = 2000;
+  int grid = 250, block = 128;
+  if (const char* e = getenv("GRID")) grid = atoi(e);
+  if (const char* e = getenv("BLOCK")) block = atoi(e);
+  printf("grid %d x block %d\n", grid, block);
+  for (long long cyc : {0LL, 5000LL, 7500LL}) {   // s_memtime ticks at 2.4 GHz on gfx950 (reported, see below)
     for (int form = 0; form < 6; ++form) {
       hipGraphExec_t ge = nullptr;
       const int glen = form == 3 ? 100 : form == 4 ? 8 : 2;

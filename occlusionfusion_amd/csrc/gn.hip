@@ -2318,10 +2318,19 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     mn[o] = (a[0] + a[1]) + (a[2] + a[3]);
   }
   OFX_STAMP(6)
-  if (!w0) return;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) d[k] = wave_sum(d[k]);
-  if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; Pn[2 * ns + wv] = d[2]; }
+  // the three per-wave partials of the next launch: kW2's second wave (idle otherwise here) sums and stores the third,
+  // from the same bits wave 0 holds, so wave 0's tail is two wave sums instead of three
+  if (!w0) {
+    if (kW2) {
+      const double s2 = wave_sum(d[2]);
+      if (lane == 0) Pn[2 * ns + wv] = s2;
+    }
+    return;
+  }
+  d[0] = wave_sum(d[0]);
+  d[1] = wave_sum(d[1]);
+  if (!kW2) d[2] = wave_sum(d[2]);
+  if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; if (!kW2) Pn[2 * ns + wv] = d[2]; }
   lead_stores();
   OFX_STAMP(7)
 }

@@ -85,7 +85,6 @@ struct GnDev {
   int32_t *map = nullptr, *row_ptr = nullptr, *col = nullptr, *row_cnt = nullptr;   // row_cnt[N]: max row length
   int2* wl = nullptr;            // per PCG wave: its first kWL blocks' columns and packed row bounds (k_wave_list)
   double* Aw = nullptr;          // per PCG wave: its kWL blocks of the operator, [wave][18][kWL] 16-B words (k_pcg_w0)
-  int32_t pcg_aw = 1;            // k_pcg_iter reads A from Aw (OFX_PCG_AW=0: from the CSR copy; read per setup)
   int max_deg = 0;               // longest block row of the pattern
   int max_wave = 0;              // most blocks of one PCG wave (kCS rows)
   int32_t* stopw = nullptr;      // per PCG wave and lane: the epoch of the last converged (or stopped) PCG solve
@@ -1689,7 +1688,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
   asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.Mcl), "s"(g.st), "s"(g.flags), "s"(g.m0), "s"(g.m1), "s"(g.Aop),
                "s"(g.part_p), "s"(g.part_b), "s"(g.nw_pad), "s"(g.nwg_row), "s"(g.ep), "s"(g.stopw), "s"(g.pcs), "s"(rhs),
-               "s"(g.prm.pcg_tol), "s"(g.prm.pcg_err_tol), "s"(g.Mcl), "s"(g.Aw), "s"(g.pcg_aw));
+               "s"(g.prm.pcg_tol), "s"(g.prm.pcg_err_tol), "s"(g.Mcl), "s"(g.Aw));
   const int lane = threadIdx.x;
   const int wv = blockIdx.x;
   const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
@@ -1715,7 +1714,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // address into the scalar block, where the iteration finds it through a preloaded pointer
   g.stopw[(int64_t)blockIdx.x * 64 + lane] = stopped ? g.ep : 0;
   if (blockIdx.x == 0 && lane == 0) {
-    reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>((kWave && g.pcg_aw) ? g.Aw : g.Aop);
+    reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(kWave ? g.Aw : g.Aop);
     g.pcs[kScTol] = g.prm.pcg_tol;
     g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
     reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = reinterpret_cast<uint64_t>(g.Mcl);
@@ -1790,8 +1789,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   // the loaded (dead) w register stays allocated to here: otherwise the compiler reuses it for a temporary of the
   // SpMV's issue and waits for its load first (a vmcnt that held trip 2 behind nearly all of trip 1)
-  // the wave's blocks into its padded copy for k_pcg_iter (kWave, pcg_aw): last, so no wait here is behind their acks
-  if (kWave && g.pcg_aw) {
+  // the wave's blocks into its padded copy for k_pcg_iter (kWave): last, so no wait here is behind their acks
+  if (kWave) {
     double2* Aw = reinterpret_cast<double2*>(g.Aw) + (int64_t)wv * 18 * kWL;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -1962,7 +1961,7 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int ep, int gn_iter, 
 // rewritten when they change): a 76-B kernel argument instead of ~290 B, which the host enqueues faster. In-process A/B
 // against the same kernel with its scalars and addresses through the kernel arguments: -0.27 / -0.28 ms per frame.
 // mc / Pc are the parity's m and partial streams.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kAw = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(
     const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const double* sc,
     const PcgIt* __restrict__ gp, int par, int ep, int gn_iter) {   // (not __restrict__: a restrict load sinks past the exit test)
@@ -2071,9 +2070,8 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
       const int2 e = j ? bl1 : bl0;
       typedef double gd2 __attribute__((ext_vector_type(2)));   // (a plain vector type: loads through address space 1)
       const int slot = kW2 ? 64 * hw + lane : 64 * j + lane;
-      const __attribute__((address_space(1))) gd2* blk = reinterpret_cast<const __attribute__((address_space(1))) gd2*>(
-          Aop + 36 * (int64_t)(e.x >= 0 ? wb0 + slot : 0));
-      // kAw: the wave's padded copy, 16-B word k of every slot contiguous (1 KB per load instruction, not 64 lines)
+      // the wave's padded copy of A (k_pcg_w0), 16-B word k of every slot contiguous (1 KB per load instruction, not 64
+      // lines as from the CSR copy: -0.08 / -0.21 ms per frame, profiles/r04_ab.json)
       const __attribute__((address_space(1))) gd2* blw =
           reinterpret_cast<const __attribute__((address_space(1))) gd2*>(Aop) + (int64_t)wv * 18 * kWL + slot;
       const double2* vc = reinterpret_cast<const double2*>(mc + 6 * (int64_t)(e.x >= 0 ? e.x : 0));
@@ -2081,21 +2079,13 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int k = 0; k < 3; ++k) xb[j][k] = vc[k];
       asm volatile("" ::: "memory");
-      if (kAw) {
-        // padding slots read the half's first slot (lines its own lane fetches anyway: no extra bytes; their products
-        // are masked) — an exec-masked load would make the compiler's waits at the join conservative
-        const __attribute__((address_space(1))) gd2* b = e.x >= 0 ? blw : blw - slot + (kW2 ? 64 * hw : 64 * j);
+      // padding slots read the half's first slot (lines its own lane fetches anyway: no extra bytes; their products
+      // are masked) — an exec-masked load would make the compiler's waits at the join conservative
+      const __attribute__((address_space(1))) gd2* b = e.x >= 0 ? blw : blw - slot + (kW2 ? 64 * hw : 64 * j);
 #pragma unroll
-        for (int k = 0; k < 18; ++k) {
-          const gd2 t = b[k * kWL];
-          ab[j][k] = make_double2(t.x, t.y);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 18; ++k) {
-          const gd2 t = blk[k];
-          ab[j][k] = make_double2(t.x, t.y);
-        }
+      for (int k = 0; k < 18; ++k) {
+        const gd2 t = b[k * kWL];
+        ab[j][k] = make_double2(t.x, t.y);
       }
     }
   asm volatile("" ::: "memory");   // keep trip 2 issued here (the compiler would sink it past the exit test)
@@ -2553,17 +2543,17 @@ static int pcg_ku_for(int waves) {
 using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const double*,
                           const PcgIt*, int, int, int);
 template <int KU>
-static void pcg_pick(bool wave, bool w2, bool aw, PcgKernel& first, PcgKernel& rest) {
+static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
   if constexpr (KU <= 3) {
     if (wave && w2) {
-      first = aw ? k_pcg_iter<true, true, KU, true, true> : k_pcg_iter<true, true, KU, true>;
-      rest = aw ? k_pcg_iter<true, false, KU, true, true> : k_pcg_iter<true, false, KU, true>;
+      first = k_pcg_iter<true, true, KU, true>;
+      rest = k_pcg_iter<true, false, KU, true>;
       return;
     }
   }
   if (wave) {
-    first = aw ? k_pcg_iter<true, true, KU, false, true> : k_pcg_iter<true, true, KU, false>;
-    rest = aw ? k_pcg_iter<true, false, KU, false, true> : k_pcg_iter<true, false, KU, false>;
+    first = k_pcg_iter<true, true, KU, false>;
+    rest = k_pcg_iter<true, false, KU, false>;
   } else {
     first = k_pcg_iter<false, true, KU, false>;
     rest = k_pcg_iter<false, false, KU, false>;
@@ -2627,11 +2617,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku <= 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
   switch (g->pcg_ku) {
-    case 2: pcg_pick<2>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
-    case 3: pcg_pick<3>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
-    case 4: pcg_pick<4>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
-    case 8: pcg_pick<8>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
-    default: pcg_pick<17>(wave, w2, wave && g->pcg_aw, iter0, iter); break;
+    case 2: pcg_pick<2>(wave, w2, iter0, iter); break;
+    case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
+    case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
+    case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
+    default: pcg_pick<17>(wave, w2, iter0, iter); break;
   }
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
@@ -3224,7 +3214,6 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->nwg_row = N / kRW;
   g->pcg_ku = pcg_ku_for(g->nwg_row);
   g->nw_pad = 128 * g->pcg_ku;
-  if (const char* e = getenv("OFX_PCG_AW")) g->pcg_aw = atoi(e) ? 1 : 0;   // (A/B)
   // every partial stream is read unconditionally up to nw_pad: the tails must be zero (the kernels write only the
   // entries of their own waves; k_pcg_w0 re-zeroes the iteration streams' tails, nothing writes the others')
   OFX_HIP(hipMemsetAsync(g->part_p, 0, (size_t)kProjP * g->nw_pad * sizeof(double), hs));

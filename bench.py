@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=1 << 24)
     p.add_argument("--json-out", default=None)
     p.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--moose", action="store_true",
+                   help="time the reference's real solver input instead (NonRigidICP moose demo pair, "
+                        "tests/golden/moose.npz): ms per GN optimize, PCG iterations, error against the f64 oracle")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL; gloo for "
                                                    "CPU launch checks and rehearsals with ranks sharing a device)")
     a = p.parse_args()
@@ -153,6 +156,8 @@ def main():
         raise SystemExit(f"bench.py: WORLD_SIZE {world} != --gpus {a.gpus}")
     if a.launch_check:
         return launch_check(a, world, rank)
+    if a.moose:
+        return moose_bench(a)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())   # rehearsals: several ranks may share one device
     torch.cuda.set_device(local)
@@ -351,6 +356,55 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def moose_bench(a):
+    """The reference's only real solver input (NonRigidICP/main.py:35-48: the moose demo pair's 427 valid Lepard
+    landmarks on the 271-node depth-mesh graph, tests/golden/moose.npz): K timed DeformNet.optimize solves after W
+    warmup ones, at the default parameters and with the round-4 preconditioner policy (precond_rot_tol = 0: the cluster
+    inverse built once per solve) beside it. Reports ms per optimize (events around the K calls), PCG iterations per
+    optimize, capped steps, and the transforms' max error against the dense f64 oracle's (the fixture)."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = np.load(os.path.join(ROOT, "tests", "golden", "moose.npz"), allow_pickle=False)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    N = g["nodes"].shape[0]
+    K = g["K"]
+    intr = (float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]))
+    args = [torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("nodes", "edges", "edge_weights", "nodes")]
+    rest = [torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("src", "anchors", "weights", "tgt")]
+    conf = torch.zeros(N, device=dev)
+
+    def run(**prm):
+        s = GaussNewtonSolver(N, 1000, dev, **prm)
+        call = lambda: s.optimize(*args, conf, *rest, intr, sync=False)
+        for _ in range(a.warmup):
+            call()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        outs = [call() for _ in range(a.steps)]
+        e1.record()
+        torch.cuda.synchronize()
+        st = np.stack([o["_status"].cpu().numpy() for o in outs])
+        o = outs[-1]
+        err = max(float(np.abs(o["node_rotations"].cpu().numpy() - g["R"]).max()),
+                  float(np.abs(o["node_translations"].cpu().numpy() - g["t"]).max()))
+        return {"ms_per_optimize": e0.elapsed_time(e1) / a.steps, "pcg_iterations": float(st[:, 2].mean()),
+                "gn_steps": float(st[:, 1].mean()), "capped_steps": int(st[:, 4].max()), "valid": int(st[:, 0].min()),
+                "max_abs_err_vs_f64_oracle": err, "pcg_per_gn_step": [int(v) for v in s.stats()[:, 0]]}
+
+    cur = run()
+    old = run(precond_rot_tol=0.0)
+    res = {"metric": "moose landmark GN optimize (NonRigidICP demo pair, 271 nodes, 427 landmarks, 10 GN steps)",
+           "value": cur["ms_per_optimize"], "unit": "ms/optimize", "higher_is_better": False, "n_gpus": 1,
+           "steps": a.steps, "warmup": a.warmup, "dtype": "f64", "data": "real (tests/golden/moose.npz: the reference's "
+           "NonRigidICP/demo/moose6OK9_AttackTrotRM pair)", "default": cur, "precond_rot_tol_0": old}
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
 
 
 def cpu_model():

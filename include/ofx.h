@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define OFX_ABI_VERSION 2
+#define OFX_ABI_VERSION 3
 
 typedef void* ofx_stream_t; /* hipStream_t; NULL = legacy default stream */
 
@@ -370,7 +370,14 @@ typedef struct ofx_gn_params {
   double pcg_err_tol;        /* error-based stop (> 0): the inner solve also runs until its estimated solution
                                 error sqrt(r^T M^-1 r) / theta <= pcg_err_tol, theta = the smallest Ritz value of
                                 the preconditioned operator's Lanczos tridiagonal (from below, within a factor
-                                sqrt 2); 0: the relative residual alone. Both stop at a relative residual of 1e-12 */
+                                2^(1/4) down to 2^-10, sqrt 2 below), or, on GN steps after the first, the previous
+                                step's final theta when
+                                that is smaller (early in a solve theta over-estimates the smallest eigenvalue);
+                                0: the relative residual alone. Both stop at a relative residual of 1e-12 */
+  double precond_rot_tol;    /* adaptive preconditioner refresh (> 0): a GN step also rebuilds the cluster inverse
+                                when some node has rotated by more than this (radians, summed |omega| of the
+                                steps since the last rebuild); real data with large rotations (the moose demo)
+                                needs it, the synthetic bench never reaches it. 0: precond_every alone */
 } ofx_gn_params;
 
 /* OFX_GN_ARAP restates DeformNet.arap (model/model.py:1639-1986), the graph-update solve for nodes
@@ -400,7 +407,9 @@ typedef struct ofx_gn_problem {
   float fx, fy, cx, cy;
 } ofx_gn_problem;
 
-/* status (device int32[4]): [valid_solve, gn_iterations_accepted, pcg_iterations_total, ill_posed]
+/* status (device int32[5]): [valid_solve, gn_iterations_accepted, pcg_iterations_total, ill_posed,
+ * pcg_capped_steps] — the last: GN steps whose PCG stopped at pcg_max_iter without meeting its stop rule (the step
+ * was taken with that iterate)
  * loss_log (device f64[num_iter*4]): per accepted iteration [total, data, arap, motion] */
 typedef struct ofx_gn_result {
   float* rot;        /* (N,9) */

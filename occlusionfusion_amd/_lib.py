@@ -31,7 +31,7 @@ class GnParams(ctypes.Structure):
                 ("lambda_flow", c_double), ("lambda_depth", c_double), ("lambda_arap", c_double),
                 ("lambda_motion", c_double), ("lm_factor", c_double), ("stop_loss_diff", c_double),
                 ("pcg_tol", c_double), ("mode", c_int32), ("precond_every", c_int32),
-                ("pcg_err_tol", c_double)]
+                ("pcg_err_tol", c_double), ("precond_rot_tol", c_double)]
 
 
 class GnProblem(ctypes.Structure):

@@ -108,6 +108,8 @@ struct GnDev {
   int64_t nnzb = 0, nnzb_cap = 0;
   // state
   double *R = nullptr, *t = nullptr;
+  double* racc = nullptr;        // per row: Σ|ω| of the GN steps since its cluster inverse was built (precond_rot_tol)
+  int32_t gn_iter_now = 0;       // GN step of the current PCG solve
   double *A_own = nullptr, *rhs_own = nullptr;
   float* Mcl = nullptr;           // cluster inverses, f32, per cluster 48x48 in the lane-interleaved order of mcl_idx
   const double* Aop = nullptr;    // PCG operator (the damped A of the current step)
@@ -224,9 +226,13 @@ static int sync_side(Gn* g) {
   return OFX_OK;
 }
 
+// F_REFRESH: the GN step whose warm start rebuilds the cluster inverse (set by the previous step's update when a node's
+// accumulated rotation passed precond_rot_tol; 0 = none); F_CAPPED: GN steps whose PCG ran into pcg_max_iter
 enum { F_DONE = 0, F_STOPPED = 1, F_ILL = 2, F_ACCEPTED = 3, F_PCG_TOTAL = 4, F_APPLY = 5, F_RES_NONFINITE = 6,
-       F_PCG_IT = 7, F_PCG_CNT = 8, F_COUNT = 9 };
-enum { S_LOSS_PREV = 0, S_BB = 1, S_COUNT = 4 };
+       F_PCG_IT = 7, F_PCG_CNT = 8, F_REFRESH = 9, F_CAPPED = 10, F_COUNT = 11 };
+// scalars: S_TH_CUR = the current solve's latest θ̂ (error-based stop), S_TH_PREV = the previous GN step's final θ̂
+// (k_pcg_w0 moves it per solve; 1e300 = none)
+enum { S_LOSS_PREV = 0, S_BB = 1, S_TH_PREV = 2, S_TH_CUR = 3, S_COUNT = 4 };
 // host-mapped flags: H_DONE holds the epoch (GnDev::ep) of the last converged PCG solve (from the converging launch's
 // lead lane);
 // H_STOPPED the epoch of the solve whose GN step stopped the loop (0: running). k_upload clears them per setup.
@@ -1289,11 +1295,10 @@ __device__ __forceinline__ double apply_mrow(const float4 mr[kCD / 4], const dou
 // in registers for all 48 (unrolled) steps; step k fetches the old row k / column k entries it needs
 // from their owner lanes by cross-lane permutes and the pivot by a lane read — no LDS, no barrier.
 // Cold start also: x = 0, r = b, u = M⁻¹ b, z = q = s = p = w = 0, u -> m1.
-__global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __restrict__ A,
-                                                 const double* __restrict__ rhs, int invert) {
-  if (g.flags[F_STOPPED]) return;
-  const int lane = threadIdx.x;
-  const int base = blockIdx.x * kCS;
+// The inversion of cluster cl (one wave, lane = node block (ti, tj)): m receives the lane's block of the symmetrised
+// f32 inverse, which is also stored to Mcl; the cluster's rows' rotation accumulators restart (precond_rot_tol).
+__device__ __forceinline__ void cluster_invert(const GnDev& g, const double* A, int cl, int lane, float m[6][6]) {
+  const int base = cl * kCS;
   const int ti = lane / kCS, tj = lane % kCS;
   const int slot = g.map[(int64_t)(base + ti) * g.N + base + tj] - 1;
   double a[6][6];
@@ -1306,7 +1311,6 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
       a[(2 * e + 1) / 6][(2 * e + 1) % 6] = v.y;
     }
   }
-  (void)lm; (void)invert;   // A arrives damped (k_assemble)
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < kCD; ++k) {
@@ -1334,7 +1338,6 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
       }
   }
   // symmetrise with the transposed block (lane (tj, ti)), round to f32, store the cluster rows
-  float m[6][6];
 #pragma unroll
   for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -1346,10 +1349,24 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
   for (int r = 0; r < 6; ++r)
 #pragma unroll
     for (int c = 0; c < 3; ++c)   // (j, j+1) with j even share a float4
-      *reinterpret_cast<float2*>(g.Mcl + mcl_idx(blockIdx.x, 6 * ti + r, 6 * tj + 2 * c)) =
+      *reinterpret_cast<float2*>(g.Mcl + mcl_idx(cl, 6 * ti + r, 6 * tj + 2 * c)) =
           make_float2(m[r][2 * c], m[r][2 * c + 1]);
+  if (lane < kCS) g.racc[base + lane] = 0.0;
+}
+
+__global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __restrict__ A,
+                                                 const double* __restrict__ rhs, int invert) {
+  if (g.flags[F_STOPPED]) return;
+  const int lane = threadIdx.x;
+  const int base = blockIdx.x * kCS;
+  const int ti = lane / kCS, tj = lane % kCS;
+  (void)lm; (void)invert;   // A arrives damped (k_assemble)
+  float m[6][6];
+  cluster_invert(g, A, blockIdx.x, lane, m);
   // PCG bookkeeping of this GN step (as k_pcg_proj: after the workgroup's loads)
-  if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; g.flags[F_REFRESH] = 0;
+  }
   if (g.warm_now) return;
   // cold start: u = M⁻¹ b with the stored (f32) operator; the 8 lanes of a block row sum in fixed order
   double bj[6], u[6];
@@ -1398,8 +1415,12 @@ __device__ __forceinline__ void proj_accumulate(const double bk[36], const doubl
 // rows' b and history values leave in the first trip with the stop flag; the second trip is every block of the wave
 // (lane l: blocks l and l + 64) with the kProj history rows it multiplies; the products meet in LDS and each row sums
 // its blocks in CSR order. (The row form's first trip is row_ptr, then col, then blocks + gathers.)
+// A GN step flagged by the previous step's update (F_REFRESH = this step: some node rotated by more than
+// precond_rot_tol since its cluster inverse was built) first rebuilds the cluster inverses here, one wave per
+// cluster as k_pcg_prep (k_pcg_proj2 applies them); otherwise the flag costs one scalar load with the stop flag.
 template <bool kWave>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs,
+                                                                                              int gn_iter) {
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
   asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.col), "s"(g.xh), "s"(g.th), "s"(g.N), "s"(g.flags), "s"(g.n_prev),
                "s"(g.Aop), "s"(g.part_p), "s"(g.nw_pad), "s"(rhs));
@@ -1421,8 +1442,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
     for (int j = 0; j < kProj; ++j) xo[j] = g.xh[j * stride + oc];
     const int stopped = g.flags[F_STOPPED];
+    const int refresh = g.flags[F_REFRESH];
     asm volatile("" ::: "memory");   // the loads above leave with the stop flag (one trip)
     if (stopped) return;
+    if (refresh == gn_iter) {
+      float mm[6][6];
+      cluster_invert(g, g.Aop, wv, lane, mm);
+    }
     const int np = g.n_prev;
     double2 ab[2][18], xb[2][kProj][3];
 #pragma unroll
@@ -1495,7 +1521,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int lane = threadIdx.x;
   const int q = lane % kSL, row = blockIdx.x * kRW + lane / kSL;
   const int b0 = g.row_ptr[row], b1 = g.row_ptr[row + 1];   // issued with the stop flag: one trip
+  const int refresh = g.flags[F_REFRESH];
   if (g.flags[F_STOPPED]) return;
+  if (refresh == gn_iter) {
+    float mm[6][6];
+    cluster_invert(g, g.Aop, blockIdx.x, lane, mm);
+  }
   const int np = g.n_prev;
   const int64_t stride = 6 * (int64_t)g.N;
   double n[kProj][6];
@@ -1720,6 +1751,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = reinterpret_cast<uint64_t>(g.Mcl);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
+    // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
+    g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? g.pcs[kScScal + S_TH_CUR] : 1e300;
+    g.pcs[kScScal + S_TH_CUR] = 1e300;
   }
   if (stopped) return;
   const double b = own ? bo : 0.0;
@@ -1823,6 +1857,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 struct StepArgs {
   double *R, *t, *xh, *stat, *loss_log, *step_state;
   const double* conf;
+  double* racc;
 };
 struct PcgIt {
   const double* Aop;
@@ -1839,6 +1874,7 @@ struct PcgIt {
   const StepArgs* sa;
   const double* tail;           // rhs + 6N: [loss² total, data, arap, motion, nonfinite]
   double stop_loss_diff;
+  double rot_tol;               // precond_rot_tol
   int32_t fuse, gn_iter, N, mode, n_iter_log, warm;
   int32_t ep;                   // this solve's epoch (stop words, H_DONE)
 };
@@ -1851,7 +1887,7 @@ static PcgIt pcg_args(const Gn* g) {
   a.flags = g->flags; a.hflags = g->hflags; a.stopw = g->stopw; a.stamps = g->stamps;
   a.nwg_row = g->nwg_row; a.nw_pad = g->nw_pad; a.prm.pcg_tol = g->prm.pcg_tol; a.prm.pcg_err_tol = g->prm.pcg_err_tol;
   a.sturm = g->sturm;
-  a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff;
+  a.sa = g->step_args; a.tail = nullptr; a.stop_loss_diff = g->prm.stop_loss_diff; a.rot_tol = g->prm.precond_rot_tol;
   a.fuse = 0; a.gn_iter = 0; a.N = g->N; a.mode = g->prm.mode; a.n_iter_log = 64; a.warm = g->prm.pcg_warm;
   a.ep = g->ep;
   return a;
@@ -1938,6 +1974,11 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int ep, int gn_iter, 
   for (int c = 0; c < 9; ++c) R[c] = Rn[c];
 #pragma unroll
   for (int c = 0; c < 3; ++c) sa.t[3 * (int64_t)row + c] += x[3 + c];
+  if (g.rot_tol > 0.0) {   // adaptive preconditioner refresh: the next step's warm start rebuilds the cluster inverses
+    const double acc = sa.racc[row] + sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    sa.racc[row] = acc;
+    if (acc > g.rot_tol) g.flags[F_REFRESH] = gi + 1;
+  }
 }
 
 // kW2 (with kWave): TWO waves per cluster. Wave h multiplies block slot h·64 + lane (one block per lane, not
@@ -2011,6 +2052,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const double2 rg = *reinterpret_cast<const double2*>(scb + kScGamma + 2);   // 1/γ of parities 0, 1
   const double2 sd = reinterpret_cast<const double2*>(scb + kScSturm)[lane];   // (every wave loads it: the lead uses it)
   const double bb_stored = scb[kScScal + S_BB];
+  const double th_prev = scb[kScScal + S_TH_PREV];
   const double2 tols = *reinterpret_cast<const double2*>(scb + kScTol);       // pcg_tol, pcg_err_tol
   asm volatile("" ::: "memory");
   constexpr int kNB = kWave ? (kW2 ? 1 : 2) : 1;   // blocks per lane
@@ -2179,30 +2221,42 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // the Lanczos tridiagonal of the preconditioned operator grows by one row per iteration: T_kk = 1/α_k + β_{k-1}/α_{k-1},
   // T_{k,k-1}² = β_{k-1}/α_{k-1}² (β_{k-1} = γ_k/γ_{k-1}); its smallest eigenvalue (Ritz value) θ_k decreases towards
   // λ_min(M⁻¹A). Lane s of the lead wave keeps the LDLᵀ pivot d_k(σ_s) = T_kk - σ_s - T²_{k,k-1}/d_{k-1}(σ_s) of
-  // T_k - σ_s I for the shift σ_s = 2^(-s/2) and the count of negative pivots, which is the number of Ritz values
-  // below σ_s (Sylvester's inertia; the bisection count of LAPACK's dstebz): O(1) per iteration. θ̂ = the largest
-  // σ_s with no Ritz value below it (θ_k / √2 < θ̂ <= θ_k; 1 if θ_k >= 1; 0 below 2^-31.5), thr = (pcg_err_tol·θ̂)².
+  // T_k - σ_s I and the count of negative pivots, which is the number of Ritz values below σ_s (Sylvester's inertia;
+  // the bisection count of LAPACK's dstebz): O(1) per iteration. Shifts σ_s = 2^(-e_s/4), e_s = s for s < 40 (quarter
+  // octaves down to 2^-9.75), 2s - 40 beyond (half octaves down to 2^-21.5). θ̂ = the largest σ_s with no Ritz value below
+  // it (θ_k / 2^(1/4) < θ̂ <= θ_k above 2^-10; 1 if θ_k >= 1; 0 below the last shift). Early in a solve θ_k still
+  // over-estimates λ_min, so a GN step after the first also takes the previous step's final θ̂ when that is smaller (the
+  // step's operator differs little from the previous one's: on the moose a warm-started step stopped after 64
+  // iterations with 3.7e-5 left without it, tools/errstop_study.py). thr = (pcg_err_tol·min(θ̂, θ̂_prev))².
   double2 sd_new = sd;
-  double thr_new = 0.0;
+  double thr_new = 0.0, th_cur = 1e300;
+  auto shift = [](int s) {   // σ_s
+    const int e = s < 40 ? s : 2 * s - 40;
+    const int k = e & 3;
+    const double c = k == 0 ? 1.0 : k == 1 ? 0.84089641525371454303 : k == 2 ? 0.70710678118654752440
+                                                                            : 0.59460355750136053336;
+    return ldexp(c, -(e >> 2));
+  };
   if (wv == 0 && hw == 0 && etol > 0.0) {   // (workgroup-uniform)
     const double rca = 1.0 / alpha;
     const double diag = kFirst ? rca : rca + beta * ralpha_prev;
     const double e2 = kFirst ? 0.0 : beta * ralpha_prev * ralpha_prev;
-    const double sig = ldexp((lane & 1) ? 0.70710678118654752440 : 1.0, -(lane >> 1));
+    const double sig = shift(lane);
     double d = (diag - sig) - (kFirst ? 0.0 : e2 / sd.x);
     if (fabs(d) < 1e-300) d = -1e-300;        // an exact zero pivot counts as negative (dstebz's pivmin)
     const double c = (kFirst ? 0.0 : sd.y) + (d < 0.0 ? 1.0 : 0.0);
     sd_new = make_double2(d, c);
     const uint64_t free_ = __ballot(c == 0.0);   // the shifts with no Ritz value below them: a suffix of the lanes
-    const double th = free_ ? ldexp(((__ffsll((unsigned long long)free_) - 1) & 1) ? 0.70710678118654752440 : 1.0,
-                                    -((__ffsll((unsigned long long)free_) - 1) >> 1))
-                            : 0.0;
-    thr_new = (etol * th) * (etol * th);
+    const double th = free_ ? shift(__ffsll((unsigned long long)free_) - 1) : 0.0;
+    th_cur = th;
+    const double tu = fmin(th, th_prev);
+    thr_new = (etol * tu) * (etol * tu);
   }
   auto lead_stores = [&]() {
     if (lead) {
       sc_w[kScAlpha + 2 + par_] = 1.0 / alpha; sc_w[kScGamma + 2 + par_] = 1.0 / gam; flags_w[F_PCG_CNT] = cnt + 1;
       sc_w[kScAlpha + 4 + par_] = thr_new;
+      if (etol > 0.0) sc_w[kScScal + S_TH_CUR] = th_cur;
     }
     if (wv == 0 && hw == 0 && etol > 0.0) reinterpret_cast<double2*>(sc_w + kScSturm)[lane] = sd_new;
     if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
@@ -2345,7 +2399,7 @@ __global__ __launch_bounds__(256) void k_step(GnDev g, const double* __restrict_
     sum_streams<1, 16>(g.part_b, g.nwg_row, bbv);
     if (threadIdx.x == 0) {
       const bool done = g.flags[F_DONE] != 0;
-      if (!done) g.flags[F_PCG_TOTAL] += pcg_max;
+      if (!done) { g.flags[F_PCG_TOTAL] += pcg_max; g.flags[F_CAPPED] += 1; }
       if (gn_iter < kMaxLog) {
         g.stat[3 * gn_iter + 0] = done ? (double)g.flags[F_PCG_IT] : (double)pcg_max;
         g.stat[3 * gn_iter + 1] = bbv[0];
@@ -2396,6 +2450,11 @@ __global__ __launch_bounds__(256) void k_step(GnDev g, const double* __restrict_
     for (int c = 0; c < 3; ++c) Rn[3 * r + c] = Ri[3 * r] * R[c] + Ri[3 * r + 1] * R[3 + c] + Ri[3 * r + 2] * R[6 + c];
   for (int c = 0; c < 9; ++c) R[c] = Rn[c];
   for (int c = 0; c < 3; ++c) g.t[3 * i + c] += x[3 + c];
+  if (g.prm.precond_rot_tol > 0.0) {   // as fused_step
+    const double acc = g.racc[i] + sqrt(a0 * a0 + a1 * a1 + a2 * a2);
+    g.racc[i] = acc;
+    if (acc > g.prm.precond_rot_tol) g.flags[F_REFRESH] = gn_iter + 1;
+  }
 }
 
 // arap mode, lambda_flow = 0: remove each connected component's mean translation from the PCG
@@ -2434,6 +2493,7 @@ __global__ void k_finish(GnDev g, float* __restrict__ rot, float* __restrict__ t
     status[1] = g.flags[F_ACCEPTED];
     status[2] = g.flags[F_PCG_TOTAL];
     status[3] = g.flags[F_ILL];
+    status[4] = g.flags[F_CAPPED];
   }
   if (loss_out && i < 4 * n_log) loss_out[i] = (i / 4 < g.flags[F_ACCEPTED]) ? g.loss_log[i] : 0.0;
 }
@@ -2451,7 +2511,7 @@ static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->Aw, g->stopw, g->blk_off, g->blk_cnt,
                   g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
-                  g->st, g->m0, g->m1, g->pcs,
+                  g->st, g->m0, g->m1, g->pcs, g->racc,
                   g->part_p, g->part_b, g->part_loss,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
                   g->up_of, g->up_slot, g->up_tr};
@@ -2563,6 +2623,7 @@ static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
 static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   double lm = lm_for_iter(g->prm.lm_factor, gn_iter);
   g->ep = g->ep_next++;   // this solve's epoch (read by the launches below through their GnDev / PcgIt copies)
+  g->gn_iter_now = gn_iter;
   g->warm_now = 0;
   if (g->prm.pcg_warm && gn_iter > 0) {   // k_step of the previous steps filled the ring
     g->n_prev = gn_iter < kProj ? gn_iter : kProj;
@@ -2577,8 +2638,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
   if (invert) hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
   if (g->warm_now) {
-    if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
-    else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
+    else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     switch (g->pcg_ku) {
       case 2: hipLaunchKernelGGL(k_pcg_proj2<2>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
       case 3: hipLaunchKernelGGL(k_pcg_proj2<3>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
@@ -2786,7 +2847,8 @@ static bool same_params(const ofx_gn_params& a, const ofx_gn_params& b) {
          a.pcg_max_iter == b.pcg_max_iter && a.pcg_warm == b.pcg_warm && a.lambda_flow == b.lambda_flow &&
          a.lambda_depth == b.lambda_depth && a.lambda_arap == b.lambda_arap && a.lambda_motion == b.lambda_motion &&
          a.lm_factor == b.lm_factor && a.stop_loss_diff == b.stop_loss_diff && a.pcg_tol == b.pcg_tol &&
-         a.mode == b.mode && a.precond_every == b.precond_every && a.pcg_err_tol == b.pcg_err_tol;
+         a.mode == b.mode && a.precond_every == b.precond_every && a.pcg_err_tol == b.pcg_err_tol &&
+         a.precond_rot_tol == b.precond_rot_tol;
 }
 
 }  // namespace ofx
@@ -2819,7 +2881,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->anc, 4 * M);
   ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 2);
   ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
-  ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N);
+  ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N); ALLOC(g->racc, N);
   ALLOC(g->Mcl, 6 * N * kCD); ALLOC(g->st, V_N * 6 * N); ALLOC(g->m0, 6 * N); ALLOC(g->m1, 6 * N);
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N); ALLOC(g->step_args, 1);
   ALLOC(g->perm, N); ALLOC(g->iperm, max_nodes); ALLOC(g->wl, N / kCS * kWL); ALLOC(g->Aw, N / kCS * kWL * 36);
@@ -2852,7 +2914,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     free_all(g); delete g; set_error("hipHostMalloc failed"); return OFX_ERR_ALLOC;
   }
   {   // the fused GN step's fixed pointers (fused_step), in device memory
-    const StepArgs h{g->R, g->t, g->xh, g->stat, g->loss_log, g->step_state, g->conf};
+    const StepArgs h{g->R, g->t, g->xh, g->stat, g->loss_log, g->step_state, g->conf, g->racc};
     if (hipMemcpy(g->step_args, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
       free_all(g); delete g; set_error("hipMemcpy failed"); return OFX_ERR_HIP;
     }
@@ -3114,6 +3176,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   OFX_CHECK_ARG(pb->n_matches == 0 || (pb->src && pb->anchors && pb->weights && pb->tgt), "null match buffers");
   OFX_CHECK_ARG(prm->num_iter >= 0 && prm->num_iter <= 64, "num_iter must be in [0,64]");
   OFX_CHECK_ARG(prm->pcg_max_iter >= 1, "pcg_max_iter must be >= 1");
+  OFX_CHECK_ARG(prm->precond_rot_tol >= 0.0, "precond_rot_tol must be >= 0");
   hipStream_t hs = as_stream(s);
   int N0 = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
   if ((int64_t)N0 * NB > 0) OFX_CHECK_ARG(pb->edges, "null edges");

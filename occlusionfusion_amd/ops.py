@@ -205,10 +205,11 @@ def _gn_problem(nodes, edges, edge_weights, tpos, conf, src, anchors, weights, t
 
 def _gn_params(fparams, iparams):
     """fparams = [lambda_flow, lambda_depth, lambda_arap, lambda_motion, lm_factor, stop_loss_diff, pcg_tol,
-    pcg_err_tol]; iparams = [num_iter, use_edge_weighting, pcg_max_iter, pcg_warm, mode, precond_every]."""
+    pcg_err_tol, precond_rot_tol]; iparams = [num_iter, use_edge_weighting, pcg_max_iter, pcg_warm, mode,
+    precond_every]."""
     p = _lib.GnParams()
     (p.lambda_flow, p.lambda_depth, p.lambda_arap, p.lambda_motion, p.lm_factor, p.stop_loss_diff,
-     p.pcg_tol, p.pcg_err_tol) = (float(v) for v in fparams)
+     p.pcg_tol, p.pcg_err_tol, p.precond_rot_tol) = (float(v) for v in fparams)
     p.num_iter, p.use_edge_weighting, p.pcg_max_iter, p.pcg_warm, p.mode, p.precond_every = (int(v) for v in iparams)
     return p
 
@@ -216,7 +217,7 @@ def _gn_params(fparams, iparams):
 def _gn_outputs(N, num_iter, device):
     # k_finish writes every element (status and all num_iter loss rows): no fill kernels
     return (torch.empty((N, 3, 3), device=device), torch.empty((N, 3), device=device),
-            torch.empty(4, dtype=torch.int32, device=device),
+            torch.empty(5, dtype=torch.int32, device=device),
             torch.empty((num_iter, 4), dtype=torch.float64, device=device))
 
 
@@ -232,7 +233,8 @@ def gn_solve(state: Tensor, handle: int, nodes: Tensor, edges: Tensor, edge_weig
              target_py: Optional[Tensor], prev_rot: Optional[Tensor], prev_trans: Optional[Tensor],
              intr: List[float], fparams: List[float], iparams: List[int]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """DeformNet.optimize (model/model.py:222-859) for one batch item on the device: -> (node_rotations (N,3,3),
-    node_translations (N,3), status int32[4] = [valid, GN steps, PCG iterations, ill-posed], loss f64[num_iter,4])."""
+    node_translations (N,3), status int32[5] = [valid, GN steps, PCG iterations, ill-posed, GN steps whose PCG hit
+    pcg_max_iter], loss f64[num_iter,4])."""
     pb = _gn_problem(nodes, edges, edge_weights, tpos, conf, src, anchors, weights, tgt, target_px, target_py,
                      prev_rot, prev_trans, intr)
     prm = _gn_params(fparams, iparams)
@@ -245,7 +247,7 @@ def gn_solve(state: Tensor, handle: int, nodes: Tensor, edges: Tensor, edge_weig
 def _(state, handle, nodes, edges, edge_weights, tpos, conf, src, anchors, weights, tgt, target_px, target_py,
       prev_rot, prev_trans, intr, fparams, iparams):
     N = nodes.shape[0]
-    return (nodes.new_empty((N, 3, 3)), nodes.new_empty((N, 3)), nodes.new_empty((4,), dtype=torch.int32),
+    return (nodes.new_empty((N, 3, 3)), nodes.new_empty((N, 3)), nodes.new_empty((5,), dtype=torch.int32),
             nodes.new_empty((int(iparams[0]), 4), dtype=torch.float64))
 
 
@@ -333,7 +335,7 @@ def gn_finish(state: Tensor, handle: int, n_nodes: int, num_iter: int) -> Tuple[
 @gn_finish.register_fake
 def _(state, handle, n_nodes, num_iter):
     return (state.new_empty((n_nodes, 3, 3), dtype=torch.float32), state.new_empty((n_nodes, 3), dtype=torch.float32),
-            state.new_empty((4,), dtype=torch.int32), state.new_empty((num_iter, 4), dtype=torch.float64))
+            state.new_empty((5,), dtype=torch.int32), state.new_empty((num_iter, 4), dtype=torch.float64))
 
 
 OPS = ("integrate", "integrate_points", "raycast", "skin_points", "deform_points", "gn_solve", "gn_prepare", "gn_setup",

@@ -25,7 +25,7 @@ from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
                    lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=2000, pcg_tol=2e-6,
-                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5)
+                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5, precond_rot_tol=0.1)
 MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
 
 
@@ -144,7 +144,7 @@ class GaussNewtonSolver:
         q = self.params
         fp = [float(q["lambda_flow"]), float(q["lambda_depth"]), float(q["lambda_arap"]), float(q["lambda_motion"]),
               float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"] if pcg_tol is None else pcg_tol),
-              float(q.get("pcg_err_tol", 0.0))]
+              float(q.get("pcg_err_tol", 0.0)), float(q.get("precond_rot_tol", 0.0))]
         ip = [int(q["num_iter"]), int(bool(q["use_edge_weighting"])), int(q["pcg_max_iter"]), int(bool(q["pcg_warm"])),
               int(mode), int(q.get("precond_every", 1))]
         return fp, ip
@@ -185,8 +185,8 @@ class GaussNewtonSolver:
             res["convergence_info"] = {"total": loss[:, 0].tolist(), "data": loss[:, 1].tolist(),
                                        "arap": loss[:, 2].tolist(), "motion": loss[:, 3].tolist(),
                                        "valid": int(st[0]), "gn_iterations": int(st[1]),
-                                       "pcg_iterations": int(st[2]), "errors": (["Solver failed: Ill-posed system!"]
-                                                                                if st[3] else [])}
+                                       "pcg_iterations": int(st[2]), "pcg_capped_steps": int(st[4]),
+                                       "errors": ["Solver failed: Ill-posed system!"] if st[3] else []}
         return res
 
     def optimize(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,
@@ -287,7 +287,8 @@ class GaussNewtonSolver:
             ci = res["convergence_info"]
             res["convergence_info"] = {"total": ci["total"], "arap": ci["arap"], "data": ci["data"],
                                        "condition_numbers": [], "valid": ci["valid"], "errors": ci["errors"],
-                                       "gn_iterations": ci["gn_iterations"], "pcg_iterations": ci["pcg_iterations"]}
+                                       "gn_iterations": ci["gn_iterations"], "pcg_iterations": ci["pcg_iterations"],
+                                       "pcg_capped_steps": ci["pcg_capped_steps"]}
         return res
 
     def optimize_distributed(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position,

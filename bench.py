@@ -282,7 +282,19 @@ def main():
     # of every listed brick + the brick's palette (64 x u16 + count); weights 16 B + tsdf/weight 8 B read
     # per skin-valid voxel; per updated voxel tsdf/weight write 8 B + colour read+write 8 B. Node records
     # and the depth/colour images are L2-resident and not counted.
-    B = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
+    B_listed = cache.n_list * (512 * 4 + 132) + n_skin_valid * 24 + U * 16
+    # with the brick cull (ofx_integrate_palette_cull, the default): the bricks it keeps move those bytes, every listed
+    # brick its palette count + ids (132 B) and flag (1 B) through the cull, and the depth image is read once for the
+    # tile maxima; the timed span covers the three kernels
+    act = getattr(vol, "_cull", None) if getattr(vol, "brick_cull", False) else None
+    if act is not None and cache.n_list:
+        live = act[1][:cache.n_list].to(torch.bool)
+        sv_slot = (cache.anchors.view(cache.n_list, 512, 4)[:, :, K - 1] != -1).sum(1)
+        n_live, sv_live = int(live.sum().item()), int(sv_slot[live].sum().item())
+        H_, W_ = (int(v) for v in vol.depth_t.shape)
+        B = n_live * (512 * 4 + 132) + cache.n_list * 133 + H_ * W_ * 4 + sv_live * 24 + U * 16
+    else:
+        n_live, sv_live, B = cache.n_list, n_skin_valid, B_listed
     achieved = B / t_kint
     # SURVEY §8(d)'s per-unit figure over the voxels this launch processes (every voxel of a listed brick):
     # 32 B skin + 8 B tsdf/weight read per voxel, 8 B tsdf/weight write per updated voxel (colour separately)
@@ -332,13 +344,18 @@ def main():
                              "kernel-boundary floor + two dependent memory trips + the wave's instruction stream "
                              "(DESIGN.md §5); the 11-12 MB working set is L2/MALL-resident across launches. frac = "
                              "bytes_per_launch / avg_launch_us / peak"},
-        "roofline_integrate": {"kernel": "k_integrate_pal4 (fused warp+integrate, LDS node palette; VALU-bound: "
-                                         "DESIGN.md section 5)", "bound": "hbm",
+        "roofline_integrate": {"kernel": "k_tile_max + k_brick_cull + k_integrate_pal4 (per-frame brick cull, then the "
+                                         "fused warp+integrate with an LDS node palette; VALU-bound: DESIGN.md "
+                                         "section 5)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp", workload),
                                "bytes_per_launch": B,
-                               "bytes_note": "this layout's minimal bytes (palette ranks, reads for skin-valid voxels "
-                                             "only); SURVEY 8(d)'s per-unit figure over the processed voxels below",
+                               "bytes_note": "this layout's minimal bytes for the bricks the per-frame cull keeps "
+                                             "(palette ranks, reads for skin-valid voxels only) + the cull's own reads; "
+                                             "frac_listed_bytes: the same per-unit bytes over every listed brick (the "
+                                             "work the launch covers); SURVEY 8(d)'s per-unit figure below",
+                               "cull_kept_bricks": n_live, "cull_kept_skin_valid_voxels": sv_live,
+                               "listed_bytes_per_launch": B_listed, "frac_listed_bytes": B_listed / t_kint / PEAK_HBM,
                                "survey_bytes_per_launch": B_survey, "frac_survey_bytes": B_survey / t_kint / PEAK_HBM,
                                "avg_launch_us": 1e6 * t_kint, "timing": "20 launches of the last frame in isolation "
                                "(library hipEvents around each launch)", "in_loop_avg_launch_us": 1e6 * t_kint_loop,

@@ -22,6 +22,7 @@
  *   ofx_integrate           WarpField.deform_tsdf + TSDFVolume.integrate    warpfield.py:369-380, tsdf.py:378-494
  *                           (fused: skin cache -> ED warp -> project -> SDF/weight/colour update)
  *   ofx_integrate_palette   same, node records staged per brick in LDS      warpfield.py:369-380, tsdf.py:442-494
+ *   ofx_integrate_palette_cull  same, bricks that provably update nothing skipped (per-frame cull)
  *   ofx_integrate_points    TSDFVolume.integrate of given (deformed) points  tsdf.py:442-494
  *   ofx_raycast             (new) depth / normal / colour images of the TSDF  — (no reference twin)
  *   ofx_deform_points       ED_warp / deform_ED / deform_mesh / normals     NonRigidICP/model/geometry.py:9-25,
@@ -174,6 +175,19 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
                           const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
                           double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
                           ofx_stream_t s);
+
+/* ofx_integrate_palette with a per-frame brick cull in front (CPU semantics, k = 4; otherwise it is
+ * ofx_integrate_palette): per 8x8 pixel tile the largest depth (tile_scratch: f32[ceil(W/8)*ceil(H/8)]), then per
+ * listed brick a conservative box of its warped voxels (each palette node's rigid image of the brick, scaled by the
+ * skin weights' sum range) tested against the camera and those tiles; bricks that provably update no voxel are
+ * skipped (active: u8[n_list] receives the flags; n_updated gets 0 for them). Bit-identical results. MI355X-specific:
+ * no reference twin (the reference walks every voxel, tsdf.py:442-494). */
+int ofx_integrate_palette_cull(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth,
+                               const float* color_im, const float* packed_nodes, int32_t n_nodes, int32_t k,
+                               const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
+                               const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
+                               double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
+                               float* tile_scratch, uint8_t* active, ofx_stream_t s);
 
 /* Profiling hook (process-wide): returns (and resets) the device time of the warped integrate kernel launches
  * (ofx_integrate warp = 1, ofx_integrate_palette) recorded since the last call, from hipEvents recorded by the

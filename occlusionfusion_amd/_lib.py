@@ -64,6 +64,8 @@ _SIGS = {
     "ofx_raycast": [P, P, P, P, P, c_float, c_float, P, P, P, P],
     "ofx_integrate_points": [P, P, P, P, P, P, P, c_int64, c_double, P, P, P, P, P],
     "ofx_integrate_palette": [P, P, P, P, P, c_int32, c_int32, P, c_int32, P, P, P, P, P, c_double, P, P, P, P, P],
+    "ofx_integrate_palette_cull": [P, P, P, P, P, c_int32, c_int32, P, c_int32, P, P, P, P, P, c_double, P, P, P, P, P,
+                                   P, P],
     "ofx_deform_points": [P, c_int64, P, P, P, c_int32, P, c_int32, c_int32, P, P],
     "ofx_deform_points_lbs": [P, c_int64, P, P, P, c_int32, P, P, c_int32, P, P],
     "ofx_visibility": [P, c_int64, P, P, c_double, P, P, P],

@@ -414,7 +414,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const float4* __restrict__ nodes, int n_nodes, const int32_t* __restrict__ list,
     const ushort4* __restrict__ anchors, const float4* __restrict__ weights, const uint16_t* __restrict__ pal_ids,
     const int32_t* __restrict__ pal_n, const uchar4* __restrict__ local, double trunc, double itrunc, double obs,
-    float* __restrict__ tsdf, float* __restrict__ weight, float* __restrict__ color, uint32_t* counter) {
+    float* __restrict__ tsdf, float* __restrict__ weight, float* __restrict__ color, uint32_t* counter,
+    const uint8_t* __restrict__ active) {
   __shared__ float4 s_node[4 * kPal];
   __shared__ float s_xyz[3 * kBrick];   // vox2world of the brick's 8 x, y and z coordinates
   __shared__ uint32_t s_cnt[4];
@@ -427,7 +428,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   uchar4 la[2];
   la[0] = local[slot * kBrickVox + tid];
   la[1] = local[slot * kBrickVox + tid + 256];
+  const int live = active ? (int)active[slot] : 1;   // (uniform: a scalar load, with trip 1)
   asm volatile("" ::: "memory");
+  if (!live) {   // k_brick_cull proved that no voxel of this brick updates (the whole workgroup leaves)
+    if (counter && tid == 0) counter[blockIdx.x] = 0;
+    return;
+  }
   int i0, j0, k0;
   brick_coords(g, bd, b, i0, j0, k0);
   const bool use_pal = pn <= kPal;
@@ -519,6 +525,147 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     __syncthreads();
     if (tid == 0) counter[blockIdx.x] = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
   }
+}
+
+// ---- brick cull of the warped integrate (ofx_integrate_palette_cull): which listed bricks can update a voxel at all.
+// Per 8x8 pixel tile the largest depth (NaN pixels never update and are skipped; +inf propagates). One thread per tile,
+// the tile's 8 rows as 2 x 16-B loads each (lanes = consecutive tiles of a tile row: coalesced); W % 4 == 0 (else the
+// per-pixel loop).
+__global__ __launch_bounds__(256) void k_tile_max(const float* __restrict__ depth, int W, int H, int TW, int TH,
+                                                  float* __restrict__ tiles) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= TW * TH) return;
+  const int tx = t % TW, ty = t / TW;
+  float m = 0.f;
+  if ((W & 3) == 0 && tx * 8 + 8 <= W && ty * 8 + 8 <= H) {
+    float4 v[16];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float4* p = reinterpret_cast<const float4*>(depth + (int64_t)(ty * 8 + r) * W + tx * 8);
+      v[2 * r] = p[0];
+      v[2 * r + 1] = p[1];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m = fmaxf(m, fmaxf(fmaxf(v[k].x, v[k].y), fmaxf(v[k].z, v[k].w)));
+  } else {
+    for (int y = ty * 8; y < min(ty * 8 + 8, H); ++y)
+      for (int x = tx * 8; x < min(tx * 8 + 8, W); ++x) m = fmaxf(m, depth[(int64_t)y * W + x]);
+  }
+  tiles[t] = m;
+}
+
+// 16 lanes per listed brick (4 bricks per wave). A voxel p of the brick warps to Σ_k w_k T_k(p) with T_k(p) =
+// R_k(p - g_k) + g_k + t_k over its (palette) anchors, weights w_k >= 0 of sum S = Σ/(Σ + 1e-6) (warpfield.py:121) with
+// S in [0.999, 1] (every valid anchor lies within 4σ: each w >= exp(-8), Σ >= 1.3e-3). T_k maps the box of the brick's
+// voxel centres [c ± h] into [T_k(c) ± |R_k| h] (any matrix R_k); so the warped voxels lie in the box B spanning those
+// boxes and their S-scaled copies, grown by a margin far above f32 rounding (1e-4 m). The brick can update a voxel only
+// if some point of B has z > 0 projecting into the image (the pixel range of B's corners, ±1 px) onto a pixel of depth
+// d > 0 with d - z >= -trunc, i.e. if the largest depth over the tiles of that range is >= z_min(B) - trunc. Bricks
+// whose box reaches z < 1e-3, spans more than 64 tiles, or whose palette overflowed are kept (active).
+__device__ __forceinline__ float grp16_min(float x) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) x = fminf(x, __shfl_xor(x, off, 16));
+  return x;
+}
+__device__ __forceinline__ float grp16_max(float x) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) x = fmaxf(x, __shfl_xor(x, off, 16));
+  return x;
+}
+__global__ __launch_bounds__(256) void k_brick_cull(BrickGeom g, BrickDiv bd, CamD c, const float4* __restrict__ nodes,
+                                                    int n_nodes, const int32_t* __restrict__ list,
+                                                    const uint16_t* __restrict__ pal_ids, const int32_t* __restrict__ pal_n,
+                                                    int n_list, const float* __restrict__ tiles, int TW, int TH,
+                                                    double trunc, uint8_t* __restrict__ active) {
+  const int sub = threadIdx.x & 15;
+  const int s = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int sc = s < n_list ? s : n_list - 1;   // (the last group of the grid may overhang: clamped, not stored)
+  const int pn = pal_n[sc];
+  const uint32_t b = (uint32_t)list[sc];
+  int pid[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pid[i] = pal_ids[(int64_t)sc * kPal + sub + 16 * i];
+  int i0, j0, k0;
+  brick_coords(g, bd, b, i0, j0, k0);
+  // the voxel centres of the brick (clipped to the volume) span [lo, hi] per axis
+  const int ni = min(kBrick, g.Dx - i0), nj = min(kBrick, g.Dy - j0), nk = min(kBrick, g.Dz - k0);
+  const float cx0 = vox2world(g.ox, g.vs, i0), cx1 = vox2world(g.ox, g.vs, i0 + ni - 1);
+  const float cy0 = vox2world(g.oy, g.vs, j0), cy1 = vox2world(g.oy, g.vs, j0 + nj - 1);
+  const float cz0 = vox2world(g.oz, g.vs, k0), cz1 = vox2world(g.oz, g.vs, k0 + nk - 1);
+  const float px = 0.5f * (cx0 + cx1), py = 0.5f * (cy0 + cy1), pz = 0.5f * (cz0 + cz1);
+  const float hx = 0.5f * (cx1 - cx0), hy = 0.5f * (cy1 - cy0), hz = 0.5f * (cz1 - cz0);
+  float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
+  float4 rec[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {   // (clamped, unconditional: one memory trip)
+    const float4* n = nodes + 4 * (int64_t)min(max(pid[i], 0), n_nodes - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rec[i][q] = n[q];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (sub + 16 * i >= pn || pn > kPal) continue;
+    // record [R00 R10 R01 R11 | R02 R12 g0 g1 | t0 t1 R20 R21 | R22 g2 t2 0] (ofx_pack_nodes)
+    const float4 a = rec[i][0], bb = rec[i][1], cc = rec[i][2], d = rec[i][3];
+    const float dx = px - bb.z, dy = py - bb.w, dz = pz - d.y;
+    const float t0 = a.x * dx + a.z * dy + bb.x * dz + bb.z + cc.x;
+    const float t1 = a.y * dx + a.w * dy + bb.y * dz + bb.w + cc.y;
+    const float t2 = cc.z * dx + cc.w * dy + d.x * dz + d.y + d.z;
+    const float e0 = fabsf(a.x) * hx + fabsf(a.z) * hy + fabsf(bb.x) * hz + 1e-4f;
+    const float e1 = fabsf(a.y) * hx + fabsf(a.w) * hy + fabsf(bb.y) * hz + 1e-4f;
+    const float e2 = fabsf(cc.z) * hx + fabsf(cc.w) * hy + fabsf(d.x) * hz + 1e-4f;
+    lo[0] = fminf(lo[0], t0 - e0); hi[0] = fmaxf(hi[0], t0 + e0);
+    lo[1] = fminf(lo[1], t1 - e1); hi[1] = fmaxf(hi[1], t1 + e1);
+    lo[2] = fminf(lo[2], t2 - e2); hi[2] = fmaxf(hi[2], t2 + e2);
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) { lo[q] = grp16_min(lo[q]); hi[q] = grp16_max(hi[q]); }
+  bool keep = pn > kPal || pn <= 0;
+  float zmin = 0.f;
+  int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+  if (!keep) {
+    constexpr float kS = 0.999f;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const float l = lo[q], h = hi[q];
+      lo[q] = fminf(l, kS * l);
+      hi[q] = fmaxf(h, kS * h);
+    }
+    zmin = lo[2];
+    if (hi[2] > 0.f) {
+      if (!(lo[2] >= 1e-3f)) {
+        keep = true;
+      } else {
+        float umin = 3e38f, umax = -3e38f, vmin = 3e38f, vmax = -3e38f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float X = (k & 1) ? hi[0] : lo[0], Y = (k & 2) ? hi[1] : lo[1], Z = (k & 4) ? hi[2] : lo[2];
+          const float iz = 1.0f / Z;
+          const float u = c.fxf * X * iz + c.cxf, v = c.fyf * Y * iz + c.cyf;
+          umin = fminf(umin, u); umax = fmaxf(umax, u); vmin = fminf(vmin, v); vmax = fmaxf(vmax, v);
+        }
+        const float x0 = fmaxf(floorf(umin) - 1.f, 0.f), x1 = fminf(ceilf(umax) + 1.f, (float)(c.W - 1));
+        const float y0 = fmaxf(floorf(vmin) - 1.f, 0.f), y1 = fminf(ceilf(vmax) + 1.f, (float)(c.H - 1));
+        if (x0 <= x1 && y0 <= y1) {
+          tx0 = (int)x0 >> 3; tx1 = (int)x1 >> 3; ty0 = (int)y0 >> 3; ty1 = (int)y1 >> 3;
+          if ((tx1 - tx0 + 1) * (ty1 - ty0 + 1) > 64) keep = true;
+        }
+      }
+    }
+  }
+  // the tiles of the pixel range, 4 per lane
+  float dm = 0.f;
+  const int ntx = tx1 - tx0 + 1, nt = (tx1 >= tx0 && ty1 >= ty0) ? ntx * (ty1 - ty0 + 1) : 0;
+  if (!keep) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = sub + 16 * i;
+      if (e < nt) dm = fmaxf(dm, tiles[(int64_t)(ty0 + e / ntx) * TW + tx0 + e % ntx]);
+    }
+  }
+  dm = grp16_max(dm);
+  const bool upd = keep || (dm > 0.f && (double)dm - (double)zmin >= -trunc - 1e-4);
+  if (sub == 0 && s < n_list) active[s] = upd ? 1 : 0;
 }
 
 // Source frame (tsdf.py:395-398: every voxel at its world position, all valid) with per-brick projection
@@ -895,12 +1042,14 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
       OFX_TIMED_LAUNCH(timer, k_integrate_pal4<true>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
                          (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
-                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated,
+                         (const uint8_t*)nullptr);
     else
       OFX_TIMED_LAUNCH(timer, k_integrate_pal4<false>, dim3((unsigned)n_list), dim3(256), 0, as_stream(s), g, make_div(g),
                          make_cam(cam), depth, color_im, (const float4*)packed_nodes, n_nodes, brick_list,
                          (const ushort4*)anchors, (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors,
-                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated);
+                         desc->trunc_margin, 1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated,
+                         (const uint8_t*)nullptr);
     OFX_LAUNCH_CHECK();
     return OFX_OK;
   }
@@ -909,6 +1058,61 @@ int ofx_integrate_palette(const ofx_volume_desc* desc, const ofx_camera* cam, co
                      depth, color_im, (const float4*)packed_nodes, k, brick_list, (const ushort4*)anchors,
                      (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,
                      obs_weight, tsdf, weight, color, n_updated);
+  OFX_LAUNCH_CHECK();
+  return OFX_OK;
+}
+
+int ofx_integrate_palette_cull(const ofx_volume_desc* desc, const ofx_camera* cam, const float* depth,
+                               const float* color_im, const float* packed_nodes, int32_t n_nodes, int32_t k,
+                               const int32_t* brick_list, int32_t n_list, const uint16_t* anchors, const float* weights,
+                               const uint16_t* pal_ids, const int32_t* pal_n, const uint8_t* local_anchors,
+                               double obs_weight, float* tsdf, float* weight, float* color, uint32_t* n_updated,
+                               float* tile_scratch, uint8_t* active, ofx_stream_t s) {
+  BrickGeom g;
+  int st = make_geom(desc, &g);
+  if (st) return st;
+  OFX_CHECK_ARG(cam && depth, "null camera/depth");
+  OFX_CHECK_ARG(cam->width > 0 && cam->height > 0, "bad camera size");
+  const bool fast = desc->semantics == OFX_SEM_CPU && k == 4 && g.n_bricks * kBrickVox < (1ll << 31) &&
+                    !getenv("OFX_INT_GENERIC");
+  if (!fast || !tile_scratch || !active)   // the cull serves the CPU-semantics K = 4 palette kernel only
+    return ofx_integrate_palette(desc, cam, depth, color_im, packed_nodes, n_nodes, k, brick_list, n_list, anchors,
+                                 weights, pal_ids, pal_n, local_anchors, obs_weight, tsdf, weight, color, n_updated, s);
+  OFX_CHECK_ARG((color == nullptr) == (color_im == nullptr), "color and color_im must both be set or both NULL");
+  OFX_CHECK_ARG(n_nodes >= k, "bad k/n_nodes");
+  OFX_CHECK_ARG(n_list >= 0 && n_list <= g.n_bricks, "bad n_list");
+  if (n_list == 0) return OFX_OK;
+  OFX_CHECK_ARG(packed_nodes && brick_list && anchors && weights && pal_ids && pal_n && local_anchors,
+                "null warp/palette buffer");
+  hipStream_t hs = as_stream(s);
+  const CamD c = make_cam(cam);
+  const BrickDiv bd = make_div(g);
+  const int TW = (cam->width + 7) / 8, TH = (cam->height + 7) / 8;
+  IntTimer timer;   // one event pair around the three kernels (tile max, cull, integrate)
+  if (timer.e0)
+    hipExtLaunchKernelGGL(k_tile_max, dim3(grid_for((int64_t)TW * TH, 256)), dim3(256), 0, hs, timer.e0, nullptr, 0,
+                          depth, cam->width, cam->height, TW, TH, tile_scratch);
+  else
+    hipLaunchKernelGGL(k_tile_max, dim3(grid_for((int64_t)TW * TH, 256)), dim3(256), 0, hs, depth, cam->width,
+                       cam->height, TW, TH, tile_scratch);
+  hipLaunchKernelGGL(k_brick_cull, dim3((unsigned)((n_list + 15) / 16)), dim3(256), 0, hs, g, bd, c,
+                     (const float4*)packed_nodes, n_nodes, brick_list, pal_ids, pal_n, n_list,
+                     (const float*)tile_scratch, TW, TH, desc->trunc_margin, active);
+  auto launch = [&](auto kern) {
+    if (timer.e0)
+      hipExtLaunchKernelGGL(kern, dim3((unsigned)n_list), dim3(256), 0, hs, nullptr, timer.e1, 0, g, bd, c, depth,
+                            color_im, (const float4*)packed_nodes, n_nodes, brick_list, (const ushort4*)anchors,
+                            (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,
+                            1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated,
+                            (const uint8_t*)active);
+    else
+      hipLaunchKernelGGL(kern, dim3((unsigned)n_list), dim3(256), 0, hs, g, bd, c, depth, color_im,
+                         (const float4*)packed_nodes, n_nodes, brick_list, (const ushort4*)anchors,
+                         (const float4*)weights, pal_ids, pal_n, (const uchar4*)local_anchors, desc->trunc_margin,
+                         1.0 / desc->trunc_margin, obs_weight, tsdf, weight, color, n_updated, (const uint8_t*)active);
+  };
+  if (color) launch(k_integrate_pal4<true>);
+  else launch(k_integrate_pal4<false>);
   OFX_LAUNCH_CHECK();
   return OFX_OK;
 }

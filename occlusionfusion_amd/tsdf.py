@@ -131,6 +131,10 @@ class TSDFVolume:
             self.owned_bricks = torch.from_numpy(np.nonzero(mask)[0].astype(np.int32)).to(self.device)
         self.with_color = True
         self.use_palette = True    # warped integrate through the skin cache's LDS node palette
+        # per-frame brick cull in front of the palette integrate (ofx_integrate_palette_cull): bricks whose warped
+        # voxels provably update nothing are skipped; bit-identical results
+        self.brick_cull = True
+        self._cull = None          # (tile maxima, per-slot flags) scratch of the cull
         call("ofx_volume_reset", byref(self.desc), ptr(self.tsdf_b), ptr(self.weight_b), ptr(self.color_b), stream_ptr())
         self.warpfield = None
         self._world_pts = None
@@ -215,10 +219,19 @@ class TSDFVolume:
         nodes = self.warpfield.packed_nodes()
         pal = self.use_palette and cache.pal_n is not None
         if pal:   # the frame loop's path: the library call of torch.ops.ofx.integrate's palette branch, made directly
-            call("ofx_integrate_palette", byref(d), byref(self.camera()), ptr(self.depth_t), ptr(color_im), ptr(nodes),
-                 self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
-                 ptr(cache.weights), ptr(cache.pal_ids), ptr(cache.pal_n), ptr(cache.local), float(obs_weight),
-                 ptr(self.tsdf_b), ptr(self.weight_b), ptr(color), ptr(nu), stream_ptr())
+            args = (byref(d), byref(self.camera()), ptr(self.depth_t), ptr(color_im), ptr(nodes),
+                    self.warpfield.num_nodes, cache.k, ptr(cache.brick_list), cache.n_list, ptr(cache.anchors),
+                    ptr(cache.weights), ptr(cache.pal_ids), ptr(cache.pal_n), ptr(cache.local), float(obs_weight),
+                    ptr(self.tsdf_b), ptr(self.weight_b), ptr(color), ptr(nu))
+            if self.brick_cull:
+                H, W = (int(v) for v in self.depth_t.shape)
+                nt = ((W + 7) // 8) * ((H + 7) // 8)
+                if self._cull is None or self._cull[0].numel() < nt or self._cull[1].numel() < cache.n_list:
+                    self._cull = (torch.empty(nt, dtype=torch.float32, device=self.device),
+                                  torch.empty(max(1, cache.n_list), dtype=torch.uint8, device=self.device))
+                call("ofx_integrate_palette_cull", *args, ptr(self._cull[0]), ptr(self._cull[1]), stream_ptr())
+            else:
+                call("ofx_integrate_palette", *args, stream_ptr())
             return
         torch.ops.ofx.integrate(self.tsdf_b, self.weight_b, color, nu, self.depth_t, color_im, *geo(),
                                 nodes, self.warpfield.num_nodes, cache.k, cache.brick_list, cache.n_list,

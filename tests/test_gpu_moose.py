@@ -126,6 +126,22 @@ def test_moose_landmark_gn_matches_dense_oracle(cuda, moose):
     assert g["loss_total"][-1] < 0.1 * g["loss_total"][0]     # the landmarks really pulled the graph
 
 
+def test_moose_preconditioner_refresh_cuts_pcg_work(cuda, moose):
+    """Real data rotates nodes by up to ~1 rad per GN step, so a cluster inverse built at step 0 goes stale: with the
+    round-4 policy (precond_rot_tol = 0: one inverse per solve) the moose optimize needed ≈10.4k PCG iterations
+    (≈1,000 per GN step). The default rebuilds a cluster inverse when a node's accumulated rotation passes 0.1 rad
+    (k_pcg_proj, F_REFRESH): ≈1.2k iterations, no step capped at pcg_max_iter, and still within 1e-5 of the f64
+    oracle. The stale-preconditioner run is also within 1e-5 (only the work differs)."""
+    g = moose
+    out, dr, dt = _moose_gn(g)
+    old, dr0, dt0 = _moose_gn(g, precond_rot_tol=0.0)
+    ci, ci0 = out["convergence_info"], old["convergence_info"]
+    assert ci["pcg_capped_steps"] == 0 and ci0["pcg_capped_steps"] == 0
+    assert ci["pcg_iterations"] <= 3000, ci["pcg_iterations"]
+    assert ci0["pcg_iterations"] >= 3 * ci["pcg_iterations"], (ci0["pcg_iterations"], ci["pcg_iterations"])
+    assert max(dr, dt, dr0, dt0) < 1e-5, (dr, dt, dr0, dt0)
+
+
 def test_moose_residual_stop_alone_misses_the_bar(cuda, moose):
     """Why the error-based stop: with the relative residual alone (pcg_err_tol = 0) the same solve stops ≈100x short
      and misses 1e-5 on the transforms — worse than the reference's own dense f32 LU on the first system

@@ -38,7 +38,7 @@ def _graph(g):
 
 def test_library_is_native(cuda):
     from occlusionfusion_amd import _lib
-    assert _lib.lib.ofx_abi_version() == 2
+    assert _lib.lib.ofx_abi_version() == 3
     assert os.path.exists(_lib.LIB_PATH)
 
 
@@ -433,6 +433,34 @@ def test_gn_stop_with_unconverged_pcg_keeps_the_stopping_step(cuda, golden_dir):
     assert b["convergence_info"]["gn_iterations"] == k
     assert torch.equal(a["node_rotations"], b["node_rotations"])
     assert torch.equal(a["node_translations"], b["node_translations"])
+
+
+def test_gn_capped_pcg_is_reported(cuda, golden_dir):
+    """A GN step whose PCG stops at pcg_max_iter (the step is taken with that iterate) is counted in status[4] /
+    convergence_info["pcg_capped_steps"] instead of passing silently; a converged solve reports 0."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    capped = GaussNewtonSolver(len(g["nodes"]), 1000, pcg_max_iter=3, stop_loss_diff=1e9).optimize(*_gn_inputs(g))
+    ci = capped["convergence_info"]
+    assert ci["gn_iterations"] == 10 and ci["pcg_capped_steps"] == 10, ci
+    assert int(capped["_status"][4].item()) == 10
+    full = GaussNewtonSolver(len(g["nodes"]), 1000).optimize(*_gn_inputs(g))
+    assert full["convergence_info"]["pcg_capped_steps"] == 0
+
+
+def test_gn_preconditioner_refresh_matches_dense_oracle(cuda, golden_dir):
+    """precond_rot_tol small enough to rebuild the cluster inverses in every warm-started step (k_pcg_proj's
+    refresh path) and the every-step rebuild through precond_every = 1 (k_pcg_prep) both stay within 1e-5 of the dense
+    oracle and are bitwise repeatable."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _g(golden_dir, "gn_small.npz")
+    for prm in (dict(precond_rot_tol=1e-9), dict(precond_every=1, precond_rot_tol=0.0)):
+        s = GaussNewtonSolver(len(g["nodes"]), 1000, **prm)
+        a, b = s.optimize(*_gn_inputs(g)), s.optimize(*_gn_inputs(g))
+        assert torch.equal(a["node_rotations"], b["node_rotations"]), prm
+        assert torch.equal(a["node_translations"], b["node_translations"]), prm
+        np.testing.assert_allclose(a["node_rotations"].cpu().numpy(), g["R"], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(a["node_translations"].cpu().numpy(), g["t"], atol=1e-5, rtol=0)
 
 
 def test_gn_duplicate_anchors_match_dense_oracle(cuda, golden_dir):

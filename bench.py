@@ -42,21 +42,22 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
+PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
 
 from occlusionfusion_amd.synthetic import BASELINE_CONFIGS as CONFIGS  # noqa: E402  (configs 1-5)
 
 
-def pmc_traffic(kernel, workload):
-    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC summary (separate counter passes
-    cannot run inside the timed bench) — only when that summary was measured on this very workload;
-    otherwise None."""
+def pmc_traffic(kernel, workload, extra=()):
+    """Per-launch HBM bytes of `kernel` (+ the kernels in `extra` that run once per launch of it, if measured) from the
+    committed rocprofv3 PMC summary (separate counter passes cannot run inside the timed bench) — only when that
+    summary was measured on this very workload; otherwise None."""
     try:
         with open(PMC_FILE) as f:
             d = json.load(f)
         if d.get("workload") != workload:
             return None
-        return d["kernels"][kernel]["traffic_bytes"]
+        return d["kernels"][kernel]["traffic_bytes"] + sum(d["kernels"][k]["traffic_bytes"] for k in extra
+                                                           if k in d["kernels"])
     except (OSError, KeyError, ValueError):
         return None
 
@@ -348,7 +349,7 @@ def main():
                                          "fused warp+integrate with an LDS node palette; VALU-bound: DESIGN.md "
                                          "section 5)", "bound": "hbm",
                                "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                               "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp", workload),
+                               "frac": achieved / PEAK_HBM, "traffic": pmc_traffic("k_integrate_warp", workload, ("k_brick_cull", "k_tile_max")),
                                "bytes_per_launch": B,
                                "bytes_note": "this layout's minimal bytes for the bricks the per-frame cull keeps "
                                              "(palette ranks, reads for skin-valid voxels only) + the cull's own reads; "

@@ -3,7 +3,7 @@
 # profiles/ afterwards). Every GPU step has its own time limit; the script stops at the first failure.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 cd $R
 bash tools/pmc_traffic.sh
 python tools/pmc_summary.py gpurun_out gpurun_out/${TAG}_pmc_traffic.json

@@ -4,7 +4,7 @@ tools/pmc_traffic.sh -> JSON (bench.py reads it into roofline.traffic).
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of
 16-B/lane coalesced reads, so traffic = 2 x FETCH_SIZE + WRITE_SIZE (both reported in KB).
 
-  python tools/pmc_summary.py gpurun_out profiles/r03_pmc_traffic.json
+  python tools/pmc_summary.py gpurun_out profiles/r05_pmc_traffic.json
 
 The workload the counters were collected on is taken from the bench line the profiled run printed
 (gpurun_out/pmc_FETCH_SIZE.log); bench.py uses `traffic` only when that workload equals its own.
@@ -19,7 +19,8 @@ import numpy as np
 
 KERNELS = {"k_pcg_iter": ("ofx::k_pcg_iter<true, false",),
            "k_integrate_warp": ("ofx::k_integrate_pal4<true>", "ofx::k_integrate<true, true"),
-           "k_assemble": ("ofx::k_assemble(",), "k_terms": ("ofx::k_terms(",)}
+           "k_assemble": ("ofx::k_assemble(",), "k_terms": ("ofx::k_terms(",),
+           "k_brick_cull": ("ofx::k_brick_cull(ofx::BrickGeom, ofx::BrickDiv",), "k_tile_max": ("ofx::k_tile_max(",)}
 
 
 def workload(d):

@@ -529,15 +529,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 
 // ---- brick cull of the warped integrate (ofx_integrate_palette_cull): which listed bricks can update a voxel at all.
 // Per 8x8 pixel tile the largest depth (NaN pixels never update and are skipped; +inf propagates). One thread per tile,
-// the tile's 8 rows as 2 x 16-B loads each (lanes = consecutive tiles of a tile row: coalesced); W % 4 == 0 (else the
-// per-pixel loop).
+// the tile's 8 rows as 2 x 16-B loads each (lanes = consecutive tiles of a tile row: coalesced); W % 4 == 0 and a 16-B
+// aligned image (else the per-pixel loop).
 __global__ __launch_bounds__(256) void k_tile_max(const float* __restrict__ depth, int W, int H, int TW, int TH,
                                                   float* __restrict__ tiles) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= TW * TH) return;
   const int tx = t % TW, ty = t / TW;
   float m = 0.f;
-  if ((W & 3) == 0 && tx * 8 + 8 <= W && ty * 8 + 8 <= H) {
+  if ((W & 3) == 0 && (reinterpret_cast<uintptr_t>(depth) & 15) == 0 && tx * 8 + 8 <= W && ty * 8 + 8 <= H) {
     float4 v[16];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {

@@ -45,6 +45,7 @@
 #include <mutex>
 #include <thread>
 #include <type_traits>
+#include <type_traits>
 #include <utility>
 #include <cstdlib>
 #include <cstdio>
@@ -59,6 +60,12 @@ constexpr int kBlk = 256;       // threads per WG
 constexpr int kProj = 4;      // warm start: Galerkin projection on the last kProj GN-step solutions
 constexpr int kCS = 8;        // nodes per preconditioner cluster (= PCG rows per wave)
 constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² entries
+// Overlapping additive Schwarz (as_on): the ring of a cluster holds its kAsRing A-neighbours with the most coupling terms,
+// and a row joins at most kAsX rings, so an output cluster has at most kAsSrc contributing subdomains and kAsRS row
+// segments (a 120-entry inverse row each); kAsGat >= kAsSrc·kAsDN rounded to 3 per thread of the apply's 192
+constexpr int kAsRing = 12, kAsX = 3, kAsDN = kCS + kAsRing, kAsD = 6 * kAsDN, kAsK = kAsD / 8, kAsSrc = 1 + kCS * kAsX,
+              kAsRS = 6 * kCS * (1 + kAsX), kAsGat = 576, kAsMeta = 64 + kAsRS;
+static_assert(kAsSrc * kAsDN <= kAsGat && kAsGat == 3 * kAsRS && kAsD % 8 == 0 && kAsD <= 128, "Schwarz tables");
 
 // Everything the kernels read: trivially copyable, passed by value as the kernel argument (host-only
 // members live in Gn below, so a launch copies these bytes and nothing else).
@@ -125,6 +132,20 @@ struct GnDev {
   int32_t nw_pad = 0;            // stride of the iteration partial streams: 128·pcg_ku, zero beyond nwg_row
   int32_t pcg_w2 = 1;            // two waves per cluster in k_pcg_iter (OFX_PCG_W1=1: one)
   int32_t pcg_ku = 3;            // partial pairs per lane and stream in k_pcg_iter (pcg_ku_for)
+  // overlapping additive Schwarz preconditioner (as_on): subdomain D_c = cluster c's kCS rows + up to kAsRing
+  // ring rows; the setup's tables (k_as_choose .. k_as_segments) and the prep's inverses (k_as_invert), applied by
+  // k_as_apply between two PCG iteration launches
+  int32_t as_on = 0;
+  int32_t *as_cand = nullptr, *as_csc = nullptr, *as_acc = nullptr;   // [cluster][kAsRing]: ring candidates, terms, kept
+  int32_t* as_dom = nullptr;     // [cluster][kAsDN]: the subdomain's rows (own rows first, -1 = none)
+  int32_t* as_meta = nullptr;    // [cluster][kAsMeta]: segment count, source count, row offsets, segment -> source slot
+  int32_t* as_gat = nullptr;     // [cluster][kAsGat]: rows gathered into the apply's LDS image (source slot · kAsDN + l)
+  int32_t* as_dst = nullptr;     // [cluster][kAsD]: subdomain row -> (output cluster · kAsRS + segment)
+  uint16_t* as_slab = nullptr;   // [cluster][kAsK][kAsRS] x 8 fp16: the segments' scaled inverse rows, segment-minor
+  int32_t* as_src = nullptr;     // [cluster][kAsSrc]: the apply's source subdomains
+  float* as_dsc = nullptr;       // [cluster][kAsD]: the subdomain inverse's scales d = √diag(Z) (k_as_invert)
+  float* as_rsc = nullptr;       // [cluster][kAsRS]: the segment rows' scales
+  double* as_w = nullptr;        // 6N: the vector the next apply reads (w of the iteration, r0, ...)
   double* scal = nullptr;
   int32_t* flags = nullptr;
   // DeformNet.arap mode with lambda_flow = 0: rows of each multi-node connected graph component
@@ -193,6 +214,8 @@ struct Gn : GnDev {
   hipEvent_t ev_side = nullptr;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   int32_t ep_next = 1;
+  int as_req = 0;                   // the Schwarz preconditioner is requested (enabled per setup: wave-list forms only)
+  int as_cap = 0;                   // clusters the Schwarz tables are allocated for
   // the PCG iteration's constant launch arguments (struct PcgIt) in device memory, and the bytes last copied there
   void* d_pcgit = nullptr;
   alignas(16) unsigned char pcgit_last[512] = {};
@@ -1389,6 +1412,468 @@ __global__ __launch_bounds__(64) void k_pcg_prep(GnDev g, double lm, double* __r
   }
 }
 
+// ---------------------------------------------------------------------------- overlapping additive Schwarz
+// M⁻¹ = Σ_c R_cᵀ (A_{D_c D_c})⁻¹ R_c over subdomains D_c = cluster c's kCS rows + its ring (on the bench graph
+// 2.46x fewer PCG iterations than the cluster blocks, tools/schwarz_study.py). The apply needs w on the neighbours'
+// rings, which the iteration has only after a kernel boundary, so each PCG iteration is two launches: k_pcg_iter<.., kAS>
+// (SpMV, recurrences, w_new -> as_w) and k_as_apply (m_new = M⁻¹ w_new). Owner computes: the workgroup of output cluster
+// c' sums, for its 48 rows, the rows of every subdomain inverse that contains them ("segments", sorted by (row, source)
+// so the sum has a fixed order), from a per-cluster slab written by k_as_invert — every slab address is static, so the
+// inverse rows leave with the gathered w in one memory trip.
+// Setup (per pattern, on the prefetch stream): k_as_choose ranks each cluster's A-neighbours by the number of terms
+// coupling them to it (blk_off counts; known before any A exists), k_as_accept lets every row keep the kAsX best of the
+// rings that chose it (bounds the tables), k_as_compact writes the subdomains, k_as_segments the apply's tables.
+
+// the candidate ring of cluster c: its distinct A-neighbours outside the cluster, best kAsRing by (terms desc, row asc)
+// (a thread per block of the cluster's rows)
+__global__ __launch_bounds__(256) void k_as_choose(GnDev g) {
+  __shared__ int s_u[256], s_n[256], s_sc[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int b0 = g.row_ptr[c * kCS], b1 = g.row_ptr[(c + 1) * kCS];
+  const int ne = min(b1 - b0, 256);
+  int u = -1, n = 0;
+  if (t < ne) {
+    const int b = b0 + t;
+    const int x = g.blk_row[b];
+    u = g.col[b];
+    if (u / kCS == c) {
+      u = -1;
+    } else {
+      const int lo = min(x, u), hi = max(x, u);
+      const int up = g.up_of[g.map[(int64_t)lo * g.N + hi] - 1];
+      n = g.blk_off[up + 1] - g.blk_off[up];
+    }
+  }
+  s_u[t] = u;
+  s_n[t] = n;
+  __syncthreads();
+  int sc = -1;   // per distinct candidate (its first entry): the terms coupling it to the cluster
+  if (u >= 0) {
+    bool first = true;
+    int sum = 0;
+    for (int f = 0; f < ne; ++f)
+      if (s_u[f] == u) { sum += s_n[f]; first = first && f >= t; }
+    sc = first ? sum : -1;
+  }
+  s_sc[t] = sc;
+  const int nrep = __syncthreads_count(sc >= 0);
+  if (sc >= 0) {
+    int rank = 0;
+    for (int f = 0; f < ne; ++f) {
+      const int s2 = s_sc[f];
+      rank += (s2 > sc || (s2 == sc && s_u[f] < u)) ? 1 : 0;
+    }
+    if (rank < kAsRing) {
+      g.as_cand[c * kAsRing + rank] = u;
+      g.as_csc[c * kAsRing + rank] = sc;
+    }
+  }
+  if (t >= nrep && t < kAsRing) g.as_cand[c * kAsRing + t] = -1;
+}
+
+// row v keeps the kAsX best (terms desc, cluster asc) of the rings that chose it (one wave per row, a lane per block:
+// each choosing cluster seen through the first of v's blocks into it — the pattern is symmetric, so a cluster that chose
+// v holds a neighbour of v)
+__global__ __launch_bounds__(256) void k_as_accept(GnDev g) {
+  __shared__ int s_ci[4][64], s_si[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int v = blockIdx.x * 4 + w;
+  if (v >= g.N) return;   // (wave-uniform: no barrier below)
+  const int cv = v / kCS;
+  const int b0 = g.row_ptr[v], b1 = g.row_ptr[v + 1];
+  const int ci = b0 + lane < b1 ? g.col[b0 + lane] / kCS : -1;
+  s_ci[w][lane] = ci;
+  wave_lds_sync();
+  bool ok = ci >= 0 && ci != cv;
+  for (int j = 0; j < lane && ok; ++j) ok = s_ci[w][j] != ci;   // first block into the cluster
+  int ki = -1, si = -1;
+  if (ok) {
+    int cand[kAsRing];
+#pragma unroll
+    for (int k = 0; k < kAsRing; ++k) cand[k] = g.as_cand[ci * kAsRing + k];
+#pragma unroll
+    for (int k = 0; k < kAsRing; ++k) ki = cand[k] == v ? k : ki;
+    if (ki >= 0) si = g.as_csc[ci * kAsRing + ki];
+  }
+  s_si[w][lane] = si;
+  wave_lds_sync();
+  if (si < 0) return;
+  int rank = 0;
+  for (int j = 0; j < b1 - b0 && j < 64; ++j) {
+    const int sj = s_si[w][j], cj = s_ci[w][j];
+    rank += (sj >= 0 && (sj > si || (sj == si && cj < ci))) ? 1 : 0;
+  }
+  g.as_acc[ci * kAsRing + ki] = rank < kAsX ? 1 : 0;
+}
+
+// subdomain rows of cluster c: its own kCS rows, then the kept ring rows in rank order, -1 after
+__global__ __launch_bounds__(64) void k_as_compact(GnDev g) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  int u = -1;
+  bool keep = false;
+  if (lane < kAsRing) {
+    u = g.as_cand[c * kAsRing + lane];
+    keep = u >= 0 && g.as_acc[c * kAsRing + lane] != 0;
+  }
+  const uint64_t m = __ballot(keep);
+  const int pos = kCS + __popcll(m & ((1ull << lane) - 1));
+  const int cnt = kCS + __popcll(m);
+  if (keep) g.as_dom[c * kAsDN + pos] = u;
+  if (lane < kCS) g.as_dom[c * kAsDN + lane] = c * kCS + lane;
+  if (lane >= cnt && lane < kAsDN) g.as_dom[c * kAsDN + lane] = -1;
+}
+
+// the apply's tables of output cluster c': its source subdomains (c' and every cluster whose ring holds one of its rows,
+// ascending), the gather list, the segments (row r, source s) in (r, s) order with their source slots and row offsets,
+// and for each segment its slab position in the source's as_dst (a thread per block of the cluster's rows)
+__global__ __launch_bounds__(256) void k_as_segments(GnDev g) {
+  __shared__ int s_c[256], s_k[256];
+  __shared__ int s_src[kAsSrc];
+  __shared__ int s_pos[kAsSrc][kCS];
+  const int cp = blockIdx.x, t = threadIdx.x;
+  const int b0 = g.row_ptr[cp * kCS], b1 = g.row_ptr[(cp + 1) * kCS];
+  const int ne = min(b1 - b0, 255);
+  const int c = t < ne ? g.col[b0 + t] / kCS : (t == ne ? cp : -1);
+  s_c[t] = c;
+  if (t < kAsSrc * kCS) s_pos[t / kCS][t % kCS] = -1;
+  __syncthreads();
+  bool keep = c >= 0;
+  for (int f = 0; f < t && keep; ++f) keep = s_c[f] != c;   // first occurrence
+  if (keep && c != cp) {
+    int dom[kAsRing];
+#pragma unroll
+    for (int l = 0; l < kAsRing; ++l) dom[l] = g.as_dom[c * kAsDN + kCS + l];
+    bool hit = false;
+#pragma unroll
+    for (int l = 0; l < kAsRing; ++l) hit = hit || (dom[l] >= 0 && dom[l] / kCS == cp);
+    keep = hit;
+  }
+  s_k[t] = keep ? c : -1;
+  const int nsrc = min(__syncthreads_count(keep), kAsSrc);   // (<= 1 + kCS·kAsX by k_as_accept)
+  if (keep) {
+    int slot = 0;
+    for (int f = 0; f < 256; ++f) slot += (s_k[f] >= 0 && s_k[f] < c) ? 1 : 0;
+    if (slot < kAsSrc) s_src[slot] = c;
+  }
+  __syncthreads();
+  for (int i = t; i < nsrc * kAsDN; i += 256) {
+    const int sl = i / kAsDN, l = i % kAsDN;
+    const int u = g.as_dom[s_src[sl] * kAsDN + l];
+    if (u >= 0 && u / kCS == cp) s_pos[sl][u % kCS] = l;
+  }
+  for (int i = t; i < kAsGat; i += 256) {
+    const int sl = i / kAsDN, l = i % kAsDN;
+    g.as_gat[(int64_t)cp * kAsGat + i] = sl < nsrc ? g.as_dom[s_src[sl] * kAsDN + l] : -1;
+  }
+  __syncthreads();
+  if (t >= 64) return;
+  // lane r < 48: output row r's segments (one per source holding its node), offsets by a wave scan
+  const int lane = t;
+  const int r = lane < 6 * kCS ? lane : 6 * kCS - 1;
+  int cnt = 0;
+  for (int sl = 0; sl < nsrc; ++sl) cnt += s_pos[sl][r / 6] >= 0 ? 1 : 0;
+  if (lane >= 6 * kCS) cnt = 0;
+  int off = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(off, o, 64);
+    if (lane >= o) off += y;
+  }
+  const int total = __shfl(off, 63, 64);
+  off -= cnt;   // exclusive
+  int32_t* mt = g.as_meta + (int64_t)cp * kAsMeta;
+  if (lane < 6 * kCS) {
+    mt[2 + lane] = off;
+    int rs = off;
+    for (int sl = 0; sl < nsrc; ++sl) {
+      const int l = s_pos[sl][r / 6];
+      if (l < 0) continue;
+      mt[64 + rs] = sl;
+      g.as_dst[(int64_t)s_src[sl] * kAsD + 6 * l + r % 6] = cp * kAsRS + rs;
+      ++rs;
+    }
+  }
+  if (lane == 0) { mt[0] = total; mt[1] = nsrc; mt[2 + 6 * kCS] = total; }
+  if (lane < kAsSrc) g.as_src[cp * kAsSrc + lane] = lane < nsrc ? s_src[lane] : 0;
+}
+
+// Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= 120 x 120, f64, 8x8 entries per
+// thread in registers: rows tr + 16a, columns tc + 16b), its in-place Gauss-Jordan inverse (SPD: no pivoting; row and
+// column k pass through LDS, double-buffered: one barrier per step), scaled and rounded to fp16 with a certified diagonal
+// margin (below) and written symmetric (the upper triangle's value to both entries) into the segments' slab rows; a
+// non-positive or non-finite pivot falls back to the identity on the cluster's own rows. mode 1: always (the solve's first GN step and precond_every steps; the cold start's
+// records x = 0, r = b and the PCG flags too); mode 0: only when the previous step flagged a refresh (precond_rot_tol).
+__global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __restrict__ A, const double* __restrict__ rhs,
+                                                   int mode, int gn_iter) {
+  __shared__ int s_dom[kAsDN];
+  __shared__ int s_sl[kAsDN][kAsDN];
+  __shared__ double s_row[2][2][128], s_col[2][2][128];
+  const int c = blockIdx.x, t = threadIdx.x, tr = t >> 4, tc = t & 15;
+  if (g.flags[F_STOPPED]) return;
+  if (mode == 0 && g.flags[F_REFRESH] != gn_iter) return;
+  if (t < kAsDN) s_dom[t] = g.as_dom[c * kAsDN + t];
+  __syncthreads();
+  int nd = 0;
+  for (int i = 0; i < kAsDN; ++i) nd += s_dom[i] >= 0 ? 1 : 0;
+  for (int p = t; p < kAsDN * kAsDN; p += 256) {
+    const int i = p / kAsDN, j = p % kAsDN;
+    s_sl[i][j] = (i < nd && j < nd) ? g.map[(int64_t)s_dom[i] * g.N + s_dom[j]] - 1 : -1;
+  }
+  __syncthreads();
+  const int n = 6 * nd;
+  // every load unconditional (clamped addresses, masked values): a load behind a branch gets its own wait, and 64 of
+  // them in a row cost ~100 us
+  int dR[8], dC[8];   // the slab positions of the thread's rows and columns (as rows of the mirrored entries)
+#pragma unroll
+  for (int a = 0; a < 8; ++a) dR[a] = g.as_dst[(int64_t)c * kAsD + min(tr + 16 * a, kAsD - 1)];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) dC[b] = g.as_dst[(int64_t)c * kAsD + min(tc + 16 * b, kAsD - 1)];
+  double M[8][8];
+  int slv[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int R = tr + 16 * a, C = tc + 16 * b;
+      const int sl = (R < n && C < n) ? s_sl[min(R / 6, kAsDN - 1)][min(C / 6, kAsDN - 1)] : -1;
+      slv[a][b] = sl;
+      M[a][b] = A[36 * (int64_t)(sl >= 0 ? sl : 0) + 6 * (R % 6) + C % 6];
+    }
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int R = tr + 16 * a, C = tc + 16 * b;
+      // (beyond n: the identity, never touched by the steps below)
+      M[a][b] = (R < n && C < n) ? (slv[a][b] >= 0 ? M[a][b] : 0.0) : (R == C ? 1.0 : 0.0);
+    }
+  bool bad = false;
+  int buf = 0;
+  // Block Gauss-Jordan with 2x2 pivot blocks P = rows / columns {k, k+1} (two elimination steps per barrier: the ~0.7 us
+  // of barrier and LDS latency per step, not the FMAs, set the kernel's time). Step k = 16·K + kk, kk even (K a compile-time
+  // register-tile index: M[K][.] / M[.][K] stay in registers).
+  auto step2 = [&](auto Kc, int kk) {
+    constexpr int K = decltype(Kc)::value;
+    const int k = 16 * K + kk;
+    if (tr == kk || tr == kk + 1)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) s_row[buf][tr - kk][tc + 16 * b] = M[K][b];
+    if (tc == kk || tc == kk + 1)
+#pragma unroll
+      for (int a = 0; a < 8; ++a) s_col[buf][tc - kk][tr + 16 * a] = M[a][K];
+    __syncthreads();
+    const double p00 = s_row[buf][0][k], p01 = s_row[buf][0][k + 1], p10 = s_row[buf][1][k], p11 = s_row[buf][1][k + 1];
+    const double det = p00 * p11 - p01 * p10;
+    bad = bad || !(p00 > 0.0) || !(det > 0.0) || !isfinite(det);
+    const double idet = 1.0 / det;
+    const double q00 = p11 * idet, q01 = -p01 * idet, q10 = -p10 * idet, q11 = p00 * idet;   // P⁻¹
+    double v0[8], v1[8], c0[8], c1[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {   // P⁻¹ A_{K,j}
+      const double r0 = s_row[buf][0][tc + 16 * b], r1 = s_row[buf][1][tc + 16 * b];
+      v0[b] = fma(q01, r1, q00 * r0);
+      v1[b] = fma(q11, r1, q10 * r0);
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) { c0[a] = s_col[buf][0][tr + 16 * a]; c1[a] = s_col[buf][1][tr + 16 * a]; }
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) M[a][b] = fma(-c1[a], v1[b], fma(-c0[a], v0[b], M[a][b]));   // (rows / columns K below)
+    if (tr == kk || tr == kk + 1)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) M[K][b] = tr == kk ? v0[b] : v1[b];
+    if (tc == kk || tc == kk + 1) {
+      const double e0 = tc == kk ? q00 : q01, e1 = tc == kk ? q10 : q11;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) M[a][K] = -fma(c1[a], e1, c0[a] * e0);
+      if (tr == kk || tr == kk + 1) M[K][K] = tr == kk ? e0 : e1;   // the pivot block: P⁻¹
+    }
+    buf ^= 1;
+  };
+#define OFX_AS_STEPS(K) \
+  for (int kk = 0; kk < 16 && 16 * (K) + kk < n; kk += 2) step2(std::integral_constant<int, (K)>{}, kk);
+  OFX_AS_STEPS(0) OFX_AS_STEPS(1) OFX_AS_STEPS(2) OFX_AS_STEPS(3)
+  OFX_AS_STEPS(4) OFX_AS_STEPS(5) OFX_AS_STEPS(6) OFX_AS_STEPS(7)
+#undef OFX_AS_STEPS
+  bad = __syncthreads_or(bad ? 1 : 0) != 0;
+  // Stored form: Z = D Ẑ D with d = √diag(Z), so Ẑ has a unit diagonal and |Ẑ_ij| <= 1 (Z is SPD), and Ẑ's off-diagonal
+  // entries as fp16 (absolute error <= 2^-12). E = the rounding of the off-diagonal entries; the diagonal is stored as
+  // 1 + σ with σ = ‖E‖_F + 2^-10 >= ‖E‖₂ + the diagonal's own rounding, so the stored Ẑ̃ >= Ẑ: positive definite whatever
+  // Z's conditioning (a plain 16-bit rounding of Z made the moose's subdomains indefinite). A bad domain: the identity on
+  // the cluster's own rows.
+  __shared__ double s_d[128], s_e[256];
+  __shared__ double s_sig;
+  if (tr == tc)
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      const int R = tr + 16 * a;
+      s_d[R] = (R < n && !bad) ? sqrt(M[a][a]) : 1.0;
+    }
+  __syncthreads();
+  double dr[8], dc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a) dr[a] = s_d[tr + 16 * a];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) dc[b] = s_d[tc + 16 * b];
+  auto h16 = [](double z) -> _Float16 { return (_Float16)(float)z; };
+  double e2 = 0.0;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int R = tr + 16 * a, C = tc + 16 * b;
+      if (R < n && C < n && R < C && !bad) {
+        const double z = M[a][b] / (dr[a] * dc[b]);
+        const double err = (double)(float)h16(z) - z;
+        e2 += 2.0 * err * err;
+      }
+    }
+  s_e[t] = e2;
+  __syncthreads();
+  if (t == 0) {
+    double sum = 0.0;
+    for (int i = 0; i < 256; ++i) sum += s_e[i];
+    s_sig = sqrt(sum) + 0x1p-10;
+  }
+  __syncthreads();
+  const double sig = s_sig;
+  auto put = [&](int d, int C, _Float16 h) {   // d: the row's slab position (output cluster · kAsRS + segment)
+    const int cp = d / kAsRS, rs = d % kAsRS;
+    g.as_slab[(((int64_t)cp * kAsK + C / 8) * kAsRS + rs) * 8 + (C & 7)] = __builtin_bit_cast(uint16_t, h);
+  };
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int R = tr + 16 * a, C = tc + 16 * b;
+      if (R >= n || C >= kAsD) continue;
+      if (C >= n) {
+        put(dR[a], C, (_Float16)0.0f);
+      } else if (R == C) {
+        put(dR[a], C, bad ? (_Float16)(R < 6 * kCS ? 1.0f : 0.0f) : h16(1.0 + sig));
+      } else if (R < C) {
+        const _Float16 h = bad ? (_Float16)0.0f : h16(M[a][b] / (dr[a] * dc[b]));
+        put(dR[a], C, h);
+        put(dC[b], R, h);
+      }
+    }
+  if (tc == 0)
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      const int R = tr + 16 * a;
+      if (R < kAsD) g.as_dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
+      if (R < n) g.as_rsc[dR[a]] = (float)dr[a];
+    }
+  if (t < kCS) g.racc[c * kCS + t] = 0.0;
+  if (mode != 1) return;
+  if (!g.warm_now && t < 6 * kCS) {   // cold start: x = 0, r = b (u = M⁻¹ b comes from k_as_apply into m1)
+    const int64_t o = 6 * (int64_t)c * kCS + t;
+    const double v[V_N] = {0.0, rhs[o], 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    store_rec(g.st, o, v);
+  }
+  if (c == 0 && t == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; g.flags[F_REFRESH] = 0; }
+}
+
+// out (48 rows of cluster c) = the Schwarz apply of `in`: the gathered rows of the cluster's source subdomains into an LDS
+// image (f32, each row times its source's column scale d; source slot s at s·kAsD), one segment per thread (its 120-entry
+// fp16 slab row of Ẑ, 16-B word k of every segment contiguous: 1 KB per load instruction), the segments' f32 dot products
+// times the row scale into LDS, and each row's segments summed in (row, source) order. 16-bit entries halve the slab
+// (~7 MB per launch on the bench graph, so it and the iteration's operator stay L2-resident: +~10 % frames/s against f32);
+// the preconditioner is still one fixed symmetric positive definite linear operator (k_as_invert's stored form).
+// Trip 1: the stop word (kTest: the PCG chain's launches after convergence end there), the gather list, the segment's
+// source slot and the row offsets; trip 2: the gathered rows and the slab rows together (static addresses; threads past
+// the segment count read the last segment's lines, one line per load instruction).
+template <bool kTest>
+__global__ __launch_bounds__(192) void k_as_apply(const int32_t* stopw, const int32_t* meta, const int32_t* gat,
+                                                  const uint16_t* slab, const double* in, double* out, const int32_t* src,
+                                                  const float* dsc, const float* rsc) {
+  __shared__ __attribute__((aligned(16))) double s_w[kAsSrc * kAsD];
+  __shared__ double s_seg[kAsRS];
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int32_t* mt = meta + (int64_t)c * kAsMeta;
+  int stop = 0;
+  if (kTest) stop = stopw[(int64_t)c * 64 + lane];
+  const int nrs = mt[0];
+  int gn[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) gn[j] = gat[(int64_t)c * kAsGat + kAsRS * j + t];
+  const int sl = mt[64 + t];
+  const float rscale = rsc[(int64_t)c * kAsRS + t];
+  int sv[3];   // the gathered rows' source subdomains
+#pragma unroll
+  for (int j = 0; j < 3; ++j) sv[j] = src[c * kAsSrc + min((kAsRS * j + t) / kAsDN, kAsSrc - 1)];
+  const int rr = t < 6 * kCS ? t : 6 * kCS - 1;
+  const int o0 = mt[2 + rr], o1 = mt[3 + rr];
+  asm volatile("" ::: "memory");
+  if (kTest) {
+    stop = __builtin_amdgcn_readfirstlane(stop);
+    if (stop != 0) return;   // the solve has converged (or stopped): a drained launch
+  }
+  double2 wg[3][3];
+  float2 dg[3][3];   // the source subdomains' column scales of the gathered rows
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double2* p = reinterpret_cast<const double2*>(in + 6 * (int64_t)(gn[j] >= 0 ? gn[j] : 0));
+    const float2* q = reinterpret_cast<const float2*>(dsc + (int64_t)sv[j] * kAsD + 6 * ((kAsRS * j + t) % kAsDN));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { wg[j][k] = p[k]; dg[j][k] = q[k]; }
+  }
+  uint4 z[kAsK];   // 8 bf16 inverse entries each
+  {
+    const int rs = t < nrs ? t : (nrs > 0 ? nrs - 1 : 0);
+    const uint4* zp = reinterpret_cast<const uint4*>(slab) + (int64_t)c * kAsK * kAsRS + rs;
+#pragma unroll
+    for (int k = 0; k < kAsK; ++k) z[k] = zp[k * kAsRS];
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = kAsRS * j + t;
+    if (i < kAsSrc * kAsDN) {
+      const bool ok = gn[j] >= 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        s_w[6 * i + 2 * k] = ok ? wg[j][k].x * (double)dg[j][k].x : 0.0;
+        s_w[6 * i + 2 * k + 1] = ok ? wg[j][k].y * (double)dg[j][k].y : 0.0;
+      }
+    }
+  }
+  __syncthreads();
+  // the segment's dot product in f64 (fp16 entries exact in f64): the apply is linear to f64 rounding. (An f32 image and
+  // f32 products, measured: 3 % faster, but the rounding made the apply nonlinear at 1e-7 — the pipelined recurrences
+  // drifted, gn_4k's loss log missed 1e-6 and the ill-conditioned moose ended 0.29 off.)
+  if (t < nrs) {
+    const double2* w2 = reinterpret_cast<const double2*>(s_w + sl * kAsD);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    auto lo = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); };
+    auto hi = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); };
+#pragma unroll
+    for (int k = 0; k < kAsK; ++k) {
+      const double2 p0 = w2[4 * k], p1 = w2[4 * k + 1], p2 = w2[4 * k + 2], p3 = w2[4 * k + 3];
+      a0 = fma(lo(z[k].x), p0.x, a0);
+      a1 = fma(hi(z[k].x), p0.y, a1);
+      a2 = fma(lo(z[k].y), p1.x, a2);
+      a3 = fma(hi(z[k].y), p1.y, a3);
+      a0 = fma(lo(z[k].z), p2.x, a0);
+      a1 = fma(hi(z[k].z), p2.y, a1);
+      a2 = fma(lo(z[k].w), p3.x, a2);
+      a3 = fma(hi(z[k].w), p3.y, a3);
+    }
+    s_seg[t] = (double)rscale * ((a0 + a1) + (a2 + a3));
+  }
+  __syncthreads();
+  if (t < 6 * kCS) {
+    double sv[kAsX + 1];
+#pragma unroll
+    for (int j = 0; j <= kAsX; ++j) sv[j] = s_seg[min(o0 + j, kAsRS - 1)];
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j <= kAsX; ++j) s += o0 + j < o1 ? sv[j] : 0.0;
+    out[(int64_t)c * 6 * kCS + t] = s;
+  }
+}
+
 // Galerkin warm start, pass 1: t_j = A x_j for the n_prev stored solutions (own rows) and per-wave
 // partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
 constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
@@ -1445,7 +1930,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const int refresh = g.flags[F_REFRESH];
     asm volatile("" ::: "memory");   // the loads above leave with the stop flag (one trip)
     if (stopped) return;
-    if (refresh == gn_iter) {
+    if (refresh == gn_iter && !g.as_on) {   // (Schwarz: k_as_invert)
       float mm[6][6];
       cluster_invert(g, g.Aop, wv, lane, mm);
     }
@@ -1700,10 +2185,16 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) { 
   }
   __syncthreads();
   if (own) {
-    const double u = apply_mrow(mr, s_v);
-    const double v[V_N] = {xv, rv, u, 0.0, 0.0, 0.0, 0.0, 0.0};
-    store_rec(g.st, o, v);
-    g.m1[o] = u;
+    if (g.as_on) {   // u0 = M⁻¹ r0 by k_as_apply (as_w -> m1)
+      const double v[V_N] = {xv, rv, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      store_rec(g.st, o, v);
+      g.as_w[o] = rv;
+    } else {
+      const double u = apply_mrow(mr, s_v);
+      const double v[V_N] = {xv, rv, u, 0.0, 0.0, 0.0, 0.0, 0.0};
+      store_rec(g.st, o, v);
+      g.m1[o] = u;
+    }
   }
 }
 
@@ -1737,6 +2228,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   double v[V_N];
   load_mrow(g, oc, mr);
   load_rec(g.st, oc, v);
+  const double u_as = g.m1[oc];  // (Schwarz: u0 came from k_as_apply into m1)
   const double w_old = v[V_W];   // unused, but kept live to the end (see the end of the kernel)
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");
@@ -1747,8 +2239,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (blockIdx.x == 0 && lane == 0) {
     reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(kWave ? g.Aw : g.Aop);
     g.pcs[kScTol] = g.prm.pcg_tol;
-    g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
-    reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = reinterpret_cast<uint64_t>(g.Mcl);
+    // The error stop bounds ‖e‖_M (M the preconditioner); ‖e‖₂ <= ‖e‖_M / √λ_min(M). The cluster blocks' λ_min(M) is a
+    // cluster matrix's smallest eigenvalue, >= λ_min(A); the Schwarz M⁻¹ sums up to 1 + kAsX overlapping subdomain
+    // inverses per row, each of a larger subdomain (whose smallest eigenvalue is at most its cluster block's), so its
+    // λ_min(M) is smaller: the tolerance is taken 4x tighter (2x for the overlap's multiplicity, 2x margin: the moose
+    // pair ended at 1.1e-5 with 2x).
+    g.pcs[kScTol + 1] = g.as_on ? 0.25 * g.prm.pcg_err_tol : g.prm.pcg_err_tol;
+    // (Schwarz: the iteration's w_new target in the inverse's slot)
+    reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = g.as_on ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
     // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
@@ -1756,6 +2254,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     g.pcs[kScScal + S_TH_CUR] = 1e300;
   }
   if (stopped) return;
+  if (g.as_on) v[V_U] = u_as;
   const double b = own ? bo : 0.0;
   double w;
   double2 ab[2][18];
@@ -1802,10 +2301,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   __syncthreads();
   double d[4] = {0.0, 0.0, 0.0, 0.0};   // (the stop words hold an older epoch: this solve's launches run)
   if (own) {
-    const double m = apply_mrow(mr, s_v);
     v[V_W] = w;
     store_rec(g.st, o, v);
-    g.m0[o] = m;
+    if (g.as_on) g.as_w[o] = w;              // m0 = M⁻¹ w0 by k_as_apply (as_w -> m0)
+    else g.m0[o] = apply_mrow(mr, s_v);
     d[0] = v[V_R] * v[V_U]; d[1] = w * v[V_U]; d[2] = v[V_R] * v[V_R]; d[3] = b * b;
   }
 #pragma unroll
@@ -2002,7 +2501,9 @@ __device__ __forceinline__ void fused_step(const PcgIt& g, int ep, int gn_iter, 
 // rewritten when they change): a 76-B kernel argument instead of ~290 B, which the host enqueues faster. In-process A/B
 // against the same kernel with its scalars and addresses through the kernel arguments: -0.27 / -0.28 ms per frame.
 // mc / Pc are the parity's m and partial streams.
-template <bool kWave, bool kFirst, int kU, bool kW2 = false>   // kU: partial pairs per lane and stream (2·64·kU >= waves)
+// kAS (overlapping Schwarz): no cluster inverse — w_new goes to as_w (its address in the scalar block's
+// inverse slot) and k_as_apply, the next launch, forms m_new.
+template <bool kWave, bool kFirst, int kU, bool kW2 = false, bool kAS = false>   // kU: partial pairs per lane and stream
 __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_iter(
     const int2* wl, const int32_t* stopw, const double* Pc, const double* st, const double* mc, const double* sc,
     const PcgIt* __restrict__ gp, int par, int ep, int gn_iter) {   // (not __restrict__: a restrict load sinks past the exit test)
@@ -2068,7 +2569,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   auto addr = [](uint2 v2) -> uint64_t {
     return ((uint64_t)__builtin_amdgcn_readfirstlane(v2.y) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(v2.x);
   };
-  {
+  if constexpr (!kAS) {
     typedef float gf4 __attribute__((ext_vector_type(4)));
     const __attribute__((address_space(1))) gf4* Mw =
         reinterpret_cast<const __attribute__((address_space(1))) gf4*>(addr(mcl_v)) + (int64_t)wv * kCD * kCD / 4;
@@ -2319,13 +2820,19 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     if (own) {
       const double nv[V_N] = {fma(alpha, p, v[V_X]), rn, un, zz, qq, sv, p, w2};
       if (w0) store_rec(stw, o, nv);   // (the same buffer as st, written)
-      s_v[hw][6 * r + q] = w2;
+      if (kAS) {
+        if (w0) reinterpret_cast<__attribute__((address_space(1))) double*>(addr(mcl_v))[o] = w2;
+      } else {
+        s_v[hw][6 * r + q] = w2;
+      }
       d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
     }
   }
   OFX_STAMP(5)
-  wave_lds_sync();
-  if (kW2) {      // split-K: wave h applies column groups [6h, 6h + 6); wave 0 adds the halves (fixed order)
+  if (!kAS) wave_lds_sync();
+  if constexpr (kAS) {
+    // (m_new: k_as_apply)
+  } else if (kW2) {      // split-K: wave h applies column groups [6h, 6h + 6); wave 0 adds the halves (fixed order)
     double hsum = 0.0;
     if (own) {
       // the half's 24 values in flight before the first FMA (left to the compiler: five LDS round trips in a row)
@@ -2514,7 +3021,8 @@ static void free_all(Gn* g) {
                   g->st, g->m0, g->m1, g->pcs, g->racc,
                   g->part_p, g->part_b, g->part_loss,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
-                  g->up_of, g->up_slot, g->up_tr};
+                  g->up_of, g->up_slot, g->up_tr, g->as_cand, g->as_csc, g->as_acc, g->as_dom, g->as_meta, g->as_gat,
+                  g->as_dst, g->as_slab, g->as_w, g->as_src, g->as_dsc, g->as_rsc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -2603,7 +3111,19 @@ static int pcg_ku_for(int waves) {
 using PcgKernel = void (*)(const int2*, const int32_t*, const double*, const double*, const double*, const double*,
                           const PcgIt*, int, int, int);
 template <int KU>
-static void pcg_pick(bool wave, bool w2, PcgKernel& first, PcgKernel& rest) {
+static void pcg_pick(bool wave, bool w2, bool as, PcgKernel& first, PcgKernel& rest) {
+  if (as) {   // (wave-list forms only)
+    if constexpr (KU <= 3) {
+      if (w2) {
+        first = k_pcg_iter<true, true, KU, true, true>;
+        rest = k_pcg_iter<true, false, KU, true, true>;
+        return;
+      }
+    }
+    first = k_pcg_iter<true, true, KU, false, true>;
+    rest = k_pcg_iter<true, false, KU, false, true>;
+    return;
+  }
   if constexpr (KU <= 3) {
     if (wave && w2) {
       first = k_pcg_iter<true, true, KU, true>;
@@ -2636,7 +3156,22 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const int invert = (!g->warm_now || gn_iter % every == 0) ? 1 : 0;
   // wave-list SpMV forms (k_pcg_proj, k_pcg_w0, k_pcg_iter) when every wave's blocks fit the list and every row kRowMax
   const bool wave = g->max_wave <= kWL && g->max_deg <= kRowMax;
-  if (invert) hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
+  const bool as = g->as_on != 0;   // (the setup enables it only with the wave-list forms)
+  const int ncl = g->N / kCS;
+  auto as_apply = [&](bool test, const double* in, double* out) {
+    auto k = test ? k_as_apply<true> : k_as_apply<false>;
+    hipLaunchKernelGGL(k, dim3(ncl), dim3(kAsRS), 0, hs, (const int32_t*)g->stopw, (const int32_t*)g->as_meta,
+                       (const int32_t*)g->as_gat, (const uint16_t*)g->as_slab, in, out, (const int32_t*)g->as_src,
+                       (const float*)g->as_dsc, (const float*)g->as_rsc);
+  };
+  if (as) {
+    // the subdomain inverses: rebuilt like the cluster inverses (invert), or when the previous step flagged a refresh
+    if (invert || g->prm.precond_rot_tol > 0.0)
+      hipLaunchKernelGGL(k_as_invert, dim3(ncl), dim3(256), 0, hs, *g, (const double*)A, (const double*)rhs, invert, gn_iter);
+    if (!g->warm_now) as_apply(false, rhs, g->m1);   // cold start: u0 = M⁻¹ b
+  } else if (invert) {
+    hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
+  }
   if (g->warm_now) {
     if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
@@ -2647,9 +3182,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       case 8: hipLaunchKernelGGL(k_pcg_proj2<8>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
       default: hipLaunchKernelGGL(k_pcg_proj2<17>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
     }
+    if (as) as_apply(false, g->as_w, g->m1);   // u0 = M⁻¹ r0
   }
   if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
   else hipLaunchKernelGGL(k_pcg_w0<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+  if (as) as_apply(false, g->as_w, g->m0);     // m0 = M⁻¹ w0
   OFX_LAUNCH_CHECK();
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g->timing) {
@@ -2678,11 +3215,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool w2 = wave && g->pcg_w2 && g->pcg_ku <= 3;
   PcgKernel iter0 = nullptr, iter = nullptr;
   switch (g->pcg_ku) {
-    case 2: pcg_pick<2>(wave, w2, iter0, iter); break;
-    case 3: pcg_pick<3>(wave, w2, iter0, iter); break;
-    case 4: pcg_pick<4>(wave, w2, iter0, iter); break;
-    case 8: pcg_pick<8>(wave, w2, iter0, iter); break;
-    default: pcg_pick<17>(wave, w2, iter0, iter); break;
+    case 2: pcg_pick<2>(wave, w2, as, iter0, iter); break;
+    case 3: pcg_pick<3>(wave, w2, as, iter0, iter); break;
+    case 4: pcg_pick<4>(wave, w2, as, iter0, iter); break;
+    case 8: pcg_pick<8>(wave, w2, as, iter0, iter); break;
+    default: pcg_pick<17>(wave, w2, as, iter0, iter); break;
   }
   const dim3 block_it(w2 ? 128 : 64);
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
@@ -2735,6 +3272,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
                          (const double*)(g->part_p + 3 * (int64_t)g->nw_pad * par), (const double*)g->st,
                          (const double*)(par ? g->m1 : g->m0), (const double*)g->pcs + par, gp, par, g->ep,
                          gn_iter);
+      if (as) as_apply(true, g->as_w, par ? g->m0 : g->m1);   // m of the next iteration = M⁻¹ w_new
     }
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
@@ -2767,7 +3305,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     (void)ran;   // the chunk ran out without convergence: next chunk
     chunk = 8;
   }
-  g->n_iter_launches += it;
+  g->n_iter_launches += as ? 2 * it : it;   // (Schwarz: each iteration is two launches)
   if (g->timing) g->ev.emplace_back(e0, e1);
 #ifdef OFX_STAMPS
   if (getenv("OFX_GAP_EVENTS")) {
@@ -2867,6 +3405,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster
     const char* e = getenv("OFX_PCG_W1");
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
+    const char* pe = getenv("OFX_PRECOND");   // A/B: "as" = overlapping Schwarz, "bj" = cluster block Jacobi
+    g->as_req = (pe && strcmp(pe, "as") == 0) ? 1 : 0;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
@@ -3391,6 +3931,39 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   std::swap(g->blk_list, g->blk_tmp);
   std::swap(g->node_list, g->node_tmp);
   OFX_LAUNCH_CHECK();
+  // Schwarz tables (blk_off still holds the per-block term counts' offsets)
+  g->as_on = 0;
+  if (g->as_req && g->max_wave <= kWL && g->max_deg <= kRowMax) {
+    const int ncl = N / kCS;
+    if (ncl > g->as_cap) {
+      for (auto pp : {(void**)&g->as_cand, (void**)&g->as_csc, (void**)&g->as_acc, (void**)&g->as_dom, (void**)&g->as_meta,
+                      (void**)&g->as_gat, (void**)&g->as_dst, (void**)&g->as_slab, (void**)&g->as_w, (void**)&g->as_src,
+                      (void**)&g->as_dsc, (void**)&g->as_rsc})
+        if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
+      const int cap = g->max_pad / kCS;
+      OFX_HIP(hipMalloc((void**)&g->as_cand, (size_t)cap * kAsRing * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_csc, (size_t)cap * kAsRing * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_acc, (size_t)cap * kAsRing * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_dom, (size_t)cap * kAsDN * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_meta, (size_t)cap * kAsMeta * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_gat, (size_t)cap * kAsGat * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_dst, (size_t)cap * kAsD * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_slab, (size_t)cap * kAsK * kAsRS * 8 * sizeof(uint16_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_w, (size_t)g->max_pad * 6 * sizeof(double)));
+      OFX_HIP(hipMalloc((void**)&g->as_src, (size_t)cap * kAsSrc * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_dsc, (size_t)cap * kAsD * sizeof(float)));
+      OFX_HIP(hipMalloc((void**)&g->as_rsc, (size_t)cap * kAsRS * sizeof(float)));
+      OFX_HIP(hipMemsetAsync(g->as_rsc, 0, (size_t)cap * kAsRS * sizeof(float), hs));
+      OFX_HIP(hipMemsetAsync(g->as_slab, 0, (size_t)cap * kAsK * kAsRS * 8 * sizeof(uint16_t), hs));
+      g->as_cap = cap;
+    }
+    hipLaunchKernelGGL(k_as_choose, dim3(ncl), dim3(256), 0, hs, *g);
+    hipLaunchKernelGGL(k_as_accept, dim3(grid_for(N, 4)), dim3(256), 0, hs, *g);
+    hipLaunchKernelGGL(k_as_compact, dim3(ncl), dim3(64), 0, hs, *g);
+    hipLaunchKernelGGL(k_as_segments, dim3(ncl), dim3(256), 0, hs, *g);
+    OFX_LAUNCH_CHECK();
+    g->as_on = 1;
+  }
   if (nnz_blocks) *nnz_blocks = nnz;
   g->setup_done = true;
   return OFX_OK;

@@ -243,6 +243,7 @@ def main():
     pcg_ms, pcg_launches, _ = pipe.solver.timing(False)
     pf_used, pf_missed = pipe.solver.prefetch_stats()
     N_, M_, nnzb, _T, rows = pipe.solver.info()
+    pci = pipe.solver.precond_info()
     t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
     t_int = np.array([m[1].elapsed_time(m[2]) for m in marks]) * 1e-3
     pcg = [int(m[3]["_status"][2].item()) for m in marks]
@@ -307,6 +308,16 @@ def main():
     # converging one (drained: they end after the first memory trip) move no algorithmic bytes, so the
     # per-launch figure is iterations x bytes / launches, over the same launches rocprof averages.
     B_pcg = nnzb * 296 + rows * (1152 + 768 + 48 + 48)
+    if pci["schwarz"]:
+        # overlapping Schwarz (the default): an iteration is k_pcg_iter without the cluster inverse (the state, own m,
+        # w_new written: 768 + 48 + 48 B per row) + k_as_apply: per segment its fp16 inverse row (240 B), row scale and
+        # source slot (8 B); per output cluster its segment count / offsets (52 x 4 B), source list (100 B) and stop word
+        # (256 B); per gathered row its index (4 B); w (48 B per row) and the subdomains' column scales (24 B per
+        # subdomain row) once; m written (48 B per row)
+        C_ = pci["clusters"]
+        B_apply = (pci["segments"] * (240 + 8) + C_ * (52 * 4 + 100 + 256) + pci["gathered_rows"] * 4 + rows * 48
+                   + pci["subdomain_rows"] * 24 + rows * 48)
+        B_pcg = nnzb * 296 + rows * (768 + 48 + 48) + B_apply
     iters = float(np.sum(pcg))
     launches = max(1, pcg_launches)
     t_pcg = pcg_ms * 1e-3 / launches
@@ -314,6 +325,10 @@ def main():
     workload = (f"{D}^3 TSDF @{a.voxel * 1e3:g} mm, {seq.nodes.shape[0]} nodes, {a.matches} matches, "
                 f"{seq.cam.width}x{seq.cam.height} depth, {cfg['motion']}{' + occluder' if cfg['occluder'] else ''}, "
                 f"GN 10 it")
+    pcg_traffic = pmc_traffic("k_pcg_iter", workload)
+    if pci["schwarz"]:   # per launch: the mean of the pair (the chain alternates them)
+        t_apply = pmc_traffic("k_as_apply", workload)
+        pcg_traffic = None if pcg_traffic is None or t_apply is None else 0.5 * (pcg_traffic + t_apply)
     res = {
         "metric": f"fusion frames/sec (warp+integrate+solve), {640 // cfg['cam_scale']}x{480 // cfg['cam_scale']} depth "
                   f"-> {D}^3 TSDF",
@@ -333,11 +348,13 @@ def main():
                          "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid)),
                          "prefetched_setups_used": pf_used, "prefetched_setups_missed": pf_missed},
         "per_rank": per_rank,
-        "roofline": {"kernel": "k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster "
-                               "block-Jacobi apply)", "bound": "latency",
+        "roofline": {"kernel": ("k_pcg_iter + k_as_apply (one pipelined PCG iteration = two launches: wave-list block "
+                                "SpMV + recurrences, then the overlapping Schwarz apply)") if pci["schwarz"] else
+                               ("k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster "
+                                "block-Jacobi apply)"), "bound": "latency", "preconditioner": pci,
                      "achieved": B_launch / t_pcg / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": B_launch / t_pcg / PEAK_HBM,
-                     "traffic": pmc_traffic("k_pcg_iter", workload), "traffic_source": os.path.relpath(PMC_FILE, ROOT),
+                     "traffic": pcg_traffic, "traffic_source": os.path.relpath(PMC_FILE, ROOT),
                      "bytes_per_iteration": B_pcg, "bytes_per_launch": B_launch, "avg_launch_us": 1e6 * t_pcg,
                      "launches_per_frame": launches / a.steps, "iterations_per_frame": iters / a.steps,
                      "us_per_iteration": 1e6 * pcg_ms * 1e-3 / max(1.0, iters), "nnz_blocks": nnzb,

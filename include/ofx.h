@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define OFX_ABI_VERSION 3
+#define OFX_ABI_VERSION 4
 
 typedef void* ofx_stream_t; /* hipStream_t; NULL = legacy default stream */
 
@@ -392,7 +392,15 @@ typedef struct ofx_gn_params {
                                 when some node has rotated by more than this (radians, summed |omega| of the
                                 steps since the last rebuild); real data with large rotations (the moose demo)
                                 needs it, the synthetic bench never reaches it. 0: precond_every alone */
+  int32_t precond;           /* PCG preconditioner: OFX_PRECOND_SCHWARZ (1, default of the Python API): overlapping
+                                additive Schwarz over the 8-node clusters extended by up to 12 coupled ring nodes
+                                (two launches per PCG iteration, ~2.7x fewer iterations on the bench graph);
+                                OFX_PRECOND_CLUSTER (0): the clusters' block Jacobi (one launch per iteration). The
+                                Schwarz form needs the wave-list PCG (every 8-row wave <= 128 blocks, rows <= 20
+                                blocks) and falls back to the cluster blocks otherwise */
+  int32_t _pad1;
 } ofx_gn_params;
+enum { OFX_PRECOND_CLUSTER = 0, OFX_PRECOND_SCHWARZ = 1 };
 
 /* OFX_GN_ARAP restates DeformNet.arap (model/model.py:1639-1986), the graph-update solve for nodes
  * that are invisible or new: no match rows (n_matches = 0); node_conf = valid-node mask (1/0) and
@@ -442,6 +450,9 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
  * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
 int ofx_gn_info(void* handle, int64_t* info);
+/* The preconditioner of the last setup (bench / tools; synchronises the device): info[6] = [Schwarz active, clusters,
+ * apply segments (inverse rows of all output clusters), source subdomains, gathered rows, subdomain rows]. */
+int ofx_gn_precond_info(void* handle, int64_t* info);
 /* Waves per PCG cluster workgroup of k_pcg_iter for the last setup (before any: for a small problem): 2 up to
  * 384 clusters (default) or 1 (environment OFX_PCG_W1 set to anything but "" / "0" at create; tuning and A/B
  * only); larger problems always run one wave per cluster. */

@@ -31,7 +31,7 @@ class GnParams(ctypes.Structure):
                 ("lambda_flow", c_double), ("lambda_depth", c_double), ("lambda_arap", c_double),
                 ("lambda_motion", c_double), ("lm_factor", c_double), ("stop_loss_diff", c_double),
                 ("pcg_tol", c_double), ("mode", c_int32), ("precond_every", c_int32),
-                ("pcg_err_tol", c_double), ("precond_rot_tol", c_double)]
+                ("pcg_err_tol", c_double), ("precond_rot_tol", c_double), ("precond", c_int32), ("_pad1", c_int32)]
 
 
 class GnProblem(ctypes.Structure):
@@ -103,6 +103,7 @@ _SIGS = {
     "ofx_gn_destroy": [P],
     "ofx_gn_timing": [P, c_int32, P, P, P],
     "ofx_gn_info": [P, P],
+    "ofx_gn_precond_info": [P, P],
     "ofx_gn_pcg_waves": [P, P],
     "ofx_gn_step_fused": [P, P],
     "ofx_gn_stopped": [P, P],

@@ -214,7 +214,7 @@ struct Gn : GnDev {
   hipEvent_t ev_side = nullptr;
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   int32_t ep_next = 1;
-  int as_req = 0;                   // the Schwarz preconditioner is requested (enabled per setup: wave-list forms only)
+  int as_env = -1;                  // OFX_PRECOND override of params.precond (-1: none)
   int as_cap = 0;                   // clusters the Schwarz tables are allocated for
   // the PCG iteration's constant launch arguments (struct PcgIt) in device memory, and the bytes last copied there
   void* d_pcgit = nullptr;
@@ -3386,7 +3386,7 @@ static bool same_params(const ofx_gn_params& a, const ofx_gn_params& b) {
          a.lambda_depth == b.lambda_depth && a.lambda_arap == b.lambda_arap && a.lambda_motion == b.lambda_motion &&
          a.lm_factor == b.lm_factor && a.stop_loss_diff == b.stop_loss_diff && a.pcg_tol == b.pcg_tol &&
          a.mode == b.mode && a.precond_every == b.precond_every && a.pcg_err_tol == b.pcg_err_tol &&
-         a.precond_rot_tol == b.precond_rot_tol;
+         a.precond_rot_tol == b.precond_rot_tol && a.precond == b.precond;
 }
 
 }  // namespace ofx
@@ -3405,8 +3405,8 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   {   // tuning / A-B: OFX_PCG_W1=1 (any value but "0" / empty) selects one wave per cluster
     const char* e = getenv("OFX_PCG_W1");
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
-    const char* pe = getenv("OFX_PRECOND");   // A/B: "as" = overlapping Schwarz, "bj" = cluster block Jacobi
-    g->as_req = (pe && strcmp(pe, "as") == 0) ? 1 : 0;
+    const char* pe = getenv("OFX_PRECOND");   // A/B override of params.precond: "as" = Schwarz, "bj" = cluster blocks
+    g->as_env = (pe && strcmp(pe, "as") == 0) ? 1 : (pe && strcmp(pe, "bj") == 0) ? 0 : -1;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;
@@ -3491,6 +3491,32 @@ int ofx_gn_info(void* handle, int64_t* info) {
   if (g) prep_wait(g);   // a prefetch thread of this handle has finished
   OFX_CHECK_ARG(g && info, "null handle/info");
   info[0] = g->N_real; info[1] = g->M; info[2] = g->nnzb; info[3] = g->T; info[4] = g->N;
+  return OFX_OK;
+}
+
+int ofx_gn_precond_info(void* handle, int64_t* info) {
+  Gn* g = (Gn*)handle;
+  if (g) prep_wait(g);
+  OFX_CHECK_ARG(g && info, "null handle/info");
+  for (int k = 0; k < 6; ++k) info[k] = 0;
+  info[0] = g->as_on;
+  if (!g->as_on) return OFX_OK;
+  const int ncl = g->N / kCS;
+  const int sd = sync_side(g);
+  if (sd) return sd;
+  OFX_HIP(hipDeviceSynchronize());
+  std::vector<int32_t> meta((size_t)ncl * kAsMeta), gat((size_t)ncl * kAsGat), dom((size_t)ncl * kAsDN);
+  OFX_HIP(hipMemcpy(meta.data(), g->as_meta, meta.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  OFX_HIP(hipMemcpy(gat.data(), g->as_gat, gat.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  OFX_HIP(hipMemcpy(dom.data(), g->as_dom, dom.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  int64_t segs = 0, srcs = 0, rows = 0, drows = 0;
+  for (int c = 0; c < ncl; ++c) {
+    segs += meta[(size_t)c * kAsMeta];
+    srcs += meta[(size_t)c * kAsMeta + 1];
+    for (int i = 0; i < kAsGat; ++i) rows += gat[(size_t)c * kAsGat + i] >= 0 ? 1 : 0;
+    for (int l = 0; l < kAsDN; ++l) drows += dom[(size_t)c * kAsDN + l] >= 0 ? 1 : 0;
+  }
+  info[1] = ncl; info[2] = segs; info[3] = srcs; info[4] = rows; info[5] = drows;
   return OFX_OK;
 }
 
@@ -3717,6 +3743,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   OFX_CHECK_ARG(prm->num_iter >= 0 && prm->num_iter <= 64, "num_iter must be in [0,64]");
   OFX_CHECK_ARG(prm->pcg_max_iter >= 1, "pcg_max_iter must be >= 1");
   OFX_CHECK_ARG(prm->precond_rot_tol >= 0.0, "precond_rot_tol must be >= 0");
+  OFX_CHECK_ARG(prm->precond == OFX_PRECOND_CLUSTER || prm->precond == OFX_PRECOND_SCHWARZ, "bad precond %d", prm->precond);
   hipStream_t hs = as_stream(s);
   int N0 = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
   if ((int64_t)N0 * NB > 0) OFX_CHECK_ARG(pb->edges, "null edges");
@@ -3933,7 +3960,8 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   OFX_LAUNCH_CHECK();
   // Schwarz tables (blk_off still holds the per-block term counts' offsets)
   g->as_on = 0;
-  if (g->as_req && g->max_wave <= kWL && g->max_deg <= kRowMax) {
+  const bool as_req = g->as_env >= 0 ? g->as_env == 1 : g->prm.precond == OFX_PRECOND_SCHWARZ;
+  if (as_req && g->max_wave <= kWL && g->max_deg <= kRowMax) {   // (the Schwarz form needs the wave-list PCG)
     const int ncl = N / kCS;
     if (ncl > g->as_cap) {
       for (auto pp : {(void**)&g->as_cand, (void**)&g->as_csc, (void**)&g->as_acc, (void**)&g->as_dom, (void**)&g->as_meta,

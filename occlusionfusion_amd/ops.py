@@ -206,11 +206,12 @@ def _gn_problem(nodes, edges, edge_weights, tpos, conf, src, anchors, weights, t
 def _gn_params(fparams, iparams):
     """fparams = [lambda_flow, lambda_depth, lambda_arap, lambda_motion, lm_factor, stop_loss_diff, pcg_tol,
     pcg_err_tol, precond_rot_tol]; iparams = [num_iter, use_edge_weighting, pcg_max_iter, pcg_warm, mode,
-    precond_every]."""
+    precond_every(, precond: OFX_PRECOND_CLUSTER 0 / OFX_PRECOND_SCHWARZ 1, default 0)]."""
     p = _lib.GnParams()
     (p.lambda_flow, p.lambda_depth, p.lambda_arap, p.lambda_motion, p.lm_factor, p.stop_loss_diff,
      p.pcg_tol, p.pcg_err_tol, p.precond_rot_tol) = (float(v) for v in fparams)
-    p.num_iter, p.use_edge_weighting, p.pcg_max_iter, p.pcg_warm, p.mode, p.precond_every = (int(v) for v in iparams)
+    p.num_iter, p.use_edge_weighting, p.pcg_max_iter, p.pcg_warm, p.mode, p.precond_every = (int(v) for v in iparams[:6])
+    p.precond = int(iparams[6]) if len(iparams) > 6 else 0
     return p
 
 

@@ -25,7 +25,9 @@ from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
                    lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=2000, pcg_tol=2e-6,
-                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5, precond_rot_tol=0.1)
+                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5, precond_rot_tol=0.1, precond="schwarz")
+# PCG preconditioner (ofx_gn_params.precond): overlapping additive Schwarz or the 8-node cluster blocks
+_PRECOND = {"cluster": 0, "schwarz": 1}
 MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
 
 
@@ -105,6 +107,13 @@ class GaussNewtonSolver:
         call("ofx_gn_info", self._h, arr)
         return list(arr)
 
+    def precond_info(self):
+        """The last setup's preconditioner: dict(schwarz, clusters, segments, sources, gathered_rows, subdomain_rows)
+        (ofx_gn_precond_info; synchronises the device: tools and bench only)."""
+        arr = (ctypes.c_int64 * 6)()
+        call("ofx_gn_precond_info", self._h, arr)
+        return dict(zip(("schwarz", "clusters", "segments", "sources", "gathered_rows", "subdomain_rows"), list(arr)))
+
     def stopped(self):
         """The solve's stop flag as the host sees it (ofx_gn_stopped: no synchronisation)."""
         f = ctypes.c_int32()
@@ -146,7 +155,7 @@ class GaussNewtonSolver:
               float(q["lm_factor"]), float(q["stop_loss_diff"]), float(q["pcg_tol"] if pcg_tol is None else pcg_tol),
               float(q.get("pcg_err_tol", 0.0)), float(q.get("precond_rot_tol", 0.0))]
         ip = [int(q["num_iter"]), int(bool(q["use_edge_weighting"])), int(q["pcg_max_iter"]), int(bool(q["pcg_warm"])),
-              int(mode), int(q.get("precond_every", 1))]
+              int(mode), int(q.get("precond_every", 1)), _PRECOND[q.get("precond", "cluster")]]
         return fp, ip
 
     def _problem(self, graph_nodes, graph_edges, graph_edges_weights, target_node_position, node_confidence,

@@ -121,7 +121,7 @@ def test_gn_solve_op_equals_direct_call(cuda, golden_dir):
     fp, ip = s._plist()
     (p.lambda_flow, p.lambda_depth, p.lambda_arap, p.lambda_motion, p.lm_factor, p.stop_loss_diff, p.pcg_tol,
      p.pcg_err_tol, p.precond_rot_tol) = fp
-    p.num_iter, p.use_edge_weighting, p.pcg_max_iter, p.pcg_warm, p.mode, p.precond_every = ip
+    p.num_iter, p.use_edge_weighting, p.pcg_max_iter, p.pcg_warm, p.mode, p.precond_every, p.precond = ip
     rot, trans = torch.empty((N, 3, 3), device=cuda), torch.empty((N, 3), device=cuda)
     status, loss = torch.zeros(5, dtype=torch.int32, device=cuda), torch.zeros((ip[0], 4), dtype=torch.float64,
                                                                                 device=cuda)

@@ -78,6 +78,7 @@ def parse():
     p.add_argument("--scene-rank", type=int, default=None,
                    help="config 5: run this rank's independent scene (default: the process's own rank)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--gn", action="append", default=[], metavar="KEY=VALUE", help=argparse.SUPPRESS)   # (A/B: GN params)
     p.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                    help="set up each frame's solve inline instead of prefetching it during the previous frame")
     p.add_argument("--cpu-sample", type=int, default=1 << 24)
@@ -182,7 +183,12 @@ def main():
     scene_seed = int(seq.seed)
     sharded = a.mode == "shard" and world > 1
     shard = (rank, world, "hash") if sharded else None   # spatial-hash brick buckets (sharding.hash_owner)
-    pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard)
+    gn_over = {}
+    for kv in a.gn:   # (tuning A/B only; the bench line is quoted at the defaults)
+        k, v = kv.split("=", 1)
+        gn_over[k] = v if k == "precond" else float(v)
+    pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard,
+                          gn_params=gn_over or None)
     total = a.warmup + a.steps + 1
     frames = [pipe.prepare(t) for t in range(total + 1)]   # + the frame the last timed step prefetches
     torch.cuda.synchronize()

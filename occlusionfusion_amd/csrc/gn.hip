@@ -215,6 +215,7 @@ struct Gn : GnDev {
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   int32_t ep_next = 1;
   int as_env = -1;                  // OFX_PRECOND override of params.precond (-1: none)
+  int as_l1 = 1;                    // k_as_apply with one lane per segment (0: two, OFX_AS_L2)
   int as_cap = 0;                   // clusters the Schwarz tables are allocated for
   // the PCG iteration's constant launch arguments (struct PcgIt) in device memory, and the bytes last copied there
   void* d_pcgit = nullptr;
@@ -1598,20 +1599,27 @@ __global__ __launch_bounds__(256) void k_as_segments(GnDev g) {
 }
 
 // Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= 120 x 120, f64, 8x8 entries per
-// thread in registers: rows tr + 16a, columns tc + 16b), its in-place Gauss-Jordan inverse (SPD: no pivoting; row and
-// column k pass through LDS, double-buffered: one barrier per step), scaled and rounded to fp16 with a certified diagonal
-// margin (below) and written symmetric (the upper triangle's value to both entries) into the segments' slab rows; a
-// non-positive or non-finite pivot falls back to the identity on the cluster's own rows. mode 1: always (the solve's first GN step and precond_every steps; the cold start's
-// records x = 0, r = b and the PCG flags too); mode 0: only when the previous step flagged a refresh (precond_rot_tol).
-__global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __restrict__ A, const double* __restrict__ rhs,
-                                                   int mode, int gn_iter) {
+// thread in registers: rows tr + 16a, columns tc + 16b), its in-place block Gauss-Jordan inverse (SPD: no pivoting;
+// 2x2 pivot blocks through LDS, double-buffered: one barrier per two steps), scaled and rounded to fp16 with a certified
+// diagonal margin (below) and written symmetric into the segments' slab rows; a non-positive or non-finite pivot falls
+// back to the identity on the cluster's own rows; the cluster's rows' rotation accumulators restart (precond_rot_tol).
+// (A workgroup of 256 threads; every thread must call it: it synchronises the workgroup.)
+__device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __restrict__ A, int c, int t) {
   __shared__ int s_dom[kAsDN];
   __shared__ int s_sl[kAsDN][kAsDN];
+  __shared__ int s_dst[kAsD];
   __shared__ double s_row[2][2][128], s_col[2][2][128];
-  const int c = blockIdx.x, t = threadIdx.x, tr = t >> 4, tc = t & 15;
-  if (g.flags[F_STOPPED]) return;
-  if (mode == 0 && g.flags[F_REFRESH] != gn_iter) return;
+  __shared__ __attribute__((aligned(16))) uint16_t s_z[kAsD * kAsD];   // the stored fp16 form, (R, C), both triangles
+  const int tr = t >> 4, tc = t & 15;
+#ifdef OFX_STAMPS   // tuning build: phase stamps of thread 0 in the stamps buffer's iteration-63 slot
+#define OFX_AS_STAMP(k) \
+  if (t == 0 && g.stamps) g.stamps[((int64_t)63 * g.nwg_row + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OFX_AS_STAMP(k)
+#endif
+  OFX_AS_STAMP(0)
   if (t < kAsDN) s_dom[t] = g.as_dom[c * kAsDN + t];
+  if (t < kAsD) s_dst[t] = g.as_dst[(int64_t)c * kAsD + t];
   __syncthreads();
   int nd = 0;
   for (int i = 0; i < kAsDN; ++i) nd += s_dom[i] >= 0 ? 1 : 0;
@@ -1621,13 +1629,7 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
   }
   __syncthreads();
   const int n = 6 * nd;
-  // every load unconditional (clamped addresses, masked values): a load behind a branch gets its own wait, and 64 of
-  // them in a row cost ~100 us
-  int dR[8], dC[8];   // the slab positions of the thread's rows and columns (as rows of the mirrored entries)
-#pragma unroll
-  for (int a = 0; a < 8; ++a) dR[a] = g.as_dst[(int64_t)c * kAsD + min(tr + 16 * a, kAsD - 1)];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) dC[b] = g.as_dst[(int64_t)c * kAsD + min(tc + 16 * b, kAsD - 1)];
+  // every load unconditional (clamped addresses, masked values): a load behind a branch gets its own wait
   double M[8][8];
   int slv[8][8];
 #pragma unroll
@@ -1648,6 +1650,7 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
       // (beyond n: the identity, never touched by the steps below)
       M[a][b] = (R < n && C < n) ? (slv[a][b] >= 0 ? M[a][b] : 0.0) : (R == C ? 1.0 : 0.0);
     }
+  OFX_AS_STAMP(1)
   bool bad = false;
   int buf = 0;
   // Block Gauss-Jordan with 2x2 pivot blocks P = rows / columns {k, k+1} (two elimination steps per barrier: the ~0.7 us
@@ -1698,6 +1701,7 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
   OFX_AS_STEPS(4) OFX_AS_STEPS(5) OFX_AS_STEPS(6) OFX_AS_STEPS(7)
 #undef OFX_AS_STEPS
   bad = __syncthreads_or(bad ? 1 : 0) != 0;
+  OFX_AS_STAMP(2)
   // Stored form: Z = D Ẑ D with d = √diag(Z), so Ẑ has a unit diagonal and |Ẑ_ij| <= 1 (Z is SPD), and Ẑ's off-diagonal
   // entries as fp16 (absolute error <= 2^-12). E = the rounding of the off-diagonal entries; the diagonal is stored as
   // 1 + σ with σ = ‖E‖_F + 2^-10 >= ‖E‖₂ + the diagonal's own rounding, so the stored Ẑ̃ >= Ẑ: positive definite whatever
@@ -1738,11 +1742,11 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
     s_sig = sqrt(sum) + 0x1p-10;
   }
   __syncthreads();
+  OFX_AS_STAMP(3)
   const double sig = s_sig;
-  auto put = [&](int d, int C, _Float16 h) {   // d: the row's slab position (output cluster · kAsRS + segment)
-    const int cp = d / kAsRS, rs = d % kAsRS;
-    g.as_slab[(((int64_t)cp * kAsK + C / 8) * kAsRS + rs) * 8 + (C & 7)] = __builtin_bit_cast(uint16_t, h);
-  };
+  // the stored form into LDS (the upper triangle's value to both entries), then the rows to their segments' slab rows
+  // as 16-B words (scattered 2-B stores of the entries cost ~80 us per solve)
+  auto b16 = [](_Float16 h) { return __builtin_bit_cast(uint16_t, h); };
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
@@ -1750,13 +1754,13 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
       const int R = tr + 16 * a, C = tc + 16 * b;
       if (R >= n || C >= kAsD) continue;
       if (C >= n) {
-        put(dR[a], C, (_Float16)0.0f);
+        s_z[R * kAsD + C] = 0;
       } else if (R == C) {
-        put(dR[a], C, bad ? (_Float16)(R < 6 * kCS ? 1.0f : 0.0f) : h16(1.0 + sig));
+        s_z[R * kAsD + C] = b16(bad ? (_Float16)(R < 6 * kCS ? 1.0f : 0.0f) : h16(1.0 + sig));
       } else if (R < C) {
-        const _Float16 h = bad ? (_Float16)0.0f : h16(M[a][b] / (dr[a] * dc[b]));
-        put(dR[a], C, h);
-        put(dC[b], R, h);
+        const uint16_t h = b16(bad ? (_Float16)0.0f : h16(M[a][b] / (dr[a] * dc[b])));
+        s_z[R * kAsD + C] = h;
+        s_z[C * kAsD + R] = h;
       }
     }
   if (tc == 0)
@@ -1764,10 +1768,27 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
     for (int a = 0; a < 8; ++a) {
       const int R = tr + 16 * a;
       if (R < kAsD) g.as_dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
-      if (R < n) g.as_rsc[dR[a]] = (float)dr[a];
+      if (R < n) g.as_rsc[s_dst[R]] = (float)dr[a];
     }
+  __syncthreads();
+  OFX_AS_STAMP(4)
+  for (int i = t; i < n * kAsK; i += 256) {
+    const int R = i / kAsK, k = i % kAsK;
+    const int d = s_dst[R], cp = d / kAsRS, rs = d % kAsRS;
+    reinterpret_cast<uint4*>(g.as_slab)[((int64_t)cp * kAsK + k) * kAsRS + rs] =
+        reinterpret_cast<const uint4*>(s_z + R * kAsD)[k];
+  }
   if (t < kCS) g.racc[c * kCS + t] = 0.0;
-  if (mode != 1) return;
+  OFX_AS_STAMP(5)
+#undef OFX_AS_STAMP
+}
+
+// The subdomain inverses of a solve's first GN step (and precond_every steps); the cold start's records x = 0, r = b and
+// the PCG flags too. (A refresh flagged by the previous step runs inside k_pcg_proj<.., true>.)
+__global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __restrict__ A, const double* __restrict__ rhs) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (g.flags[F_STOPPED]) return;
+  as_invert_body(g, A, c, t);
   if (!g.warm_now && t < 6 * kCS) {   // cold start: x = 0, r = b (u = M⁻¹ b comes from k_as_apply into m1)
     const int64_t o = 6 * (int64_t)c * kCS + t;
     const double v[V_N] = {0.0, rhs[o], 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1785,25 +1806,30 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
 // Trip 1: the stop word (kTest: the PCG chain's launches after convergence end there), the gather list, the segment's
 // source slot and the row offsets; trip 2: the gathered rows and the slab rows together (static addresses; threads past
 // the segment count read the last segment's lines, one line per load instruction).
-template <bool kTest>
-__global__ __launch_bounds__(192) void k_as_apply(const int32_t* stopw, const int32_t* meta, const int32_t* gat,
-                                                  const uint16_t* slab, const double* in, double* out, const int32_t* src,
-                                                  const float* dsc, const float* rsc) {
+template <bool kTest, int kL>   // kL: lanes per segment (1: 192 threads, 2: 384 — the dot products spread over 4 SIMDs)
+__global__ __launch_bounds__(kAsRS * kL) void k_as_apply(const int32_t* stopw, const int32_t* meta, const int32_t* gat,
+                                                        const uint16_t* slab, const double* in, double* out,
+                                                        const int32_t* src, const float* dsc, const float* rsc) {
+  constexpr int kT = kAsRS * kL;                 // threads
+  constexpr int kG = (kAsGat + kT - 1) / kT;     // gathered rows per thread
+  constexpr int kKL = (kAsK + kL - 1) / kL;      // 16-B words of its segment per lane
   __shared__ __attribute__((aligned(16))) double s_w[kAsSrc * kAsD];
   __shared__ double s_seg[kAsRS];
   const int c = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int sg = t / kL, hl = t % kL;            // the thread's segment and its part
   const int32_t* mt = meta + (int64_t)c * kAsMeta;
   int stop = 0;
   if (kTest) stop = stopw[(int64_t)c * 64 + lane];
   const int nrs = mt[0];
-  int gn[3];
+  int gn[kG], sv[kG];   // gathered rows and their source subdomains
 #pragma unroll
-  for (int j = 0; j < 3; ++j) gn[j] = gat[(int64_t)c * kAsGat + kAsRS * j + t];
-  const int sl = mt[64 + t];
-  const float rscale = rsc[(int64_t)c * kAsRS + t];
-  int sv[3];   // the gathered rows' source subdomains
-#pragma unroll
-  for (int j = 0; j < 3; ++j) sv[j] = src[c * kAsSrc + min((kAsRS * j + t) / kAsDN, kAsSrc - 1)];
+  for (int j = 0; j < kG; ++j) {
+    const int i = min(kT * j + t, kAsGat - 1);
+    gn[j] = gat[(int64_t)c * kAsGat + i];
+    sv[j] = src[c * kAsSrc + min(i / kAsDN, kAsSrc - 1)];
+  }
+  const int sl = mt[64 + sg];
+  const float rscale = rsc[(int64_t)c * kAsRS + sg];
   const int rr = t < 6 * kCS ? t : 6 * kCS - 1;
   const int o0 = mt[2 + rr], o1 = mt[3 + rr];
   asm volatile("" ::: "memory");
@@ -1811,25 +1837,26 @@ __global__ __launch_bounds__(192) void k_as_apply(const int32_t* stopw, const in
     stop = __builtin_amdgcn_readfirstlane(stop);
     if (stop != 0) return;   // the solve has converged (or stopped): a drained launch
   }
-  double2 wg[3][3];
-  float2 dg[3][3];   // the source subdomains' column scales of the gathered rows
+  double2 wg[kG][3];
+  float2 dg[kG][3];   // the source subdomains' column scales of the gathered rows
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
+  for (int j = 0; j < kG; ++j) {
+    const int i = min(kT * j + t, kAsGat - 1);
     const double2* p = reinterpret_cast<const double2*>(in + 6 * (int64_t)(gn[j] >= 0 ? gn[j] : 0));
-    const float2* q = reinterpret_cast<const float2*>(dsc + (int64_t)sv[j] * kAsD + 6 * ((kAsRS * j + t) % kAsDN));
+    const float2* q = reinterpret_cast<const float2*>(dsc + (int64_t)sv[j] * kAsD + 6 * (i % kAsDN));
 #pragma unroll
     for (int k = 0; k < 3; ++k) { wg[j][k] = p[k]; dg[j][k] = q[k]; }
   }
-  uint4 z[kAsK];   // 8 bf16 inverse entries each
+  uint4 z[kKL];   // 8 fp16 entries each: words hl·kKL .. of the segment (clamped; the tail word is masked)
   {
-    const int rs = t < nrs ? t : (nrs > 0 ? nrs - 1 : 0);
+    const int rs = sg < nrs ? sg : (nrs > 0 ? nrs - 1 : 0);
     const uint4* zp = reinterpret_cast<const uint4*>(slab) + (int64_t)c * kAsK * kAsRS + rs;
 #pragma unroll
-    for (int k = 0; k < kAsK; ++k) z[k] = zp[k * kAsRS];
+    for (int k = 0; k < kKL; ++k) z[k] = zp[min(hl * kKL + k, kAsK - 1) * kAsRS];
   }
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int i = kAsRS * j + t;
+  for (int j = 0; j < kG; ++j) {
+    const int i = kT * j + t;
     if (i < kAsSrc * kAsDN) {
       const bool ok = gn[j] >= 0;
 #pragma unroll
@@ -1843,14 +1870,17 @@ __global__ __launch_bounds__(192) void k_as_apply(const int32_t* stopw, const in
   // the segment's dot product in f64 (fp16 entries exact in f64): the apply is linear to f64 rounding. (An f32 image and
   // f32 products, measured: 3 % faster, but the rounding made the apply nonlinear at 1e-7 — the pipelined recurrences
   // drifted, gn_4k's loss log missed 1e-6 and the ill-conditioned moose ended 0.29 off.)
-  if (t < nrs) {
+  double dot = 0.0;
+  if (sg < nrs) {
     const double2* w2 = reinterpret_cast<const double2*>(s_w + sl * kAsD);
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     auto lo = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); };
     auto hi = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); };
 #pragma unroll
-    for (int k = 0; k < kAsK; ++k) {
-      const double2 p0 = w2[4 * k], p1 = w2[4 * k + 1], p2 = w2[4 * k + 2], p3 = w2[4 * k + 3];
+    for (int k = 0; k < kKL; ++k) {
+      const int kw = hl * kKL + k;
+      if (kw >= kAsK) break;   // (compile-time for kL = 1; the last lane's tail word for kL = 2)
+      const double2 p0 = w2[4 * kw], p1 = w2[4 * kw + 1], p2 = w2[4 * kw + 2], p3 = w2[4 * kw + 3];
       a0 = fma(lo(z[k].x), p0.x, a0);
       a1 = fma(hi(z[k].x), p0.y, a1);
       a2 = fma(lo(z[k].y), p1.x, a2);
@@ -1860,17 +1890,19 @@ __global__ __launch_bounds__(192) void k_as_apply(const int32_t* stopw, const in
       a2 = fma(lo(z[k].w), p3.x, a2);
       a3 = fma(hi(z[k].w), p3.y, a3);
     }
-    s_seg[t] = (double)rscale * ((a0 + a1) + (a2 + a3));
+    dot = (a0 + a1) + (a2 + a3);
   }
+  if (kL == 2) dot += dpp_mov<0xB1>(dot);   // quad_perm [1, 0, 3, 2]: the pair's two parts (the same sum in both lanes)
+  if (sg < nrs && hl == 0) s_seg[sg] = (double)rscale * dot;
   __syncthreads();
   if (t < 6 * kCS) {
-    double sv[kAsX + 1];
+    double sv2[kAsX + 1];
 #pragma unroll
-    for (int j = 0; j <= kAsX; ++j) sv[j] = s_seg[min(o0 + j, kAsRS - 1)];
-    double s = 0.0;
+    for (int j = 0; j <= kAsX; ++j) sv2[j] = s_seg[min(o0 + j, kAsRS - 1)];
+    double sum = 0.0;
 #pragma unroll
-    for (int j = 0; j <= kAsX; ++j) s += o0 + j < o1 ? sv[j] : 0.0;
-    out[(int64_t)c * 6 * kCS + t] = s;
+    for (int j = 0; j <= kAsX; ++j) sum += o0 + j < o1 ? sv2[j] : 0.0;
+    out[(int64_t)c * 6 * kCS + t] = sum;
   }
 }
 
@@ -1903,9 +1935,16 @@ __device__ __forceinline__ void proj_accumulate(const double bk[36], const doubl
 // A GN step flagged by the previous step's update (F_REFRESH = this step: some node rotated by more than
 // precond_rot_tol since its cluster inverse was built) first rebuilds the cluster inverses here, one wave per
 // cluster as k_pcg_prep (k_pcg_proj2 applies them); otherwise the flag costs one scalar load with the stop flag.
-template <bool kWave>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs,
+// kAS (Schwarz): four waves; a refresh flagged by the previous step (F_REFRESH = this step) rebuilds the cluster's
+// subdomain inverse first (as_invert_body, all four waves), then wave 0 does the projection.
+template <bool kWave, bool kAS = false>
+__global__ __launch_bounds__(kAS ? 256 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs,
                                                                                               int gn_iter) {
+  if constexpr (kAS) {
+    if (g.flags[F_STOPPED]) return;
+    if (g.flags[F_REFRESH] == gn_iter) as_invert_body(g, g.Aop, blockIdx.x, threadIdx.x);
+    if (threadIdx.x >= 64) return;
+  }
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
   asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.col), "s"(g.xh), "s"(g.th), "s"(g.N), "s"(g.flags), "s"(g.n_prev),
                "s"(g.Aop), "s"(g.part_p), "s"(g.nw_pad), "s"(rhs));
@@ -3159,21 +3198,23 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool as = g->as_on != 0;   // (the setup enables it only with the wave-list forms)
   const int ncl = g->N / kCS;
   auto as_apply = [&](bool test, const double* in, double* out) {
-    auto k = test ? k_as_apply<true> : k_as_apply<false>;
-    hipLaunchKernelGGL(k, dim3(ncl), dim3(kAsRS), 0, hs, (const int32_t*)g->stopw, (const int32_t*)g->as_meta,
+    auto k = g->as_l1 ? (test ? k_as_apply<true, 1> : k_as_apply<false, 1>)
+                      : (test ? k_as_apply<true, 2> : k_as_apply<false, 2>);
+    hipLaunchKernelGGL(k, dim3(ncl), dim3(g->as_l1 ? kAsRS : 2 * kAsRS), 0, hs, (const int32_t*)g->stopw, (const int32_t*)g->as_meta,
                        (const int32_t*)g->as_gat, (const uint16_t*)g->as_slab, in, out, (const int32_t*)g->as_src,
                        (const float*)g->as_dsc, (const float*)g->as_rsc);
   };
   if (as) {
-    // the subdomain inverses: rebuilt like the cluster inverses (invert), or when the previous step flagged a refresh
-    if (invert || g->prm.precond_rot_tol > 0.0)
-      hipLaunchKernelGGL(k_as_invert, dim3(ncl), dim3(256), 0, hs, *g, (const double*)A, (const double*)rhs, invert, gn_iter);
+    // the subdomain inverses: rebuilt like the cluster inverses (invert); a refresh flagged by the previous step runs
+    // inside k_pcg_proj<.., true>
+    if (invert) hipLaunchKernelGGL(k_as_invert, dim3(ncl), dim3(256), 0, hs, *g, (const double*)A, (const double*)rhs);
     if (!g->warm_now) as_apply(false, rhs, g->m1);   // cold start: u0 = M⁻¹ b
   } else if (invert) {
     hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
   }
   if (g->warm_now) {
-    if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
+    if (as) hipLaunchKernelGGL((k_pcg_proj<true, true>), dim3(g->nwg_row), dim3(256), 0, hs, *g, (const double*)rhs, gn_iter);
+    else if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     switch (g->pcg_ku) {
       case 2: hipLaunchKernelGGL(k_pcg_proj2<2>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
@@ -3407,6 +3448,9 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
     const char* pe = getenv("OFX_PRECOND");   // A/B override of params.precond: "as" = Schwarz, "bj" = cluster blocks
     g->as_env = (pe && strcmp(pe, "as") == 0) ? 1 : (pe && strcmp(pe, "bj") == 0) ? 0 : -1;
+    // A/B: two lanes per Schwarz segment (OFX_AS_L2=1; 342 / 373 against 373 / 357 frames/s with one, one box: noise)
+    const char* le = getenv("OFX_AS_L2");
+    g->as_l1 = (le && le[0] && strcmp(le, "0") != 0) ? 0 : 1;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;

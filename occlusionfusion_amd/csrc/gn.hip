@@ -3299,6 +3299,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       chunk = std::max(4, (int)std::lround(lp * ratio) + ratio_margin);
     }
   }
+  // iterations per top-up after a chunk ran out (OFX_PCG_TOPUP=<n>, A/B; read per solve): 8 for the cluster blocks, 4 for
+  // Schwarz (two launches each: 472 -> 458 launches per frame, 360 / 344 -> 378 / 361 frames/s; 2 with a margin of 1:
+  // 442 launches but 4.0 us each, slower; profiles/r05_ab.json)
+  const char* te = getenv("OFX_PCG_TOPUP");
+  const int topup = te && atoi(te) > 0 ? atoi(te) : (as ? 4 : 8);
   int it = 0;
   while (it < max_it) {
     const int n = chunk < max_it - it ? chunk : max_it - it;
@@ -3344,7 +3349,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       break;
     }
     (void)ran;   // the chunk ran out without convergence: next chunk
-    chunk = 8;
+    chunk = topup;
   }
   g->n_iter_launches += as ? 2 * it : it;   // (Schwarz: each iteration is two launches)
   if (g->timing) g->ev.emplace_back(e0, e1);

@@ -20,3 +20,6 @@ rm -rf gpurun_out/prof_final
 timeout -k 10 900 python bench.py > gpurun_out/bench_full.log 2>&1
 tail -1 gpurun_out/bench_full.log > gpurun_out/${TAG}_bench.json
 cat gpurun_out/${TAG}_bench.json
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.log 2>&1
+tail -1 gpurun_out/bench_driver.log > gpurun_out/${TAG}_bench_driver_form.json
+cat gpurun_out/${TAG}_bench_driver_form.json

@@ -17,7 +17,8 @@ import sys
 
 import numpy as np
 
-KERNELS = {"k_pcg_iter": ("ofx::k_pcg_iter<true, false",),
+KERNELS = {"k_pcg_iter": ("ofx::k_pcg_iter<true, false",), "k_as_apply": ("ofx::k_as_apply<true",),
+           "k_as_invert": ("ofx::k_as_invert(",),
            "k_integrate_warp": ("ofx::k_integrate_pal4<true>", "ofx::k_integrate<true, true"),
            "k_assemble": ("ofx::k_assemble(",), "k_terms": ("ofx::k_terms(",),
            "k_brick_cull": ("ofx::k_brick_cull(ofx::BrickGeom, ofx::BrickDiv",), "k_tile_max": ("ofx::k_tile_max(",)}

@@ -3792,7 +3792,8 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   OFX_CHECK_ARG(prm->num_iter >= 0 && prm->num_iter <= 64, "num_iter must be in [0,64]");
   OFX_CHECK_ARG(prm->pcg_max_iter >= 1, "pcg_max_iter must be >= 1");
   OFX_CHECK_ARG(prm->precond_rot_tol >= 0.0, "precond_rot_tol must be >= 0");
-  OFX_CHECK_ARG(prm->precond == OFX_PRECOND_CLUSTER || prm->precond == OFX_PRECOND_SCHWARZ, "bad precond %d", prm->precond);
+  OFX_CHECK_ARG(prm->precond == OFX_PRECOND_CLUSTER || prm->precond == OFX_PRECOND_SCHWARZ || prm->precond == OFX_PRECOND_AUTO,
+                "bad precond %d", prm->precond);
   hipStream_t hs = as_stream(s);
   int N0 = pb->n_nodes, M = pb->n_matches, NB = pb->n_neighbors;
   if ((int64_t)N0 * NB > 0) OFX_CHECK_ARG(pb->edges, "null edges");
@@ -4009,7 +4010,10 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   OFX_LAUNCH_CHECK();
   // Schwarz tables (blk_off still holds the per-block term counts' offsets)
   g->as_on = 0;
-  const bool as_req = g->as_env >= 0 ? g->as_env == 1 : g->prm.precond == OFX_PRECOND_SCHWARZ;
+  constexpr int kAsAutoNodes = 1536;   // OFX_PRECOND_AUTO: Schwarz from this graph size on (ofx.h)
+  const bool as_req = g->as_env >= 0 ? g->as_env == 1
+                                     : (g->prm.precond == OFX_PRECOND_SCHWARZ ||
+                                        (g->prm.precond == OFX_PRECOND_AUTO && g->N_real >= kAsAutoNodes));
   if (as_req && g->max_wave <= kWL && g->max_deg <= kRowMax) {   // (the Schwarz form needs the wave-list PCG)
     const int ncl = N / kCS;
     if (ncl > g->as_cap) {

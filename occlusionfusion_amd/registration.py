@@ -25,9 +25,10 @@ from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
                    lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=2000, pcg_tol=2e-6,
-                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5, precond_rot_tol=0.3, precond="schwarz")
-# PCG preconditioner (ofx_gn_params.precond): overlapping additive Schwarz or the 8-node cluster blocks
-_PRECOND = {"cluster": 0, "schwarz": 1}
+                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5, precond_rot_tol=0.3, precond="auto")
+# PCG preconditioner (ofx_gn_params.precond): overlapping additive Schwarz, the 8-node cluster blocks, or
+# auto (Schwarz for graphs of >= 1536 nodes)
+_PRECOND = {"cluster": 0, "schwarz": 1, "auto": 2}
 MAX_MATCHES_EVAL = 10000   # settings/custom_settings.py:36
 
 

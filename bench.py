@@ -316,12 +316,12 @@ def main():
     B_pcg = nnzb * 296 + rows * (1152 + 768 + 48 + 48)
     if pci["schwarz"]:
         # overlapping Schwarz (the default): an iteration is k_pcg_iter without the cluster inverse (the state, own m,
-        # w_new written: 768 + 48 + 48 B per row) + k_as_apply: per segment its fp16 inverse row (240 B), row scale and
+        # w_new written: 768 + 48 + 48 B per row) + k_as_apply: per segment its fp16 inverse row (2 B per entry), row scale and
         # source slot (8 B); per output cluster its segment count / offsets (52 x 4 B), source list (100 B) and stop word
         # (256 B); per gathered row its index (4 B); w (48 B per row) and the subdomains' column scales (24 B per
         # subdomain row) once; m written (48 B per row)
         C_ = pci["clusters"]
-        B_apply = (pci["segments"] * (240 + 8) + C_ * (52 * 4 + 100 + 256) + pci["gathered_rows"] * 4 + rows * 48
+        B_apply = (pci["segments"] * (2 * pci["row_length"] + 8) + C_ * (52 * 4 + 100 + 256) + pci["gathered_rows"] * 4 + rows * 48
                    + pci["subdomain_rows"] * 24 + rows * 48)
         B_pcg = nnzb * 296 + rows * (768 + 48 + 48) + B_apply
     iters = float(np.sum(pcg))

@@ -454,8 +454,9 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
  * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
 int ofx_gn_info(void* handle, int64_t* info);
-/* The preconditioner of the last setup (bench / tools; synchronises the device): info[6] = [Schwarz active, clusters,
- * apply segments (inverse rows of all output clusters), source subdomains, gathered rows, subdomain rows]. */
+/* The preconditioner of the last setup (bench / tools; synchronises the device): info[7] = [Schwarz active, clusters,
+ * apply segments (inverse rows of all output clusters), source subdomains, gathered rows, subdomain rows, entries per
+ * segment row]. */
 int ofx_gn_precond_info(void* handle, int64_t* info);
 /* Waves per PCG cluster workgroup of k_pcg_iter for the last setup (before any: for a small problem): 2 up to
  * 384 clusters (default) or 1 (environment OFX_PCG_W1 set to anything but "" / "0" at create; tuning and A/B

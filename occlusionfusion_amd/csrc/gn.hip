@@ -63,9 +63,14 @@ constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² en
 // Overlapping additive Schwarz (as_on): the ring of a cluster holds its kAsRing A-neighbours with the most coupling terms,
 // and a row joins at most kAsX rings, so an output cluster has at most kAsSrc contributing subdomains and kAsRS row
 // segments (a 120-entry inverse row each); kAsGat >= kAsSrc·kAsDN rounded to 3 per thread of the apply's 192
-constexpr int kAsRing = 12, kAsX = 3, kAsDN = kCS + kAsRing, kAsD = 6 * kAsDN, kAsK = kAsD / 8, kAsSrc = 1 + kCS * kAsX,
-              kAsRS = 6 * kCS * (1 + kAsX), kAsGat = 576, kAsMeta = 64 + kAsRS;
-static_assert(kAsSrc * kAsDN <= kAsGat && kAsGat == 3 * kAsRS && kAsD % 8 == 0 && kAsD <= 128, "Schwarz tables");
+#ifndef OFX_AS_RING   // (tuning builds: -DOFX_AS_RING=16)
+#define OFX_AS_RING 16
+#endif
+constexpr int kAsRing = OFX_AS_RING, kAsX = 3, kAsDN = kCS + kAsRing, kAsD = 6 * kAsDN, kAsK = kAsD / 8,
+              kAsSrc = 1 + kCS * kAsX, kAsRS = 6 * kCS * (1 + kAsX),
+              kAsGat = (kAsSrc * kAsDN + kAsRS - 1) / kAsRS * kAsRS, kAsMeta = 64 + kAsRS;
+constexpr int kAsTi = (kAsD + 15) / 16;   // k_as_invert's register tile (16 x 16 threads, kAsTi x kAsTi entries each)
+static_assert(kAsSrc * kAsDN <= kAsGat && kAsD % 8 == 0 && kAsTi <= 9, "Schwarz tables");
 
 // Everything the kernels read: trivially copyable, passed by value as the kernel argument (host-only
 // members live in Gn below, so a launch copies these bytes and nothing else).
@@ -1598,8 +1603,8 @@ __global__ __launch_bounds__(256) void k_as_segments(GnDev g) {
   if (lane < kAsSrc) g.as_src[cp * kAsSrc + lane] = lane < nsrc ? s_src[lane] : 0;
 }
 
-// Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= 120 x 120, f64, 8x8 entries per
-// thread in registers: rows tr + 16a, columns tc + 16b), its in-place block Gauss-Jordan inverse (SPD: no pivoting;
+// Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= kAsD x kAsD, f64, kAsTi x kAsTi
+// entries per thread in registers: rows tr + 16a, columns tc + 16b), its in-place block Gauss-Jordan inverse (SPD: no pivoting;
 // 2x2 pivot blocks through LDS, double-buffered: one barrier per two steps), scaled and rounded to fp16 with a certified
 // diagonal margin (below) and written symmetric into the segments' slab rows; a non-positive or non-finite pivot falls
 // back to the identity on the cluster's own rows; the cluster's rows' rotation accumulators restart (precond_rot_tol).
@@ -1608,7 +1613,7 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   __shared__ int s_dom[kAsDN];
   __shared__ int s_sl[kAsDN][kAsDN];
   __shared__ int s_dst[kAsD];
-  __shared__ double s_row[2][2][128], s_col[2][2][128];
+  __shared__ double s_row[2][2][16 * kAsTi], s_col[2][2][16 * kAsTi];
   __shared__ __attribute__((aligned(16))) uint16_t s_z[kAsD * kAsD];   // the stored fp16 form, (R, C), both triangles
   const int tr = t >> 4, tc = t & 15;
 #ifdef OFX_STAMPS   // tuning build: phase stamps of thread 0 in the stamps buffer's iteration-63 slot
@@ -1630,12 +1635,12 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   __syncthreads();
   const int n = 6 * nd;
   // every load unconditional (clamped addresses, masked values): a load behind a branch gets its own wait
-  double M[8][8];
-  int slv[8][8];
+  double M[kAsTi][kAsTi];
+  int slv[kAsTi][kAsTi];
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < kAsTi; ++a)
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < kAsTi; ++b) {
       const int R = tr + 16 * a, C = tc + 16 * b;
       const int sl = (R < n && C < n) ? s_sl[min(R / 6, kAsDN - 1)][min(C / 6, kAsDN - 1)] : -1;
       slv[a][b] = sl;
@@ -1643,9 +1648,9 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
     }
   asm volatile("" ::: "memory");
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < kAsTi; ++a)
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < kAsTi; ++b) {
       const int R = tr + 16 * a, C = tc + 16 * b;
       // (beyond n: the identity, never touched by the steps below)
       M[a][b] = (R < n && C < n) ? (slv[a][b] >= 0 ? M[a][b] : 0.0) : (R == C ? 1.0 : 0.0);
@@ -1658,47 +1663,50 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   // register-tile index: M[K][.] / M[.][K] stay in registers).
   auto step2 = [&](auto Kc, int kk) {
     constexpr int K = decltype(Kc)::value;
+    if constexpr (K < kAsTi) {   // (discarded for K = 8 with the 8 x 8 tile)
     const int k = 16 * K + kk;
     if (tr == kk || tr == kk + 1)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) s_row[buf][tr - kk][tc + 16 * b] = M[K][b];
+      for (int b = 0; b < kAsTi; ++b) s_row[buf][tr - kk][tc + 16 * b] = M[K][b];
     if (tc == kk || tc == kk + 1)
 #pragma unroll
-      for (int a = 0; a < 8; ++a) s_col[buf][tc - kk][tr + 16 * a] = M[a][K];
+      for (int a = 0; a < kAsTi; ++a) s_col[buf][tc - kk][tr + 16 * a] = M[a][K];
     __syncthreads();
     const double p00 = s_row[buf][0][k], p01 = s_row[buf][0][k + 1], p10 = s_row[buf][1][k], p11 = s_row[buf][1][k + 1];
     const double det = p00 * p11 - p01 * p10;
     bad = bad || !(p00 > 0.0) || !(det > 0.0) || !isfinite(det);
     const double idet = 1.0 / det;
     const double q00 = p11 * idet, q01 = -p01 * idet, q10 = -p10 * idet, q11 = p00 * idet;   // P⁻¹
-    double v0[8], v1[8], c0[8], c1[8];
+    double v0[kAsTi], v1[kAsTi], c0[kAsTi], c1[kAsTi];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {   // P⁻¹ A_{K,j}
+    for (int b = 0; b < kAsTi; ++b) {   // P⁻¹ A_{K,j}
       const double r0 = s_row[buf][0][tc + 16 * b], r1 = s_row[buf][1][tc + 16 * b];
       v0[b] = fma(q01, r1, q00 * r0);
       v1[b] = fma(q11, r1, q10 * r0);
     }
 #pragma unroll
-    for (int a = 0; a < 8; ++a) { c0[a] = s_col[buf][0][tr + 16 * a]; c1[a] = s_col[buf][1][tr + 16 * a]; }
+    for (int a = 0; a < kAsTi; ++a) { c0[a] = s_col[buf][0][tr + 16 * a]; c1[a] = s_col[buf][1][tr + 16 * a]; }
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
+    for (int a = 0; a < kAsTi; ++a)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) M[a][b] = fma(-c1[a], v1[b], fma(-c0[a], v0[b], M[a][b]));   // (rows / columns K below)
+      for (int b = 0; b < kAsTi; ++b) M[a][b] = fma(-c1[a], v1[b], fma(-c0[a], v0[b], M[a][b]));   // (rows / columns K below)
     if (tr == kk || tr == kk + 1)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) M[K][b] = tr == kk ? v0[b] : v1[b];
+      for (int b = 0; b < kAsTi; ++b) M[K][b] = tr == kk ? v0[b] : v1[b];
     if (tc == kk || tc == kk + 1) {
       const double e0 = tc == kk ? q00 : q01, e1 = tc == kk ? q10 : q11;
 #pragma unroll
-      for (int a = 0; a < 8; ++a) M[a][K] = -fma(c1[a], e1, c0[a] * e0);
+      for (int a = 0; a < kAsTi; ++a) M[a][K] = -fma(c1[a], e1, c0[a] * e0);
       if (tr == kk || tr == kk + 1) M[K][K] = tr == kk ? e0 : e1;   // the pivot block: P⁻¹
     }
     buf ^= 1;
+    }
   };
 #define OFX_AS_STEPS(K) \
   for (int kk = 0; kk < 16 && 16 * (K) + kk < n; kk += 2) step2(std::integral_constant<int, (K)>{}, kk);
   OFX_AS_STEPS(0) OFX_AS_STEPS(1) OFX_AS_STEPS(2) OFX_AS_STEPS(3)
   OFX_AS_STEPS(4) OFX_AS_STEPS(5) OFX_AS_STEPS(6) OFX_AS_STEPS(7)
+  OFX_AS_STEPS(8)
 #undef OFX_AS_STEPS
   bad = __syncthreads_or(bad ? 1 : 0) != 0;
   OFX_AS_STAMP(2)
@@ -1707,26 +1715,26 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   // 1 + σ with σ = ‖E‖_F + 2^-10 >= ‖E‖₂ + the diagonal's own rounding, so the stored Ẑ̃ >= Ẑ: positive definite whatever
   // Z's conditioning (a plain 16-bit rounding of Z made the moose's subdomains indefinite). A bad domain: the identity on
   // the cluster's own rows.
-  __shared__ double s_d[128], s_e[256];
+  __shared__ double s_d[16 * kAsTi], s_e[256];
   __shared__ double s_sig;
   if (tr == tc)
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
+    for (int a = 0; a < kAsTi; ++a) {
       const int R = tr + 16 * a;
       s_d[R] = (R < n && !bad) ? sqrt(M[a][a]) : 1.0;
     }
   __syncthreads();
-  double dr[8], dc[8];
+  double dr[kAsTi], dc[kAsTi];
 #pragma unroll
-  for (int a = 0; a < 8; ++a) dr[a] = s_d[tr + 16 * a];
+  for (int a = 0; a < kAsTi; ++a) dr[a] = s_d[tr + 16 * a];
 #pragma unroll
-  for (int b = 0; b < 8; ++b) dc[b] = s_d[tc + 16 * b];
+  for (int b = 0; b < kAsTi; ++b) dc[b] = s_d[tc + 16 * b];
   auto h16 = [](double z) -> _Float16 { return (_Float16)(float)z; };
   double e2 = 0.0;
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < kAsTi; ++a)
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < kAsTi; ++b) {
       const int R = tr + 16 * a, C = tc + 16 * b;
       if (R < n && C < n && R < C && !bad) {
         const double z = M[a][b] / (dr[a] * dc[b]);
@@ -1748,9 +1756,9 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   // as 16-B words (scattered 2-B stores of the entries cost ~80 us per solve)
   auto b16 = [](_Float16 h) { return __builtin_bit_cast(uint16_t, h); };
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < kAsTi; ++a)
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < kAsTi; ++b) {
       const int R = tr + 16 * a, C = tc + 16 * b;
       if (R >= n || C >= kAsD) continue;
       if (C >= n) {
@@ -1765,7 +1773,7 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
     }
   if (tc == 0)
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
+    for (int a = 0; a < kAsTi; ++a) {
       const int R = tr + 16 * a;
       if (R < kAsD) g.as_dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
       if (R < n) g.as_rsc[s_dst[R]] = (float)dr[a];
@@ -3547,8 +3555,9 @@ int ofx_gn_precond_info(void* handle, int64_t* info) {
   Gn* g = (Gn*)handle;
   if (g) prep_wait(g);
   OFX_CHECK_ARG(g && info, "null handle/info");
-  for (int k = 0; k < 6; ++k) info[k] = 0;
+  for (int k = 0; k < 7; ++k) info[k] = 0;
   info[0] = g->as_on;
+  info[6] = kAsD;
   if (!g->as_on) return OFX_OK;
   const int ncl = g->N / kCS;
   const int sd = sync_side(g);

@@ -111,9 +111,10 @@ class GaussNewtonSolver:
     def precond_info(self):
         """The last setup's preconditioner: dict(schwarz, clusters, segments, sources, gathered_rows, subdomain_rows)
         (ofx_gn_precond_info; synchronises the device: tools and bench only)."""
-        arr = (ctypes.c_int64 * 6)()
+        arr = (ctypes.c_int64 * 7)()
         call("ofx_gn_precond_info", self._h, arr)
-        return dict(zip(("schwarz", "clusters", "segments", "sources", "gathered_rows", "subdomain_rows"), list(arr)))
+        return dict(zip(("schwarz", "clusters", "segments", "sources", "gathered_rows", "subdomain_rows", "row_length"),
+                        list(arr)))
 
     def stopped(self):
         """The solve's stop flag as the host sees it (ofx_gn_stopped: no synchronisation)."""

@@ -1,0 +1,20 @@
+# Round check + measurement with 16-row Schwarz rings: GPU suite, smoke, measurement (PMC, kernel stats, bench lines),
+# configs 2 / 4 and the moose line
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-.}
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests/ > gpurun_out/r05_gputest_final.txt 2>&1; rc=$?
+tail -3 gpurun_out/r05_gputest_final.txt
+if [ $rc -ne 0 ]; then grep -h "FAILED\|Error" gpurun_out/r05_gputest_final.txt | head -20; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/c14_smoke.log 2>&1 || { tail -20 gpurun_out/c14_smoke.log; exit 1; }
+tail -1 gpurun_out/c14_smoke.log
+bash tools/measure_round.sh > gpurun_out/c14_measure.log 2>&1 || { tail -30 gpurun_out/c14_measure.log; exit 1; }
+for c in 2 4; do
+  timeout -k 10 400 python bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/r05s_bench_config$c.log 2>&1 || exit $?
+  tail -1 gpurun_out/r05s_bench_config$c.log > gpurun_out/r05_bench_config$c.json
+done
+timeout -k 10 300 python bench.py --moose --steps 20 --warmup 3 > gpurun_out/moose.log 2>&1 || exit $?
+tail -1 gpurun_out/moose.log > gpurun_out/r05_moose.json
+for f in r05_bench r05_bench_driver_form r05_bench_config2 r05_bench_config4; do python -c "import json; d=json.loads(open('gpurun_out/$f.json').read()); r=d['roofline']; print('$f', round(d['value'],1), r['iterations_per_frame'], r['launches_per_frame'], round(r['avg_launch_us'],3), round(r['frac'],3))"; done
+python -c "import json; d=json.loads(open('gpurun_out/r05_moose.json').read()); print('moose', d['value'], d['default']['pcg_iterations'], d['default']['max_abs_err_vs_f64_oracle'])"
+head -20 gpurun_out/kstats.txt

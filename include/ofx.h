@@ -393,13 +393,13 @@ typedef struct ofx_gn_params {
                                 steps since the last rebuild); real data with large rotations (the moose demo)
                                 needs it, the synthetic bench never reaches it. 0: precond_every alone */
   int32_t precond;           /* PCG preconditioner: OFX_PRECOND_SCHWARZ (1): overlapping additive Schwarz over the
-                                8-node clusters extended by up to 12 coupled ring nodes (two launches per PCG
-                                iteration, ~2.7x fewer iterations on the bench graph); OFX_PRECOND_CLUSTER (0): the
+                                8-node clusters extended by up to 16 coupled ring nodes (two launches per PCG
+                                iteration, ~3.4x fewer iterations on the bench graph); OFX_PRECOND_CLUSTER (0): the
                                 clusters' block Jacobi (one launch per iteration); OFX_PRECOND_AUTO (2, default of the
                                 Python API): Schwarz for graphs of >= 1536 nodes, where the cluster blocks' iteration
                                 count has grown past what two launches per iteration and the per-solve subdomain
                                 inversion cost (config 2's 1020 nodes: 464.7 vs 419.2 frames/s; config 3's 1998:
-                                292 vs 346; config 4's 4016: 106.5 vs 150.2). The Schwarz form needs the wave-list PCG
+                                292 vs 378; config 4's 4016: 106.5 vs 159.9). The Schwarz form needs the wave-list PCG
                                 (every 8-row wave <= 128 blocks, rows <= 20 blocks) and falls back to the cluster
                                 blocks otherwise */
   int32_t _pad1;

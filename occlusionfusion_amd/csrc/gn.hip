@@ -62,8 +62,8 @@ constexpr int kCS = 8;        // nodes per preconditioner cluster (= PCG rows pe
 constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² entries
 // Overlapping additive Schwarz (as_on): the ring of a cluster holds its kAsRing A-neighbours with the most coupling terms,
 // and a row joins at most kAsX rings, so an output cluster has at most kAsSrc contributing subdomains and kAsRS row
-// segments (a 120-entry inverse row each); kAsGat >= kAsSrc·kAsDN rounded to 3 per thread of the apply's 192
-#ifndef OFX_AS_RING   // (tuning builds: -DOFX_AS_RING=16)
+// segments (a kAsD-entry inverse row each); kAsGat >= kAsSrc·kAsDN rounded up to whole passes of the apply's 192
+#ifndef OFX_AS_RING   // (tuning builds: -DOFX_AS_RING=<n>; 12 -> 16: 198 -> 158 PCG iterations per bench frame, +10 %)
 #define OFX_AS_RING 16
 #endif
 constexpr int kAsRing = OFX_AS_RING, kAsX = 3, kAsDN = kCS + kAsRing, kAsD = 6 * kAsDN, kAsK = kAsD / 8,
@@ -1806,10 +1806,10 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
 }
 
 // out (48 rows of cluster c) = the Schwarz apply of `in`: the gathered rows of the cluster's source subdomains into an LDS
-// image (f32, each row times its source's column scale d; source slot s at s·kAsD), one segment per thread (its 120-entry
-// fp16 slab row of Ẑ, 16-B word k of every segment contiguous: 1 KB per load instruction), the segments' f32 dot products
+// image (f64, each row times its source's column scale d; source slot s at s·kAsD), one segment per thread (its kAsD-entry
+// fp16 slab row of Ẑ, 16-B word k of every segment contiguous: 1 KB per load instruction), the segments' f64 dot products
 // times the row scale into LDS, and each row's segments summed in (row, source) order. 16-bit entries halve the slab
-// (~7 MB per launch on the bench graph, so it and the iteration's operator stay L2-resident: +~10 % frames/s against f32);
+// (~10 MB per launch on the bench graph; with 12-row rings +~10 % frames/s against f32 rows);
 // the preconditioner is still one fixed symmetric positive definite linear operator (k_as_invert's stored form).
 // Trip 1: the stop word (kTest: the PCG chain's launches after convergence end there), the gather list, the segment's
 // source slot and the row offsets; trip 2: the gathered rows and the slab rows together (static addresses; threads past

@@ -220,7 +220,7 @@ struct Gn : GnDev {
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   int32_t ep_next = 1;
   int as_env = -1;                  // OFX_PRECOND override of params.precond (-1: none)
-  int as_l1 = 1;                    // k_as_apply with one lane per segment (0: two, OFX_AS_L2)
+  int as_lanes = 2;                 // k_as_apply's lanes per segment (OFX_AS_LANES)
   int as_cap = 0;                   // clusters the Schwarz tables are allocated for
   // the PCG iteration's constant launch arguments (struct PcgIt) in device memory, and the bytes last copied there
   void* d_pcgit = nullptr;
@@ -1814,7 +1814,7 @@ __global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __rest
 // Trip 1: the stop word (kTest: the PCG chain's launches after convergence end there), the gather list, the segment's
 // source slot and the row offsets; trip 2: the gathered rows and the slab rows together (static addresses; threads past
 // the segment count read the last segment's lines, one line per load instruction).
-template <bool kTest, int kL>   // kL: lanes per segment (1: 192 threads, 2: 384 — the dot products spread over 4 SIMDs)
+template <bool kTest, int kL>   // kL: lanes per segment (1: 192 threads, 2: 384, 4: 768 — the dot products over more waves)
 __global__ __launch_bounds__(kAsRS * kL) void k_as_apply(const int32_t* stopw, const int32_t* meta, const int32_t* gat,
                                                         const uint16_t* slab, const double* in, double* out,
                                                         const int32_t* src, const float* dsc, const float* rsc) {
@@ -1900,7 +1900,8 @@ __global__ __launch_bounds__(kAsRS * kL) void k_as_apply(const int32_t* stopw, c
     }
     dot = (a0 + a1) + (a2 + a3);
   }
-  if (kL == 2) dot += dpp_mov<0xB1>(dot);   // quad_perm [1, 0, 3, 2]: the pair's two parts (the same sum in both lanes)
+  if (kL >= 2) dot += dpp_mov<0xB1>(dot);   // quad_perm [1, 0, 3, 2]: the pair's two parts (the same sum in both lanes)
+  if (kL == 4) dot += dpp_mov<0x4E>(dot);   // quad_perm [2, 3, 0, 1]: the two pairs (fixed order, equal in all four)
   if (sg < nrs && hl == 0) s_seg[sg] = (double)rscale * dot;
   __syncthreads();
   if (t < 6 * kCS) {
@@ -3206,9 +3207,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const bool as = g->as_on != 0;   // (the setup enables it only with the wave-list forms)
   const int ncl = g->N / kCS;
   auto as_apply = [&](bool test, const double* in, double* out) {
-    auto k = g->as_l1 ? (test ? k_as_apply<true, 1> : k_as_apply<false, 1>)
-                      : (test ? k_as_apply<true, 2> : k_as_apply<false, 2>);
-    hipLaunchKernelGGL(k, dim3(ncl), dim3(g->as_l1 ? kAsRS : 2 * kAsRS), 0, hs, (const int32_t*)g->stopw, (const int32_t*)g->as_meta,
+    auto k = g->as_lanes == 1 ? (test ? k_as_apply<true, 1> : k_as_apply<false, 1>)
+           : g->as_lanes == 4 ? (test ? k_as_apply<true, 4> : k_as_apply<false, 4>)
+                              : (test ? k_as_apply<true, 2> : k_as_apply<false, 2>);
+    hipLaunchKernelGGL(k, dim3(ncl), dim3(g->as_lanes * kAsRS), 0, hs, (const int32_t*)g->stopw, (const int32_t*)g->as_meta,
                        (const int32_t*)g->as_gat, (const uint16_t*)g->as_slab, in, out, (const int32_t*)g->as_src,
                        (const float*)g->as_dsc, (const float*)g->as_rsc);
   };
@@ -3461,9 +3463,11 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
     g->pcg_w2 = (e && e[0] && strcmp(e, "0") != 0) ? 0 : 1;
     const char* pe = getenv("OFX_PRECOND");   // A/B override of params.precond: "as" = Schwarz, "bj" = cluster blocks
     g->as_env = (pe && strcmp(pe, "as") == 0) ? 1 : (pe && strcmp(pe, "bj") == 0) ? 0 : -1;
-    // A/B: two lanes per Schwarz segment (OFX_AS_L2=1; 342 / 373 against 373 / 357 frames/s with one, one box: noise)
-    const char* le = getenv("OFX_AS_L2");
-    g->as_l1 = (le && le[0] && strcmp(le, "0") != 0) ? 0 : 1;
+    // lanes per Schwarz segment in k_as_apply (OFX_AS_LANES=1|2|4, A/B): 2 (16-row rings: 410 / 432 / 412 against
+    // 387 / 390 / 372 frames/s with one, one box; with 12-row rings one and two were within noise)
+    const char* le = getenv("OFX_AS_LANES");
+    const int lv = le ? atoi(le) : 2;
+    g->as_lanes = (lv == 1 || lv == 4) ? lv : 2;
   }
   g->max_nodes = max_nodes;
   g->max_matches = max_matches;

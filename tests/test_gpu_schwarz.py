@@ -108,3 +108,22 @@ def test_schwarz_moose_meets_the_bar(cuda, monkeypatch):
     print(f"moose Schwarz: PCG iterations {ci['pcg_iterations']}, max error {max(dr, dt):.3g}")
     assert ci["pcg_capped_steps"] == 0
     assert max(dr, dt) < TOL, (dr, dt)
+
+
+def test_auto_preconditioner_picks_by_graph_size(cuda, monkeypatch):
+    """precond="auto" (the default): Schwarz for graphs of >= 1536 nodes (gn_2k's 1998), the cluster blocks below
+    (gn_1k); "schwarz" / "cluster" force either (ofx_gn_precond_info reports what the setup built)."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    monkeypatch.delenv("OFX_PRECOND", raising=False)
+    for name, want in (("gn_2k.npz", 1), ("gn_1k.npz", 0)):
+        g = _load(name)
+        for pc, expect in (("auto", want), ("schwarz", 1), ("cluster", 0)):
+            N = g["nodes"].shape[0]
+            s = GaussNewtonSolver(N, 10000, precond=pc)
+            out = s.optimize(g["nodes"], g["edges"], g["edge_weights"], g["f0_tpos"], g["f0_conf"], g["f0_src"],
+                             g["f0_anchors"], g["f0_weights"], g["f0_tgt"], tuple(float(v) for v in g["intr"]))
+            info = s.precond_info()
+            assert info["schwarz"] == expect, (name, pc, info)
+            if expect:
+                assert info["segments"] > 0 and info["row_length"] == 144
+            assert _err(out, g, 0) < TOL

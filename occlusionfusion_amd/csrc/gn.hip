@@ -57,7 +57,10 @@ namespace ofx {
 
 // --------------------------------------------------------------------------------------------
 constexpr int kBlk = 256;       // threads per WG
-constexpr int kProj = 4;      // warm start: Galerkin projection on the last kProj GN-step solutions
+#ifndef OFX_KPROJ   // (tuning builds: -DOFX_KPROJ=<n>)
+#define OFX_KPROJ 4
+#endif
+constexpr int kProj = OFX_KPROJ;   // warm start: Galerkin projection on the last kProj GN-step solutions
 constexpr int kCS = 8;        // nodes per preconditioner cluster (= PCG rows per wave)
 constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² entries
 // Overlapping additive Schwarz (as_on): the ring of a cluster holds its kAsRing A-neighbours with the most coupling terms,

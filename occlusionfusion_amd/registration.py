@@ -15,6 +15,7 @@
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -57,7 +58,7 @@ class GaussNewtonSolver:
         self._side = None               # torch stream that orders a prefetch before the current solve
         # GN steps of the current solve a prefetch overlaps: its setup starts when the solve begins step
         # num_iter - prefetch_lead (ofx_gn_prepare_after); 0 = when the solve's host loop returns
-        self.prefetch_lead = 1
+        self.prefetch_lead = int(os.environ.get("OFX_PREFETCH_LEAD", "1"))   # (env: A/B only)
         self._h, self._state = self._slots[0]   # the last solve's slot (info / stats / stopped / arap / distributed)
 
     def _new_slot(self):

@@ -41,6 +41,16 @@ def rings(P, A, groups, kind, cap=None):
             adj[r].add(int(c))
     Ad = A.tocsr()
     cnt = None
+    if kind == "e":   # graph-only proxy (static per graph): the number of deformation-graph edges to the cluster
+        cnt = {}
+        ed, _ = fo.gn_edges(P["edges"])
+        for x, y in ed:
+            for k in ((int(x), int(y)), (int(y), int(x))):
+                cnt[k] = cnt.get(k, 0) + 1
+        adj = [set() for _ in range(N)]
+        for (x, y) in cnt:
+            if x != y:
+                adj[x].add(y)
     if kind == "c":   # coupling proxy known at setup: the number of terms (matches' anchor pairs, graph edges) per block
         cnt = {}
         for a in np.asarray(P["anc"], np.int64):

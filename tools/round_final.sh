@@ -1,14 +1,14 @@
-# Round check + measurement with 16-row Schwarz rings: GPU suite, smoke, measurement (PMC, kernel stats, bench lines),
-# configs 2 / 4 and the moose line
+# Round-end check + measurement of the default tree: GPU suite, smoke, measure_round.sh (PMC, kernel stats, bench
+# lines), configs 2 / 4 and the moose line. Outputs under gpurun_out/ (copied into profiles/ afterwards).
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests/ > gpurun_out/r05_gputest_final.txt 2>&1; rc=$?
 tail -3 gpurun_out/r05_gputest_final.txt
 if [ $rc -ne 0 ]; then grep -h "FAILED\|Error" gpurun_out/r05_gputest_final.txt | head -20; exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/c14_smoke.log 2>&1 || { tail -20 gpurun_out/c14_smoke.log; exit 1; }
-tail -1 gpurun_out/c14_smoke.log
-bash tools/measure_round.sh > gpurun_out/c14_measure.log 2>&1 || { tail -30 gpurun_out/c14_measure.log; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final_smoke.log 2>&1 || { tail -20 gpurun_out/final_smoke.log; exit 1; }
+tail -1 gpurun_out/final_smoke.log
+bash tools/measure_round.sh > gpurun_out/final_measure.log 2>&1 || { tail -30 gpurun_out/final_measure.log; exit 1; }
 for c in 2 4; do
   timeout -k 10 400 python bench.py --config $c --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/r05s_bench_config$c.log 2>&1 || exit $?
   tail -1 gpurun_out/r05s_bench_config$c.log > gpurun_out/r05_bench_config$c.json

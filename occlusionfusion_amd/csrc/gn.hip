@@ -1054,8 +1054,15 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(4))) void 
                "s"(g.part_loss), "s"(g.res), "s"(g.J), "s"(g.blk_list), "s"(g.blk_off), "s"(g.nnzb), "s"(g.up_slot),
                "s"(g.up_tr), "s"(A), "s"(rhs), "s"(nrw), "s"(lm));
   asm volatile("" :: "s"(dc.lf), "s"(dc.ld), "s"(dc.la), "s"(dc.lm), "s"(dc.fx), "s"(dc.fy), "s"(dc.cx), "s"(dc.cy));
-  if ((int)blockIdx.x < nrw) rhs_body(g, dc, rhs, blockIdx.x);
-  else blocks_coop(g, dc, A, blockIdx.x - nrw, lm);
+  // XCD-aware order: workgroups b and b + 8 share an XCD, so each XCD takes a contiguous run of nodes / upper
+  // blocks and the term records they share stay in one L2 (nrw is a multiple of 8, so both halves keep b % 8); a
+  // relabelling of which workgroup computes what: A and b are unchanged. Fetch 20.2 -> 7.9 MB per launch, time
+  // unchanged (the re-reads were served by the MALL): profiles/r05_ab.json
+  const int hw = blockIdx.x, part = hw < nrw ? nrw : (int)gridDim.x - nrw, i = hw < nrw ? hw : hw - nrw;
+  const int q = part >> 3, r = part & 7, x = i & 7;
+  const int L = x * q + min(x, r) + (i >> 3);
+  if (hw < nrw) rhs_body(g, dc, rhs, L);
+  else blocks_coop(g, dc, A, L, lm);
 }
 #ifdef OFX_SPLIT_ASSEMBLE
 __global__ __launch_bounds__(kBlk) void k_assemble_blocks(GnDev g, DataCoef dc, double* __restrict__ A, double lm) {
@@ -2150,7 +2157,7 @@ __global__ __launch_bounds__(kAS ? 256 : 64) __attribute__((amdgpu_waves_per_eu(
 // z = q = s = p = w = 0, u0 -> m1.
 // The projection partials are read as KU pairs per lane and stream at the iteration streams' padded stride nw_pad =
 // 128·KU (zero beyond the wave count: cleared at setup): unconditional loads, no per-load branches.
-template <int KU>
+template <int KU, bool kAS = false>   // kAS: Schwarz (no cluster inverse; r0 -> as_w for k_as_apply)
 __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) {   // (not __restrict__: see k_pcg_w0)
   __shared__ __attribute__((aligned(16))) double s_v[kCD];
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
@@ -2164,7 +2171,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) { 
   const int64_t oc = 6 * (int64_t)row + (own ? q : 5);   // every lane loads (clamped): one memory trip in all
   const int64_t stride = 6 * (int64_t)g.N;
   float4 mr[kCD / 4];
-  load_mrow(g, oc, mr);
+  if constexpr (!kAS) load_mrow(g, oc, mr);
   const double rb = rhs[oc];
   double xo[kProj], to[kProj];
 #pragma unroll
@@ -2236,7 +2243,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) { 
   }
   __syncthreads();
   if (own) {
-    if (g.as_on) {   // u0 = M⁻¹ r0 by k_as_apply (as_w -> m1)
+    if constexpr (kAS) {   // u0 = M⁻¹ r0 by k_as_apply (as_w -> m1)
       const double v[V_N] = {xv, rv, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
       store_rec(g.st, o, v);
       g.as_w[o] = rv;
@@ -2254,7 +2261,7 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) { 
 // kWave: the SpMV in k_pcg_iter's wave-list form — the wave's (col, slot) list leaves in the first trip with the state
 // and the stop flag, so the blocks and gathers are the second (the row form needs row_ptr -> col -> blocks: three);
 // lane l multiplies the wave's blocks l and l + 64, the products meet in LDS, each row sums its blocks in CSR order.
-template <bool kWave>
+template <bool kWave, bool kAS = false>   // kAS: Schwarz (u0 from m1, w0 -> as_w, no cluster inverse)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_w0(GnDev g, const double* rhs) {   // (rhs not __restrict__: a restrict load sinks past the exit test)
   __shared__ __attribute__((aligned(16))) double s_v[kCD];
   __shared__ double s_prod[kWave ? (kWL + kRowMax) * 6 : 1];
@@ -2277,7 +2284,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const double bo = rhs[oc];
   float4 mr[kCD / 4];
   double v[V_N];
-  load_mrow(g, oc, mr);
+  if constexpr (!kAS) load_mrow(g, oc, mr);
   load_rec(g.st, oc, v);
   const double u_as = g.m1[oc];  // (Schwarz: u0 came from k_as_apply into m1)
   const double w_old = v[V_W];   // unused, but kept live to the end (see the end of the kernel)
@@ -2295,9 +2302,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // inverses per row, each of a larger subdomain (whose smallest eigenvalue is at most its cluster block's), so its
     // λ_min(M) is smaller: the tolerance is taken 4x tighter (2x for the overlap's multiplicity, 2x margin: the moose
     // pair ended at 1.1e-5 with 2x).
-    g.pcs[kScTol + 1] = g.as_on ? 0.25 * g.prm.pcg_err_tol : g.prm.pcg_err_tol;
+    g.pcs[kScTol + 1] = kAS ? 0.25 * g.prm.pcg_err_tol : g.prm.pcg_err_tol;
     // (Schwarz: the iteration's w_new target in the inverse's slot)
-    reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = g.as_on ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
+    reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = kAS ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
     // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
@@ -2305,7 +2312,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     g.pcs[kScScal + S_TH_CUR] = 1e300;
   }
   if (stopped) return;
-  if (g.as_on) v[V_U] = u_as;
+  if (kAS) v[V_U] = u_as;
   const double b = own ? bo : 0.0;
   double w;
   double2 ab[2][18];
@@ -2354,7 +2361,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   if (own) {
     v[V_W] = w;
     store_rec(g.st, o, v);
-    if (g.as_on) g.as_w[o] = w;              // m0 = M⁻¹ w0 by k_as_apply (as_w -> m0)
+    if constexpr (kAS) g.as_w[o] = w;        // m0 = M⁻¹ w0 by k_as_apply (as_w -> m0)
     else g.m0[o] = apply_mrow(mr, s_v);
     d[0] = v[V_R] * v[V_U]; d[1] = w * v[V_U]; d[2] = v[V_R] * v[V_R]; d[3] = b * b;
   }
@@ -3230,15 +3237,21 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     else if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     switch (g->pcg_ku) {
-      case 2: hipLaunchKernelGGL(k_pcg_proj2<2>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
-      case 3: hipLaunchKernelGGL(k_pcg_proj2<3>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
-      case 4: hipLaunchKernelGGL(k_pcg_proj2<4>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
-      case 8: hipLaunchKernelGGL(k_pcg_proj2<8>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
-      default: hipLaunchKernelGGL(k_pcg_proj2<17>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      case 2: if (as) hipLaunchKernelGGL((k_pcg_proj2<2, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+              else hipLaunchKernelGGL(k_pcg_proj2<2>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      case 3: if (as) hipLaunchKernelGGL((k_pcg_proj2<3, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+              else hipLaunchKernelGGL(k_pcg_proj2<3>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      case 4: if (as) hipLaunchKernelGGL((k_pcg_proj2<4, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+              else hipLaunchKernelGGL(k_pcg_proj2<4>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      case 8: if (as) hipLaunchKernelGGL((k_pcg_proj2<8, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+              else hipLaunchKernelGGL(k_pcg_proj2<8>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
+      default: if (as) hipLaunchKernelGGL((k_pcg_proj2<17, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+               else hipLaunchKernelGGL(k_pcg_proj2<17>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
     }
     if (as) as_apply(false, g->as_w, g->m1);   // u0 = M⁻¹ r0
   }
-  if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+  if (as) hipLaunchKernelGGL((k_pcg_w0<true, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+  else if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
   else hipLaunchKernelGGL(k_pcg_w0<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
   if (as) as_apply(false, g->as_w, g->m0);     // m0 = M⁻¹ w0
   OFX_LAUNCH_CHECK();
@@ -4115,8 +4128,8 @@ int ofx_gn_linearize(void* handle, int32_t gn_iter, int32_t m0, int32_t m1, int3
   if (nwb) hipLaunchKernelGGL(k_assemble_blocks, dim3(nwb), dim3(kBlk), 0, hs, *g, dc, A, lm);
   hipLaunchKernelGGL(k_assemble_rhs, dim3(grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, rhs);
 #else
-  hipLaunchKernelGGL(k_assemble, dim3(nwb + grid_for(g->N, kBlk / 64)), dim3(kBlk), 0, hs, *g, dc, A, rhs,
-                     (int)grid_for(g->N, kBlk / 64), lm);
+  const int nrw = ((int)grid_for(g->N, kBlk / 64) + 7) & ~7;   // (a multiple of 8: see k_assemble)
+  hipLaunchKernelGGL(k_assemble, dim3(nwb + nrw), dim3(kBlk), 0, hs, *g, dc, A, rhs, nrw, lm);
 #endif
   OFX_LAUNCH_CHECK();
   return OFX_OK;

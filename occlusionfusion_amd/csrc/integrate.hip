@@ -402,8 +402,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 // y and z), three dependent memory trips —
 //   1. brick id, palette count / ids, the voxels' palette ranks;
 //   2. the palette's node records (into LDS, one barrier) + the skin-valid voxels' weights and old
-//      tsdf / weight (exec-masked);
-//   3. depth, colour image and old colour of the skin-valid voxels;
+//      tsdf / weight (branch-free: the other voxels re-read the brick's first voxel);
+//   3. depth, colour image and old colour (likewise branch-free);
 // then the stores. Warp with the anchors unrolled (no dynamic register indexing), pixel in certified f32
 // (pixel_of), SDF rounding certified cheaply (sdf_color_update), per-wave update counts by ballot;
 // bit-identical to k_integrate<1,1,0>. The kernel is VALU-bound: every per-wave instruction
@@ -456,13 +456,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   const float4 nrec = nodes[4 * (int64_t)min(pid, n_nodes - 1) + (tid & 3)];
   float4 ww[2];
   float t_old[2], w_old[2];
+  // branch-free: a voxel outside the skin loads the brick's first voxel instead (a line the brick reads anyway), so
+  // no load sits in a branch and the waits before the barrier / the warp count exactly (masked loads made the
+  // compiler wait for each voxel's weights inside its branch and for every load of the trip before the barrier:
+  // 94.7 -> 90.9 us isolated, 100.6 -> 94.1 us in the frame loop, profiles/r05_ab.json)
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (act[h]) {
-      ww[h] = weights[slot * kBrickVox + tid + 256 * h];
-      t_old[h] = tsdf[vb + 256 * h];
-      w_old[h] = weight[vb + 256 * h];
-    }
+    const uint32_t e = act[h] ? (uint32_t)(tid + 256 * h) : 0u;
+    ww[h] = weights[slot * kBrickVox + e];
+    t_old[h] = tsdf[b * (uint32_t)kBrickVox + e];
+    w_old[h] = weight[b * (uint32_t)kBrickVox + e];
   }
   if (use_pal && tid < 4 * pn) s_node[tid] = nrec;
   if (tid >= 256 - 3 * kBrick) {   // the last 24 lanes (one wave): x, y, z world coordinates of the brick
@@ -495,11 +498,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
   float d[2], nc[2], oc[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (act[h]) {
-      const int pc = pix[h] >= 0 ? pix[h] : 0;
-      d[h] = depth[pc];
-      if (COLOR) { nc[h] = color_im[pc]; oc[h] = color[vb + 256 * h]; }
-    }
+    const int pc = pix[h] >= 0 ? pix[h] : 0;
+    d[h] = depth[pc];
+    if (COLOR) { nc[h] = color_im[pc]; oc[h] = color[b * (uint32_t)kBrickVox + (act[h] ? (uint32_t)(tid + 256 * h) : 0u)]; }
+  }
+  // the loaded values pass through an empty asm: both halves' loads are issued before the first use (else the second
+  // half's loads sink into its update branch: two more dependent trips)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (COLOR) asm volatile("" : "+v"(d[h]), "+v"(nc[h]), "+v"(oc[h]));
+    else asm volatile("" : "+v"(d[h]));
   }
   asm volatile("" ::: "memory");
   uint32_t n_upd = 0;

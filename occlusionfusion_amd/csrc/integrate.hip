@@ -408,8 +408,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 // (pixel_of), SDF rounding certified cheaply (sdf_color_update), per-wave update counts by ballot;
 // bit-identical to k_integrate<1,1,0>. The kernel is VALU-bound: every per-wave instruction
 // is shared by two voxels.
+#ifndef OFX_INT_WPE
+#define OFX_INT_WPE 7   // (tuning builds: -DOFX_INT_WPE=n; 7: 72 VGPRs, 12 B of scratch, 90.0 -> 84.9 us against 6;
+                        // 8: 64 VGPRs, 56 B of scratch, 146 us: profiles/r05_ab.json)
+#endif
 template <bool COLOR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_integrate_pal4(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFX_INT_WPE))) void k_integrate_pal4(
     BrickGeom g, BrickDiv bd, CamD c, const float* __restrict__ depth, const float* __restrict__ color_im,
     const float4* __restrict__ nodes, int n_nodes, const int32_t* __restrict__ list,
     const ushort4* __restrict__ anchors, const float4* __restrict__ weights, const uint16_t* __restrict__ pal_ids,

@@ -120,6 +120,9 @@ struct GnDev {
   int32_t *blk_off = nullptr, *blk_cnt = nullptr, *blk_list = nullptr, *blk_tmp = nullptr;
   int32_t *up_of = nullptr, *up_slot = nullptr, *up_tr = nullptr;   // slot -> u (+ total at [nnzb]), u -> slot, transpose
   int32_t *node_off = nullptr, *node_cnt = nullptr, *node_list = nullptr, *node_tmp = nullptr;
+  // the first chunk of every assembly workgroup's list (kCoop codes) and of every node's rhs list (128), at fixed
+  // offsets (k_first_codes): k_assemble's first memory trip carries them
+  int32_t *blk_first = nullptr, *node_first = nullptr;
   int64_t nnzb = 0, nnzb_cap = 0;
   // state
   double *R = nullptr, *t = nullptr;
@@ -743,17 +746,15 @@ __device__ __forceinline__ void term_block(int kind, int slot, const double x[4]
   }
 }
 
-// the record words of (t, slot): two 16-B loads, plus two for a data term's tail
+// the record words of (t, slot): two 16-B loads, plus the two of a data term's tail — loaded for every kind (every
+// record has them) and zeroed for the others: a load in a kind branch was waited for inside it, one term after another
 __device__ __forceinline__ void load_record(const GnDev& g, int64_t t, int slot, int kind, double x[4], double tail[4]) {
   const double2* r = reinterpret_cast<const double2*>(g.J + t * kRec);
   const double2 a = r[2 * slot], b = r[2 * slot + 1];
+  const double2 c = r[8], d = r[9];
   x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
-  if (kind == kData) {
-    const double2 c = r[8], d = r[9];
-    tail[0] = c.x; tail[1] = c.y; tail[2] = d.x; tail[3] = d.y;
-  } else {
-    tail[0] = tail[1] = tail[2] = tail[3] = 0.0;
-  }
+  const bool dt = kind == kData;
+  tail[0] = dt ? c.x : 0.0; tail[1] = dt ? c.y : 0.0; tail[2] = dt ? d.x : 0.0; tail[3] = dt ? d.y : 0.0;
 }
 
 // Anchor k's summand of the deformed point of match m: w_k (R_k (x - g_k) + g_k + t_k) (ED_warp, geometry.py:9-25)
@@ -904,28 +905,39 @@ __device__ __forceinline__ void rhs_body(const GnDev& g, const DataCoef& dc, dou
   // pass of two dependent trips — code, then J + r — where 10 slots took ~10 serial passes); every load
   // unconditional (clamped index, masked value) so no branch splits a trip; fixed-order wave sums
   const int b = g.node_off[n], e = g.node_off[n + 1];
+  int code[2];   // the first pass's codes come with the bounds (node_first), later passes' from the list
+#pragma unroll
+  for (int j = 0; j < 2; ++j) code[j] = g.node_first[(int64_t)n * 128 + lane + 64 * j];
+  asm volatile("" ::: "memory");   // (issued with the bounds, not sunk into the loop behind its entry test)
   double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int k0 = b; k0 < e; k0 += 128) {
-    int code[2];
     bool ok[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int k = k0 + lane + 64 * j;
       ok[j] = k < e;
-      code[j] = g.node_list[ok[j] ? k : e - 1];
+      if (k0 != b) code[j] = g.node_list[ok[j] ? k : e - 1];
     }
+    // both entries' records and residuals first (one trip), then the blocks (left in the loop, the second entry's loads
+    // issued after the first entry's kind branches: two trips)
+    int kind[2];
+    double x[2][4], tail[2][4], rv[2][3];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t t = code[j] >> 2;
-      const int kind = term_kind(g, t);
+      kind[j] = term_kind(g, t);
+      load_record(g, t, code[j] & 3, kind[j], x[j], tail[j]);
       const double* rr = g.res + 3 * t;
-      double x[4], tail[4], P[18];
-      load_record(g, t, code[j] & 3, kind, x, tail);
-      term_block(kind, code[j] & 3, x, tail, dc, P);
-      const double r0 = rr[0], r1 = rr[1], r2 = rr[2];
+      rv[j][0] = rr[0]; rv[j][1] = rr[1]; rv[j][2] = rr[2];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      double P[18];
+      term_block(kind[j], code[j] & 3, x[j], tail[j], dc, P);
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
-        const double t3 = P[c] * r0 + P[6 + c] * r1 + P[12 + c] * r2;
+        const double t3 = P[c] * rv[j][0] + P[6 + c] * rv[j][1] + P[12 + c] * rv[j][2];
         v[c] += ok[j] ? t3 : 0.0;
       }
     }
@@ -958,7 +970,10 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
   constexpr int kPairs = (kBlk / 16) * 36;
   constexpr int kU = (kPairs + kBlk - 1) / kBlk;
   // first trip: the 17 list offsets and every pair's output slots (consumed at the end, in flight all along)
-  if (tid <= kBlk / 16) s_off[tid] = g.blk_off[min<int64_t>(sb + tid, g.nnzb)];
+  // (every load unconditional, the list offsets first: a load inside the offsets' branch was waited for there, before
+  // the other loads issued)
+  const int offv = g.blk_off[min<int64_t>(sb + min(tid, kBlk / 16), g.nnzb)];
+  int code_next = g.blk_first[wg * kCoop + min(tid, kCoop - 1)];   // the first chunk's codes (k_first_codes)
   int pb[kU], po[kU], os[kU], ot[kU];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
@@ -967,6 +982,7 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
     os[u] = g.up_slot[sb + pb[u]];
     ot[u] = g.up_tr[sb + pb[u]];
   }
+  if (tid <= kBlk / 16) s_off[tid] = offv;
   __syncthreads();
   const int E0 = s_off[0], E1 = s_off[kBlk / 16];
   if (E0 == E1) return;   // no upper block here (uniform over the workgroup)
@@ -979,7 +995,6 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
     hi[u] = ok ? s_off[pb[u] + 1] : 0;
     acc[u] = 0.0;
   }
-  int code_next = tid < kCoop && E0 + tid < E1 ? g.blk_list[E0 + tid] : 0;
   for (int c0 = E0; c0 < E1; c0 += kCoop) {
     if (tid < kCoop) {
       const int k = c0 + tid;
@@ -1041,6 +1056,21 @@ __device__ __forceinline__ void blocks_coop(const GnDev& g, const DataCoef& dc, 
     if (lm != 0.0 && po[u] % 7 == 0 && s == st) v += lm;
     A[36 * s + po[u]] = v;
     if (st != s) A[36 * st + 6 * (po[u] % 6) + po[u] / 6] = v;   // the lower block: the transpose
+  }
+}
+
+// The first chunk of every assembly workgroup's contribution list and of every node's rhs list at fixed offsets (setup,
+// after the lists are sorted): k_assemble loads them with the list bounds instead of one memory trip after them.
+__global__ __launch_bounds__(kBlk) void k_first_codes(GnDev g, int nwb) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (b < nwb) {
+    const int64_t sb = (int64_t)b * (kBlk / 16);
+    const int E0 = g.blk_off[min<int64_t>(sb, g.nnzb)], E1 = g.blk_off[min<int64_t>(sb + kBlk / 16, g.nnzb)];
+    if (t < kCoop) g.blk_first[(int64_t)b * kCoop + t] = E0 + t < E1 ? g.blk_list[E0 + t] : 0;
+  } else if (t < 128) {
+    const int n = b - nwb;
+    const int s0 = g.node_off[n], e = g.node_off[n + 1];
+    g.node_first[(int64_t)n * 128 + t] = e > s0 ? g.node_list[s0 + t < e ? s0 + t : e - 1] : 0;
   }
 }
 
@@ -1954,111 +1984,124 @@ __device__ __forceinline__ void proj_accumulate(const double bk[36], const doubl
 // A GN step flagged by the previous step's update (F_REFRESH = this step: some node rotated by more than
 // precond_rot_tol since its cluster inverse was built) first rebuilds the cluster inverses here, one wave per
 // cluster as k_pcg_prep (k_pcg_proj2 applies them); otherwise the flag costs one scalar load with the stop flag.
-// kAS (Schwarz): four waves; a refresh flagged by the previous step (F_REFRESH = this step) rebuilds the cluster's
-// subdomain inverse first (as_invert_body, all four waves), then wave 0 does the projection.
+// kAS (Schwarz): four waves; wave 0 does the projection (its flags in its first trip), then a refresh flagged by the
+// previous step (F_REFRESH = this step) rebuilds the cluster's subdomain inverse (as_invert_body, all four waves: waves
+// 1-3 wait for wave 0 at its first barrier; the projection has no workgroup barrier and reads A, not the inverse). (The
+// refresh test ahead of the projection cost two dependent scalar trips before its first: 9.2 µs per launch against 7.6
+// for the cluster-block form.)
 template <bool kWave, bool kAS = false>
 __global__ __launch_bounds__(kAS ? 256 : 64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_pcg_proj(GnDev g, const double* rhs,
                                                                                               int gn_iter) {
-  if constexpr (kAS) {
-    if (g.flags[F_STOPPED]) return;
-    if (g.flags[F_REFRESH] == gn_iter) as_invert_body(g, g.Aop, blockIdx.x, threadIdx.x);
-    if (threadIdx.x >= 64) return;
-  }
   // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
   asm volatile("" :: "s"(g.wl), "s"(g.row_ptr), "s"(g.col), "s"(g.xh), "s"(g.th), "s"(g.N), "s"(g.flags), "s"(g.n_prev),
                "s"(g.Aop), "s"(g.part_p), "s"(g.nw_pad), "s"(rhs));
   if constexpr (kWave) {
     __shared__ double s_prod[kProj][(kWL + kRowMax) * 6];
-    const int lane = threadIdx.x;
-    const int wv = blockIdx.x;
-    const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
-    const int qc = q < 6 ? q : 5;
-    const int64_t oc = 6 * (int64_t)row + qc;
-    const int64_t stride = 6 * (int64_t)g.N;
-    int2 bl[2];
-    bl[0] = g.wl[(int64_t)wv * kWL + lane];
-    bl[1] = g.wl[(int64_t)wv * kWL + 64 + lane];
-    const int wb0 = g.row_ptr[wv * kRW];
-    const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];
-    const double b = rhs[oc];
-    double xo[kProj];
-#pragma unroll
-    for (int j = 0; j < kProj; ++j) xo[j] = g.xh[j * stride + oc];
-    const int stopped = g.flags[F_STOPPED];
-    const int refresh = g.flags[F_REFRESH];
-    asm volatile("" ::: "memory");   // the loads above leave with the stop flag (one trip)
-    if (stopped) return;
-    if (refresh == gn_iter && !g.as_on) {   // (Schwarz: k_as_invert)
-      float mm[6][6];
-      cluster_invert(g, g.Aop, wv, lane, mm);
-    }
-    const int np = g.n_prev;
-    double2 ab[2][18], xb[2][kProj][3];
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {   // unconditional (padding entries read block 0 / row 0, masked below)
-      const int64_t cc = 6 * (int64_t)(bl[jj].x >= 0 ? bl[jj].x : 0);
-#pragma unroll
-      for (int h = 0; h < kProj; ++h)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) xb[jj][h][k] = reinterpret_cast<const double2*>(g.xh + h * stride + cc)[k];
-      const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)(bl[jj].x >= 0 ? wl_base(bl[jj]) + 64 * jj + lane : 0));
-#pragma unroll
-      for (int k = 0; k < 18; ++k) ab[jj][k] = blk[k];
-    }
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const bool ok = bl[jj].x >= 0;
-#pragma unroll
-      for (int h = 0; h < kProj; ++h) {
-        double x[6];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { x[2 * k] = xb[jj][h][k].x; x[2 * k + 1] = xb[jj][h][k].y; }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const double2 b01 = ab[jj][3 * i], b23 = ab[jj][3 * i + 1], b45 = ab[jj][3 * i + 2];
-          const double t = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
-          s_prod[h][(jj * 64 + lane) * 6 + i] = (ok && h < np) ? t : 0.0;
+    // the projection (wave 0): returns whether a refresh is flagged for this step (0 when the solve stopped)
+    auto project = [&]() -> int {
+      const int lane = threadIdx.x;
+      const int wv = blockIdx.x;
+      const int r = lane / kSL, q = lane % kSL, row = wv * kRW + r;
+      const int qc = q < 6 ? q : 5;
+      const int64_t oc = 6 * (int64_t)row + qc;
+      const int64_t stride = 6 * (int64_t)g.N;
+      int2 bl[2];
+      bl[0] = g.wl[(int64_t)wv * kWL + lane];
+      bl[1] = g.wl[(int64_t)wv * kWL + 64 + lane];
+      const int wb0 = g.row_ptr[wv * kRW];
+      const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];
+      const double b = rhs[oc];
+      double xo[kProj];
+  #pragma unroll
+      for (int j = 0; j < kProj; ++j) xo[j] = g.xh[j * stride + oc];
+      const int stopped = g.flags[F_STOPPED];
+      const int refresh = g.flags[F_REFRESH];
+      asm volatile("" ::: "memory");   // the loads above leave with the stop flag (one trip)
+      if (stopped) return 0;
+      if (!kAS && refresh == gn_iter) {   // (Schwarz: as_invert_body below)
+        float mm[6][6];
+        cluster_invert(g, g.Aop, wv, lane, mm);
+      }
+      const int np = g.n_prev;
+      double2 ab[2][18], xb[2][kProj][3];
+  #pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {   // unconditional (padding entries read block 0 / row 0, masked below)
+        const int64_t cc = 6 * (int64_t)(bl[jj].x >= 0 ? bl[jj].x : 0);
+  #pragma unroll
+        for (int h = 0; h < kProj; ++h)
+  #pragma unroll
+          for (int k = 0; k < 3; ++k) xb[jj][h][k] = reinterpret_cast<const double2*>(g.xh + h * stride + cc)[k];
+        const double2* blk = reinterpret_cast<const double2*>(g.Aop + 36 * (int64_t)(bl[jj].x >= 0 ? wl_base(bl[jj]) + 64 * jj + lane : 0));
+  #pragma unroll
+        for (int k = 0; k < 18; ++k) ab[jj][k] = blk[k];
+      }
+  #pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const bool ok = bl[jj].x >= 0;
+  #pragma unroll
+        for (int h = 0; h < kProj; ++h) {
+          double x[6];
+  #pragma unroll
+          for (int k = 0; k < 3; ++k) { x[2 * k] = xb[jj][h][k].x; x[2 * k + 1] = xb[jj][h][k].y; }
+  #pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            const double2 b01 = ab[jj][3 * i], b23 = ab[jj][3 * i + 1], b45 = ab[jj][3 * i + 2];
+            const double t = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+            s_prod[h][(jj * 64 + lane) * 6 + i] = (ok && h < np) ? t : 0.0;
+          }
         }
       }
-    }
-    wave_lds_sync();
-    const int len = rb1 - rb0;
-    double t[kProj];
-#pragma unroll
-    for (int h = 0; h < kProj; ++h) {   // per history vector: its kRowMax reads in flight, then the adds in CSR order
-      const double* sp = s_prod[h] + (rb0 - wb0) * 6 + qc;
-      double tv[kRowMax];
-#pragma unroll
-      for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
-      __builtin_amdgcn_sched_barrier(0);
-      double a = 0.0;
-#pragma unroll
-      for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
-      t[h] = a;
-    }
-    double v[kProjP];
-#pragma unroll
-    for (int k = 0; k < kProjP; ++k) v[k] = 0.0;
-    if (q < 6) {
-      double x[kProj];
-#pragma unroll
-      for (int j = 0; j < kProj; ++j) {
-        x[j] = j < np ? xo[j] : 0.0;
-        if (j < np) g.th[j * stride + oc] = t[j];
+      wave_lds_sync();
+      const int len = rb1 - rb0;
+      double t[kProj];
+  #pragma unroll
+      for (int h = 0; h < kProj; ++h) {   // per history vector: its kRowMax reads in flight, then the adds in CSR order
+        const double* sp = s_prod[h] + (rb0 - wb0) * 6 + qc;
+        double tv[kRowMax];
+  #pragma unroll
+        for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+        __builtin_amdgcn_sched_barrier(0);
+        double a = 0.0;
+  #pragma unroll
+        for (int k = 0; k < kRowMax; ++k) a += k < len ? tv[k] : 0.0;
+        t[h] = a;
       }
-#pragma unroll
-      for (int j = 0; j < kProj; ++j) {
-#pragma unroll
-        for (int i = 0; i <= j; ++i) v[tri(i, j)] = x[i] * t[j];
-        v[kProj * (kProj + 1) / 2 + j] = x[j] * b;
+      double v[kProjP];
+  #pragma unroll
+      for (int k = 0; k < kProjP; ++k) v[k] = 0.0;
+      if (q < 6) {
+        double x[kProj];
+  #pragma unroll
+        for (int j = 0; j < kProj; ++j) {
+          x[j] = j < np ? xo[j] : 0.0;
+          if (j < np) g.th[j * stride + oc] = t[j];
+        }
+  #pragma unroll
+        for (int j = 0; j < kProj; ++j) {
+  #pragma unroll
+          for (int i = 0; i <= j; ++i) v[tri(i, j)] = x[i] * t[j];
+          v[kProj * (kProj + 1) / 2 + j] = x[j] * b;
+        }
       }
+  #pragma unroll
+      for (int k = 0; k < kProjP; ++k) v[k] = wave_sum(v[k]);
+      if (lane == 0)
+  #pragma unroll
+        for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nw_pad + blockIdx.x] = v[k];
+      if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
+      return refresh == gn_iter ? 1 : 0;
+    };
+    int ref;
+    if (!kAS || threadIdx.x < 64) {
+      ref = project();
+    } else {
+      const int stopped = g.flags[F_STOPPED], refresh = g.flags[F_REFRESH];
+      ref = !stopped && refresh == gn_iter ? 1 : 0;
     }
-#pragma unroll
-    for (int k = 0; k < kProjP; ++k) v[k] = wave_sum(v[k]);
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < kProjP; ++k) g.part_p[(int64_t)k * g.nw_pad + blockIdx.x] = v[k];
-    if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
+    if constexpr (kAS) {
+      if (ref) as_invert_body(g, g.Aop, blockIdx.x, threadIdx.x);
+    }
+    (void)ref;
     return;
   }
   const int lane = threadIdx.x;
@@ -2288,6 +2331,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   load_rec(g.st, oc, v);
   const double u_as = g.m1[oc];  // (Schwarz: u0 came from k_as_apply into m1)
   const double w_old = v[V_W];   // unused, but kept live to the end (see the end of the kernel)
+  // the previous step's final θ̂ (the lead's bookkeeping below), with trip 1: read inside the lead's branch it was one
+  // more trip for workgroup 0 before its SpMV
+  const double th_cur_old = g.pcs[kScScal + S_TH_CUR];
   const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");
   // this solve's stop words: the epoch if the solve already stopped (its iteration launches end after trip 1), else 0
@@ -2308,7 +2354,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
     reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
     // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
-    g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? g.pcs[kScScal + S_TH_CUR] : 1e300;
+    g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? th_cur_old : 1e300;
     g.pcs[kScScal + S_TH_CUR] = 1e300;
   }
   if (stopped) return;
@@ -3075,7 +3121,7 @@ static double lm_for_iter(double lm0, int gn_iter) {
 static void free_all(Gn* g) {
   void* ptrs[] = {g->nodes, g->tpos, g->conf, g->src, g->wts, g->tgt, g->tpx, g->tpy, g->ew, g->anc, g->edges,
                   g->term_node, g->J, g->res, g->map, g->row_ptr, g->col, g->blk_row, g->row_cnt, g->wl, g->Aw, g->stopw, g->blk_off, g->blk_cnt,
-                  g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
+                  g->blk_list, g->blk_tmp, g->node_tmp, g->node_off, g->node_cnt, g->node_list, g->blk_first, g->node_first, g->R, g->t, g->A_own, g->rhs_own, g->Mcl,
                   g->st, g->m0, g->m1, g->pcs, g->racc,
                   g->part_p, g->part_b, g->part_loss,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
@@ -3497,7 +3543,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   ALLOC(g->src, 3 * M); ALLOC(g->wts, 4 * M); ALLOC(g->tgt, 3 * M); ALLOC(g->tpx, M); ALLOC(g->tpy, M);
   ALLOC(g->anc, 4 * M);
   ALLOC(g->map, N * N); ALLOC(g->row_ptr, N + 1); ALLOC(g->row_cnt, N + 2);
-  ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1);
+  ALLOC(g->node_off, N + 1); ALLOC(g->node_cnt, N + 1); ALLOC(g->node_first, N * 128);
   ALLOC(g->R, 9 * N); ALLOC(g->t, 3 * N); ALLOC(g->racc, N);
   ALLOC(g->Mcl, 6 * N * kCD); ALLOC(g->st, V_N * 6 * N); ALLOC(g->m0, 6 * N); ALLOC(g->m1, 6 * N);
   ALLOC(g->xh, kProj * 6 * N); ALLOC(g->th, kProj * 6 * N); ALLOC(g->step_args, 1);
@@ -3998,7 +4044,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->max_wave = lens[1];
   if ((int64_t)nnz + 1 > g->nnzb_cap) {
     for (auto pp : {(void**)&g->col, (void**)&g->blk_row, (void**)&g->A_own, (void**)&g->blk_off,
-                    (void**)&g->blk_cnt, (void**)&g->up_of, (void**)&g->up_slot, (void**)&g->up_tr})
+                    (void**)&g->blk_cnt, (void**)&g->up_of, (void**)&g->up_slot, (void**)&g->up_tr, (void**)&g->blk_first})
       if (*pp) { OFX_HIP(hipFree(*pp)); *pp = nullptr; }
     g->nnzb_cap = (int64_t)nnz + nnz / 4 + 64;
     OFX_HIP(hipMalloc((void**)&g->col, g->nnzb_cap * sizeof(int32_t)));
@@ -4009,6 +4055,8 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
     OFX_HIP(hipMalloc((void**)&g->up_of, (g->nnzb_cap + 1) * sizeof(int32_t)));
     OFX_HIP(hipMalloc((void**)&g->up_slot, (g->nnzb_cap + 32) * sizeof(int32_t)));   // + a workgroup's overhang
     OFX_HIP(hipMalloc((void**)&g->up_tr, (g->nnzb_cap + 32) * sizeof(int32_t)));
+    // k_assemble's block workgroups: (nnzb + N) / 2 + 1 upper blocks at most, 16 per workgroup
+    OFX_HIP(hipMalloc((void**)&g->blk_first, ((g->nnzb_cap + g->max_pad) / 2 / 16 + 2) * kCoop * sizeof(int32_t)));
   }
   g->nnzb = nnz;
   hipLaunchKernelGGL(k_row_assign, dim3(N), dim3(256), 0, hs, N, g->map, g->row_ptr, g->col, g->blk_row);
@@ -4036,6 +4084,10 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
                      (const int32_t*)g->node_list, g->node_tmp);
   std::swap(g->blk_list, g->blk_tmp);
   std::swap(g->node_list, g->node_tmp);
+  {
+    const int nwb = nnz > 0 ? (int)grid_for((nnz + N) / 2 + 1, kBlk / 16, 1 << 30) : 0;   // (as the assembly's launch)
+    hipLaunchKernelGGL(k_first_codes, dim3(nwb + N), dim3(kBlk), 0, hs, *g, nwb);
+  }
   OFX_LAUNCH_CHECK();
   // Schwarz tables (blk_off still holds the per-block term counts' offsets)
   g->as_on = 0;

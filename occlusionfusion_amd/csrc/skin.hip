@@ -276,13 +276,20 @@ __global__ __launch_bounds__(256) void k_skin_palette(const ushort4* __restrict_
 }
 
 // ---- per-point k-NN (all nodes) ----
+// kSP adjacent lanes per point, each scanning every kSP-th node of the LDS tile into its own top-K, then a butterfly
+// merge over the kSP lanes (each round inserts the partner's K entries): the K smallest by (distance, id) are unique,
+// so every lane ends with the single-thread scan's result, bit for bit. (One thread per point left 40 workgroups for
+// 10k matches scanning 2k nodes each: ~330 us on the prefetch stream beside the solve.)
+constexpr int kSP = 16;
+static_assert(64 % kSP == 0, "a point's lanes within one wave");
 __global__ __launch_bounds__(256) void k_skin_points(const float* __restrict__ pts, int64_t n_pts,
                                                       const float* __restrict__ nodes, int n_nodes, float cutoff,
                                                       float denom, int K, int32_t* __restrict__ anchors,
                                                       float* __restrict__ weights, uint8_t* __restrict__ valid) {
   __shared__ float4 sn[kTile];
-  int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  bool act = p < n_pts;
+  const int part = threadIdx.x % kSP;
+  const int64_t p = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kSP;
+  const bool act = p < n_pts;
   float x = 0, y = 0, z = 0;
   if (act) { x = pts[3 * p]; y = pts[3 * p + 1]; z = pts[3 * p + 2]; }
   TopK tk;
@@ -296,12 +303,21 @@ __global__ __launch_bounds__(256) void k_skin_points(const float* __restrict__ p
     }
     __syncthreads();
     if (act)
-      for (int i = 0; i < nt; ++i) {
+      for (int i = part; i < nt; i += kSP) {
         float4 n = sn[i];
         tk.insert(sqdist(x, y, z, n.x, n.y, n.z), t0 + i);
       }
   }
-  if (!act) return;
+#pragma unroll
+  for (int o = 1; o < kSP; o <<= 1) {   // (every lane takes part: the shuffles precede any exit)
+    float od[4];
+    int oi[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) { od[s2] = __shfl_xor(tk.d[s2], o, 64); oi[s2] = __shfl_xor(tk.id[s2], o, 64); }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) tk.insert(od[s2], oi[s2]);
+  }
+  if (!act || part != 0) return;
   int ids[4];
   float w[4];
   finish_skin(tk, K, cutoff, denom, ids, w);
@@ -420,7 +436,7 @@ int ofx_skin_points(const float* points, int64_t n_points, const float* nodes, i
   if (n_points == 0) return OFX_OK;
   OFX_CHECK_ARG(points && nodes && anchors && weights && valid, "null buffer");
   SkinConsts c = skin_consts(node_coverage);
-  hipLaunchKernelGGL(k_skin_points, dim3(grid_for(n_points, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
+  hipLaunchKernelGGL(k_skin_points, dim3(grid_for(n_points * kSP, 256, 1 << 30)), dim3(256), 0, as_stream(s), points,
                      n_points, nodes, n_nodes, c.cutoff, c.denom, k, anchors, weights, valid);
   OFX_LAUNCH_CHECK();
   return OFX_OK;

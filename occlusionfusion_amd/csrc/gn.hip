@@ -821,15 +821,21 @@ __global__ __launch_bounds__(kBlk) void k_terms(GnDev g, DataCoef dc, int m0, in
     } else if (t < g.M + (int64_t)g.N * g.NB) {
       const int64_t e = t - g.M;
       const int j = g.edges[e];
+      // the edge's weight and node i's R, g, t leave with the edge's j (none depends on j; behind the j >= 0 test the
+      // weight was a trip of its own, then i's and j's records another)
+      const int i = (int)(e / g.NB);
+      const double ewv = g.ew[e];
+      double Ri[9], gi[3], ti[3];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Ri[q] = g.R[9 * (int64_t)i + q];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) { gi[q] = g.nodes[3 * (int64_t)i + q]; ti[q] = g.t[3 * (int64_t)i + q]; }
+      asm volatile("" ::: "memory");
       if (j >= 0 && k < 2) {
         if (add_reg) {
-          const int i = (int)(e / g.NB);
-          const double s = dc.la * g.ew[e];
+          const double s = dc.la * ewv;
           if (k == 0) {
-            const double* Ri = g.R + 9 * (int64_t)i;
-            const double* gi = g.nodes + 3 * (int64_t)i;
             const double* gj = g.nodes + 3 * (int64_t)j;
-            const double* ti = g.t + 3 * (int64_t)i;
             const double* tj = g.t + 3 * (int64_t)j;
             double e0 = gj[0] - gi[0], e1 = gj[1] - gi[1], e2 = gj[2] - gi[2];
             double d0 = Ri[0] * e0 + Ri[1] * e1 + Ri[2] * e2;

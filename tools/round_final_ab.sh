@@ -1,5 +1,5 @@
-# Round end: bitwise digests of the gn_2k / gn_4k chains against the previous library (k_terms' edge loads must not
-# change a bit), then tools/round_final.sh (suite, smoke, measurement, configs 2 / 4, moose)
+# Round end with a bitwise check: gn_2k / gn_4k chain digests of the current library against a previous build copied to
+# ./libofx_base_tmp.so (tools/ab_gn.py; a change meant to keep every bit must match), then tools/round_final.sh
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out

@@ -2328,6 +2328,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // (wave list,) row bounds, own state, M⁻¹ row and b issued with the stop flag: one trip
   int2 bl[2] = {make_int2(-1, 0), make_int2(-1, 0)};
   if (kWave) { bl[0] = g.wl[(int64_t)wv * kWL + lane]; bl[1] = g.wl[(int64_t)wv * kWL + 64 + lane]; }
+  // the list and the stop flag leave first (loads retire in issue order): the stop test and trip 2's issue wait for
+  // them only, the rest of trip 1 lands under trip 2's flight
+  const int stopped = g.flags[F_STOPPED];
+  asm volatile("" ::: "memory");
   const int wb0 = g.row_ptr[wv * kRW];
   const int rb0 = g.row_ptr[row], rb1 = g.row_ptr[row + 1];
   const double bo = rhs[oc];
@@ -2340,30 +2344,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // the previous step's final θ̂ (the lead's bookkeeping below), with trip 1: read inside the lead's branch it was one
   // more trip for workgroup 0 before its SpMV
   const double th_cur_old = g.pcs[kScScal + S_TH_CUR];
-  const int stopped = g.flags[F_STOPPED];
   asm volatile("" ::: "memory");
   // this solve's stop words: the epoch if the solve already stopped (its iteration launches end after trip 1), else 0
   // (a converging iteration sets them to the epoch), so the iteration's stop test needs no epoch; and the operator's
-  // address into the scalar block, where the iteration finds it through a preloaded pointer
-  g.stopw[(int64_t)blockIdx.x * 64 + lane] = stopped ? g.ep : 0;
-  if (blockIdx.x == 0 && lane == 0) {
-    reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(kWave ? g.Aw : g.Aop);
-    g.pcs[kScTol] = g.prm.pcg_tol;
-    // The error stop bounds ‖e‖_M (M the preconditioner); ‖e‖₂ <= ‖e‖_M / √λ_min(M). The cluster blocks' λ_min(M) is a
-    // cluster matrix's smallest eigenvalue, >= λ_min(A); the Schwarz M⁻¹ sums up to 1 + kAsX overlapping subdomain
-    // inverses per row, each of a larger subdomain (whose smallest eigenvalue is at most its cluster block's), so its
-    // λ_min(M) is smaller: the tolerance is taken 4x tighter (2x for the overlap's multiplicity, 2x margin: the moose
-    // pair ended at 1.1e-5 with 2x).
-    g.pcs[kScTol + 1] = kAS ? 0.25 * g.prm.pcg_err_tol : g.prm.pcg_err_tol;
-    // (Schwarz: the iteration's w_new target in the inverse's slot)
-    reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = kAS ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
-    reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
-    reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
-    // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
-    g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? th_cur_old : 1e300;
-    g.pcs[kScScal + S_TH_CUR] = 1e300;
+  // address into the scalar block, where the iteration finds it through a preloaded pointer. Both are stored last on the
+  // main path: vmcnt counts stores too, so stores ahead of trip 2 held its issue until their acks (workgroup 0's eight)
+  auto lead_stores = [&]() {
+    if (blockIdx.x == 0 && lane == 0) {
+      reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(kWave ? g.Aw : g.Aop);
+      g.pcs[kScTol] = g.prm.pcg_tol;
+      // The error stop bounds ‖e‖_M (M the preconditioner); ‖e‖₂ <= ‖e‖_M / √λ_min(M). The cluster blocks' λ_min(M) is a
+      // cluster matrix's smallest eigenvalue, >= λ_min(A); the Schwarz M⁻¹ sums up to 1 + kAsX overlapping subdomain
+      // inverses per row, each of a larger subdomain (whose smallest eigenvalue is at most its cluster block's), so its
+      // λ_min(M) is smaller: the tolerance is taken 4x tighter (2x for the overlap's multiplicity, 2x margin: the moose
+      // pair ended at 1.1e-5 with 2x).
+      g.pcs[kScTol + 1] = kAS ? 0.25 * g.prm.pcg_err_tol : g.prm.pcg_err_tol;
+      // (Schwarz: the iteration's w_new target in the inverse's slot)
+      reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = kAS ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
+      reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
+      reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
+      // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
+      g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? th_cur_old : 1e300;
+      g.pcs[kScScal + S_TH_CUR] = 1e300;
+    }
+  };
+  if (stopped) {
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
+    lead_stores();
+    return;
   }
-  if (stopped) return;
   if (kAS) v[V_U] = u_as;
   const double b = own ? bo : 0.0;
   double w;
@@ -2442,6 +2451,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       for (int k = 0; k < 18; ++k) Aw[k * kWL + 64 * j + lane] = ok ? ab[j][k] : make_double2(0.0, 0.0);
     }
   }
+  g.stopw[(int64_t)blockIdx.x * 64 + lane] = 0;
+  lead_stores();
   asm volatile("" ::"v"(w_old));
 }
 

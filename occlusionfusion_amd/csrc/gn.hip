@@ -45,7 +45,6 @@
 #include <mutex>
 #include <thread>
 #include <type_traits>
-#include <type_traits>
 #include <utility>
 #include <cstdlib>
 #include <cstdio>
@@ -283,6 +282,7 @@ constexpr int32_t kEpochWrap = 1 << 30;   // GnDev::ep restarts at 1 from a setu
 // (pcg_tol, pcg_err_tol) at 152, 153, the cluster inverses' address at 154, m0 / m1's at 156 / 157. The iteration gets
 // the block's address with its parity in bit 3 (the block is 256-B aligned), so it needs no kernel-argument fetch for
 // any of them.
+constexpr int kPcgStreams = 4;   // k_pcg_iter's per-wave partial streams per parity: γ = r·u, δ = w·u, r·r, p·p
 constexpr int kScAlpha = 0, kScGamma = 6, kScScal = 12, kScSturm = 16, kScFlags = 144, kScAop = 150, kScTol = 152,
               kScMcl = 154, kScM = 156, kScSize = 160;
 
@@ -2353,12 +2353,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (blockIdx.x == 0 && lane == 0) {
       reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(kWave ? g.Aw : g.Aop);
       g.pcs[kScTol] = g.prm.pcg_tol;
-      // The error stop bounds ‖e‖_M (M the preconditioner); ‖e‖₂ <= ‖e‖_M / √λ_min(M). The cluster blocks' λ_min(M) is a
-      // cluster matrix's smallest eigenvalue, >= λ_min(A); the Schwarz M⁻¹ sums up to 1 + kAsX overlapping subdomain
-      // inverses per row, each of a larger subdomain (whose smallest eigenvalue is at most its cluster block's), so its
-      // λ_min(M) is smaller: the tolerance is taken 4x tighter (2x for the overlap's multiplicity, 2x margin: the moose
-      // pair ended at 1.1e-5 with 2x).
-      g.pcs[kScTol + 1] = kAS ? 0.25 * g.prm.pcg_err_tol : g.prm.pcg_err_tol;
+      // the error stop's τ: one value for both preconditioners (the estimate is Euclidean, k_pcg_iter)
+      g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
       // (Schwarz: the iteration's w_new target in the inverse's slot)
       reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = kAS ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
       reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
@@ -2431,12 +2427,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int ns = g.nw_pad;
   if (lane == 0) {
     g.part_p[blockIdx.x] = d[0]; g.part_p[ns + blockIdx.x] = d[1]; g.part_p[2 * ns + blockIdx.x] = d[2];
+    g.part_p[3 * ns + blockIdx.x] = 0.0;   // (the direction stream: no direction before the first iteration)
     g.part_b[blockIdx.x] = d[3];
   }
   if (blockIdx.x == 0)   // zero tails of both parities' streams (part_p is also proj scratch) and of part_b
     for (int i = g.nwg_row + lane; i < ns; i += 64) {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) g.part_p[k * ns + i] = 0.0;
+      for (int k = 0; k < 2 * kPcgStreams; ++k) g.part_p[k * ns + i] = 0.0;
       g.part_b[i] = 0.0;
     }
   // the loaded (dead) w register stays allocated to here: otherwise the compiler reuses it for a temporary of the
@@ -2660,14 +2657,14 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const bool own = q < 6;
   const int qc = own ? q : 5;
   const int64_t o = 6 * (int64_t)row + qc;
-  double2 tp[3][kU];              // the streams are zero beyond nw up to 128·kU: no masks
+  double2 tp[kPcgStreams][kU];   // the streams are zero beyond nw up to 128·kU: no masks
 #pragma unroll
-  for (int k = 0; k < 3; ++k)
+  for (int k = 0; k < kPcgStreams; ++k)
 #pragma unroll
     for (int u = 0; u < kU; ++u) tp[k][u] = *reinterpret_cast<const double2*>(Pc + k * kNs + 2 * (lane + 64 * u));
-  double own_p[3];
+  double own_p[kPcgStreams];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) own_p[k] = Pc[k * kNs + wv];
+  for (int k = 0; k < kPcgStreams; ++k) own_p[k] = Pc[k * kNs + wv];
   const int cnt = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
   const double2 ra = *reinterpret_cast<const double2*>(scb + kScAlpha + 2);   // 1/α of parities 0, 1
   const double2 rt = *reinterpret_cast<const double2*>(scb + kScAlpha + 4);   // the error-stop bound of parities 0, 1
@@ -2768,7 +2765,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // the state, the stop words, the lead's scalars
   __attribute__((address_space(1))) double* mn = reinterpret_cast<__attribute__((address_space(1))) double*>(addr(mn_v));
   const int ns = kNs;
-  double* Pn = const_cast<double*>(Pc) + (par_ ? -3 : 3) * (int64_t)kNs;
+  double* Pn = const_cast<double*>(Pc) + (par_ ? -kPcgStreams : kPcgStreams) * (int64_t)kNs;
   double* stw = const_cast<double*>(st);
   int32_t* stopw_w = const_cast<int32_t*>(stopw);
   double* sc_w = const_cast<double*>(scb);
@@ -2784,9 +2781,9 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   const double ralpha_prev = kFirst ? 1.0 : ((par_ ^ 1) ? ra.y : ra.x);
   const double thr_prev = kFirst ? 0.0 : ((par_ ^ 1) ? rt.y : rt.x);       // error-based stop: bound on γ (below)
   // ---- scalars from the partials (trip-1 data)
-  double pa[3];
+  double pa[kPcgStreams];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < kPcgStreams; ++k) {
     double t = 0.0;
 #pragma unroll
     for (int u = 0; u < kU; ++u) t += tp[k][u].x + tp[k][u].y;
@@ -2803,7 +2800,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     for (int u = 0; u < 2 * kU; ++u) t += tb[u];
     bb = wave_sum(t);
   }
-  const double gam = pa[0], del = pa[1], rr = pa[2];
+  const double gam = pa[0], del = pa[1], rr = pa[2], pp = pa[3];   // pp = ‖p‖² of the previous iteration's direction
   const double tol = tol_s;
   const bool lead = wv == 0 && lane == 0 && hw == 0;
   const bool w0 = hw == 0;   // the wave that stores (kW2: both compute the same bits)
@@ -2814,19 +2811,27 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     beta = gam * rgam_prev;
     alpha = div_nr(gam, del - beta * gam * ralpha_prev);
   }
-  // Stop: the relative residual ‖r‖ <= tol·‖b‖ AND (pcg_err_tol > 0) the error estimate √γ / θ̂ <= pcg_err_tol, or
-  // the relative residual at the f64 floor (1e-12). γ = rᵀM⁻¹r = ‖z‖²_M (z = M⁻¹r), so the error e = (M⁻¹A)⁻¹z has
-  // ‖e‖_M <= √γ / λ_min(M⁻¹A); θ̂ is the previous iteration's estimate of λ_min(M⁻¹A) from below, kept by the lead
-  // wave (sturm_step). The residual alone cannot see the error of an ill-conditioned system (real data: DESIGN §6).
+  // Stop: the relative residual ‖r‖ <= tol·‖b‖ AND (pcg_err_tol = τ > 0) the estimated Euclidean norm of the solution
+  // error ‖e‖₂ ≈ √(γ·μ/θ̂) <= τ, or the relative residual at the f64 floor (1e-12). The estimate (round 6):
+  // ‖e‖²_A = rᵀA⁻¹r <= γ/λ_min(M⁻¹A) with γ = rᵀM⁻¹r, θ̂ the previous iteration's estimate of λ_min(M⁻¹A) from below
+  // (kept by the lead wave, below); late in a solve the error lies along the slowest modes, which the last search
+  // direction p follows, so ‖e‖²₂ ≈ ‖e‖²_A·μ with μ = ‖p‖²/pᵀAp = pp·α/γ of the previous iteration (Hestenes–Stiefel:
+  // ‖e_k‖² - ‖e_k+1‖² = (‖p_k‖²/p_kᵀAp_k)(‖e_k‖²_A + ‖e_k+1‖²_A)). Measured in the norm of the 1e-5 bar, it needs no
+  // preconditioner-specific factor (round 5 tightened an M-norm rule 4x under Schwarz). thr = τ²·θ̂; the test is
+  // γ·pp/γ_prev <= thr/α_prev (the reciprocals are carried). The residual alone cannot see the error of an
+  // ill-conditioned system (real data: DESIGN §6).
   const double etol = etol_s;
-  const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam <= thr_prev)) || gam == 0.0 || rr <= 1e-24 * bb;
+  const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam * pp * rgam_prev <= thr_prev * ralpha_prev)) ||
+                    gam == 0.0 || rr <= 1e-24 * bb;
   int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
   leave = __builtin_amdgcn_readfirstlane(leave);
   OFX_STAMPX(5)
   if (leave) {   // converged, or breakdown (A SPD => alpha > 0): keep x
     if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
     if (!w0) return;
-    if (lane == 0) { Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; }
+    if (lane == 0) {
+      Pn[wv] = own_p[0]; Pn[ns + wv] = own_p[1]; Pn[2 * ns + wv] = conv ? own_p[2] : 0.0; Pn[3 * ns + wv] = own_p[3];
+    }
     stopw_w[(int64_t)wv * 64 + lane] = ep;
     const bool ill = !conv && !isfinite(alpha);
     if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, ep, gn_iter, wv, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
@@ -2849,7 +2854,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   // it (θ_k / 2^(1/4) < θ̂ <= θ_k above 2^-10; 1 if θ_k >= 1; 0 below the last shift). Early in a solve θ_k still
   // over-estimates λ_min, so a GN step after the first also takes the previous step's final θ̂ when that is smaller (the
   // step's operator differs little from the previous one's: on the moose a warm-started step stopped after 64
-  // iterations with 3.7e-5 left without it, tools/errstop_study.py). thr = (pcg_err_tol·min(θ̂, θ̂_prev))².
+  // iterations with 3.7e-5 left without it, tools/errstop_study.py). thr = pcg_err_tol²·min(θ̂, θ̂_prev).
   double2 sd_new = sd;
   double thr_new = 0.0, th_cur = 1e300;
   auto shift = [](int s) {   // σ_s
@@ -2872,7 +2877,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     const double th = free_ ? shift(__ffsll((unsigned long long)free_) - 1) : 0.0;
     th_cur = th;
     const double tu = fmin(th, th_prev);
-    thr_new = (etol * tu) * (etol * tu);
+    thr_new = (etol * etol) * tu;
   }
   auto lead_stores = [&]() {
     if (lead) {
@@ -2929,7 +2934,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     nc = pick6(n, qc);
   }
   OFX_STAMP(4)
-  double d[3] = {0.0, 0.0, 0.0};
+  double d[kPcgStreams] = {0.0, 0.0, 0.0, 0.0};
   {
     const double zz = fma(beta, v[V_Z], nc);
     const double qq = fma(beta, v[V_Q], m);
@@ -2946,7 +2951,7 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
       } else {
         s_v[hw][6 * r + q] = w2;
       }
-      d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn;
+      d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn; d[3] = p * p;
     }
   }
   OFX_STAMP(5)
@@ -2990,19 +2995,22 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
     mn[o] = (a[0] + a[1]) + (a[2] + a[3]);
   }
   OFX_STAMP(6)
-  // the three per-wave partials of the next launch: kW2's second wave (idle otherwise here) sums and stores the third,
-  // from the same bits wave 0 holds, so wave 0's tail is two wave sums instead of three
+  // the four per-wave partials of the next launch: kW2's second wave (idle otherwise here) sums and stores the third and
+  // fourth, from the same bits wave 0 holds, so wave 0's tail is two wave sums instead of four
   if (!w0) {
     if (kW2) {
-      const double s2 = wave_sum(d[2]);
-      if (lane == 0) Pn[2 * ns + wv] = s2;
+      const double s2 = wave_sum(d[2]), s3 = wave_sum(d[3]);
+      if (lane == 0) { Pn[2 * ns + wv] = s2; Pn[3 * ns + wv] = s3; }
     }
     return;
   }
   d[0] = wave_sum(d[0]);
   d[1] = wave_sum(d[1]);
-  if (!kW2) d[2] = wave_sum(d[2]);
-  if (lane == 0) { Pn[wv] = d[0]; Pn[ns + wv] = d[1]; if (!kW2) Pn[2 * ns + wv] = d[2]; }
+  if (!kW2) { d[2] = wave_sum(d[2]); d[3] = wave_sum(d[3]); }
+  if (lane == 0) {
+    Pn[wv] = d[0]; Pn[ns + wv] = d[1];
+    if (!kW2) { Pn[2 * ns + wv] = d[2]; Pn[3 * ns + wv] = d[3]; }
+  }
   lead_stores();
   OFX_STAMP(7)
 }
@@ -3404,7 +3412,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     for (int k = 0; k < n; ++k, ++it) {
       const int par = it & 1;
       hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, (const int2*)g->wl, (const int32_t*)g->stopw,
-                         (const double*)(g->part_p + 3 * (int64_t)g->nw_pad * par), (const double*)g->st,
+                         (const double*)(g->part_p + kPcgStreams * (int64_t)g->nw_pad * par), (const double*)g->st,
                          (const double*)(par ? g->m1 : g->m0), (const double*)g->pcs + par, gp, par, g->ep,
                          gn_iter);
       if (as) as_apply(true, g->as_w, par ? g->m0 : g->m1);   // m of the next iteration = M⁻¹ w_new
@@ -3569,7 +3577,7 @@ int ofx_gn_create(int32_t max_nodes, int32_t max_matches, void** handle) {
   const int64_t max_row_wg = ((N + kRW - 1) / kRW + 1) & ~1;
   const int64_t max_ns = 128 * 17;   // nw_pad bound: 2·64·17 >= max_pad / kCS waves
   static_assert(2 * 64 * 17 * kCS >= 2 * kMaxNodes + kCS, "partial stream width");
-  static_assert(kProjP >= 6, "part_p: kProjP projection streams / 6 iteration streams, stride nw_pad");
+  static_assert(kProjP >= 2 * kPcgStreams, "part_p: kProjP projection streams / 2 x 4 iteration streams, stride nw_pad");
   (void)max_row_wg;
   ALLOC(g->part_p, kProjP * max_ns); ALLOC(g->part_b, max_ns);
   static_assert(S_COUNT <= kScSturm - kScScal && 2 * kScFlags + F_COUNT <= 2 * kScAop && kScAop < kScSize,

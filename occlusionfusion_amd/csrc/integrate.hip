@@ -594,6 +594,7 @@ __global__ __launch_bounds__(256) void k_brick_cull(BrickGeom g, BrickDiv bd, Ca
   const int sc = s < n_list ? s : n_list - 1;   // (the last group of the grid may overhang: clamped, not stored)
   const int pn = pal_n[sc];
   const uint32_t b = (uint32_t)list[sc];
+  static_assert(kPal == 16 * 4, "k_brick_cull: 16 lanes x 4 palette slots must cover the palette (else not conservative)");
   int pid[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) pid[i] = pal_ids[(int64_t)sc * kPal + sub + 16 * i];

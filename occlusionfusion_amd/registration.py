@@ -26,7 +26,7 @@ from .sharding import match_range
 
 GN_DEFAULTS = dict(num_iter=10, lambda_flow=0.0, lambda_depth=1.0, lambda_arap=0.5, lambda_motion=1.0,
                    lm_factor=1e-7, stop_loss_diff=1.0, use_edge_weighting=False, pcg_max_iter=2000, pcg_tol=2e-6,
-                   pcg_warm=True, precond_every=10, pcg_err_tol=1e-5, precond_rot_tol=0.3, precond="auto")
+                   pcg_warm=True, precond_every=10, pcg_err_tol=2e-6, precond_rot_tol=0.3, precond="auto")
 # PCG preconditioner (ofx_gn_params.precond): overlapping additive Schwarz, the 8-node cluster blocks, or
 # auto (Schwarz for graphs of >= 1536 nodes)
 _PRECOND = {"cluster": 0, "schwarz": 1, "auto": 2}
@@ -41,6 +41,15 @@ def _t(x, device, dtype):
             return x   # per-frame fast path (host time: no .to / .contiguous dispatch)
         return x.to(device=device, dtype=dtype).contiguous()
     return torch.as_tensor(np.ascontiguousarray(x), device=device).to(dtype).contiguous()
+
+
+def _prefetch_lead(num_iter):
+    """OFX_PREFETCH_LEAD (A/B only): an integer clamped to [0, num_iter]; anything else is the default 1."""
+    try:
+        v = int(os.environ.get("OFX_PREFETCH_LEAD", "1"))
+    except ValueError:
+        return 1
+    return min(max(v, 0), int(num_iter))
 
 
 class GaussNewtonSolver:
@@ -58,7 +67,7 @@ class GaussNewtonSolver:
         self._side = None               # torch stream that orders a prefetch before the current solve
         # GN steps of the current solve a prefetch overlaps: its setup starts when the solve begins step
         # num_iter - prefetch_lead (ofx_gn_prepare_after); 0 = when the solve's host loop returns
-        self.prefetch_lead = int(os.environ.get("OFX_PREFETCH_LEAD", "1"))   # (env: A/B only)
+        self.prefetch_lead = _prefetch_lead(self.params["num_iter"])   # (env: A/B only)
         self._h, self._state = self._slots[0]   # the last solve's slot (info / stats / stopped / arap / distributed)
 
     def _new_slot(self):

@@ -22,6 +22,8 @@
                         chained from the first, ~2k nodes of the SURVEY §8(d) depth-mesh graph built by the
                         reference's C++, 10k matches) by the f64 oracle with a sparse JᵀJ + dense LU.
   gn_4k.npz           — the same at config 4's graph (~4k nodes, frame 10).
+  gn_2k_hole.npz      — gn_2k's frame 10 with the matches of a 48-node patch removed (the patch held only by ARAP and
+                        confidence-0.3 motion rows): a differently conditioned spectrum for the PCG stop rule.
   gn_c5r1.npz,        — BASELINE config 5 (one independent 512³ scene per GPU): the scenes of ranks 1 and 7
   gn_c5r7.npz           (synthetic.config_scene(5, r): their own sphere, occluder and motion phase), frame 10, the
                         same solve at their own ~2k-node depth-mesh graphs.
@@ -393,6 +395,40 @@ def make_gn_chain(name, config, frames, n_matches=10000, rank=0):
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
 
 
+HOLE_CENTER = (0.10, -0.05, 1.10)   # a point on the sphere's visible front (config 3's scene)
+HOLE_RADIUS = 0.12
+
+
+def make_gn_hole():
+    """gn_2k_hole.npz — a differently conditioned spectrum at the headline size (round 6): gn_2k's frame 10 with every
+    match anchored to a node within 12 cm of a point on the sphere's front removed, and those nodes' motion-term
+    confidence set to 0.3, so a 48-node patch is held only by ARAP and confidence-0.3 motion rows; solved by the
+    f64 oracle (gn_optimize_sparse) from the identity."""
+    import time
+    g = np.load(os.path.join(HERE, "gn_2k.npz"), allow_pickle=False)
+    nodes = g["nodes"]
+    c = nodes[np.argmin(((nodes - np.asarray(HOLE_CENTER, np.float32)) ** 2).sum(1))]
+    hole = np.sqrt(((nodes - c) ** 2).sum(1)) < HOLE_RADIUS
+    keep = ~hole[g["f0_anchors"]].any(1)
+    conf = g["f0_conf"].copy()
+    conf[hole] = np.float32(0.3)
+    pb = dict(src=g["f0_src"][keep], tgt=g["f0_tgt"][keep], tpos=g["f0_tpos"], conf=conf,
+              anchors=g["f0_anchors"][keep], weights=g["f0_weights"][keep])
+    intr = g["intr"]
+    t0 = time.time()
+    res = fo.gn_optimize_sparse(nodes, g["edges"], g["edge_weights"], pb["tpos"], pb["conf"], pb["src"], pb["anchors"],
+                                pb["weights"], pb["tgt"], intr)
+    ci = res["convergence_info"]
+    out = dict(nodes=nodes, edges=g["edges"], edge_weights=g["edge_weights"], node_coverage=g["node_coverage"],
+               intr=intr, config=g["config"], frames=np.array([10], np.int32), seed=g["seed"], hole=hole)
+    out.update({f"f0_{k}": v for k, v in pb.items()})
+    out.update(f0_R=res["node_rotations"], f0_t=res["node_translations"], f0_valid=res["valid_solve"],
+               f0_loss_total=np.array(ci["total"]), f0_loss_data=np.array(ci["data"]))
+    np.savez_compressed(os.path.join(HERE, "gn_2k_hole.npz"), **out)
+    print(f"gn_2k_hole: {int(hole.sum())} hole nodes, {pb['src'].shape[0]} matches, {len(ci['total'])} GN steps, loss "
+          f"{ci['total'][0]:.6f} -> {ci['total'][-1]:.6f} ({time.time() - t0:.0f} s)", flush=True)
+
+
 MOOSE = "/root/reference/NonRigidICP/demo/moose6OK9_AttackTrotRM"   # read here only; the fixture travels
 
 
@@ -478,6 +514,8 @@ if __name__ == "__main__":
         make_gn_chain("gn_2k", 3, (10, 11))
     if "gn4k" in which:
         make_gn_chain("gn_4k", 4, (10,))
+    if "hole" in which:
+        make_gn_hole()
     if "gn5" in which:   # BASELINE config 5: rank 1's and rank 7's independent scenes (one GPU each)
         make_gn_chain("gn_c5r1", 5, (10,), rank=1)
         make_gn_chain("gn_c5r7", 5, (10,), rank=7)

@@ -116,9 +116,10 @@ def _moose_gn(g, **params):
 def test_moose_landmark_gn_matches_dense_oracle(cuda, moose):
     """Default parameters. Real data is ill-conditioned where the synthetic bench is not: 53 of the 271 nodes anchor
     no landmark and the data-constrained spectrum spans 3e-4 … 27.5, so the preconditioned operator's smallest
-    eigenvalue is ≈5e-4 (≈2e-2 on the bench). The default stop adds the error estimate √(rᵀM⁻¹r)/θ <= 1e-5 to the
-    relative residual 1e-6 (θ: the smallest Ritz value of the PCG's Lanczos tridiagonal), so the solve runs until
-    the estimated error, not only the residual, is small: within the north star's 1e-5 on the transforms."""
+    eigenvalue is ≈5e-4 (≈2e-2 on the bench). The default stop adds the estimated Euclidean solution error
+    √(γ·μ/θ) <= 2e-6 to the relative residual 2e-6 (γ = rᵀM⁻¹r, θ: the smallest Ritz value of the PCG's Lanczos
+    tridiagonal, μ = ‖p‖²/pᵀAp), so the solve runs until the estimated error, not only the residual, is
+    small: within the north star's 1e-5 on the transforms."""
     g = moose
     out, dr, dt = _moose_gn(g)
     np.testing.assert_allclose(out["convergence_info"]["total"], g["loss_total"], rtol=1e-6, atol=0)
@@ -129,7 +130,7 @@ def test_moose_landmark_gn_matches_dense_oracle(cuda, moose):
 def test_moose_preconditioner_refresh_cuts_pcg_work(cuda, moose):
     """Real data rotates nodes by up to ~1 rad per GN step, so a cluster inverse built at step 0 goes stale: with the
     round-4 policy (precond_rot_tol = 0: one inverse per solve) the moose optimize needed ≈10.4k PCG iterations
-    (≈1,000 per GN step). The default rebuilds a cluster inverse when a node's accumulated rotation passes 0.1 rad
+    (≈1,000 per GN step). The default rebuilds a cluster inverse when a node's accumulated rotation passes 0.3 rad
     (k_pcg_proj, F_REFRESH): ≈1.2k iterations, no step capped at pcg_max_iter, and still within 1e-5 of the f64
     oracle. The stale-preconditioner run is also within 1e-5 (only the work differs)."""
     g = moose

@@ -1,7 +1,7 @@
 """GPU: the overlapping additive Schwarz preconditioner (OFX_PRECOND=as) against the f64 oracle fixtures.
 
-Each 8-node cluster's subdomain adds up to 12 ring rows (its A-neighbours with the most coupling terms, a row joining at
-most 3 rings); M⁻¹ = Σ_c R_cᵀ A_{D_c}⁻¹ R_c is applied by k_as_apply between two PCG iteration launches. The solution
+Each 8-node cluster's subdomain adds up to 16 ring rows (kAsRing: its A-neighbours with the most coupling terms, a row
+joining at most 3 rings); M⁻¹ = Σ_c R_cᵀ A_{D_c}⁻¹ R_c is applied by k_as_apply between two PCG iteration launches. The solution
 must meet the same 1e-5 bar as the cluster block Jacobi, with far fewer PCG iterations on the bench graph (numpy study,
 tools/schwarz_study.py: 2.46x on gn_2k), bitwise repeatably (fixed-order segment sums).
 """

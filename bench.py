@@ -324,6 +324,14 @@ def main():
         B_apply = (pci["segments"] * (2 * pci["row_length"] + 8) + C_ * (52 * 4 + 100 + 256) + pci["gathered_rows"] * 4 + rows * 48
                    + pci["subdomain_rows"] * 24 + rows * 48)
         B_pcg = nnzb * 296 + rows * (768 + 48 + 48) + B_apply
+    one = bool(pci["schwarz"]) and pci.get("launches_per_iteration", 2) == 1
+    if one:
+        # one launch per iteration (k_as_iter, round 6): the operator's blocks once (288 B; the kernel re-reads each block
+        # for up to 1 + kAsX subdomains from L2), each subdomain's fp16 inverse rows (288 B per segment) and their scales
+        # (4 B), the own rows' state read + written (768 B per row), the ring rows' ghost (w, z) read + written (32 B per
+        # component), the contributions written and read (16 B per segment)
+        ring_rows = max(0, pci["subdomain_rows"] - rows)
+        B_pcg = nnzb * 288 + pci["segments"] * (288 + 4 + 16) + rows * 768 + ring_rows * 6 * 32
     iters = float(np.sum(pcg))
     launches = max(1, pcg_launches)
     t_pcg = pcg_ms * 1e-3 / launches
@@ -331,8 +339,8 @@ def main():
     workload = (f"{D}^3 TSDF @{a.voxel * 1e3:g} mm, {seq.nodes.shape[0]} nodes, {a.matches} matches, "
                 f"{seq.cam.width}x{seq.cam.height} depth, {cfg['motion']}{' + occluder' if cfg['occluder'] else ''}, "
                 f"GN 10 it")
-    pcg_traffic = pmc_traffic("k_pcg_iter", workload)
-    if pci["schwarz"]:   # per launch: the mean of the pair (the chain alternates them)
+    pcg_traffic = pmc_traffic("k_as_iter" if one else "k_pcg_iter", workload)
+    if pci["schwarz"] and not one:   # per launch: the mean of the pair (the chain alternates them)
         t_apply = pmc_traffic("k_as_apply", workload)
         pcg_traffic = None if pcg_traffic is None or t_apply is None else 0.5 * (pcg_traffic + t_apply)
     res = {
@@ -354,7 +362,9 @@ def main():
                          "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid)),
                          "prefetched_setups_used": pf_used, "prefetched_setups_missed": pf_missed},
         "per_rank": per_rank,
-        "roofline": {"kernel": ("k_pcg_iter + k_as_apply (one pipelined PCG iteration = two launches: wave-list block "
+        "roofline": {"kernel": ("k_as_iter (one launch per pipelined PCG iteration: the subdomain's block SpMV with ghost "
+                                "ring rows, the recurrences and its overlapping Schwarz inverse)") if one else
+                               ("k_pcg_iter + k_as_apply (one pipelined PCG iteration = two launches: wave-list block "
                                 "SpMV + recurrences, then the overlapping Schwarz apply)") if pci["schwarz"] else
                                ("k_pcg_iter (pipelined PCG iteration: wave-list block SpMV + recurrences + cluster "
                                 "block-Jacobi apply)"), "bound": "latency", "preconditioner": pci,

@@ -66,7 +66,7 @@
 extern "C" {
 #endif
 
-#define OFX_ABI_VERSION 4
+#define OFX_ABI_VERSION 5
 
 typedef void* ofx_stream_t; /* hipStream_t; NULL = legacy default stream */
 
@@ -381,13 +381,15 @@ typedef struct ofx_gn_params {
   int32_t precond_every;     /* the cluster preconditioner is rebuilt on GN steps gn_iter % precond_every == 0
                                 (0 or 1: every step) and reused by the warm-started steps in between; it only
                                 shapes convergence, the stop test is unchanged */
-  double pcg_err_tol;        /* error-based stop (> 0): the inner solve also runs until its estimated solution
-                                error sqrt(r^T M^-1 r) / theta <= pcg_err_tol, theta = the smallest Ritz value of
-                                the preconditioned operator's Lanczos tridiagonal (from below, within a factor
-                                2^(1/4) down to 2^-10, sqrt 2 below), or, on GN steps after the first, the previous
-                                step's final theta when
-                                that is smaller (early in a solve theta over-estimates the smallest eigenvalue);
-                                0: the relative residual alone. Both stop at a relative residual of 1e-12 */
+  double pcg_err_tol;        /* error-based stop (> 0; ABI 5: one Euclidean estimate for every preconditioner): the
+                                inner solve also runs until the estimated Euclidean norm of its solution error
+                                sqrt(gamma * mu / theta) <= pcg_err_tol (default 2e-6, a fifth of the 1e-5 bar), with
+                                gamma = r^T M^-1 r (||e||_A^2 <= gamma / theta), mu = ||p||^2 / p^T A p of the last
+                                search direction (||e||_2^2 ~ ||e||_A^2 mu, Hestenes-Stiefel), theta = the smallest
+                                Ritz value of the preconditioned operator's Lanczos tridiagonal (from below, within a
+                                factor 2^(1/4) down to 2^-10, sqrt 2 below), or, on GN steps after the first, the
+                                previous step's final theta when that is smaller; 0: the relative residual alone. Both
+                                stop at a relative residual of 1e-12 */
   double precond_rot_tol;    /* adaptive preconditioner refresh (> 0): a GN step also rebuilds the cluster inverse
                                 when some node has rotated by more than this (radians, summed |omega| of the
                                 steps since the last rebuild); real data with large rotations (the moose demo)
@@ -454,9 +456,10 @@ int ofx_gn_timing(void* handle, int32_t enable, double* pcg_ms, int64_t* iter_la
 /* info (host int64[5]) = [n_nodes, n_matches, JᵀJ block count (nnzb), residual terms, rows] of the last
  * setup; rows = nodes in preconditioner-cluster order padded to whole clusters of 8 (<= 2·n_nodes + 8) */
 int ofx_gn_info(void* handle, int64_t* info);
-/* The preconditioner of the last setup (bench / tools; synchronises the device): info[7] = [Schwarz active, clusters,
+/* The preconditioner of the last setup (bench / tools; synchronises the device): info[8] = [Schwarz active, clusters,
  * apply segments (inverse rows of all output clusters), source subdomains, gathered rows, subdomain rows, entries per
- * segment row]. */
+ * segment row, kernel launches per PCG iteration (ABI 5: 1 = the one-launch Schwarz iteration k_as_iter, 2 = k_pcg_iter
+ * + k_as_apply; 1 for the cluster blocks)]. */
 int ofx_gn_precond_info(void* handle, int64_t* info);
 /* Waves per PCG cluster workgroup of k_pcg_iter for the last setup (before any: for a small problem): 2 up to
  * 384 clusters (default) or 1 (environment OFX_PCG_W1 set to anything but "" / "0" at create; tuning and A/B

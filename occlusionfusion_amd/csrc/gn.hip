@@ -72,6 +72,11 @@ constexpr int kAsRing = OFX_AS_RING, kAsX = 3, kAsDN = kCS + kAsRing, kAsD = 6 *
               kAsSrc = 1 + kCS * kAsX, kAsRS = 6 * kCS * (1 + kAsX),
               kAsGat = (kAsSrc * kAsDN + kAsRS - 1) / kAsRS * kAsRS, kAsMeta = 64 + kAsRS;
 constexpr int kAsTi = (kAsD + 15) / 16;   // k_as_invert's register tile (16 x 16 threads, kAsTi x kAsTi entries each)
+// One launch per Schwarz PCG iteration (k_as_iter, round 6): per subdomain a table of its rows' blocks (<= kAsDN rows of
+// <= kRowMax blocks), the columns they touch (S2, <= kGS nodes) with the <= 1 + kAsX subdomain contributions that sum to m
+// there, and the scaled inverse rows in subdomain order (the "tab" buffer, AsTab below)
+constexpr int kGB = 512, kGS = 480, kGRow = 96;
+constexpr int kAsIterT = 1024;   // k_as_iter's threads: blocks 0..511, S2 nodes from 512, the row waves 13..15
 static_assert(kAsSrc * kAsDN <= kAsGat && kAsD % 8 == 0 && kAsTi <= 9, "Schwarz tables");
 
 // Everything the kernels read: trivially copyable, passed by value as the kernel argument (host-only
@@ -156,6 +161,11 @@ struct GnDev {
   float* as_dsc = nullptr;       // [cluster][kAsD]: the subdomain inverse's scales d = √diag(Z) (k_as_invert)
   float* as_rsc = nullptr;       // [cluster][kAsRS]: the segment rows' scales
   double* as_w = nullptr;        // 6N: the vector the next apply reads (w of the iteration, r0, ...)
+  // one launch per iteration (k_as_iter, as_one): the per-subdomain tables, ghost (w, z) of the ring rows, the parity's
+  // contributions y_c = Z_c w[D_c] and the subdomain-ordered inverse rows, in ONE buffer (offsets: AsTab)
+  int32_t as_one = 0, as_tab_cap = 0;
+  char* as_tab = nullptr;
+  int32_t *as_mem = nullptr, *as_memn = nullptr;   // per row: its subdomain memberships (c·kAsD + 6·l, <= 1 + kAsX)
   double* scal = nullptr;
   int32_t* flags = nullptr;
   // DeformNet.arap mode with lambda_flow = 0: rows of each multi-node connected graph component
@@ -186,6 +196,37 @@ struct GnDev {
   int64_t n_iter_launches = 0;
 };
 static_assert(std::is_trivially_copyable<GnDev>::value, "kernel argument");
+
+// The as_tab buffer (k_as_iter), for a capacity of cap clusters: region by region, [cluster][...] each (16-B aligned)
+//   blk  [kGB]  int2  the subdomain rows' blocks in row order (CSR order within a row): (A slot, S2 index << 5 | row)
+//   con  [kGS]  int4  per S2 node the y indices (c'·kAsD + 6·l') of the subdomains holding it, ascending, -1 after
+//   s2n  [kGS]  int   S2 node -> row (the first iteration gathers m from the warm start's m0)
+//   row  [kGRow] int  row starts [0, kAsDN], then nd at 25, nb at 26, ns at 27; S2 index of each subdomain row at 32 + l,
+//                     its node (row) at 64 + l
+//   dsc  [kAsD] f32   the inverse's scales d = √diag Z (k_as_invert)
+//   gh   [kAsRing·6] double2  ghost (w, z) of the ring rows (the owners' recurrences, repeated bit for bit)
+//   y    [2][cap][kAsD] f64  per parity the contributions y_c = D Ẑ D w[D_c]
+//   slab [kAsK][kAsD] uint4  Ẑ's rows (8 fp16 per word), word k of every row contiguous
+struct AsTabP {
+  int2* blk; int4* con; int32_t* s2n; int32_t* row; float* dsc; double2* gh; double* y; uint4* slab;
+};
+__host__ __device__ __forceinline__ AsTabP as_tab_at(char* base, int64_t cap) {
+  AsTabP p;
+  char* q = base;
+  p.blk = reinterpret_cast<int2*>(q); q += cap * kGB * 8;
+  p.con = reinterpret_cast<int4*>(q); q += cap * kGS * 16;
+  p.s2n = reinterpret_cast<int32_t*>(q); q += cap * kGS * 4;
+  p.row = reinterpret_cast<int32_t*>(q); q += cap * kGRow * 4;
+  p.dsc = reinterpret_cast<float*>(q); q += cap * kAsD * 4;
+  p.gh = reinterpret_cast<double2*>(q); q += cap * kAsRing * 6 * 16;
+  p.y = reinterpret_cast<double*>(q); q += 2 * cap * kAsD * 8;
+  p.slab = reinterpret_cast<uint4*>(q);
+  return p;
+}
+static inline int64_t as_tab_bytes(int64_t cap) {
+  return cap * ((int64_t)kGB * 8 + (int64_t)kGS * 16 + (int64_t)kGS * 4 + kGRow * 4 + kAsD * 4 + kAsRing * 6 * 16 +
+                2 * kAsD * 8 + (int64_t)kAsK * kAsD * 16);
+}
 
 // The solver handle: the kernel-visible state plus host-only members.
 struct Gn : GnDev {
@@ -1649,6 +1690,108 @@ __global__ __launch_bounds__(256) void k_as_segments(GnDev g) {
   if (lane < kAsSrc) g.as_src[cp * kAsSrc + lane] = lane < nsrc ? s_src[lane] : 0;
 }
 
+// ---- tables of the one-launch iteration (k_as_iter; setup, per pattern)
+// every row's subdomain memberships as y indices c·kAsD + 6·l (its own subdomain + <= kAsX rings; as_memn zeroed first)
+__global__ __launch_bounds__(256) void k_as_members(GnDev g, int ncl) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ncl * kAsDN) return;
+  const int c = i / kAsDN, l = i % kAsDN;
+  const int u = g.as_dom[i];
+  if (u < 0) return;
+  const int pos = atomicAdd(g.as_memn + u, 1);
+  if (pos < 1 + kAsX) g.as_mem[4 * (int64_t)u + pos] = c * kAsD + 6 * l;
+}
+
+// per subdomain c (one workgroup): its rows' blocks in row order, the distinct columns S2 (ascending) with each block's
+// S2 index, per S2 node its memberships ascending (the order the apply sums a row's segments in), the row starts and
+// every subdomain row's S2 index (its diagonal block's column)
+__global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
+  __shared__ int s_dom[kAsDN], s_rs[kAsDN + 1];
+  __shared__ int s_col[kGB], s_slot[kGB], s_l[kGB], s_first[kGB], s_rank[kGB];
+  __shared__ int s_ns;
+  const int c = blockIdx.x, t = threadIdx.x;
+  const AsTabP tp = as_tab_at(g.as_tab, g.as_tab_cap);
+  if (t < kAsDN) s_dom[t] = g.as_dom[c * kAsDN + t];
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0, l = 0;
+    for (; l < kAsDN && s_dom[l] >= 0; ++l) {
+      s_rs[l] = acc;
+      acc += g.row_ptr[s_dom[l] + 1] - g.row_ptr[s_dom[l]];
+    }
+    for (; l <= kAsDN; ++l) s_rs[l] = acc;
+  }
+  __syncthreads();
+  int nd = 0;
+  while (nd < kAsDN && s_dom[nd] >= 0) ++nd;
+  const int nb = s_rs[kAsDN];   // (<= kAsDN·kRowMax <= kGB: the Schwarz form needs rows of <= kRowMax blocks)
+  for (int i = t; i < kGB; i += 256) {
+    if (i < nb) {
+      int l = 0;
+      while (l + 1 < nd && s_rs[l + 1] <= i) ++l;
+      const int b = g.row_ptr[s_dom[l]] + (i - s_rs[l]);
+      s_col[i] = g.col[b]; s_slot[i] = b; s_l[i] = l;
+    } else {
+      s_col[i] = 0x7FFFFFFF; s_slot[i] = 0; s_l[i] = 0;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < nb; i += 256) {
+    bool f = true;
+    for (int j = 0; j < i && f; ++j) f = s_col[j] != s_col[i];
+    s_first[i] = f ? 1 : 0;
+  }
+  __syncthreads();
+  for (int i = t; i < nb; i += 256) {
+    int rk = 0;
+    for (int j = 0; j < nb; ++j) rk += (s_first[j] && s_col[j] < s_col[i]) ? 1 : 0;
+    s_rank[i] = rk;
+  }
+  if (t == 0) {
+    int n = 0;
+    for (int j = 0; j < nb; ++j) n += s_first[j];
+    s_ns = n;
+  }
+  __syncthreads();
+  const int ns = s_ns;
+  // entries past nb / ns repeat the last valid one: k_as_iter's idle lanes load unconditionally, and a common padding
+  // address (block 0, y[0]) would be one L2 channel hit by every workgroup
+  for (int i = t; i < kGB; i += 256) {
+    const int j = i < nb ? i : nb - 1;
+    tp.blk[(int64_t)c * kGB + i] = make_int2(s_slot[j], (s_rank[j] << 5) | s_l[j]);
+  }
+  __syncthreads();
+  for (int i = t; i < nb; i += 256) {
+    if (!s_first[i]) continue;
+    const int u = s_col[i], k = s_rank[i];
+    const int n = min(g.as_memn[u], 1 + kAsX);
+    int m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m[j] = j < n ? g.as_mem[4 * (int64_t)u + j] : 0x7FFFFFFF;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)   // ascending (the y index grows with the subdomain)
+#pragma unroll
+      for (int b = 0; b < 3 - a; ++b)
+        if (m[b] > m[b + 1]) { const int x = m[b]; m[b] = m[b + 1]; m[b + 1] = x; }
+    const int4 e = make_int4(m[0] == 0x7FFFFFFF ? -1 : m[0], m[1] == 0x7FFFFFFF ? -1 : m[1],
+                             m[2] == 0x7FFFFFFF ? -1 : m[2], m[3] == 0x7FFFFFFF ? -1 : m[3]);
+    tp.con[(int64_t)c * kGS + k] = e;
+    tp.s2n[(int64_t)c * kGS + k] = u;
+    if (k == ns - 1)   // (the padding past ns: copies of the last node's entries)
+      for (int kk = ns; kk < kGS; ++kk) { tp.con[(int64_t)c * kGS + kk] = e; tp.s2n[(int64_t)c * kGS + kk] = u; }
+  }
+  int32_t* rt = tp.row + (int64_t)c * kGRow;
+  if (t <= kAsDN) rt[t] = s_rs[t];
+  if (t == 0) { rt[25] = nd; rt[26] = nb; rt[27] = ns; }
+  if (t < kAsDN) {   // the subdomain row's S2 index: the rank of its own column (the diagonal block)
+    int rk = 0;
+    if (t < nd)
+      for (int j = 0; j < nb; ++j) rk += (s_first[j] && s_col[j] < s_dom[t]) ? 1 : 0;
+    rt[32 + t] = rk;
+    rt[64 + t] = t < nd ? s_dom[t] : 0;
+  }
+}
+
 // Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= kAsD x kAsD, f64, kAsTi x kAsTi
 // entries per thread in registers: rows tr + 16a, columns tc + 16b), its in-place block Gauss-Jordan inverse (SPD: no pivoting;
 // 2x2 pivot blocks through LDS, double-buffered: one barrier per two steps), scaled and rounded to fp16 with a certified
@@ -1822,6 +1965,7 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
     for (int a = 0; a < kAsTi; ++a) {
       const int R = tr + 16 * a;
       if (R < kAsD) g.as_dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
+      if (R < kAsD && g.as_one) as_tab_at(g.as_tab, g.as_tab_cap).dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
       if (R < n) g.as_rsc[s_dst[R]] = (float)dr[a];
     }
   __syncthreads();
@@ -1831,6 +1975,13 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
     const int d = s_dst[R], cp = d / kAsRS, rs = d % kAsRS;
     reinterpret_cast<uint4*>(g.as_slab)[((int64_t)cp * kAsK + k) * kAsRS + rs] =
         reinterpret_cast<const uint4*>(s_z + R * kAsD)[k];
+  }
+  if (g.as_one) {   // k_as_iter's subdomain-ordered copy: word k of row R at slab[(c·kAsK + k)·kAsD + R] (rows fastest)
+    uint4* sl = as_tab_at(g.as_tab, g.as_tab_cap).slab + (int64_t)c * kAsK * kAsD;
+    for (int i = t; i < n * kAsK; i += 256) {
+      const int k = i / n, R = i - k * n;
+      sl[(int64_t)k * kAsD + R] = reinterpret_cast<const uint4*>(s_z + R * kAsD)[k];
+    }
   }
   if (t < kCS) g.racc[c * kCS + t] = 0.0;
   OFX_AS_STAMP(5)
@@ -3015,6 +3166,349 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
   OFX_STAMP(7)
 }
 
+// One launch per Schwarz PCG iteration (round 6; OFX_AS_ONE=0 restores k_pcg_iter<.., kAS> + k_as_apply).
+// The two-launch form needs two exchanges per iteration — the SpMV n = A m reads m on the neighbours' rows, the apply
+// m = M⁻¹ w reads w on the subdomains' rings — and a kernel boundary for each. Here workgroup c works on its whole
+// subdomain D_c (own 8 rows + ring): it keeps ghost copies of the ring rows' recurrence vectors (w, z), forms n = A m on
+// all of D_c's rows (3x the SpMV rows) and the ring rows' z, w updates exactly as their owners do (the same blocks, the
+// same m bits, the same operations: bit-identical copies), and applies its own subdomain inverse, y_c = D Ẑ D w[D_c]. The
+// next launch sums m on the columns it needs from the <= 1 + kAsX contributions per node in ascending subdomain order —
+// the order in which k_as_apply sums a row's segments, each contribution being that segment's value — so the iterates are
+// bitwise those of the two-launch form. One exchange per iteration: one kernel boundary.
+// Roles (1024 threads): waves 0-7 one block of D_c's rows each (the A block and the product); waves 8-12 one S2 node each
+// (its contributions summed into m; a second pass past 320 nodes) and one inverse row half each (the dot product, as
+// k_as_apply's two lanes); waves 13-15 the rows: 13 the own rows (k_pcg_iter's wave: scalars, stop, recurrences,
+// partials, the converging launch's GN step), 14-15 the ring rows (ghost z, w). Trip 1: the stop word, tables, state,
+// partials, inverse rows; trip 2: the A blocks and the contributions. Three barriers (m, products, the w image).
+template <bool kFirst, int kU>
+__global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, const double* Pc, const double* st,
+                                                      const double* sc, const char* tab, const PcgIt* gp, int cap, int ep,
+                                                      int gn_iter) {
+  const PcgIt& g = *gp;
+  constexpr int kNs = 128 * kU;
+  constexpr int kS2W = 5 * 64;   // S2 nodes per pass (waves 8-12)
+  __shared__ __attribute__((aligned(16))) double s_m[kGS * 6];
+  __shared__ __attribute__((aligned(16))) double s_prod[(kGB + kRowMax) * 6];
+  __shared__ __attribute__((aligned(16))) double s_w[kAsD];
+  __shared__ int s_leave;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);   // (uniform: the roles below are scalar branches)
+  const int c = blockIdx.x;
+  const AsTabP tp = as_tab_at(const_cast<char*>(tab), cap);
+  const int par_ = (int)((reinterpret_cast<uintptr_t>(sc) >> 3) & 1);
+  const double* scb = sc - par_;
+  const int32_t* rt = tp.row + (int64_t)c * kGRow;
+  const double* yr = tp.y + (int64_t)par_ * cap * kAsD;   // the previous launch's contributions
+  // Each role issues trip 1 (the stop word first), tests the stop word (drained launches end there, before any
+  // barrier), issues trip 2, and meets the others at three barriers: (1) m on S2 + the stop decision, (2) the block
+  // products, (3) the w image. Loads are unconditional (clamped), the roles' data live only inside their branch.
+  if (wave < 8) {   // ---------------- blocks
+    int stop_ep = stopw[(int64_t)c * 64 + lane];
+    const int2 be = tp.blk[(int64_t)c * kGB + t];
+    const int nb = rt[26];
+    asm volatile("" ::: "memory");
+    stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
+    if (stop_ep != 0) return;
+    typedef double gd2 __attribute__((ext_vector_type(2)));
+    const __attribute__((address_space(1))) gd2* b = reinterpret_cast<const __attribute__((address_space(1))) gd2*>(
+        reinterpret_cast<uint64_t>(g.Aop)) + 18 * (int64_t)be.x;
+    const bool any = t - lane < nb;   // (wave-uniform: waves past the subdomain's blocks load nothing)
+    double2 ab[18];
+    if (any)
+#pragma unroll
+      for (int k = 0; k < 18; ++k) { const gd2 x = b[k]; ab[k] = make_double2(x.x, x.y); }
+    __syncthreads();   // (1)
+    if (s_leave) return;
+    if (any && t < nb) {   // k_pcg_iter's operation order
+      const int k = be.y >> 5;
+      double x[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) x[j] = s_m[6 * k + j];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double2 b01 = ab[3 * i], b23 = ab[3 * i + 1], b45 = ab[3 * i + 2];
+        s_prod[t * 6 + i] =
+            fma(b45.y, x[5], fma(b45.x, x[4], fma(b23.y, x[3], fma(b23.x, x[2], fma(b01.y, x[1], b01.x * x[0])))));
+      }
+    }
+    __syncthreads();   // (2)
+    __syncthreads();   // (3)
+    return;
+  }
+  if (wave < 13) {  // ---------------- S2 nodes (m) and inverse rows (y)
+    const int ts = t - kGB;
+    int stop_ep = stopw[(int64_t)c * 64 + lane];
+    const int k2 = ts < kGS ? ts : kGS - 1;
+    int4 cn = make_int4(-1, -1, -1, -1);
+    int s2u = 0;
+    if (kFirst) s2u = tp.s2n[(int64_t)c * kGS + k2];
+    else cn = tp.con[(int64_t)c * kGS + k2];
+    const int nd = rt[25], ns = rt[27];
+    const int ry = min(ts >> 1, kAsD - 1), hl = ts & 1;
+    uint4 z[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) z[k] = tp.slab[((int64_t)c * kAsK + 9 * hl + k) * kAsD + ry];
+    const float dsc_r = tp.dsc[(int64_t)c * kAsD + ry];
+    asm volatile("" ::: "memory");
+    stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
+    if (stop_ep != 0) return;
+    const double* m0 = kFirst ? reinterpret_cast<const double*>(reinterpret_cast<const uint64_t*>(scb)[kScM]) : nullptr;
+    // m on S2: 0 + the contributions in ascending subdomain order (k_as_apply's sum of a row's segments, each
+    // contribution being that segment's value); the first iteration reads the warm start's m0
+    auto gather = [&](int4 e4, int u, double mv[6]) {
+      double2 cz[4][3];
+      if (kFirst) {
+        const double2* p = reinterpret_cast<const double2*>(m0 + 6 * (int64_t)u);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cz[0][k] = p[k];
+      } else {
+        const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // (an absent one re-reads the first: no extra lines)
+          const double2* p = reinterpret_cast<const double2*>(yr + (e[j] >= 0 ? e[j] : e[0]));
+#pragma unroll
+          for (int k = 0; k < 3; ++k) cz[j][k] = p[k];
+        }
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        if (kFirst) {
+          mv[2 * k] = cz[0][k].x; mv[2 * k + 1] = cz[0][k].y;
+        } else {
+          const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+          double mx = 0.0, my = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { mx += e[j] >= 0 ? cz[j][k].x : 0.0; my += e[j] >= 0 ? cz[j][k].y : 0.0; }
+          mv[2 * k] = mx; mv[2 * k + 1] = my;
+        }
+      }
+    };
+    if (ts - lane < ns) {   // (wave-uniform: waves past the S2 nodes gather nothing)
+      double mv[6];
+      gather(cn, s2u, mv);
+      if (ts < ns)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) s_m[6 * ts + j] = mv[j];
+    }
+    if (ns > kS2W)   // (rare: more than 320 distinct columns) further passes, one more trip each
+      for (int kk = ts + kS2W; kk < ns; kk += kS2W) {
+        double mv[6];
+        gather(kFirst ? make_int4(-1, -1, -1, -1) : tp.con[(int64_t)c * kGS + kk],
+               kFirst ? tp.s2n[(int64_t)c * kGS + kk] : 0, mv);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) s_m[6 * kk + j] = mv[j];
+      }
+    __syncthreads();   // (1)
+    if (s_leave) return;
+    __syncthreads();   // (2)
+    __syncthreads();   // (3)
+    // y_c = D Ẑ (D w): k_as_apply's segment dot (two lanes, four chains, the pair summed by DPP) times the row scale
+    const double2* w2p = reinterpret_cast<const double2*>(s_w);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    auto lo = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); };
+    auto hi = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); };
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int kw = 9 * hl + k;
+      const double2 p0 = w2p[4 * kw], p1 = w2p[4 * kw + 1], p2 = w2p[4 * kw + 2], p3 = w2p[4 * kw + 3];
+      a0 = fma(lo(z[k].x), p0.x, a0);
+      a1 = fma(hi(z[k].x), p0.y, a1);
+      a2 = fma(lo(z[k].y), p1.x, a2);
+      a3 = fma(hi(z[k].y), p1.y, a3);
+      a0 = fma(lo(z[k].z), p2.x, a0);
+      a1 = fma(hi(z[k].z), p2.y, a1);
+      a2 = fma(lo(z[k].w), p3.x, a2);
+      a3 = fma(hi(z[k].w), p3.y, a3);
+    }
+    double dot = (a0 + a1) + (a2 + a3);
+    dot += dpp_mov<0xB1>(dot);   // quad_perm [1, 0, 3, 2]: the row's two halves
+    if (hl == 0 && ts < 2 * kAsD && (ts >> 1) < 6 * nd)
+      tp.y[(int64_t)(par_ ^ 1) * cap * kAsD + (int64_t)c * kAsD + (ts >> 1)] = (double)dsc_r * dot;
+    return;
+  }
+  // ---------------- rows: wave 13 the own rows (k_pcg_iter's wave), 14-15 the ring rows (ghost z, w)
+  const int jr = wave - 13, r = lane >> 3, q = lane & 7;
+  const bool own = q < 6;
+  const int qc = own ? q : 5;
+  const int l = 8 * jr + r;                       // subdomain row
+  const int row = c * kCS + r;                    // (own rows)
+  const int64_t o = 6 * (int64_t)row + qc;
+  int stop_ep = stopw[(int64_t)c * 64 + lane];
+  double2 tpp[kPcgStreams][kU];
+#pragma unroll
+  for (int k = 0; k < kPcgStreams; ++k)
+#pragma unroll
+    for (int u = 0; u < kU; ++u) tpp[k][u] = *reinterpret_cast<const double2*>(Pc + k * kNs + 2 * (lane + 64 * u));
+  double own_p[kPcgStreams];
+#pragma unroll
+  for (int k = 0; k < kPcgStreams; ++k) own_p[k] = Pc[k * kNs + c];
+  const int cnt = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
+  const double2 ra = *reinterpret_cast<const double2*>(scb + kScAlpha + 2);
+  const double2 rtb = *reinterpret_cast<const double2*>(scb + kScAlpha + 4);
+  const double2 rg = *reinterpret_cast<const double2*>(scb + kScGamma + 2);
+  const double2 sd = reinterpret_cast<const double2*>(scb + kScSturm)[lane];
+  const double bb_stored = scb[kScScal + S_BB];
+  const double th_prev = scb[kScScal + S_TH_PREV];
+  const double2 tols = *reinterpret_cast<const double2*>(scb + kScTol);
+  const int nd = rt[25];
+  const int rs = rt[l], re = rt[l + 1], rk = rt[32 + l];
+  const float dsc_l = tp.dsc[(int64_t)c * kAsD + 6 * l + qc];
+  double v[V_N];
+  double wg = 0.0, zg = 0.0;
+  const int gi = (c * kAsRing + (l >= kCS ? l - kCS : 0)) * 6 + qc;
+  if (jr == 0) {
+    load_rec(st, o, v);
+  } else if (kFirst) {   // the owners' w0 from as_w (k_pcg_w0), z0 = +0 (their records hold +0 there). Not their state
+    // records: the owners rewrite those in this very launch, and with more workgroups than CUs a later workgroup would
+    // read the new values
+    const double* w0v = reinterpret_cast<const double*>(reinterpret_cast<const uint64_t*>(scb)[kScMcl]);
+    wg = w0v[6 * (int64_t)rt[64 + l] + qc];
+    zg = 0.0;
+  } else {
+    const double2 gz = tp.gh[gi];
+    wg = gz.x;
+    zg = gz.y;
+  }
+  asm volatile("" ::: "memory");
+  stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
+  if (stop_ep != 0) return;
+  double tb[kFirst ? 2 * kU : 1];
+  if (kFirst) {   // the first iteration's |b|² partials
+    const __attribute__((address_space(1))) double* pb =
+        reinterpret_cast<const __attribute__((address_space(1))) double*>(reinterpret_cast<uint64_t>(g.part_b));
+#pragma unroll
+    for (int u = 0; u < 2 * kU; ++u) tb[u] = pb[lane + 64 * u];
+  }
+  // ---- scalars (every row wave derives the same bits from the partials), the stop decision (k_pcg_iter's)
+  const double tol = tols.x, etol = tols.y;
+  const double rgam_prev = kFirst ? 1.0 : ((par_ ^ 1) ? rg.y : rg.x);
+  const double ralpha_prev = kFirst ? 1.0 : ((par_ ^ 1) ? ra.y : ra.x);
+  const double thr_prev = kFirst ? 0.0 : ((par_ ^ 1) ? rtb.y : rtb.x);
+  double pa[kPcgStreams];
+#pragma unroll
+  for (int k = 0; k < kPcgStreams; ++k) {
+    double tt = 0.0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) tt += tpp[k][u].x + tpp[k][u].y;
+    pa[k] = wave_sum(tt);
+  }
+  double bb = bb_stored;
+  if (kFirst) {
+    double tt = 0.0;
+#pragma unroll
+    for (int u = 0; u < 2 * kU; ++u) tt += tb[u];
+    bb = wave_sum(tt);
+  }
+  const double gam = pa[0], del = pa[1], rr = pa[2], pp = pa[3];
+  const bool lead = c == 0 && jr == 0 && lane == 0;
+  double beta = 0.0, alpha;
+  if (kFirst) {
+    alpha = div_nr(gam, del);
+  } else {
+    beta = gam * rgam_prev;
+    alpha = div_nr(gam, del - beta * gam * ralpha_prev);
+  }
+  const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam * pp * rgam_prev <= thr_prev * ralpha_prev)) ||
+                    gam == 0.0 || rr <= 1e-24 * bb;
+  int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
+  leave = __builtin_amdgcn_readfirstlane(leave);
+  if (jr == 0 && lane == 0) s_leave = leave;
+  __syncthreads();   // (1)
+  if (leave) {       // converged, or breakdown (A SPD => alpha > 0): keep x (k_pcg_iter's leave path)
+    if (jr != 0) return;
+    const bool ill = !conv && !isfinite(alpha);
+    if (kFirst && lead) const_cast<double*>(scb)[kScScal + S_BB] = bb;
+    double* Pn = const_cast<double*>(Pc) + (par_ ? -kPcgStreams : kPcgStreams) * (int64_t)kNs;
+    if (lane == 0) {
+      Pn[c] = own_p[0]; Pn[kNs + c] = own_p[1]; Pn[2 * kNs + c] = conv ? own_p[2] : 0.0; Pn[3 * kNs + c] = own_p[3];
+    }
+    const_cast<int32_t*>(stopw)[(int64_t)c * 64 + lane] = ep;
+    if (g.fuse && !g.flags[F_STOPPED]) fused_step(g, ep, gn_iter, c, lane, r, q, own, o, row, v[V_X], ill, cnt, bb);
+    if (lead && !g.flags[F_DONE] && !g.flags[F_STOPPED]) {
+      g.flags[F_DONE] = 1; g.flags[F_PCG_IT] = cnt; g.flags[F_PCG_TOTAL] += cnt;
+      if (ill) g.flags[F_ILL] = 1;
+      host_flag(g.hflags, H_PCG_IT, cnt);
+      __hip_atomic_store(g.hflags + H_DONE, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
+  // the lead wave's Ritz bracket (k_pcg_iter's Sturm step) and the error-stop threshold τ²·min(θ̂, θ̂_prev)
+  double2 sd_new = sd;
+  double thr_new = 0.0, th_cur = 1e300;
+  auto shift = [](int s) {
+    const int e = s < 40 ? s : 2 * s - 40;
+    const int k = e & 3;
+    const double cc = k == 0 ? 1.0 : k == 1 ? 0.84089641525371454303 : k == 2 ? 0.70710678118654752440
+                                                                             : 0.59460355750136053336;
+    return ldexp(cc, -(e >> 2));
+  };
+  if (c == 0 && jr == 0 && etol > 0.0) {
+    const double rca = 1.0 / alpha;
+    const double diag = kFirst ? rca : rca + beta * ralpha_prev;
+    const double e2 = kFirst ? 0.0 : beta * ralpha_prev * ralpha_prev;
+    const double sig = shift(lane);
+    double dd = (diag - sig) - (kFirst ? 0.0 : e2 / sd.x);
+    if (fabs(dd) < 1e-300) dd = -1e-300;
+    const double cc = (kFirst ? 0.0 : sd.y) + (dd < 0.0 ? 1.0 : 0.0);
+    sd_new = make_double2(dd, cc);
+    const uint64_t free_ = __ballot(cc == 0.0);
+    const double th = free_ ? shift(__ffsll((unsigned long long)free_) - 1) : 0.0;
+    th_cur = th;
+    const double tu = fmin(th, th_prev);
+    thr_new = (etol * etol) * tu;
+  }
+  __syncthreads();   // (2)
+  // n on the subdomain row: its blocks in CSR order (k_pcg_iter's row sum)
+  const int rlen = l < nd ? re - rs : 0;
+  const double* sp = s_prod + rs * 6 + qc;
+  double tv[kRowMax];
+#pragma unroll
+  for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+  __builtin_amdgcn_sched_barrier(0);
+  double nc = 0.0;
+#pragma unroll
+  for (int k = 0; k < kRowMax; ++k) nc += k < rlen ? tv[k] : 0.0;
+  double d[kPcgStreams] = {0.0, 0.0, 0.0, 0.0};
+  double w2;
+  if (jr == 0) {
+    const double m = s_m[6 * rk + qc];
+    const double zz = fma(beta, v[V_Z], nc);
+    const double qq = fma(beta, v[V_Q], m);
+    const double sv = fma(beta, v[V_S], v[V_W]);
+    const double p = fma(beta, v[V_P], v[V_U]);
+    const double rn = fma(-alpha, sv, v[V_R]);
+    const double un = fma(-alpha, qq, v[V_U]);
+    w2 = fma(-alpha, zz, v[V_W]);
+    if (own) {
+      const double nv[V_N] = {fma(alpha, p, v[V_X]), rn, un, zz, qq, sv, p, w2};
+      store_rec(const_cast<double*>(st), o, nv);
+      d[0] = rn * un; d[1] = w2 * un; d[2] = rn * rn; d[3] = p * p;
+    }
+  } else {
+    const double zz = fma(beta, zg, nc);
+    w2 = fma(-alpha, zz, wg);
+    if (own && l < nd) tp.gh[gi] = make_double2(w2, zz);
+  }
+  if (own) s_w[6 * l + q] = l < nd ? w2 * (double)dsc_l : 0.0;
+  __syncthreads();   // (3)
+  if (jr != 0) return;
+  // ---- the own rows' partials of the next launch, the lead's scalars
+  double* Pn = const_cast<double*>(Pc) + (par_ ? -kPcgStreams : kPcgStreams) * (int64_t)kNs;
+#pragma unroll
+  for (int k = 0; k < kPcgStreams; ++k) d[k] = wave_sum(d[k]);
+  if (lane == 0) { Pn[c] = d[0]; Pn[kNs + c] = d[1]; Pn[2 * kNs + c] = d[2]; Pn[3 * kNs + c] = d[3]; }
+  double* sc_w = const_cast<double*>(scb);
+  int32_t* flags_w = reinterpret_cast<int32_t*>(sc_w + kScFlags);
+  if (lead) {
+    sc_w[kScAlpha + 2 + par_] = 1.0 / alpha; sc_w[kScGamma + 2 + par_] = 1.0 / gam; flags_w[F_PCG_CNT] = cnt + 1;
+    sc_w[kScAlpha + 4 + par_] = thr_new;
+    if (etol > 0.0) sc_w[kScScal + S_TH_CUR] = th_cur;
+  }
+  if (c == 0 && etol > 0.0) reinterpret_cast<double2*>(sc_w + kScSturm)[lane] = sd_new;
+  if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
+}
+
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
 // if accepted, the kornia 0.7.0 angle_axis_to_rotation_matrix + left-multiplicative update
 // (model.py:744-748) — one launch. Every workgroup derives the same decision from read-only inputs
@@ -3151,7 +3645,7 @@ static void free_all(Gn* g) {
                   g->part_p, g->part_b, g->part_loss,
                   g->loss_log, g->stat, g->step_state, g->xh, g->th, g->step_args, g->d_gnodes, g->d_gedges, g->d_gdiff, g->perm, g->iperm, g->comp_rows, g->comp_off,
                   g->up_of, g->up_slot, g->up_tr, g->as_cand, g->as_csc, g->as_acc, g->as_dom, g->as_meta, g->as_gat,
-                  g->as_dst, g->as_slab, g->as_w, g->as_src, g->as_dsc, g->as_rsc};
+                  g->as_dst, g->as_slab, g->as_w, g->as_src, g->as_dsc, g->as_rsc, g->as_tab, g->as_mem, g->as_memn};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (g->host_flags) (void)hipHostFree(g->host_flags);
@@ -3360,6 +3854,20 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     default: pcg_pick<17>(wave, w2, as, iter0, iter); break;
   }
   const dim3 block_it(w2 ? 128 : 64);
+  // one launch per Schwarz iteration (k_as_iter; the setup built its tables)
+  using AsIterKernel = void (*)(const int32_t*, const double*, const double*, const double*, const char*, const PcgIt*,
+                                int, int, int);
+  const bool one = as && g->as_one;
+  AsIterKernel one0 = nullptr, one1 = nullptr;
+  if (one) {
+    switch (g->pcg_ku) {
+      case 2: one0 = k_as_iter<true, 2>; one1 = k_as_iter<false, 2>; break;
+      case 3: one0 = k_as_iter<true, 3>; one1 = k_as_iter<false, 3>; break;
+      case 4: one0 = k_as_iter<true, 4>; one1 = k_as_iter<false, 4>; break;
+      case 8: one0 = k_as_iter<true, 8>; one1 = k_as_iter<false, 8>; break;
+      default: one0 = k_as_iter<true, 17>; one1 = k_as_iter<false, 17>; break;
+    }
+  }
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
   // spins on it, so the next GN step is enqueued while the chunk's remaining (no-op) launches drain.
   // The chunk event only tells "all launched iterations ran without converging" -> launch more. (Measured
@@ -3409,13 +3917,22 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (it == 0 && gn_iter > 0 && g->t_seen.time_since_epoch().count())
       g->prologue_us += std::chrono::duration<double, std::micro>(h0 - g->t_seen).count();
 #endif
-    for (int k = 0; k < n; ++k, ++it) {
-      const int par = it & 1;
-      hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, (const int2*)g->wl, (const int32_t*)g->stopw,
-                         (const double*)(g->part_p + kPcgStreams * (int64_t)g->nw_pad * par), (const double*)g->st,
-                         (const double*)(par ? g->m1 : g->m0), (const double*)g->pcs + par, gp, par, g->ep,
-                         gn_iter);
-      if (as) as_apply(true, g->as_w, par ? g->m0 : g->m1);   // m of the next iteration = M⁻¹ w_new
+    if (one) {   // one launch per iteration (k_as_iter)
+      for (int k = 0; k < n; ++k, ++it) {
+        const int par = it & 1;
+        hipLaunchKernelGGL(it == 0 ? one0 : one1, dim3(ncl), dim3(kAsIterT), 0, hs, (const int32_t*)g->stopw,
+                           (const double*)(g->part_p + kPcgStreams * (int64_t)g->nw_pad * par), (const double*)g->st,
+                           (const double*)g->pcs + par, (const char*)g->as_tab, gp, g->as_tab_cap, g->ep, gn_iter);
+      }
+    } else {
+      for (int k = 0; k < n; ++k, ++it) {
+        const int par = it & 1;
+        hipLaunchKernelGGL(it == 0 ? iter0 : iter, grid, block_it, 0, hs, (const int2*)g->wl, (const int32_t*)g->stopw,
+                           (const double*)(g->part_p + kPcgStreams * (int64_t)g->nw_pad * par), (const double*)g->st,
+                           (const double*)(par ? g->m1 : g->m0), (const double*)g->pcs + par, gp, par, g->ep,
+                           gn_iter);
+        if (as) as_apply(true, g->as_w, par ? g->m0 : g->m1);   // m of the next iteration = M⁻¹ w_new
+      }
     }
 #ifdef OFX_STAMPS
     g->host_enqueue_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
@@ -3448,7 +3965,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     (void)ran;   // the chunk ran out without convergence: next chunk
     chunk = topup;
   }
-  g->n_iter_launches += as ? 2 * it : it;   // (Schwarz: each iteration is two launches)
+  g->n_iter_launches += (as && !one) ? 2 * it : it;   // (two-launch Schwarz: each iteration is two launches)
   if (g->timing) g->ev.emplace_back(e0, e1);
 #ifdef OFX_STAMPS
   if (getenv("OFX_GAP_EVENTS")) {
@@ -3646,9 +4163,10 @@ int ofx_gn_precond_info(void* handle, int64_t* info) {
   Gn* g = (Gn*)handle;
   if (g) prep_wait(g);
   OFX_CHECK_ARG(g && info, "null handle/info");
-  for (int k = 0; k < 7; ++k) info[k] = 0;
+  for (int k = 0; k < 8; ++k) info[k] = 0;
   info[0] = g->as_on;
   info[6] = kAsD;
+  info[7] = (g->as_on && !g->as_one) ? 2 : 1;
   if (!g->as_on) return OFX_OK;
   const int ncl = g->N / kCS;
   const int sd = sync_side(g);
@@ -4142,12 +4660,28 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
       OFX_HIP(hipMalloc((void**)&g->as_rsc, (size_t)cap * kAsRS * sizeof(float)));
       OFX_HIP(hipMemsetAsync(g->as_rsc, 0, (size_t)cap * kAsRS * sizeof(float), hs));
       OFX_HIP(hipMemsetAsync(g->as_slab, 0, (size_t)cap * kAsK * kAsRS * 8 * sizeof(uint16_t), hs));
+      if (g->as_tab) OFX_HIP(hipFree(g->as_tab));
+      if (g->as_mem) OFX_HIP(hipFree(g->as_mem));
+      if (g->as_memn) OFX_HIP(hipFree(g->as_memn));
+      OFX_HIP(hipMalloc((void**)&g->as_tab, (size_t)as_tab_bytes(cap)));
+      OFX_HIP(hipMemsetAsync(g->as_tab, 0, (size_t)as_tab_bytes(cap), hs));
+      OFX_HIP(hipMalloc((void**)&g->as_mem, (size_t)g->max_pad * 4 * sizeof(int32_t)));
+      OFX_HIP(hipMalloc((void**)&g->as_memn, (size_t)g->max_pad * sizeof(int32_t)));
       g->as_cap = cap;
+      g->as_tab_cap = cap;
     }
     hipLaunchKernelGGL(k_as_choose, dim3(ncl), dim3(256), 0, hs, *g);
     hipLaunchKernelGGL(k_as_accept, dim3(grid_for(N, 4)), dim3(256), 0, hs, *g);
     hipLaunchKernelGGL(k_as_compact, dim3(ncl), dim3(64), 0, hs, *g);
     hipLaunchKernelGGL(k_as_segments, dim3(ncl), dim3(256), 0, hs, *g);
+    // one launch per iteration (k_as_iter) unless OFX_AS_ONE=0 (A/B: k_pcg_iter<.., kAS> + k_as_apply, bitwise the same)
+    const char* one = getenv("OFX_AS_ONE");
+    g->as_one = ((one && atoi(one) == 0) || g->pcg_ku > 4) ? 0 : 1;   // (kU > 4: its partial registers spill)
+    if (g->as_one) {
+      OFX_HIP(hipMemsetAsync(g->as_memn, 0, (size_t)N * sizeof(int32_t), hs));
+      hipLaunchKernelGGL(k_as_members, dim3(grid_for((int64_t)ncl * kAsDN, 256)), dim3(256), 0, hs, *g, ncl);
+      hipLaunchKernelGGL(k_as_tab, dim3(ncl), dim3(256), 0, hs, *g);
+    }
     OFX_LAUNCH_CHECK();
     g->as_on = 1;
   }

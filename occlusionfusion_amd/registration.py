@@ -119,12 +119,13 @@ class GaussNewtonSolver:
         return list(arr)
 
     def precond_info(self):
-        """The last setup's preconditioner: dict(schwarz, clusters, segments, sources, gathered_rows, subdomain_rows)
+        """The last setup's preconditioner: dict(schwarz, clusters, segments, sources, gathered_rows, subdomain_rows,
+        row_length, launches_per_iteration)
         (ofx_gn_precond_info; synchronises the device: tools and bench only)."""
-        arr = (ctypes.c_int64 * 7)()
+        arr = (ctypes.c_int64 * 8)()
         call("ofx_gn_precond_info", self._h, arr)
-        return dict(zip(("schwarz", "clusters", "segments", "sources", "gathered_rows", "subdomain_rows", "row_length"),
-                        list(arr)))
+        return dict(zip(("schwarz", "clusters", "segments", "sources", "gathered_rows", "subdomain_rows", "row_length",
+                         "launches_per_iteration"), list(arr)))
 
     def stopped(self):
         """The solve's stop flag as the host sees it (ofx_gn_stopped: no synchronisation)."""

@@ -38,7 +38,7 @@ def _graph(g):
 
 def test_library_is_native(cuda):
     from occlusionfusion_amd import _lib
-    assert _lib.lib.ofx_abi_version() == 4
+    assert _lib.lib.ofx_abi_version() == 5
     assert os.path.exists(_lib.LIB_PATH)
 
 

@@ -127,3 +127,46 @@ def test_auto_preconditioner_picks_by_graph_size(cuda, monkeypatch):
             if expect:
                 assert info["segments"] > 0 and info["row_length"] == 144
             assert _err(out, g, 0) < TOL
+
+
+@pytest.mark.parametrize("name", ["gn_2k.npz", "gn_4k.npz"])
+def test_one_launch_iteration_is_bitwise_the_two_launch_form(cuda, monkeypatch, name):
+    """k_as_iter (one launch per Schwarz PCG iteration: ghost ring rows, each subdomain's own inverse, the next launch
+    summing m from the contributions in k_as_apply's segment order) reproduces k_pcg_iter<.., kAS> + k_as_apply bit for
+    bit: the same transforms, loss logs and PCG iteration counts, through the prefetched chain (gn_2k: two-wave
+    clusters, kU = 2; gn_4k: one-wave clusters, kU = 4), in half the launches."""
+    from occlusionfusion_amd import GaussNewtonSolver
+    g = _load(name)
+    monkeypatch.setenv("OFX_PRECOND", "as")
+    monkeypatch.setenv("OFX_AS_ONE", "0")
+    two = _chain(g, cuda)
+    monkeypatch.setenv("OFX_AS_ONE", "1")
+    one = _chain(g, cuda)
+    for q, (a, b) in enumerate(zip(two, one)):
+        assert torch.equal(a["node_rotations"], b["node_rotations"]), (name, q)
+        assert torch.equal(a["node_translations"], b["node_translations"]), (name, q)
+        assert a["convergence_info"]["total"] == b["convergence_info"]["total"]
+        assert a["convergence_info"]["pcg_iterations"] == b["convergence_info"]["pcg_iterations"]
+        assert _err(b, g, q) < TOL
+    s = GaussNewtonSolver(g["nodes"].shape[0], 10000)
+    s.optimize(g["nodes"], g["edges"], g["edge_weights"], g["f0_tpos"], g["f0_conf"], g["f0_src"], g["f0_anchors"],
+               g["f0_weights"], g["f0_tgt"], tuple(float(v) for v in g["intr"]))
+    info = s.precond_info()
+    assert info["schwarz"] == 1 and info["launches_per_iteration"] == 1, info
+    print(f"{name}: one-launch = two-launch bit for bit, PCG iterations {_pcg(one)}")
+
+
+def test_one_launch_moose_is_bitwise_the_two_launch_form(cuda, monkeypatch):
+    """The same on the reference's real moose pair (271 nodes, Schwarz forced; its refresh steps rebuild the
+    subdomain inverses inside the warm start, which now also writes the one-launch copy)."""
+    from test_gpu_moose import _moose_gn
+    g = np.load(os.path.join(GOLDEN, "moose.npz"), allow_pickle=False)
+    monkeypatch.setenv("OFX_PRECOND", "as")
+    monkeypatch.setenv("OFX_AS_ONE", "0")
+    two, _, _ = _moose_gn(g)
+    monkeypatch.setenv("OFX_AS_ONE", "1")
+    one, dr, dt = _moose_gn(g)
+    assert torch.equal(two["node_rotations"], one["node_rotations"])
+    assert torch.equal(two["node_translations"], one["node_translations"])
+    assert two["convergence_info"]["pcg_iterations"] == one["convergence_info"]["pcg_iterations"]
+    assert max(dr, dt) < TOL

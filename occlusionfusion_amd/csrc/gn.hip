@@ -1708,7 +1708,7 @@ __global__ __launch_bounds__(256) void k_as_members(GnDev g, int ncl) {
 __global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
   __shared__ int s_dom[kAsDN], s_rs[kAsDN + 1];
   __shared__ int s_col[kGB], s_slot[kGB], s_l[kGB], s_first[kGB], s_rank[kGB];
-  __shared__ int s_ns;
+  __shared__ int s_key[kGB], s_scan[kGB];
   const int c = blockIdx.x, t = threadIdx.x;
   const AsTabP tp = as_tab_at(g.as_tab, g.as_tab_cap);
   if (t < kAsDN) s_dom[t] = g.as_dom[c * kAsDN + t];
@@ -1731,36 +1731,49 @@ __global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
       while (l + 1 < nd && s_rs[l + 1] <= i) ++l;
       const int b = g.row_ptr[s_dom[l]] + (i - s_rs[l]);
       s_col[i] = g.col[b]; s_slot[i] = b; s_l[i] = l;
+      s_key[i] = (g.col[b] << 9) | i;   // (rows < 2^22)
     } else {
       s_col[i] = 0x7FFFFFFF; s_slot[i] = 0; s_l[i] = 0;
+      s_key[i] = 0x7FFFFFFF;
     }
   }
   __syncthreads();
+  // bitonic sort of (column, block) keys: S2 = the distinct columns in ascending order, each block's rank among them,
+  // and "first" = the lowest block index of its column (the key breaks ties by block)
+  for (int k = 2; k <= kGB; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < kGB; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const int a = s_key[i], b = s_key[ixj];
+          if (((i & k) == 0) == (a > b)) { s_key[i] = b; s_key[ixj] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = t; i < kGB; i += 256)
+    s_scan[i] = (i < nb && (i == 0 || (s_key[i] >> 9) != (s_key[i - 1] >> 9))) ? 1 : 0;
+  __syncthreads();
+  for (int o = 1; o < kGB; o <<= 1) {   // inclusive scan of the first flags
+    int v[2];
+    for (int q = 0; q < 2; ++q) { const int i = t + 256 * q; v[q] = s_scan[i] + (i >= o ? s_scan[i - o] : 0); }
+    __syncthreads();
+    for (int q = 0; q < 2; ++q) s_scan[t + 256 * q] = v[q];
+    __syncthreads();
+  }
   for (int i = t; i < nb; i += 256) {
-    bool f = true;
-    for (int j = 0; j < i && f; ++j) f = s_col[j] != s_col[i];
-    s_first[i] = f ? 1 : 0;
+    const int idx = s_key[i] & (kGB - 1);
+    s_rank[idx] = s_scan[i] - 1;
+    s_first[idx] = (i == 0 || (s_key[i] >> 9) != (s_key[i - 1] >> 9)) ? 1 : 0;
   }
   __syncthreads();
-  for (int i = t; i < nb; i += 256) {
-    int rk = 0;
-    for (int j = 0; j < nb; ++j) rk += (s_first[j] && s_col[j] < s_col[i]) ? 1 : 0;
-    s_rank[i] = rk;
-  }
-  if (t == 0) {
-    int n = 0;
-    for (int j = 0; j < nb; ++j) n += s_first[j];
-    s_ns = n;
-  }
-  __syncthreads();
-  const int ns = s_ns;
+  const int ns = nb > 0 ? s_scan[nb - 1] : 0;
   // entries past nb / ns repeat the last valid one: k_as_iter's idle lanes load unconditionally, and a common padding
   // address (block 0, y[0]) would be one L2 channel hit by every workgroup
   for (int i = t; i < kGB; i += 256) {
     const int j = i < nb ? i : nb - 1;
     tp.blk[(int64_t)c * kGB + i] = make_int2(s_slot[j], (s_rank[j] << 5) | s_l[j]);
   }
-  __syncthreads();
   for (int i = t; i < nb; i += 256) {
     if (!s_first[i]) continue;
     const int u = s_col[i], k = s_rank[i];
@@ -1783,13 +1796,10 @@ __global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
   int32_t* rt = tp.row + (int64_t)c * kGRow;
   if (t <= kAsDN) rt[t] = s_rs[t];
   if (t == 0) { rt[25] = nd; rt[26] = nb; rt[27] = ns; }
-  if (t < kAsDN) {   // the subdomain row's S2 index: the rank of its own column (the diagonal block)
-    int rk = 0;
-    if (t < nd)
-      for (int j = 0; j < nb; ++j) rk += (s_first[j] && s_col[j] < s_dom[t]) ? 1 : 0;
-    rt[32 + t] = rk;
-    rt[64 + t] = t < nd ? s_dom[t] : 0;
-  }
+  if (t < kAsDN) rt[64 + t] = t < nd ? s_dom[t] : 0;
+  for (int i = t; i < nb; i += 256)   // the subdomain row's S2 index: the rank of its diagonal block's column
+    if (s_col[i] == s_dom[s_l[i]]) rt[32 + s_l[i]] = s_rank[i];
+  if (t >= nd && t < kAsDN) rt[32 + t] = 0;
 }
 
 // Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= kAsD x kAsD, f64, kAsTi x kAsTi
@@ -2502,7 +2512,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // main path: vmcnt counts stores too, so stores ahead of trip 2 held its issue until their acks (workgroup 0's eight)
   auto lead_stores = [&]() {
     if (blockIdx.x == 0 && lane == 0) {
-      reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>(kWave ? g.Aw : g.Aop);
+      // (the operator the iteration reads: the padded per-wave copy, or A itself for the one-launch Schwarz iteration)
+      reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>((kWave && !g.as_one) ? g.Aw : g.Aop);
       g.pcs[kScTol] = g.prm.pcg_tol;
       // the error stop's τ: one value for both preconditioners (the estimate is Euclidean, k_pcg_iter)
       g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
@@ -2589,8 +2600,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
   // the loaded (dead) w register stays allocated to here: otherwise the compiler reuses it for a temporary of the
   // SpMV's issue and waits for its load first (a vmcnt that held trip 2 behind nearly all of trip 1)
-  // the wave's blocks into its padded copy for k_pcg_iter (kWave): last, so no wait here is behind their acks
-  if (kWave) {
+  // the wave's blocks into its padded copy for k_pcg_iter (kWave): last, so no wait here is behind their acks (the
+  // one-launch Schwarz iteration reads A itself: no copy)
+  if (kWave && !g.as_one) {
     double2* Aw = reinterpret_cast<double2*>(g.Aw) + (int64_t)wv * 18 * kWL;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -3175,25 +3187,43 @@ __global__ __launch_bounds__(kW2 ? 128 : 64) __attribute__((amdgpu_waves_per_eu(
 // next launch sums m on the columns it needs from the <= 1 + kAsX contributions per node in ascending subdomain order —
 // the order in which k_as_apply sums a row's segments, each contribution being that segment's value — so the iterates are
 // bitwise those of the two-launch form. One exchange per iteration: one kernel boundary.
-// Roles (1024 threads): waves 0-7 one block of D_c's rows each (the A block and the product); waves 8-12 one S2 node each
+// Roles (1024 threads; the rows first in dispatch order): waves 0-2 the rows: 0 the own rows (k_pcg_iter's wave: scalars,
+// stop, recurrences, partials, the converging launch's GN step), 1-2 the ring rows (ghost z, w); waves 3-7 one S2 node each
 // (its contributions summed into m; a second pass past 320 nodes) and one inverse row half each (the dot product, as
-// k_as_apply's two lanes); waves 13-15 the rows: 13 the own rows (k_pcg_iter's wave: scalars, stop, recurrences,
-// partials, the converging launch's GN step), 14-15 the ring rows (ghost z, w). Trip 1: the stop word, tables, state,
+// k_as_apply's two lanes); waves 8-15 the blocks of D_c's rows (the A rows and the products). Trip 1: the stop word, tables, state,
 // partials, inverse rows; trip 2: the A blocks and the contributions. Three barriers (m, products, the w image).
-template <bool kFirst, int kU>
+// k_as_iter's workgroup barrier: LDS writes complete (lgkmcnt(0)), then s_barrier — no memory fence: __syncthreads()
+// would also wait for every outstanding global load and store of the wave (the A rows, the inverse rows, the state
+// stores), which the roles consume or retire later
+__device__ __forceinline__ void as_lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+}
+#ifdef OFX_STAMPS   // tuning build: per (iteration < 64, cluster) 8 clock stamps — 0 entry, 1 trip 1 landed, 2 after barrier 1,
+                    // 3 scalars done, 4 after barrier 2, 5 after barrier 3 (own-row wave), 6 end; 7: an S2 wave at barrier 1
+#define OFX_AS_ITER_STAMP(k, cn) \
+  if (lane == 0 && g.stamps && (cn) < 64) g.stamps[((int64_t)(cn) * nwg + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OFX_AS_ITER_STAMP(k, cn)
+#endif
+template <bool kFirst, int kU, bool kRowSplit>
 __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, const double* Pc, const double* st,
-                                                      const double* sc, const char* tab, const PcgIt* gp, int cap, int ep,
-                                                      int gn_iter) {
+                                                      const double* sc, const char* tab, const PcgIt* gp, int cap,
+                                                      int xcd_per, int nwg, int ep, int gn_iter) {
   const PcgIt& g = *gp;
   constexpr int kNs = 128 * kU;
-  constexpr int kS2W = 5 * 64;   // S2 nodes per pass (waves 8-12)
+  constexpr int kS2W = 5 * 64;   // S2 nodes per pass (waves 3-7)
   __shared__ __attribute__((aligned(16))) double s_m[kGS * 6];
   __shared__ __attribute__((aligned(16))) double s_prod[(kGB + kRowMax) * 6];
   __shared__ __attribute__((aligned(16))) double s_w[kAsD];
   __shared__ int s_leave;
+  __shared__ double s_ab[2];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);   // (uniform: the roles below are scalar branches)
-  const int c = blockIdx.x;
+  // workgroups are dealt to the 8 XCDs round robin: with xcd_per > 0 XCD x runs clusters [x·xcd_per, (x+1)·xcd_per), so
+  // its L2 holds one contiguous run of subdomains with their shared ring rows and blocks (the grid is 8·xcd_per)
+  const int c = xcd_per > 0 ? (int)(blockIdx.x & 7) * xcd_per + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (c >= nwg) return;   // (the padding workgroups of the XCD form, before any barrier)
   const AsTabP tp = as_tab_at(const_cast<char*>(tab), cap);
   const int par_ = (int)((reinterpret_cast<uintptr_t>(sc) >> 3) & 1);
   const double* scb = sc - par_;
@@ -3202,24 +3232,61 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   // Each role issues trip 1 (the stop word first), tests the stop word (drained launches end there, before any
   // barrier), issues trip 2, and meets the others at three barriers: (1) m on S2 + the stop decision, (2) the block
   // products, (3) the w image. Loads are unconditional (clamped), the roles' data live only inside their branch.
-  if (wave < 8) {   // ---------------- blocks
+  if (wave >= 8) {  // ---------------- blocks (waves 8-15; tb = block index)
+    const int tb = t - kGB;
     int stop_ep = stopw[(int64_t)c * 64 + lane];
-    const int2 be = tp.blk[(int64_t)c * kGB + t];
     const int nb = rt[26];
+    typedef double gd2 __attribute__((ext_vector_type(2)));
+    const __attribute__((address_space(1))) gd2* A2 =
+        reinterpret_cast<const __attribute__((address_space(1))) gd2*>(reinterpret_cast<const uint64_t*>(scb)[kScAop]);
+    if (kRowSplit) {
+      // one thread per (block, row): pair p = t + 512 j, block p / 6, row p % 6 — the wave's 64 lanes read ~11 blocks'
+      // rows as consecutive 48-B pieces (a thread per whole 288-B block touched 64 lines per load instruction)
+      constexpr int kP = (kGB * 6 + kGB - 1) / kGB;   // pairs per thread (6)
+      int2 be[kP];
+#pragma unroll
+      for (int j = 0; j < kP; ++j) be[j] = tp.blk[(int64_t)c * kGB + (tb + kGB * j) / 6];
+      asm volatile("" ::: "memory");
+      stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
+      if (stop_ep != 0) return;
+      double2 ar[kP][3];
+#pragma unroll
+      for (int j = 0; j < kP; ++j)
+        if (tb - lane + kGB * j < 6 * nb)   // (wave-uniform)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const gd2 x = A2[18 * (int64_t)be[j].x + 3 * ((tb + kGB * j) % 6) + k];
+            ar[j][k] = make_double2(x.x, x.y);
+          }
+      as_lds_barrier();   // (1)
+#pragma unroll
+      for (int j = 0; j < kP; ++j) {
+        const int pp = tb + kGB * j;
+        if (pp < 6 * nb) {   // k_pcg_iter's operation order (row i of the block's product)
+          const int k = be[j].y >> 5;
+          double x[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) x[q] = s_m[6 * k + q];
+          const double2 b01 = ar[j][0], b23 = ar[j][1], b45 = ar[j][2];
+          s_prod[pp] = fma(b45.y, x[5], fma(b45.x, x[4], fma(b23.y, x[3], fma(b23.x, x[2], fma(b01.y, x[1], b01.x * x[0])))));
+        }
+      }
+      as_lds_barrier();   // (2)
+      as_lds_barrier();   // (3)
+      return;
+    }
+    const int2 be = tp.blk[(int64_t)c * kGB + tb];
     asm volatile("" ::: "memory");
     stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
     if (stop_ep != 0) return;
-    typedef double gd2 __attribute__((ext_vector_type(2)));
-    const __attribute__((address_space(1))) gd2* b = reinterpret_cast<const __attribute__((address_space(1))) gd2*>(
-        reinterpret_cast<uint64_t>(g.Aop)) + 18 * (int64_t)be.x;
-    const bool any = t - lane < nb;   // (wave-uniform: waves past the subdomain's blocks load nothing)
+    const __attribute__((address_space(1))) gd2* b = A2 + 18 * (int64_t)be.x;
+    const bool any = tb - lane < nb;   // (wave-uniform: waves past the subdomain's blocks load nothing)
     double2 ab[18];
     if (any)
 #pragma unroll
       for (int k = 0; k < 18; ++k) { const gd2 x = b[k]; ab[k] = make_double2(x.x, x.y); }
-    __syncthreads();   // (1)
-    if (s_leave) return;
-    if (any && t < nb) {   // k_pcg_iter's operation order
+    as_lds_barrier();   // (1)
+    if (any && tb < nb) {   // k_pcg_iter's operation order
       const int k = be.y >> 5;
       double x[6];
 #pragma unroll
@@ -3227,16 +3294,16 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const double2 b01 = ab[3 * i], b23 = ab[3 * i + 1], b45 = ab[3 * i + 2];
-        s_prod[t * 6 + i] =
+        s_prod[tb * 6 + i] =
             fma(b45.y, x[5], fma(b45.x, x[4], fma(b23.y, x[3], fma(b23.x, x[2], fma(b01.y, x[1], b01.x * x[0])))));
       }
     }
-    __syncthreads();   // (2)
-    __syncthreads();   // (3)
+    as_lds_barrier();   // (2)
+    as_lds_barrier();   // (3)
     return;
   }
-  if (wave < 13) {  // ---------------- S2 nodes (m) and inverse rows (y)
-    const int ts = t - kGB;
+  if (wave >= 3) {  // ---------------- S2 nodes (m) and inverse rows (y): waves 3-7
+    const int ts = t - 192;
     int stop_ep = stopw[(int64_t)c * 64 + lane];
     const int k2 = ts < kGS ? ts : kGS - 1;
     int4 cn = make_int4(-1, -1, -1, -1);
@@ -3245,10 +3312,6 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
     else cn = tp.con[(int64_t)c * kGS + k2];
     const int nd = rt[25], ns = rt[27];
     const int ry = min(ts >> 1, kAsD - 1), hl = ts & 1;
-    uint4 z[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) z[k] = tp.slab[((int64_t)c * kAsK + 9 * hl + k) * kAsD + ry];
-    const float dsc_r = tp.dsc[(int64_t)c * kAsD + ry];
     asm volatile("" ::: "memory");
     stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
     if (stop_ep != 0) return;
@@ -3291,6 +3354,9 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
 #pragma unroll
         for (int j = 0; j < 6; ++j) s_m[6 * ts + j] = mv[j];
     }
+#ifdef OFX_STAMPS
+    if (wave == 3) { const int cn_ = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT]; OFX_AS_ITER_STAMP(7, cn_) }
+#endif
     if (ns > kS2W)   // (rare: more than 320 distinct columns) further passes, one more trip each
       for (int kk = ts + kS2W; kk < ns; kk += kS2W) {
         double mv[6];
@@ -3299,10 +3365,16 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
 #pragma unroll
         for (int j = 0; j < 6; ++j) s_m[6 * kk + j] = mv[j];
       }
-    __syncthreads();   // (1)
-    if (s_leave) return;
-    __syncthreads();   // (2)
-    __syncthreads();   // (3)
+    as_lds_barrier();   // (1)
+    // the inverse rows now (only the last phase reads them; issued with the first trip they queued the whole
+    // workgroup's small loads behind 46 KB per workgroup)
+    uint4 z[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) z[k] = tp.slab[((int64_t)c * kAsK + 9 * hl + k) * kAsD + ry];
+    const float dsc_r = tp.dsc[(int64_t)c * kAsD + ry];
+    as_lds_barrier();   // (2)
+    as_lds_barrier();   // (3)
+    if (s_leave) return;   // (converged: no contributions; the row waves took the leave path)
     // y_c = D Ẑ (D w): k_as_apply's segment dot (two lanes, four chains, the pair summed by DPP) times the row scale
     const double2* w2p = reinterpret_cast<const double2*>(s_w);
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
@@ -3327,30 +3399,40 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
       tp.y[(int64_t)(par_ ^ 1) * cap * kAsD + (int64_t)c * kAsD + (ts >> 1)] = (double)dsc_r * dot;
     return;
   }
-  // ---------------- rows: wave 13 the own rows (k_pcg_iter's wave), 14-15 the ring rows (ghost z, w)
-  const int jr = wave - 13, r = lane >> 3, q = lane & 7;
+  // ---------------- rows: wave 0 the own rows (k_pcg_iter's wave), 1-2 the ring rows (ghost z, w)
+  const int jr = wave, r = lane >> 3, q = lane & 7;
+#ifdef OFX_STAMPS
+  const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
   const bool own = q < 6;
   const int qc = own ? q : 5;
   const int l = 8 * jr + r;                       // subdomain row
   const int row = c * kCS + r;                    // (own rows)
   const int64_t o = 6 * (int64_t)row + qc;
   int stop_ep = stopw[(int64_t)c * 64 + lane];
+  // wave 0 alone reads the partials and the step scalars (every wave of every workgroup reading the same few KB, written
+  // by all workgroups of the previous launch, made them one hot spot) and hands alpha, beta and the decision to 1-2
   double2 tpp[kPcgStreams][kU];
-#pragma unroll
-  for (int k = 0; k < kPcgStreams; ++k)
-#pragma unroll
-    for (int u = 0; u < kU; ++u) tpp[k][u] = *reinterpret_cast<const double2*>(Pc + k * kNs + 2 * (lane + 64 * u));
   double own_p[kPcgStreams];
+  int cnt = 0;
+  double2 ra = make_double2(0.0, 0.0), rtb = ra, rg = ra, sd = ra, tols = ra;
+  double bb_stored = 0.0, th_prev = 0.0;
+  if (jr == 0) {
 #pragma unroll
-  for (int k = 0; k < kPcgStreams; ++k) own_p[k] = Pc[k * kNs + c];
-  const int cnt = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
-  const double2 ra = *reinterpret_cast<const double2*>(scb + kScAlpha + 2);
-  const double2 rtb = *reinterpret_cast<const double2*>(scb + kScAlpha + 4);
-  const double2 rg = *reinterpret_cast<const double2*>(scb + kScGamma + 2);
-  const double2 sd = reinterpret_cast<const double2*>(scb + kScSturm)[lane];
-  const double bb_stored = scb[kScScal + S_BB];
-  const double th_prev = scb[kScScal + S_TH_PREV];
-  const double2 tols = *reinterpret_cast<const double2*>(scb + kScTol);
+    for (int k = 0; k < kPcgStreams; ++k)
+#pragma unroll
+      for (int u = 0; u < kU; ++u) tpp[k][u] = *reinterpret_cast<const double2*>(Pc + k * kNs + 2 * (lane + 64 * u));
+#pragma unroll
+    for (int k = 0; k < kPcgStreams; ++k) own_p[k] = Pc[k * kNs + c];
+    cnt = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
+    ra = *reinterpret_cast<const double2*>(scb + kScAlpha + 2);
+    rtb = *reinterpret_cast<const double2*>(scb + kScAlpha + 4);
+    rg = *reinterpret_cast<const double2*>(scb + kScGamma + 2);
+    sd = reinterpret_cast<const double2*>(scb + kScSturm)[lane];
+    bb_stored = scb[kScScal + S_BB];
+    th_prev = scb[kScScal + S_TH_PREV];
+    tols = *reinterpret_cast<const double2*>(scb + kScTol);
+  }
   const int nd = rt[25];
   const int rs = rt[l], re = rt[l + 1], rk = rt[32 + l];
   const float dsc_l = tp.dsc[(int64_t)c * kAsD + 6 * l + qc];
@@ -3373,50 +3455,71 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   asm volatile("" ::: "memory");
   stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
   if (stop_ep != 0) return;
+#ifdef OFX_STAMPS
+  if (jr == 0 && lane == 0 && g.stamps && cnt < 64) g.stamps[((int64_t)cnt * nwg + c) * 8] = t_entry;
+#endif
+  if (jr == 0) { OFX_AS_ITER_STAMP(1, cnt) }
   double tb[kFirst ? 2 * kU : 1];
-  if (kFirst) {   // the first iteration's |b|² partials
+  if (kFirst && jr == 0) {   // the first iteration's |b|² partials
     const __attribute__((address_space(1))) double* pb =
         reinterpret_cast<const __attribute__((address_space(1))) double*>(reinterpret_cast<uint64_t>(g.part_b));
 #pragma unroll
     for (int u = 0; u < 2 * kU; ++u) tb[u] = pb[lane + 64 * u];
   }
-  // ---- scalars (every row wave derives the same bits from the partials), the stop decision (k_pcg_iter's)
-  const double tol = tols.x, etol = tols.y;
-  const double rgam_prev = kFirst ? 1.0 : ((par_ ^ 1) ? rg.y : rg.x);
-  const double ralpha_prev = kFirst ? 1.0 : ((par_ ^ 1) ? ra.y : ra.x);
-  const double thr_prev = kFirst ? 0.0 : ((par_ ^ 1) ? rtb.y : rtb.x);
-  double pa[kPcgStreams];
-#pragma unroll
-  for (int k = 0; k < kPcgStreams; ++k) {
-    double tt = 0.0;
-#pragma unroll
-    for (int u = 0; u < kU; ++u) tt += tpp[k][u].x + tpp[k][u].y;
-    pa[k] = wave_sum(tt);
-  }
-  double bb = bb_stored;
-  if (kFirst) {
-    double tt = 0.0;
-#pragma unroll
-    for (int u = 0; u < 2 * kU; ++u) tt += tb[u];
-    bb = wave_sum(tt);
-  }
-  const double gam = pa[0], del = pa[1], rr = pa[2], pp = pa[3];
+  as_lds_barrier();   // (1) — the scalars below overlap the block waves' products
+  if (jr == 0) { OFX_AS_ITER_STAMP(2, cnt) }
+  // ---- scalars and the stop decision (k_pcg_iter's), wave 0
+  const double etol = tols.y;
+  double alpha = 0.0, beta = 0.0, gam = 0.0, bb = bb_stored, ralpha_prev = 1.0;
+  bool conv = false;
+  int leave = 0;
   const bool lead = c == 0 && jr == 0 && lane == 0;
-  double beta = 0.0, alpha;
-  if (kFirst) {
-    alpha = div_nr(gam, del);
-  } else {
-    beta = gam * rgam_prev;
-    alpha = div_nr(gam, del - beta * gam * ralpha_prev);
+  if (jr == 0) {
+    const double tol = tols.x;
+    const double rgam_prev = kFirst ? 1.0 : ((par_ ^ 1) ? rg.y : rg.x);
+    ralpha_prev = kFirst ? 1.0 : ((par_ ^ 1) ? ra.y : ra.x);
+    const double thr_prev = kFirst ? 0.0 : ((par_ ^ 1) ? rtb.y : rtb.x);
+    double pa[kPcgStreams];
+#pragma unroll
+    for (int k = 0; k < kPcgStreams; ++k) {
+      double tt = 0.0;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) tt += tpp[k][u].x + tpp[k][u].y;
+      pa[k] = wave_sum(tt);
+    }
+    if (kFirst) {
+      double tt = 0.0;
+#pragma unroll
+      for (int u = 0; u < 2 * kU; ++u) tt += tb[u];
+      bb = wave_sum(tt);
+    }
+    gam = pa[0];
+    const double del = pa[1], rr = pa[2], pp = pa[3];
+    if (kFirst) {
+      alpha = div_nr(gam, del);
+    } else {
+      beta = gam * rgam_prev;
+      alpha = div_nr(gam, del - beta * gam * ralpha_prev);
+    }
+    conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam * pp * rgam_prev <= thr_prev * ralpha_prev)) || gam == 0.0 ||
+           rr <= 1e-24 * bb;
+    leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
+    leave = __builtin_amdgcn_readfirstlane(leave);
+    if (lane == 0) { s_leave = leave; s_ab[0] = alpha; s_ab[1] = beta; }
+    OFX_AS_ITER_STAMP(3, cnt)
   }
-  const bool conv = (rr <= tol * tol * bb && (etol <= 0.0 || gam * pp * rgam_prev <= thr_prev * ralpha_prev)) ||
-                    gam == 0.0 || rr <= 1e-24 * bb;
-  int leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
-  leave = __builtin_amdgcn_readfirstlane(leave);
-  if (jr == 0 && lane == 0) s_leave = leave;
-  __syncthreads();   // (1)
+  as_lds_barrier();   // (2)
+  if (jr == 0) { OFX_AS_ITER_STAMP(4, cnt) }
+  if (jr != 0) {
+    leave = s_leave;
+    alpha = s_ab[0];
+    beta = s_ab[1];
+  }
   if (leave) {       // converged, or breakdown (A SPD => alpha > 0): keep x (k_pcg_iter's leave path)
-    if (jr != 0) return;
+    if (jr != 0) {
+      as_lds_barrier();   // (3)
+      return;
+    }
     const bool ill = !conv && !isfinite(alpha);
     if (kFirst && lead) const_cast<double*>(scb)[kScScal + S_BB] = bb;
     double* Pn = const_cast<double*>(Pc) + (par_ ? -kPcgStreams : kPcgStreams) * (int64_t)kNs;
@@ -3431,34 +3534,9 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
       host_flag(g.hflags, H_PCG_IT, cnt);
       __hip_atomic_store(g.hflags + H_DONE, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    as_lds_barrier();   // (3)
     return;
   }
-  // the lead wave's Ritz bracket (k_pcg_iter's Sturm step) and the error-stop threshold τ²·min(θ̂, θ̂_prev)
-  double2 sd_new = sd;
-  double thr_new = 0.0, th_cur = 1e300;
-  auto shift = [](int s) {
-    const int e = s < 40 ? s : 2 * s - 40;
-    const int k = e & 3;
-    const double cc = k == 0 ? 1.0 : k == 1 ? 0.84089641525371454303 : k == 2 ? 0.70710678118654752440
-                                                                             : 0.59460355750136053336;
-    return ldexp(cc, -(e >> 2));
-  };
-  if (c == 0 && jr == 0 && etol > 0.0) {
-    const double rca = 1.0 / alpha;
-    const double diag = kFirst ? rca : rca + beta * ralpha_prev;
-    const double e2 = kFirst ? 0.0 : beta * ralpha_prev * ralpha_prev;
-    const double sig = shift(lane);
-    double dd = (diag - sig) - (kFirst ? 0.0 : e2 / sd.x);
-    if (fabs(dd) < 1e-300) dd = -1e-300;
-    const double cc = (kFirst ? 0.0 : sd.y) + (dd < 0.0 ? 1.0 : 0.0);
-    sd_new = make_double2(dd, cc);
-    const uint64_t free_ = __ballot(cc == 0.0);
-    const double th = free_ ? shift(__ffsll((unsigned long long)free_) - 1) : 0.0;
-    th_cur = th;
-    const double tu = fmin(th, th_prev);
-    thr_new = (etol * etol) * tu;
-  }
-  __syncthreads();   // (2)
   // n on the subdomain row: its blocks in CSR order (k_pcg_iter's row sum)
   const int rlen = l < nd ? re - rs : 0;
   const double* sp = s_prod + rs * 6 + qc;
@@ -3491,8 +3569,34 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
     if (own && l < nd) tp.gh[gi] = make_double2(w2, zz);
   }
   if (own) s_w[6 * l + q] = l < nd ? w2 * (double)dsc_l : 0.0;
-  __syncthreads();   // (3)
+  as_lds_barrier();   // (3)
   if (jr != 0) return;
+  OFX_AS_ITER_STAMP(5, cnt)
+  // ---- the lead wave's Ritz bracket (k_pcg_iter's Sturm step) and the error-stop threshold τ²·min(θ̂, θ̂_prev)
+  double2 sd_new = sd;
+  double thr_new = 0.0, th_cur = 1e300;
+  auto shift = [](int s) {
+    const int e = s < 40 ? s : 2 * s - 40;
+    const int k = e & 3;
+    const double cc = k == 0 ? 1.0 : k == 1 ? 0.84089641525371454303 : k == 2 ? 0.70710678118654752440
+                                                                             : 0.59460355750136053336;
+    return ldexp(cc, -(e >> 2));
+  };
+  if (c == 0 && etol > 0.0) {
+    const double rca = 1.0 / alpha;
+    const double diag = kFirst ? rca : rca + beta * ralpha_prev;
+    const double e2 = kFirst ? 0.0 : beta * ralpha_prev * ralpha_prev;
+    const double sig = shift(lane);
+    double dd = (diag - sig) - (kFirst ? 0.0 : e2 / sd.x);
+    if (fabs(dd) < 1e-300) dd = -1e-300;
+    const double cc = (kFirst ? 0.0 : sd.y) + (dd < 0.0 ? 1.0 : 0.0);
+    sd_new = make_double2(dd, cc);
+    const uint64_t free_ = __ballot(cc == 0.0);
+    const double th = free_ ? shift(__ffsll((unsigned long long)free_) - 1) : 0.0;
+    th_cur = th;
+    const double tu = fmin(th, th_prev);
+    thr_new = (etol * etol) * tu;
+  }
   // ---- the own rows' partials of the next launch, the lead's scalars
   double* Pn = const_cast<double*>(Pc) + (par_ ? -kPcgStreams : kPcgStreams) * (int64_t)kNs;
 #pragma unroll
@@ -3507,6 +3611,7 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   }
   if (c == 0 && etol > 0.0) reinterpret_cast<double2*>(sc_w + kScSturm)[lane] = sd_new;
   if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
+  OFX_AS_ITER_STAMP(6, cnt)
 }
 
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
@@ -3856,16 +3961,25 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   const dim3 block_it(w2 ? 128 : 64);
   // one launch per Schwarz iteration (k_as_iter; the setup built its tables)
   using AsIterKernel = void (*)(const int32_t*, const double*, const double*, const double*, const char*, const PcgIt*,
-                                int, int, int);
+                                int, int, int, int, int);
   const bool one = as && g->as_one;
   AsIterKernel one0 = nullptr, one1 = nullptr;
+  int xcd_per = 0, one_grid = ncl;
   if (one) {
+    // XCD-contiguous cluster runs (OFX_AS_XCD=0: workgroup = cluster; A/B, read per solve)
+    const char* xe = getenv("OFX_AS_XCD");
+    xcd_per = (xe && atoi(xe) == 0) ? 0 : (ncl + 7) / 8;
+    one_grid = xcd_per > 0 ? 8 * xcd_per : ncl;
+    // the block loads: a thread per (block, row) (default) or per block (OFX_AS_ROWSPLIT=0; A/B, read per solve)
+    const char* rse = getenv("OFX_AS_ROWSPLIT");
+    const bool rsp = !(rse && atoi(rse) == 0);
     switch (g->pcg_ku) {
-      case 2: one0 = k_as_iter<true, 2>; one1 = k_as_iter<false, 2>; break;
-      case 3: one0 = k_as_iter<true, 3>; one1 = k_as_iter<false, 3>; break;
-      case 4: one0 = k_as_iter<true, 4>; one1 = k_as_iter<false, 4>; break;
-      case 8: one0 = k_as_iter<true, 8>; one1 = k_as_iter<false, 8>; break;
-      default: one0 = k_as_iter<true, 17>; one1 = k_as_iter<false, 17>; break;
+      case 2: if (rsp) { one0 = k_as_iter<true, 2, true>; one1 = k_as_iter<false, 2, true>; }
+              else { one0 = k_as_iter<true, 2, false>; one1 = k_as_iter<false, 2, false>; } break;
+      case 3: if (rsp) { one0 = k_as_iter<true, 3, true>; one1 = k_as_iter<false, 3, true>; }
+              else { one0 = k_as_iter<true, 3, false>; one1 = k_as_iter<false, 3, false>; } break;
+      default: if (rsp) { one0 = k_as_iter<true, 4, true>; one1 = k_as_iter<false, 4, true>; }
+               else { one0 = k_as_iter<true, 4, false>; one1 = k_as_iter<false, 4, false>; } break;
     }
   }
   // No stream sync: the converging launch stores H_DONE straight into host memory and the host
@@ -3920,9 +4034,10 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (one) {   // one launch per iteration (k_as_iter)
       for (int k = 0; k < n; ++k, ++it) {
         const int par = it & 1;
-        hipLaunchKernelGGL(it == 0 ? one0 : one1, dim3(ncl), dim3(kAsIterT), 0, hs, (const int32_t*)g->stopw,
+        hipLaunchKernelGGL(it == 0 ? one0 : one1, dim3(one_grid), dim3(kAsIterT), 0, hs, (const int32_t*)g->stopw,
                            (const double*)(g->part_p + kPcgStreams * (int64_t)g->nw_pad * par), (const double*)g->st,
-                           (const double*)g->pcs + par, (const char*)g->as_tab, gp, g->as_tab_cap, g->ep, gn_iter);
+                           (const double*)g->pcs + par, (const char*)g->as_tab, gp, g->as_tab_cap, xcd_per, ncl, g->ep,
+                           gn_iter);
       }
     } else {
       for (int k = 0; k < n; ++k, ++it) {

@@ -3199,8 +3199,8 @@ __device__ __forceinline__ void as_lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
 }
-#ifdef OFX_STAMPS   // tuning build: per (iteration < 64, cluster) 8 clock stamps — 0 entry, 1 trip 1 landed, 2 after barrier 1,
-                    // 3 scalars done, 4 after barrier 2, 5 after barrier 3 (own-row wave), 6 end; 7: an S2 wave at barrier 1
+#ifdef OFX_STAMPS   // tuning build: per (iteration < 64, cluster) 8 clock stamps — 0 entry, 1 trip 1 landed, 2 scalars done,
+                    // 3 after barrier 1, 4 after barrier 2, 5 after barrier 3 (own-row wave), 6 end; 7: the last wave's entry
 #define OFX_AS_ITER_STAMP(k, cn) \
   if (lane == 0 && g.stamps && (cn) < 64) g.stamps[((int64_t)(cn) * nwg + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();
 #else
@@ -3208,8 +3208,8 @@ __device__ __forceinline__ void as_lds_barrier() {
 #endif
 template <bool kFirst, int kU, bool kRowSplit>
 __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, const double* Pc, const double* st,
-                                                      const double* sc, const char* tab, const PcgIt* gp, int cap,
-                                                      int xcd_per, int nwg, int ep, int gn_iter) {
+                                                      const double* sc, const char* tab, int cap, int xcd_per, int nwg,
+                                                      int ep, const PcgIt* gp, int gn_iter) {
   const PcgIt& g = *gp;
   constexpr int kNs = 128 * kU;
   constexpr int kS2W = 5 * 64;   // S2 nodes per pass (waves 3-7)
@@ -3234,6 +3234,13 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   // products, (3) the w image. Loads are unconditional (clamped), the roles' data live only inside their branch.
   if (wave >= 8) {  // ---------------- blocks (waves 8-15; tb = block index)
     const int tb = t - kGB;
+#ifdef OFX_STAMPS
+    if (wave == 15) {   // the last block wave's entry
+      const uint64_t t7 = __builtin_amdgcn_s_memtime();
+      const int cn_ = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
+      if (lane == 0 && g.stamps && cn_ < 64) g.stamps[((int64_t)cn_ * nwg + c) * 8 + 7] = t7;
+    }
+#endif
     int stop_ep = stopw[(int64_t)c * 64 + lane];
     const int nb = rt[26];
     typedef double gd2 __attribute__((ext_vector_type(2)));
@@ -3327,10 +3334,20 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
       } else {
         const int e[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {   // (an absent one re-reads the first: no extra lines)
+        for (int j = 0; j < 4; ++j) {
+#ifndef OFX_AS_NOSKIP   // absent contributions (a node is in 3.1 subdomains on average) load nothing: exec-masked lanes
+          if (j == 0 || e[j] >= 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cz[j][k] = reinterpret_cast<const double2*>(yr + e[j])[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cz[j][k] = make_double2(0.0, 0.0);
+          }
+#else                   // (an absent one re-reads the first: no extra lines)
           const double2* p = reinterpret_cast<const double2*>(yr + (e[j] >= 0 ? e[j] : e[0]));
 #pragma unroll
           for (int k = 0; k < 3; ++k) cz[j][k] = p[k];
+#endif
         }
       }
       asm volatile("" ::: "memory");
@@ -3354,9 +3371,6 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
 #pragma unroll
         for (int j = 0; j < 6; ++j) s_m[6 * ts + j] = mv[j];
     }
-#ifdef OFX_STAMPS
-    if (wave == 3) { const int cn_ = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT]; OFX_AS_ITER_STAMP(7, cn_) }
-#endif
     if (ns > kS2W)   // (rare: more than 320 distinct columns) further passes, one more trip each
       for (int kk = ts + kS2W; kk < ns; kk += kS2W) {
         double mv[6];
@@ -3466,9 +3480,8 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
 #pragma unroll
     for (int u = 0; u < 2 * kU; ++u) tb[u] = pb[lane + 64 * u];
   }
-  as_lds_barrier();   // (1) — the scalars below overlap the block waves' products
-  if (jr == 0) { OFX_AS_ITER_STAMP(2, cnt) }
-  // ---- scalars and the stop decision (k_pcg_iter's), wave 0
+  // ---- scalars and the stop decision (k_pcg_iter's), wave 0, ahead of barrier 1: the S2 waves' contributions (a
+  // second dependent trip behind their static table) land after the partials, so the scalars cost no time here
   const double etol = tols.y;
   double alpha = 0.0, beta = 0.0, gam = 0.0, bb = bb_stored, ralpha_prev = 1.0;
   bool conv = false;
@@ -3506,8 +3519,10 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
     leave = (conv || !isfinite(alpha) || !(alpha > 0.0)) ? 1 : 0;
     leave = __builtin_amdgcn_readfirstlane(leave);
     if (lane == 0) { s_leave = leave; s_ab[0] = alpha; s_ab[1] = beta; }
-    OFX_AS_ITER_STAMP(3, cnt)
+    OFX_AS_ITER_STAMP(2, cnt)
   }
+  as_lds_barrier();   // (1)
+  if (jr == 0) { OFX_AS_ITER_STAMP(3, cnt) }
   as_lds_barrier();   // (2)
   if (jr == 0) { OFX_AS_ITER_STAMP(4, cnt) }
   if (jr != 0) {
@@ -3960,8 +3975,9 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   }
   const dim3 block_it(w2 ? 128 : 64);
   // one launch per Schwarz iteration (k_as_iter; the setup built its tables)
-  using AsIterKernel = void (*)(const int32_t*, const double*, const double*, const double*, const char*, const PcgIt*,
-                                int, int, int, int, int);
+  // (the arguments up to ep fill the 14 preloaded SGPRs: the workgroup's cluster test and trip 1 wait for no kernarg fetch)
+  using AsIterKernel = void (*)(const int32_t*, const double*, const double*, const double*, const char*, int, int, int,
+                                int, const PcgIt*, int);
   const bool one = as && g->as_one;
   AsIterKernel one0 = nullptr, one1 = nullptr;
   int xcd_per = 0, one_grid = ncl;
@@ -4036,7 +4052,7 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
         const int par = it & 1;
         hipLaunchKernelGGL(it == 0 ? one0 : one1, dim3(one_grid), dim3(kAsIterT), 0, hs, (const int32_t*)g->stopw,
                            (const double*)(g->part_p + kPcgStreams * (int64_t)g->nw_pad * par), (const double*)g->st,
-                           (const double*)g->pcs + par, (const char*)g->as_tab, gp, g->as_tab_cap, xcd_per, ncl, g->ep,
+                           (const double*)g->pcs + par, (const char*)g->as_tab, g->as_tab_cap, xcd_per, ncl, g->ep, gp,
                            gn_iter);
       }
     } else {

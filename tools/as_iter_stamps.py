@@ -2,8 +2,8 @@
 
 Needs the stamps build: python -c "from occlusionfusion_amd import build; build.build(out='tools/stampslib/libofx_stamps.so',
 defines=['OFX_STAMPS'])", then OFX_LIB=tools/stampslib/libofx_stamps.so python tools/as_iter_stamps.py
-Stamps of the own-row wave (s_memtime): 0 entry | 1 trip 1 landed | 2 barrier 1 (m on S2) | 3 scalars done |
-4 barrier 2 (products) | 5 barrier 3 (recurrences, w image) | 6 end; 7 = an S2 wave reaching barrier 1.
+Stamps of the own-row wave (s_memtime): 0 entry | 1 trip 1 landed | 2 scalars done | 3 barrier 1 (m on S2) |
+4 barrier 2 (products) | 5 barrier 3 (recurrences, w image) | 6 end; 7 = the last wave's (15) entry.
 """
 import ctypes
 import os
@@ -41,7 +41,7 @@ fn(h, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
 st = buf.reshape(64, nw, 8).astype(np.int64)
 ok = (st[:, :, :7] > 0).all(axis=2)
 print(f"clusters {nw}, sampled (iteration, cluster) pairs {int(ok.sum())}, precond {pipe.solver.precond_info()}")
-names = ["trip1", "to bar1", "scalars", "to bar2", "bar3+recur", "tail"]
+names = ["trip1", "scalars", "to bar1", "to bar2", "bar3+recur", "tail"]
 d = np.diff(st[:, :, :7], axis=2)[ok]
 for k, nme in enumerate(names):
     x = d[:, k]
@@ -49,7 +49,7 @@ for k, nme in enumerate(names):
 tot = (st[:, :, 6] - st[:, :, 0])[ok]
 print(f"  total       median {np.median(tot):7.0f}  p90 {np.percentile(tot, 90):7.0f}")
 s7 = (st[:, :, 7] - st[:, :, 0])[ok & (st[:, :, 7] > 0)]
-print(f"  S2 wave at barrier 1 (from the row wave's entry): median {np.median(s7):7.0f}")
+print(f"  the last wave (15) entered (from the row wave's entry): median {np.median(s7):7.0f}")
 # spread of entry across clusters in one iteration, and iteration period
 for it in (5, 10):
     e = st[it, :, 0][st[it, :, 0] > 0]

@@ -2466,6 +2466,22 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) { 
   }
 }
 
+// The warm start's per-solve scalar-block stores (workgroup 0, lane 0; k_pcg_w0 and k_as_w0): the operator the iteration
+// reads (the padded per-wave copy, or A itself for the one-launch Schwarz iteration), the tolerances, the iteration's w_new
+// target in the inverse's slot (Schwarz) and the m buffers, the error stop's θ̂ carried over from the previous GN step
+__device__ __forceinline__ void w0_lead_stores(const GnDev& g, double th_cur_old, bool wave_copy, bool as) {
+  reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>((wave_copy && !g.as_one) ? g.Aw : g.Aop);
+  g.pcs[kScTol] = g.prm.pcg_tol;
+  // the error stop's τ: one value for both preconditioners (the estimate is Euclidean, k_pcg_iter)
+  g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
+  reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = as ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
+  reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
+  reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
+  // (none for the first GN step of the solve)
+  g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? th_cur_old : 1e300;
+  g.pcs[kScScal + S_TH_CUR] = 1e300;
+}
+
 // w0 = A u0 (u0 gathered from m1), m0 = M⁻¹ w0 (cluster, via LDS); per-wave partials
 // (γ0 = r·u, δ0 = w·u, r·r) -> parity 0, b·b -> part_b.
 // kWave: the SpMV in k_pcg_iter's wave-list form — the wave's (col, slot) list leaves in the first trip with the state
@@ -2511,20 +2527,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // address into the scalar block, where the iteration finds it through a preloaded pointer. Both are stored last on the
   // main path: vmcnt counts stores too, so stores ahead of trip 2 held its issue until their acks (workgroup 0's eight)
   auto lead_stores = [&]() {
-    if (blockIdx.x == 0 && lane == 0) {
-      // (the operator the iteration reads: the padded per-wave copy, or A itself for the one-launch Schwarz iteration)
-      reinterpret_cast<uint64_t*>(g.pcs)[kScAop] = reinterpret_cast<uint64_t>((kWave && !g.as_one) ? g.Aw : g.Aop);
-      g.pcs[kScTol] = g.prm.pcg_tol;
-      // the error stop's τ: one value for both preconditioners (the estimate is Euclidean, k_pcg_iter)
-      g.pcs[kScTol + 1] = g.prm.pcg_err_tol;
-      // (Schwarz: the iteration's w_new target in the inverse's slot)
-      reinterpret_cast<uint64_t*>(g.pcs)[kScMcl] = kAS ? reinterpret_cast<uint64_t>(g.as_w) : reinterpret_cast<uint64_t>(g.Mcl);
-      reinterpret_cast<uint64_t*>(g.pcs)[kScM] = reinterpret_cast<uint64_t>(g.m0);
-      reinterpret_cast<uint64_t*>(g.pcs)[kScM + 1] = reinterpret_cast<uint64_t>(g.m1);
-      // the error-based stop's θ̂ carried over from the previous GN step of this solve (none for the first)
-      g.pcs[kScScal + S_TH_PREV] = g.gn_iter_now > 0 ? th_cur_old : 1e300;
-      g.pcs[kScScal + S_TH_CUR] = 1e300;
-    }
+    if (blockIdx.x == 0 && lane == 0) w0_lead_stores(g, th_cur_old, kWave, kAS);
   };
   if (stopped) {
     g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
@@ -3313,25 +3316,17 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
     const int ts = t - 192;
     int stop_ep = stopw[(int64_t)c * 64 + lane];
     const int k2 = ts < kGS ? ts : kGS - 1;
-    int4 cn = make_int4(-1, -1, -1, -1);
-    int s2u = 0;
-    if (kFirst) s2u = tp.s2n[(int64_t)c * kGS + k2];
-    else cn = tp.con[(int64_t)c * kGS + k2];
+    const int4 cn = tp.con[(int64_t)c * kGS + k2];
     const int nd = rt[25], ns = rt[27];
     const int ry = min(ts >> 1, kAsD - 1), hl = ts & 1;
     asm volatile("" ::: "memory");
     stop_ep = __builtin_amdgcn_readfirstlane(stop_ep);
     if (stop_ep != 0) return;
-    const double* m0 = kFirst ? reinterpret_cast<const double*>(reinterpret_cast<const uint64_t*>(scb)[kScM]) : nullptr;
     // m on S2: 0 + the contributions in ascending subdomain order (k_as_apply's sum of a row's segments, each
-    // contribution being that segment's value); the first iteration reads the warm start's m0
-    auto gather = [&](int4 e4, int u, double mv[6]) {
+    // contribution being that segment's value); the first iteration's (m0 = M⁻¹ w0) k_as_w0 left in y[0]
+    auto gather = [&](int4 e4, double mv[6]) {
       double2 cz[4][3];
-      if (kFirst) {
-        const double2* p = reinterpret_cast<const double2*>(m0 + 6 * (int64_t)u);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) cz[0][k] = p[k];
-      } else {
+      {
         const int e[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -3353,20 +3348,16 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        if (kFirst) {
-          mv[2 * k] = cz[0][k].x; mv[2 * k + 1] = cz[0][k].y;
-        } else {
-          const int e[4] = {e4.x, e4.y, e4.z, e4.w};
-          double mx = 0.0, my = 0.0;
+        const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+        double mx = 0.0, my = 0.0;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { mx += e[j] >= 0 ? cz[j][k].x : 0.0; my += e[j] >= 0 ? cz[j][k].y : 0.0; }
-          mv[2 * k] = mx; mv[2 * k + 1] = my;
-        }
+        for (int j = 0; j < 4; ++j) { mx += e[j] >= 0 ? cz[j][k].x : 0.0; my += e[j] >= 0 ? cz[j][k].y : 0.0; }
+        mv[2 * k] = mx; mv[2 * k + 1] = my;
       }
     };
     if (ts - lane < ns) {   // (wave-uniform: waves past the S2 nodes gather nothing)
       double mv[6];
-      gather(cn, s2u, mv);
+      gather(cn, mv);
       if (ts < ns)
 #pragma unroll
         for (int j = 0; j < 6; ++j) s_m[6 * ts + j] = mv[j];
@@ -3374,8 +3365,7 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
     if (ns > kS2W)   // (rare: more than 320 distinct columns) further passes, one more trip each
       for (int kk = ts + kS2W; kk < ns; kk += kS2W) {
         double mv[6];
-        gather(kFirst ? make_int4(-1, -1, -1, -1) : tp.con[(int64_t)c * kGS + kk],
-               kFirst ? tp.s2n[(int64_t)c * kGS + kk] : 0, mv);
+        gather(tp.con[(int64_t)c * kGS + kk], mv);
 #pragma unroll
         for (int j = 0; j < 6; ++j) s_m[6 * kk + j] = mv[j];
       }
@@ -3627,6 +3617,179 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   if (c == 0 && etol > 0.0) reinterpret_cast<double2*>(sc_w + kScSturm)[lane] = sd_new;
   if (kFirst && lead) sc_w[kScScal + S_BB] = bb;
   OFX_AS_ITER_STAMP(6, cnt)
+}
+
+// The Schwarz warm start's w0 launch of the one-launch iteration (as_one; in place of k_pcg_w0<true, true> + the apply of
+// w0): per subdomain c (the k_as_iter tables and workgroup mapping), u0 (the apply's M⁻¹ r0 in m1) gathered on S2, w0 = A u0
+// on every subdomain row with k_pcg_w0's products and CSR-order row sums, the own rows' records, as_w and partials exactly
+// as k_pcg_w0, and the contributions y_c = D Ẑ D w0[D_c] into y[0], which the first k_as_iter sums into m0 = M⁻¹ w0 (the
+// apply's segment sums, bit for bit). Roles as k_as_iter: waves 0-2 the rows (0 own), 3-7 S2 and the inverse rows, 8-15
+// the (block, row) products; barriers (1) u0 on S2, (2) the products, (3) the w image.
+__global__ __launch_bounds__(kAsIterT) void k_as_w0(GnDev g, const double* rhs, int xcd_per) {   // (rhs: see k_pcg_w0)
+  __shared__ __attribute__((aligned(16))) double s_m[kGS * 6];
+  __shared__ __attribute__((aligned(16))) double s_prod[(kGB + kRowMax) * 6];
+  __shared__ __attribute__((aligned(16))) double s_w[kAsD];
+  asm volatile("" :: "s"(g.as_tab), "s"(g.as_tab_cap), "s"(g.N), "s"(g.flags), "s"(g.m1), "s"(g.Aop), "s"(g.st),
+               "s"(g.stopw), "s"(g.ep), "s"(g.pcs), "s"(rhs), "s"(g.part_p), "s"(g.part_b), "s"(g.nw_pad), "s"(g.as_w));
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nwg = g.N / kCS;
+  const int c = xcd_per > 0 ? (int)(blockIdx.x & 7) * xcd_per + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (c >= nwg) return;
+  const AsTabP tp = as_tab_at(g.as_tab, g.as_tab_cap);
+  const int32_t* rt = tp.row + (int64_t)c * kGRow;
+  const int stopped = g.flags[F_STOPPED];   // (the same for every wave: all leave before the first barrier)
+  if (wave >= 8) {  // ---------------- (block, row) products (waves 8-15)
+    const int tb = t - kGB;
+    constexpr int kP = (kGB * 6 + kGB - 1) / kGB;
+    int2 be[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j) be[j] = tp.blk[(int64_t)c * kGB + (tb + kGB * j) / 6];
+    const int nb = rt[26];
+    asm volatile("" ::: "memory");
+    if (stopped) return;
+    const double2* A2 = reinterpret_cast<const double2*>(g.Aop);
+    double2 ar[kP][3];
+#pragma unroll
+    for (int j = 0; j < kP; ++j)
+      if (tb - lane + kGB * j < 6 * nb)   // (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ar[j][k] = A2[18 * (int64_t)be[j].x + 3 * ((tb + kGB * j) % 6) + k];
+    as_lds_barrier();   // (1)
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const int pp = tb + kGB * j;
+      if (pp < 6 * nb) {   // k_pcg_w0's operation order
+        const int k = be[j].y >> 5;
+        double x[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) x[q] = s_m[6 * k + q];
+        const double2 b01 = ar[j][0], b23 = ar[j][1], b45 = ar[j][2];
+        s_prod[pp] = ((b01.x * x[0] + b01.y * x[1]) + (b23.x * x[2] + b23.y * x[3])) + (b45.x * x[4] + b45.y * x[5]);
+      }
+    }
+    as_lds_barrier();   // (2)
+    as_lds_barrier();   // (3)
+    return;
+  }
+  if (wave >= 3) {  // ---------------- u0 on S2, then the inverse rows (y): waves 3-7
+    constexpr int kS2W = 5 * 64;
+    const int ts = t - 192;
+    const int k2 = ts < kGS ? ts : kGS - 1;
+    const int s2u = tp.s2n[(int64_t)c * kGS + k2];
+    const int nd = rt[25], ns = rt[27];
+    const int ry = min(ts >> 1, kAsD - 1), hl = ts & 1;
+    asm volatile("" ::: "memory");
+    if (stopped) return;
+    if (ts - lane < ns) {   // (wave-uniform)
+      const double2* p = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)s2u);
+      double2 u[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) u[k] = p[k];
+      if (ts < ns)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { s_m[6 * ts + 2 * k] = u[k].x; s_m[6 * ts + 2 * k + 1] = u[k].y; }
+    }
+    if (ns > kS2W)   // (rare: more than 320 distinct columns)
+      for (int kk = ts + kS2W; kk < ns; kk += kS2W) {
+        const double2* p = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)tp.s2n[(int64_t)c * kGS + kk]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { const double2 u = p[k]; s_m[6 * kk + 2 * k] = u.x; s_m[6 * kk + 2 * k + 1] = u.y; }
+      }
+    as_lds_barrier();   // (1)
+    uint4 z[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) z[k] = tp.slab[((int64_t)c * kAsK + 9 * hl + k) * kAsD + ry];
+    const float dsc_r = tp.dsc[(int64_t)c * kAsD + ry];
+    as_lds_barrier();   // (2)
+    as_lds_barrier();   // (3)
+    // y_c = D Ẑ (D w0): k_as_iter's (k_as_apply's) segment dot times the row scale
+    const double2* w2p = reinterpret_cast<const double2*>(s_w);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    auto lo = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); };
+    auto hi = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); };
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int kw = 9 * hl + k;
+      const double2 p0 = w2p[4 * kw], p1 = w2p[4 * kw + 1], p2 = w2p[4 * kw + 2], p3 = w2p[4 * kw + 3];
+      a0 = fma(lo(z[k].x), p0.x, a0);
+      a1 = fma(hi(z[k].x), p0.y, a1);
+      a2 = fma(lo(z[k].y), p1.x, a2);
+      a3 = fma(hi(z[k].y), p1.y, a3);
+      a0 = fma(lo(z[k].z), p2.x, a0);
+      a1 = fma(hi(z[k].z), p2.y, a1);
+      a2 = fma(lo(z[k].w), p3.x, a2);
+      a3 = fma(hi(z[k].w), p3.y, a3);
+    }
+    double dot = (a0 + a1) + (a2 + a3);
+    dot += dpp_mov<0xB1>(dot);   // the row's two halves
+    if (hl == 0 && ts < 2 * kAsD && (ts >> 1) < 6 * nd)
+      tp.y[(int64_t)c * kAsD + (ts >> 1)] = (double)dsc_r * dot;   // (parity 0: the first iteration's)
+    return;
+  }
+  // ---------------- rows: wave 0 the own rows (k_pcg_w0's wave), 1-2 the ring rows (w0 for the image only)
+  const int jr = wave, r = lane >> 3, q = lane & 7;
+  const bool own = q < 6;
+  const int qc = own ? q : 5;
+  const int l = 8 * jr + r;
+  const int row = c * kCS + r;
+  const int64_t o = 6 * (int64_t)row + q, oc = 6 * (int64_t)row + qc;
+  const int nd = rt[25];
+  const int rs = rt[l], re = rt[l + 1];
+  const float dsc_l = tp.dsc[(int64_t)c * kAsD + 6 * l + qc];
+  double v[V_N];
+  double u_as = 0.0, bo = 0.0, th_cur_old = 0.0;
+  if (jr == 0) {
+    load_rec(g.st, oc, v);
+    u_as = g.m1[oc];
+    bo = rhs[oc];
+    th_cur_old = g.pcs[kScScal + S_TH_CUR];
+  }
+  asm volatile("" ::: "memory");
+  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
+    if (jr == 0) {
+      g.stopw[(int64_t)c * 64 + lane] = g.ep;
+      if (c == 0 && lane == 0) w0_lead_stores(g, th_cur_old, true, true);
+    }
+    return;
+  }
+  as_lds_barrier();   // (1)
+  as_lds_barrier();   // (2)
+  const int len = l < nd ? re - rs : 0;
+  const double* sp = s_prod + rs * 6 + qc;
+  double tv[kRowMax];
+#pragma unroll
+  for (int k = 0; k < kRowMax; ++k) tv[k] = sp[6 * k];
+  double w = 0.0;
+#pragma unroll
+  for (int k = 0; k < kRowMax; ++k) w += k < len ? tv[k] : 0.0;
+  double d[4] = {0.0, 0.0, 0.0, 0.0};
+  if (jr == 0 && own) {
+    v[V_U] = u_as;
+    v[V_W] = w;
+    store_rec(g.st, o, v);
+    g.as_w[o] = w;
+    d[0] = v[V_R] * v[V_U]; d[1] = w * v[V_U]; d[2] = v[V_R] * v[V_R]; d[3] = bo * bo;
+  }
+  if (own) s_w[6 * l + q] = l < nd ? w * (double)dsc_l : 0.0;
+  as_lds_barrier();   // (3)
+  if (jr != 0) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = wave_sum(d[k]);
+  const int ns = g.nw_pad;
+  if (lane == 0) {
+    g.part_p[c] = d[0]; g.part_p[ns + c] = d[1]; g.part_p[2 * ns + c] = d[2];
+    g.part_p[3 * ns + c] = 0.0;   // (the direction stream: no direction before the first iteration)
+    g.part_b[c] = d[3];
+  }
+  if (c == 0)   // zero tails of both parities' streams and of part_b
+    for (int i = nwg + lane; i < ns; i += 64) {
+#pragma unroll
+      for (int k = 0; k < 2 * kPcgStreams; ++k) g.part_p[k * ns + i] = 0.0;
+      g.part_b[i] = 0.0;
+    }
+  g.stopw[(int64_t)c * 64 + lane] = 0;
+  if (c == 0 && lane == 0) w0_lead_stores(g, th_cur_old, true, true);
 }
 
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
@@ -3935,10 +4098,23 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     }
     if (as) as_apply(false, g->as_w, g->m1);   // u0 = M⁻¹ r0
   }
-  if (as) hipLaunchKernelGGL((k_pcg_w0<true, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
-  else if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
-  else hipLaunchKernelGGL(k_pcg_w0<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
-  if (as) as_apply(false, g->as_w, g->m0);     // m0 = M⁻¹ w0
+  // the one-launch iteration's workgroups: XCD-contiguous cluster runs (OFX_AS_XCD=0: workgroup = cluster; A/B, read per
+  // solve), XCD x running clusters [x·xcd_per, (x+1)·xcd_per)
+  const bool one = as && g->as_one;
+  int xcd_per = 0, one_grid = ncl;
+  if (one) {
+    const char* xe = getenv("OFX_AS_XCD");
+    xcd_per = (xe && atoi(xe) == 0) ? 0 : (ncl + 7) / 8;
+    one_grid = xcd_per > 0 ? 8 * xcd_per : ncl;
+  }
+  if (one) {   // w0 = A u0 and the contributions of m0 = M⁻¹ w0 in one launch (k_as_w0)
+    hipLaunchKernelGGL(k_as_w0, dim3(one_grid), dim3(kAsIterT), 0, hs, *g, (const double*)rhs, xcd_per);
+  } else {
+    if (as) hipLaunchKernelGGL((k_pcg_w0<true, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    else if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    else hipLaunchKernelGGL(k_pcg_w0<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
+    if (as) as_apply(false, g->as_w, g->m0);     // m0 = M⁻¹ w0
+  }
   OFX_LAUNCH_CHECK();
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g->timing) {
@@ -3978,14 +4154,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   // (the arguments up to ep fill the 14 preloaded SGPRs: the workgroup's cluster test and trip 1 wait for no kernarg fetch)
   using AsIterKernel = void (*)(const int32_t*, const double*, const double*, const double*, const char*, int, int, int,
                                 int, const PcgIt*, int);
-  const bool one = as && g->as_one;
   AsIterKernel one0 = nullptr, one1 = nullptr;
-  int xcd_per = 0, one_grid = ncl;
   if (one) {
-    // XCD-contiguous cluster runs (OFX_AS_XCD=0: workgroup = cluster; A/B, read per solve)
-    const char* xe = getenv("OFX_AS_XCD");
-    xcd_per = (xe && atoi(xe) == 0) ? 0 : (ncl + 7) / 8;
-    one_grid = xcd_per > 0 ? 8 * xcd_per : ncl;
     // the block loads: a thread per (block, row) (default) or per block (OFX_AS_ROWSPLIT=0; A/B, read per solve)
     const char* rse = getenv("OFX_AS_ROWSPLIT");
     const bool rsp = !(rse && atoi(rse) == 0);

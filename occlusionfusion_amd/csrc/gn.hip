@@ -2361,43 +2361,15 @@ __global__ __launch_bounds__(kAS ? 256 : 64) __attribute__((amdgpu_waves_per_eu(
   if (blockIdx.x == 0 && threadIdx.x == 0) { g.flags[F_DONE] = 0; g.flags[F_PCG_IT] = 0; g.flags[F_PCG_CNT] = 0; }
 }
 
-// Galerkin warm start, pass 2: every wave re-derives G and f from the partials (fixed order,
-// identical bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get
-// c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0 (cluster, via LDS),
-// z = q = s = p = w = 0, u0 -> m1.
-// The projection partials are read as KU pairs per lane and stream at the iteration streams' padded stride nw_pad =
-// 128·KU (zero beyond the wave count: cleared at setup): unconditional loads, no per-load branches.
-template <int KU, bool kAS = false>   // kAS: Schwarz (no cluster inverse; r0 -> as_w for k_as_apply)
-__global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) {   // (not __restrict__: see k_pcg_w0)
-  __shared__ __attribute__((aligned(16))) double s_v[kCD];
-  // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
-  asm volatile("" :: "s"(g.n_prev), "s"(g.N), "s"(g.Mcl), "s"(g.xh), "s"(g.th), "s"(g.part_p), "s"(g.nw_pad),
-               "s"(g.flags), "s"(g.stopw), "s"(g.ep), "s"(g.st), "s"(g.m1), "s"(rhs));
-  const int lane = threadIdx.x;
-  const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
-  const int np = g.n_prev;
-  const bool own = q < 6;
-  const int64_t o = 6 * (int64_t)row + q;
-  const int64_t oc = 6 * (int64_t)row + (own ? q : 5);   // every lane loads (clamped): one memory trip in all
-  const int64_t stride = 6 * (int64_t)g.N;
-  float4 mr[kCD / 4];
-  if constexpr (!kAS) load_mrow(g, oc, mr);
-  const double rb = rhs[oc];
-  double xo[kProj], to[kProj];
-#pragma unroll
-  for (int j = 0; j < kProj; ++j) { xo[j] = g.xh[j * stride + oc]; to[j] = g.th[j * stride + oc]; }
-  double2 pt[kProjP][KU];
-  load_streams2_padded<kProjP, KU>(g.part_p, g.nw_pad, pt);
-  const int stopped = g.flags[F_STOPPED];
-  asm volatile("" ::: "memory");   // keep the loads above the exit test (one trip with the flag)
-  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
-    g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
-    return;
-  }
+// The warm start's Galerkin coefficients c (k_pcg_proj2, k_as_proj2; every wave that needs them computes them the same
+// way): the Gram partials of k_pcg_proj summed, the <= kProj system G c = X^T b solved by Cholesky on the upper triangle
+// (dependent / degenerate directions dropped); false if a coefficient is not finite
+template <int KU>
+__device__ __forceinline__ bool galerkin_coeffs(const GnDev& g, int np, double2 pt[kProjP][KU], double c[kProj]) {
   double p[kProjP];
   reduce_streams2<kProjP, KU>(g.part_p, g.nw_pad, g.nw_pad, pt, p);
   // G is symmetric in exact arithmetic; use the upper triangle G_ij = x_i·A x_j (i <= j)
-  double L[kProj][kProj], y[kProj], c[kProj];
+  double L[kProj][kProj], y[kProj];
   bool use[kProj];
 #pragma unroll
   for (int j = 0; j < kProj; ++j) {
@@ -2443,6 +2415,44 @@ __global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) { 
   bool fin = true;
 #pragma unroll
   for (int j = 0; j < kProj; ++j) fin = fin && isfinite(c[j]);
+  return fin;
+}
+
+// Galerkin warm start, pass 2: every wave re-derives G and f from the partials (fixed order,
+// identical bits), solves G c = f by pivot-guarded Cholesky (near-dependent history vectors get
+// c = 0), and sets x0 = Σ c_j x_j, r0 = b - Σ c_j t_j, u0 = M⁻¹ r0 (cluster, via LDS),
+// z = q = s = p = w = 0, u0 -> m1.
+// The projection partials are read as KU pairs per lane and stream at the iteration streams' padded stride nw_pad =
+// 128·KU (zero beyond the wave count: cleared at setup): unconditional loads, no per-load branches.
+template <int KU, bool kAS = false>   // kAS: Schwarz (no cluster inverse; r0 -> as_w for k_as_apply)
+__global__ __launch_bounds__(64) void k_pcg_proj2(GnDev g, const double* rhs) {   // (not __restrict__: see k_pcg_w0)
+  __shared__ __attribute__((aligned(16))) double s_v[kCD];
+  // the kernel-argument fields in SGPRs up front (one scalar trip, see k_terms)
+  asm volatile("" :: "s"(g.n_prev), "s"(g.N), "s"(g.Mcl), "s"(g.xh), "s"(g.th), "s"(g.part_p), "s"(g.nw_pad),
+               "s"(g.flags), "s"(g.stopw), "s"(g.ep), "s"(g.st), "s"(g.m1), "s"(rhs));
+  const int lane = threadIdx.x;
+  const int r = lane / kSL, q = lane % kSL, row = blockIdx.x * kRW + r;
+  const int np = g.n_prev;
+  const bool own = q < 6;
+  const int64_t o = 6 * (int64_t)row + q;
+  const int64_t oc = 6 * (int64_t)row + (own ? q : 5);   // every lane loads (clamped): one memory trip in all
+  const int64_t stride = 6 * (int64_t)g.N;
+  float4 mr[kCD / 4];
+  if constexpr (!kAS) load_mrow(g, oc, mr);
+  const double rb = rhs[oc];
+  double xo[kProj], to[kProj];
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) { xo[j] = g.xh[j * stride + oc]; to[j] = g.th[j * stride + oc]; }
+  double2 pt[kProjP][KU];
+  load_streams2_padded<kProjP, KU>(g.part_p, g.nw_pad, pt);
+  const int stopped = g.flags[F_STOPPED];
+  asm volatile("" ::: "memory");   // keep the loads above the exit test (one trip with the flag)
+  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
+    g.stopw[(int64_t)blockIdx.x * 64 + lane] = g.ep;
+    return;
+  }
+  double c[kProj];
+  const bool fin = galerkin_coeffs<KU>(g, np, pt, c);
   double xv = 0.0, rv = 0.0;
   if (own) {
     rv = rb;
@@ -3620,11 +3630,13 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
 }
 
 // The Schwarz warm start's w0 launch of the one-launch iteration (as_one; in place of k_pcg_w0<true, true> + the apply of
-// w0): per subdomain c (the k_as_iter tables and workgroup mapping), u0 (the apply's M⁻¹ r0 in m1) gathered on S2, w0 = A u0
+// w0): per subdomain c (the k_as_iter tables and workgroup mapping), u0 on S2 — kGather: summed from the contributions
+// k_as_proj2 left in y[1] (the apply's sums, bit for bit), else the cold start's apply of b in m1 — w0 = A u0
 // on every subdomain row with k_pcg_w0's products and CSR-order row sums, the own rows' records, as_w and partials exactly
 // as k_pcg_w0, and the contributions y_c = D Ẑ D w0[D_c] into y[0], which the first k_as_iter sums into m0 = M⁻¹ w0 (the
 // apply's segment sums, bit for bit). Roles as k_as_iter: waves 0-2 the rows (0 own), 3-7 S2 and the inverse rows, 8-15
 // the (block, row) products; barriers (1) u0 on S2, (2) the products, (3) the w image.
+template <bool kGather>
 __global__ __launch_bounds__(kAsIterT) void k_as_w0(GnDev g, const double* rhs, int xcd_per) {   // (rhs: see k_pcg_w0)
   __shared__ __attribute__((aligned(16))) double s_m[kGS * 6];
   __shared__ __attribute__((aligned(16))) double s_prod[(kGB + kRowMax) * 6];
@@ -3676,25 +3688,57 @@ __global__ __launch_bounds__(kAsIterT) void k_as_w0(GnDev g, const double* rhs, 
     constexpr int kS2W = 5 * 64;
     const int ts = t - 192;
     const int k2 = ts < kGS ? ts : kGS - 1;
-    const int s2u = tp.s2n[(int64_t)c * kGS + k2];
+    int s2u = 0;
+    int4 cn = make_int4(-1, -1, -1, -1);
+    if (kGather) cn = tp.con[(int64_t)c * kGS + k2];
+    else s2u = tp.s2n[(int64_t)c * kGS + k2];
     const int nd = rt[25], ns = rt[27];
     const int ry = min(ts >> 1, kAsD - 1), hl = ts & 1;
     asm volatile("" ::: "memory");
     if (stopped) return;
-    if (ts - lane < ns) {   // (wave-uniform)
-      const double2* p = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)s2u);
-      double2 u[3];
+    const double* yr = tp.y + (int64_t)g.as_tab_cap * kAsD;   // (y[1])
+    auto gather = [&](int4 e4, int u, double mv[6]) {
+      if (kGather) {   // 0 + the contributions in ascending subdomain order (k_as_iter's sums)
+        const int e[4] = {e4.x, e4.y, e4.z, e4.w};
+        double2 cz[4][3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) u[k] = p[k];
+        for (int j = 0; j < 4; ++j) {
+          if (j == 0 || e[j] >= 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cz[j][k] = reinterpret_cast<const double2*>(yr + e[j])[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cz[j][k] = make_double2(0.0, 0.0);
+          }
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          double mx = 0.0, my = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { mx += e[j] >= 0 ? cz[j][k].x : 0.0; my += e[j] >= 0 ? cz[j][k].y : 0.0; }
+          mv[2 * k] = mx; mv[2 * k + 1] = my;
+        }
+      } else {
+        const double2* p = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)u);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { const double2 x = p[k]; mv[2 * k] = x.x; mv[2 * k + 1] = x.y; }
+      }
+    };
+    if (ts - lane < ns) {   // (wave-uniform)
+      double mv[6];
+      gather(cn, s2u, mv);
       if (ts < ns)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { s_m[6 * ts + 2 * k] = u[k].x; s_m[6 * ts + 2 * k + 1] = u[k].y; }
+        for (int k = 0; k < 6; ++k) s_m[6 * ts + k] = mv[k];
     }
     if (ns > kS2W)   // (rare: more than 320 distinct columns)
       for (int kk = ts + kS2W; kk < ns; kk += kS2W) {
-        const double2* p = reinterpret_cast<const double2*>(g.m1 + 6 * (int64_t)tp.s2n[(int64_t)c * kGS + kk]);
+        double mv[6];
+        gather(kGather ? tp.con[(int64_t)c * kGS + kk] : make_int4(-1, -1, -1, -1),
+               kGather ? 0 : tp.s2n[(int64_t)c * kGS + kk], mv);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { const double2 u = p[k]; s_m[6 * kk + 2 * k] = u.x; s_m[6 * kk + 2 * k + 1] = u.y; }
+        for (int k = 0; k < 6; ++k) s_m[6 * kk + k] = mv[k];
       }
     as_lds_barrier();   // (1)
     uint4 z[9];
@@ -3737,11 +3781,12 @@ __global__ __launch_bounds__(kAsIterT) void k_as_w0(GnDev g, const double* rhs, 
   const int nd = rt[25];
   const int rs = rt[l], re = rt[l + 1];
   const float dsc_l = tp.dsc[(int64_t)c * kAsD + 6 * l + qc];
+  const int rk = rt[32 + l];   // (the row's S2 index: its u0 in s_m)
   double v[V_N];
   double u_as = 0.0, bo = 0.0, th_cur_old = 0.0;
   if (jr == 0) {
     load_rec(g.st, oc, v);
-    u_as = g.m1[oc];
+    if (!kGather) u_as = g.m1[oc];
     bo = rhs[oc];
     th_cur_old = g.pcs[kScScal + S_TH_CUR];
   }
@@ -3754,6 +3799,7 @@ __global__ __launch_bounds__(kAsIterT) void k_as_w0(GnDev g, const double* rhs, 
     return;
   }
   as_lds_barrier();   // (1)
+  if (kGather && jr == 0) u_as = s_m[6 * rk + qc];
   as_lds_barrier();   // (2)
   const int len = l < nd ? re - rs : 0;
   const double* sp = s_prod + rs * 6 + qc;
@@ -3790,6 +3836,107 @@ __global__ __launch_bounds__(kAsIterT) void k_as_w0(GnDev g, const double* rhs, 
     }
   g.stopw[(int64_t)c * 64 + lane] = 0;
   if (c == 0 && lane == 0) w0_lead_stores(g, th_cur_old, true, true);
+}
+
+// The Schwarz warm start's second projection launch of the one-launch iteration (as_one, warm steps; in place of
+// k_pcg_proj2<KU, true> + the apply of r0): per subdomain c, the Galerkin coefficients (wave 0, k_pcg_proj2's), x0 and
+// r0 = b - Σ c_j A x_j on the own rows (their records, as k_pcg_proj2) and r0 on the ring rows (the same expression on
+// the stored A x_j: no SpMV), and the contributions y_c = D Ẑ D r0[D_c] into y[1], which k_as_w0<true> sums into
+// u0 = M⁻¹ r0. Waves 0-2 the rows, 3-7 the inverse rows; barriers (1) the coefficients, (2) the r0 image.
+template <int KU>
+__global__ __launch_bounds__(512) void k_as_proj2(GnDev g, const double* rhs, int xcd_per) {   // (rhs: see k_pcg_w0)
+  __shared__ __attribute__((aligned(16))) double s_w[kAsD];
+  __shared__ double s_c[kProj];
+  __shared__ int s_fin;
+  asm volatile("" :: "s"(g.as_tab), "s"(g.as_tab_cap), "s"(g.N), "s"(g.flags), "s"(g.n_prev), "s"(g.xh), "s"(g.th),
+               "s"(g.part_p), "s"(g.nw_pad), "s"(g.stopw), "s"(g.ep), "s"(g.st), "s"(rhs));
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nwg = g.N / kCS;
+  const int c = xcd_per > 0 ? (int)(blockIdx.x & 7) * xcd_per + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (c >= nwg) return;
+  const AsTabP tp = as_tab_at(g.as_tab, g.as_tab_cap);
+  const int32_t* rt = tp.row + (int64_t)c * kGRow;
+  const int stopped = g.flags[F_STOPPED];   // (the same for every wave: all leave before the first barrier)
+  if (wave >= 3) {  // ---------------- the inverse rows (static: issued first), the dot after barrier 2
+    const int ts = t - 192;
+    const int ry = min(ts >> 1, kAsD - 1), hl = ts & 1;
+    const int nd = rt[25];
+    uint4 z[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) z[k] = tp.slab[((int64_t)c * kAsK + 9 * hl + k) * kAsD + ry];
+    const float dsc_r = tp.dsc[(int64_t)c * kAsD + ry];
+    asm volatile("" ::: "memory");
+    if (stopped) return;
+    as_lds_barrier();   // (1)
+    as_lds_barrier();   // (2)
+    const double2* w2p = reinterpret_cast<const double2*>(s_w);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    auto lo = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); };
+    auto hi = [](uint32_t u) { return (double)(float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); };
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int kw = 9 * hl + k;
+      const double2 p0 = w2p[4 * kw], p1 = w2p[4 * kw + 1], p2 = w2p[4 * kw + 2], p3 = w2p[4 * kw + 3];
+      a0 = fma(lo(z[k].x), p0.x, a0);
+      a1 = fma(hi(z[k].x), p0.y, a1);
+      a2 = fma(lo(z[k].y), p1.x, a2);
+      a3 = fma(hi(z[k].y), p1.y, a3);
+      a0 = fma(lo(z[k].z), p2.x, a0);
+      a1 = fma(hi(z[k].z), p2.y, a1);
+      a2 = fma(lo(z[k].w), p3.x, a2);
+      a3 = fma(hi(z[k].w), p3.y, a3);
+    }
+    double dot = (a0 + a1) + (a2 + a3);
+    dot += dpp_mov<0xB1>(dot);   // the row's two halves
+    if (hl == 0 && ts < 2 * kAsD && (ts >> 1) < 6 * nd)
+      tp.y[(int64_t)g.as_tab_cap * kAsD + (int64_t)c * kAsD + (ts >> 1)] = (double)dsc_r * dot;   // (y[1])
+    return;
+  }
+  // ---------------- rows: wave 0 the own rows (k_pcg_proj2's wave), 1-2 the ring rows (r0 for the image only)
+  const int jr = wave, r = lane >> 3, q = lane & 7;
+  const bool own = q < 6;
+  const int qc = own ? q : 5;
+  const int l = 8 * jr + r;
+  const int row = c * kCS + r;
+  const int64_t o = 6 * (int64_t)row + q;
+  const int nd = rt[25];
+  const int64_t og = jr == 0 ? 6 * (int64_t)row + qc : 6 * (int64_t)rt[64 + l] + qc;   // (ring rows past nd: row 0)
+  const float dsc_l = tp.dsc[(int64_t)c * kAsD + 6 * l + qc];
+  const int np = g.n_prev;
+  const int64_t stride = 6 * (int64_t)g.N;
+  const double rb = rhs[og];
+  double xo[kProj], to[kProj];
+#pragma unroll
+  for (int j = 0; j < kProj; ++j) { xo[j] = jr == 0 ? g.xh[j * stride + og] : 0.0; to[j] = g.th[j * stride + og]; }
+  double2 pt[kProjP][KU];
+  if (jr == 0) load_streams2_padded<kProjP, KU>(g.part_p, g.nw_pad, pt);
+  asm volatile("" ::: "memory");
+  if (stopped) {   // the solve already stopped: this step's iteration launches end after trip 1
+    if (jr == 0) g.stopw[(int64_t)c * 64 + lane] = g.ep;
+    return;
+  }
+  if (jr == 0) {
+    double cj[kProj];
+    const bool fin = galerkin_coeffs<KU>(g, np, pt, cj);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < kProj; ++j) s_c[j] = cj[j];
+      s_fin = fin ? 1 : 0;
+    }
+  }
+  as_lds_barrier();   // (1)
+  const bool fin = s_fin != 0;
+  double xv = 0.0, rv = rb;
+#pragma unroll
+  for (int j = 0; j < kProj; ++j)
+    if (j < np && fin) { const double cj = s_c[j]; xv += cj * xo[j]; rv -= cj * to[j]; }
+  if (jr == 0 && own) {
+    const double v[V_N] = {xv, rv, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    store_rec(g.st, o, v);
+  }
+  if (own) s_w[6 * l + q] = l < nd ? rv * (double)dsc_l : 0.0;
+  as_lds_barrier();   // (2)
 }
 
 // After the solve of GN step k: ill-posed check, loss bookkeeping, early stop (model.py:696-732) and,
@@ -4080,11 +4227,26 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   } else if (invert) {
     hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
   }
+  // the one-launch iteration's workgroups: XCD-contiguous cluster runs (OFX_AS_XCD=0: workgroup = cluster; A/B, read per
+  // solve), XCD x running clusters [x·xcd_per, (x+1)·xcd_per)
+  const bool one = as && g->as_one;
+  int xcd_per = 0, one_grid = ncl;
+  if (one) {
+    const char* xe = getenv("OFX_AS_XCD");
+    xcd_per = (xe && atoi(xe) == 0) ? 0 : (ncl + 7) / 8;
+    one_grid = xcd_per > 0 ? 8 * xcd_per : ncl;
+  }
   if (g->warm_now) {
     if (as) hipLaunchKernelGGL((k_pcg_proj<true, true>), dim3(g->nwg_row), dim3(256), 0, hs, *g, (const double*)rhs, gn_iter);
     else if (wave) hipLaunchKernelGGL(k_pcg_proj<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
     else hipLaunchKernelGGL(k_pcg_proj<false>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs, gn_iter);
-    switch (g->pcg_ku) {
+    if (one) {   // x0, r0 and the contributions of u0 = M⁻¹ r0 in one launch (k_as_proj2)
+      switch (g->pcg_ku) {
+        case 2: hipLaunchKernelGGL(k_as_proj2<2>, dim3(one_grid), dim3(512), 0, hs, *g, (const double*)rhs, xcd_per); break;
+        case 3: hipLaunchKernelGGL(k_as_proj2<3>, dim3(one_grid), dim3(512), 0, hs, *g, (const double*)rhs, xcd_per); break;
+        default: hipLaunchKernelGGL(k_as_proj2<4>, dim3(one_grid), dim3(512), 0, hs, *g, (const double*)rhs, xcd_per); break;
+      }
+    } else switch (g->pcg_ku) {
       case 2: if (as) hipLaunchKernelGGL((k_pcg_proj2<2, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
               else hipLaunchKernelGGL(k_pcg_proj2<2>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
       case 3: if (as) hipLaunchKernelGGL((k_pcg_proj2<3, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
@@ -4096,19 +4258,11 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
       default: if (as) hipLaunchKernelGGL((k_pcg_proj2<17, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
                else hipLaunchKernelGGL(k_pcg_proj2<17>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs); break;
     }
-    if (as) as_apply(false, g->as_w, g->m1);   // u0 = M⁻¹ r0
+    if (as && !one) as_apply(false, g->as_w, g->m1);   // u0 = M⁻¹ r0
   }
-  // the one-launch iteration's workgroups: XCD-contiguous cluster runs (OFX_AS_XCD=0: workgroup = cluster; A/B, read per
-  // solve), XCD x running clusters [x·xcd_per, (x+1)·xcd_per)
-  const bool one = as && g->as_one;
-  int xcd_per = 0, one_grid = ncl;
-  if (one) {
-    const char* xe = getenv("OFX_AS_XCD");
-    xcd_per = (xe && atoi(xe) == 0) ? 0 : (ncl + 7) / 8;
-    one_grid = xcd_per > 0 ? 8 * xcd_per : ncl;
-  }
-  if (one) {   // w0 = A u0 and the contributions of m0 = M⁻¹ w0 in one launch (k_as_w0)
-    hipLaunchKernelGGL(k_as_w0, dim3(one_grid), dim3(kAsIterT), 0, hs, *g, (const double*)rhs, xcd_per);
+  if (one) {   // w0 = A u0 and the contributions of m0 = M⁻¹ w0 in one launch (k_as_w0; u0 from k_as_proj2's contributions)
+    if (g->warm_now) hipLaunchKernelGGL(k_as_w0<true>, dim3(one_grid), dim3(kAsIterT), 0, hs, *g, (const double*)rhs, xcd_per);
+    else hipLaunchKernelGGL(k_as_w0<false>, dim3(one_grid), dim3(kAsIterT), 0, hs, *g, (const double*)rhs, xcd_per);
   } else {
     if (as) hipLaunchKernelGGL((k_pcg_w0<true, true>), dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);
     else if (wave) hipLaunchKernelGGL(k_pcg_w0<true>, dim3(g->nwg_row), dim3(64), 0, hs, *g, (const double*)rhs);

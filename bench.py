@@ -42,7 +42,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM = 8.0e12   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")   # tools/pmc_traffic.sh + tools/pmc_summary.py
+# tools/pmc_traffic.sh + tools/pmc_summary.py: the newest round's summary
+PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", f"r{r:02d}_pmc_traffic.json") for r in range(9, 0, -1))
+                 if os.path.exists(f)), os.path.join(ROOT, "profiles", "r05_pmc_traffic.json"))
 
 from occlusionfusion_amd.synthetic import BASELINE_CONFIGS as CONFIGS  # noqa: E402  (configs 1-5)
 

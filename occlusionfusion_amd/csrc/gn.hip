@@ -60,6 +60,7 @@ constexpr int kBlk = 256;       // threads per WG
 #define OFX_KPROJ 4
 #endif
 constexpr int kProj = OFX_KPROJ;   // warm start: Galerkin projection on the last kProj GN-step solutions
+constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;   // projection partial streams (Gram upper triangle + Xᵀb)
 constexpr int kCS = 8;        // nodes per preconditioner cluster (= PCG rows per wave)
 constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² entries
 // Overlapping additive Schwarz (as_on): the ring of a cluster holds its kAsRing A-neighbours with the most coupling terms,
@@ -71,13 +72,12 @@ constexpr int kMaxNodes = 8192;   // dense slot map of (2·max_nodes + kCS)² en
 constexpr int kAsRing = OFX_AS_RING, kAsX = 3, kAsDN = kCS + kAsRing, kAsD = 6 * kAsDN, kAsK = kAsD / 8,
               kAsSrc = 1 + kCS * kAsX, kAsRS = 6 * kCS * (1 + kAsX),
               kAsGat = (kAsSrc * kAsDN + kAsRS - 1) / kAsRS * kAsRS, kAsMeta = 64 + kAsRS;
-constexpr int kAsTi = (kAsD + 15) / 16;   // k_as_invert's register tile (16 x 16 threads, kAsTi x kAsTi entries each)
 // One launch per Schwarz PCG iteration (k_as_iter, round 6): per subdomain a table of its rows' blocks (<= kAsDN rows of
 // <= kRowMax blocks), the columns they touch (S2, <= kGS nodes) with the <= 1 + kAsX subdomain contributions that sum to m
 // there, and the scaled inverse rows in subdomain order (the "tab" buffer, AsTab below)
 constexpr int kGB = 512, kGS = 480, kGRow = 96;
 constexpr int kAsIterT = 1024;   // k_as_iter's threads: blocks 0..511, S2 nodes from 512, the row waves 13..15
-static_assert(kAsSrc * kAsDN <= kAsGat && kAsD % 8 == 0 && kAsTi <= 9, "Schwarz tables");
+static_assert(kAsSrc * kAsDN <= kAsGat && kAsD % 8 == 0 && kAsD <= 144, "Schwarz tables");
 
 // Everything the kernels read: trivially copyable, passed by value as the kernel argument (host-only
 // members live in Gn below, so a launch copies these bytes and nothing else).
@@ -478,6 +478,11 @@ __global__ __launch_bounds__(256) void k_upload(GnDev g, Upload u) {
     }
     for (int k = 0; k < 4; ++k) g.term_node[i * 4 + k] = n[k];
   }
+  // (cleared here rather than by fill dispatches: every partial stream is read unconditionally up to nw_pad; the wave
+  // maximum's slot; the one-launch tables' membership counts, atomically counted again by k_as_members)
+  if (i < kProjP * (int64_t)g.nw_pad) g.part_p[i] = 0.0;
+  if (i == 0) g.row_cnt[N + 1] = 0;
+  if (g.as_memn && i < N) g.as_memn[i] = 0;
   if (i < F_COUNT) g.flags[i] = 0;
   if (i < H_COUNT) host_flag(g.hflags, (int)i, 0);
   if (i < S_COUNT) g.scal[i] = 0.0;
@@ -583,8 +588,8 @@ __global__ __launch_bounds__(256) void k_wave_list(GnDev g) {
 // exclusive scan of cnt[0..n) into off[0..n] (off[n] = total), single workgroup: contiguous chunk
 // per thread, one block scan of the chunk sums
 // (max_out, nullable: max of cnt)
-__global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restrict__ cnt, int32_t* __restrict__ off,
-                                               int32_t* __restrict__ max_out) {
+__global__ __launch_bounds__(1024) void k_scan(int64_t n, int32_t* cnt, int32_t* __restrict__ off,
+                                               int32_t* __restrict__ max_out, bool clear) {   // clear: cnt = 0 after
   // tiles of 1024 x 8 counts: thread t scans its 8 contiguous entries (two coalesced 16-B loads), the
   // block scan combines the threads, a carry runs across tiles (fixed order)
   __shared__ int s_w[16];
@@ -601,6 +606,10 @@ __global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restr
 #pragma unroll
       for (int k = 0; k < kPer; ++k) v[k] = s0 + k < n ? cnt[s0 + k] : 0;
     }
+    if (clear)
+#pragma unroll
+      for (int k = 0; k < kPer; ++k)
+        if (s0 + k < n) cnt[s0 + k] = 0;
     int c = 0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) { c += v[k]; mx = max(mx, v[k]); }
@@ -612,6 +621,7 @@ __global__ __launch_bounds__(1024) void k_scan(int64_t n, const int32_t* __restr
     carry += total;
   }
   if (threadIdx.x == 0) off[n] = carry;
+  if (clear && threadIdx.x == 0) cnt[n] = 0;
   if (max_out) {
 #pragma unroll
     for (int k = 32; k > 0; k >>= 1) mx = max(mx, __shfl_xor(mx, k, 64));
@@ -651,9 +661,10 @@ __global__ __launch_bounds__(256) void k_row_assign(int N, int32_t* __restrict__
 // the setup's host-read scalars into host-mapped memory in one kernel (five small D2H copies through pageable
 // memory cost ~15-20 us each on the frame-boundary critical path)
 __global__ void k_setup_status(const int32_t* __restrict__ row_ptr, int N, const int32_t* __restrict__ row_cnt,
-                               const int32_t* __restrict__ gdiff, int32_t* out) {
+                               int32_t* __restrict__ gdiff, int32_t* out) {
   if (threadIdx.x != 0) return;
   const int32_t v[4] = {row_ptr[N], row_cnt[N], row_cnt[N + 1], gdiff ? *gdiff : 0};
+  if (gdiff) *gdiff = 0;   // (the next optimistic compare starts from zero: no fill dispatch)
 #pragma unroll
   for (int k = 0; k < 4; ++k) __hip_atomic_store(out + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -692,9 +703,15 @@ __global__ void k_pair_scatter(GnDev g) {
 __global__ __launch_bounds__(256) void k_up_flags(GnDev g, int32_t* __restrict__ flag) {
   const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (s < g.nnzb) flag[s] = g.col[s] >= g.blk_row[s] ? 1 : 0;
+  for (int64_t i = s; i < g.nnzb + 32; i += (int64_t)gridDim.x * blockDim.x) g.up_slot[i] = -1;   // -1: no upper block
 }
 __global__ __launch_bounds__(256) void k_up_list(GnDev g) {
   const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // the contribution counts start from zero (k_pair_count); blk_cnt held the flags the scan before this read
+  for (int64_t i = s; i <= g.nnzb || i <= g.N; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i <= g.nnzb) g.blk_cnt[i] = 0;
+    if (i <= g.N) g.node_cnt[i] = 0;
+  }
   if (s >= g.nnzb) return;
   const int r = g.blk_row[s], c = g.col[s];
   if (c < r) return;
@@ -1802,19 +1819,25 @@ __global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
   if (t >= nd && t < kAsDN) rt[32 + t] = 0;
 }
 
-// Per subdomain c (one workgroup of 16x16 threads): the dense damped A_{D_c D_c} (<= kAsD x kAsD, f64, kAsTi x kAsTi
-// entries per thread in registers: rows tr + 16a, columns tc + 16b), its in-place block Gauss-Jordan inverse (SPD: no pivoting;
+// Per subdomain c (one workgroup of TR x TC threads): the dense damped A_{D_c D_c} (<= kAsD x kAsD, f64, NA x NB entries
+// per thread in registers: rows tr + TR·a, columns tc + TC·b), its in-place block Gauss-Jordan inverse (SPD: no pivoting;
 // 2x2 pivot blocks through LDS, double-buffered: one barrier per two steps), scaled and rounded to fp16 with a certified
 // diagonal margin (below) and written symmetric into the segments' slab rows; a non-positive or non-finite pivot falls
 // back to the identity on the cluster's own rows; the cluster's rows' rotation accumulators restart (precond_rot_tol).
-// (A workgroup of 256 threads; every thread must call it: it synchronises the workgroup.)
+// k_as_invert and the refresh inside k_pcg_proj run it on 16 x 16 threads (four waves, 9 x 9 entries each; a 16 x 48
+// grid was measured slower, k_as_invert). The arithmetic per entry is the same for any grid. (Every thread of the
+// workgroup must call it: it synchronises the workgroup.)
+template <int TR, int TC>
 __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __restrict__ A, int c, int t) {
+  static_assert(TR == 16 && TC % 16 == 0, "pivot steps: row tile K = k / 16, column tile k / TC");
+  constexpr int T = TR * TC, NA = (kAsD + TR - 1) / TR, NB = (kAsD + TC - 1) / TC, kTM = TC / 16;
+  constexpr int kSR = TR * NA > TC * NB ? TR * NA : TC * NB;
   __shared__ int s_dom[kAsDN];
   __shared__ int s_sl[kAsDN][kAsDN];
   __shared__ int s_dst[kAsD];
-  __shared__ double s_row[2][2][16 * kAsTi], s_col[2][2][16 * kAsTi];
+  __shared__ double s_row[2][2][kSR], s_col[2][2][kSR];
   __shared__ __attribute__((aligned(16))) uint16_t s_z[kAsD * kAsD];   // the stored fp16 form, (R, C), both triangles
-  const int tr = t >> 4, tc = t & 15;
+  const int tr = t / TC, tc = t % TC;
 #ifdef OFX_STAMPS   // tuning build: phase stamps of thread 0 in the stamps buffer's iteration-63 slot
 #define OFX_AS_STAMP(k) \
   if (t == 0 && g.stamps) g.stamps[((int64_t)63 * g.nwg_row + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();
@@ -1827,76 +1850,78 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   __syncthreads();
   int nd = 0;
   for (int i = 0; i < kAsDN; ++i) nd += s_dom[i] >= 0 ? 1 : 0;
-  for (int p = t; p < kAsDN * kAsDN; p += 256) {
+  for (int p = t; p < kAsDN * kAsDN; p += T) {
     const int i = p / kAsDN, j = p % kAsDN;
     s_sl[i][j] = (i < nd && j < nd) ? g.map[(int64_t)s_dom[i] * g.N + s_dom[j]] - 1 : -1;
   }
   __syncthreads();
   const int n = 6 * nd;
   // every load unconditional (clamped addresses, masked values): a load behind a branch gets its own wait
-  double M[kAsTi][kAsTi];
-  int slv[kAsTi][kAsTi];
+  double M[NA][NB];
+  int slv[NA][NB];
 #pragma unroll
-  for (int a = 0; a < kAsTi; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < kAsTi; ++b) {
-      const int R = tr + 16 * a, C = tc + 16 * b;
+    for (int b = 0; b < NB; ++b) {
+      const int R = tr + TR * a, C = tc + TC * b;
       const int sl = (R < n && C < n) ? s_sl[min(R / 6, kAsDN - 1)][min(C / 6, kAsDN - 1)] : -1;
       slv[a][b] = sl;
       M[a][b] = A[36 * (int64_t)(sl >= 0 ? sl : 0) + 6 * (R % 6) + C % 6];
     }
   asm volatile("" ::: "memory");
 #pragma unroll
-  for (int a = 0; a < kAsTi; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < kAsTi; ++b) {
-      const int R = tr + 16 * a, C = tc + 16 * b;
+    for (int b = 0; b < NB; ++b) {
+      const int R = tr + TR * a, C = tc + TC * b;
       // (beyond n: the identity, never touched by the steps below)
       M[a][b] = (R < n && C < n) ? (slv[a][b] >= 0 ? M[a][b] : 0.0) : (R == C ? 1.0 : 0.0);
     }
   OFX_AS_STAMP(1)
   bool bad = false;
   int buf = 0;
-  // Block Gauss-Jordan with 2x2 pivot blocks P = rows / columns {k, k+1} (two elimination steps per barrier: the ~0.7 us
-  // of barrier and LDS latency per step, not the FMAs, set the kernel's time). Step k = 16·K + kk, kk even (K a compile-time
-  // register-tile index: M[K][.] / M[.][K] stay in registers).
+  // Block Gauss-Jordan with 2x2 pivot blocks P = rows / columns {k, k+1} (two elimination steps per barrier: the barrier
+  // and LDS latency per step, not the FMAs, set the time with four waves). Step k = 16·K + kk, kk even: the pivot rows are
+  // row tile K of threads tr = kk, kk + 1, the pivot columns column tile KB = K / kTM of threads tc = 16·(K % kTM) + kk,
+  // + 1 (compile-time tile indices: M[K][.] / M[.][KB] stay in registers).
   auto step2 = [&](auto Kc, int kk) {
     constexpr int K = decltype(Kc)::value;
-    if constexpr (K < kAsTi) {   // (discarded for K = 8 with the 8 x 8 tile)
+    if constexpr (K < NA) {   // (discarded for K = 8 with 8-row tiles)
+    constexpr int KB = K / kTM, kc0 = 16 * (K % kTM);
     const int k = 16 * K + kk;
     if (tr == kk || tr == kk + 1)
 #pragma unroll
-      for (int b = 0; b < kAsTi; ++b) s_row[buf][tr - kk][tc + 16 * b] = M[K][b];
-    if (tc == kk || tc == kk + 1)
+      for (int b = 0; b < NB; ++b) s_row[buf][tr - kk][tc + TC * b] = M[K][b];
+    if (tc == kc0 + kk || tc == kc0 + kk + 1)
 #pragma unroll
-      for (int a = 0; a < kAsTi; ++a) s_col[buf][tc - kk][tr + 16 * a] = M[a][K];
+      for (int a = 0; a < NA; ++a) s_col[buf][tc - kc0 - kk][tr + TR * a] = M[a][KB];
     __syncthreads();
     const double p00 = s_row[buf][0][k], p01 = s_row[buf][0][k + 1], p10 = s_row[buf][1][k], p11 = s_row[buf][1][k + 1];
     const double det = p00 * p11 - p01 * p10;
     bad = bad || !(p00 > 0.0) || !(det > 0.0) || !isfinite(det);
     const double idet = 1.0 / det;
     const double q00 = p11 * idet, q01 = -p01 * idet, q10 = -p10 * idet, q11 = p00 * idet;   // P⁻¹
-    double v0[kAsTi], v1[kAsTi], c0[kAsTi], c1[kAsTi];
+    double v0[NB], v1[NB], c0[NA], c1[NA];
 #pragma unroll
-    for (int b = 0; b < kAsTi; ++b) {   // P⁻¹ A_{K,j}
-      const double r0 = s_row[buf][0][tc + 16 * b], r1 = s_row[buf][1][tc + 16 * b];
+    for (int b = 0; b < NB; ++b) {   // P⁻¹ A_{K,j}
+      const double r0 = s_row[buf][0][tc + TC * b], r1 = s_row[buf][1][tc + TC * b];
       v0[b] = fma(q01, r1, q00 * r0);
       v1[b] = fma(q11, r1, q10 * r0);
     }
 #pragma unroll
-    for (int a = 0; a < kAsTi; ++a) { c0[a] = s_col[buf][0][tr + 16 * a]; c1[a] = s_col[buf][1][tr + 16 * a]; }
+    for (int a = 0; a < NA; ++a) { c0[a] = s_col[buf][0][tr + TR * a]; c1[a] = s_col[buf][1][tr + TR * a]; }
 #pragma unroll
-    for (int a = 0; a < kAsTi; ++a)
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int b = 0; b < kAsTi; ++b) M[a][b] = fma(-c1[a], v1[b], fma(-c0[a], v0[b], M[a][b]));   // (rows / columns K below)
+      for (int b = 0; b < NB; ++b) M[a][b] = fma(-c1[a], v1[b], fma(-c0[a], v0[b], M[a][b]));   // (pivot rows / columns below)
     if (tr == kk || tr == kk + 1)
 #pragma unroll
-      for (int b = 0; b < kAsTi; ++b) M[K][b] = tr == kk ? v0[b] : v1[b];
-    if (tc == kk || tc == kk + 1) {
-      const double e0 = tc == kk ? q00 : q01, e1 = tc == kk ? q10 : q11;
+      for (int b = 0; b < NB; ++b) M[K][b] = tr == kk ? v0[b] : v1[b];
+    if (tc == kc0 + kk || tc == kc0 + kk + 1) {
+      const double e0 = tc == kc0 + kk ? q00 : q01, e1 = tc == kc0 + kk ? q10 : q11;
 #pragma unroll
-      for (int a = 0; a < kAsTi; ++a) M[a][K] = -fma(c1[a], e1, c0[a] * e0);
-      if (tr == kk || tr == kk + 1) M[K][K] = tr == kk ? e0 : e1;   // the pivot block: P⁻¹
+      for (int a = 0; a < NA; ++a) M[a][KB] = -fma(c1[a], e1, c0[a] * e0);
+      if (tr == kk || tr == kk + 1) M[K][KB] = tr == kk ? e0 : e1;   // the pivot block: P⁻¹
     }
     buf ^= 1;
     }
@@ -1914,27 +1939,28 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   // 1 + σ with σ = ‖E‖_F + 2^-10 >= ‖E‖₂ + the diagonal's own rounding, so the stored Ẑ̃ >= Ẑ: positive definite whatever
   // Z's conditioning (a plain 16-bit rounding of Z made the moose's subdomains indefinite). A bad domain: the identity on
   // the cluster's own rows.
-  __shared__ double s_d[16 * kAsTi], s_e[256];
+  __shared__ double s_d[kSR], s_e[T];
   __shared__ double s_sig;
-  if (tr == tc)
 #pragma unroll
-    for (int a = 0; a < kAsTi; ++a) {
-      const int R = tr + 16 * a;
-      s_d[R] = (R < n && !bad) ? sqrt(M[a][a]) : 1.0;
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int R = tr + TR * a, C = tc + TC * b;
+      if (R == C) s_d[R] = (R < n && !bad) ? sqrt(M[a][b]) : 1.0;
     }
   __syncthreads();
-  double dr[kAsTi], dc[kAsTi];
+  double dr[NA], dc[NB];
 #pragma unroll
-  for (int a = 0; a < kAsTi; ++a) dr[a] = s_d[tr + 16 * a];
+  for (int a = 0; a < NA; ++a) dr[a] = s_d[tr + TR * a];
 #pragma unroll
-  for (int b = 0; b < kAsTi; ++b) dc[b] = s_d[tc + 16 * b];
+  for (int b = 0; b < NB; ++b) dc[b] = s_d[tc + TC * b];
   auto h16 = [](double z) -> _Float16 { return (_Float16)(float)z; };
   double e2 = 0.0;
 #pragma unroll
-  for (int a = 0; a < kAsTi; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < kAsTi; ++b) {
-      const int R = tr + 16 * a, C = tc + 16 * b;
+    for (int b = 0; b < NB; ++b) {
+      const int R = tr + TR * a, C = tc + TC * b;
       if (R < n && C < n && R < C && !bad) {
         const double z = M[a][b] / (dr[a] * dc[b]);
         const double err = (double)(float)h16(z) - z;
@@ -1943,10 +1969,11 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
     }
   s_e[t] = e2;
   __syncthreads();
-  if (t == 0) {
+  if (t < 64) {   // ‖E‖²_F: each lane its strided share of the threads' sums, then the wave (a fixed order)
     double sum = 0.0;
-    for (int i = 0; i < 256; ++i) sum += s_e[i];
-    s_sig = sqrt(sum) + 0x1p-10;
+    for (int i = t; i < T; i += 64) sum += s_e[i];
+    sum = wave_sum(sum);
+    if (t == 0) s_sig = sqrt(sum) + 0x1p-10;
   }
   __syncthreads();
   OFX_AS_STAMP(3)
@@ -1955,10 +1982,10 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   // as 16-B words (scattered 2-B stores of the entries cost ~80 us per solve)
   auto b16 = [](_Float16 h) { return __builtin_bit_cast(uint16_t, h); };
 #pragma unroll
-  for (int a = 0; a < kAsTi; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < kAsTi; ++b) {
-      const int R = tr + 16 * a, C = tc + 16 * b;
+    for (int b = 0; b < NB; ++b) {
+      const int R = tr + TR * a, C = tc + TC * b;
       if (R >= n || C >= kAsD) continue;
       if (C >= n) {
         s_z[R * kAsD + C] = 0;
@@ -1972,15 +1999,15 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
     }
   if (tc == 0)
 #pragma unroll
-    for (int a = 0; a < kAsTi; ++a) {
-      const int R = tr + 16 * a;
+    for (int a = 0; a < NA; ++a) {
+      const int R = tr + TR * a;
       if (R < kAsD) g.as_dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
       if (R < kAsD && g.as_one) as_tab_at(g.as_tab, g.as_tab_cap).dsc[(int64_t)c * kAsD + R] = R < n ? (float)dr[a] : 0.f;
       if (R < n) g.as_rsc[s_dst[R]] = (float)dr[a];
     }
   __syncthreads();
   OFX_AS_STAMP(4)
-  for (int i = t; i < n * kAsK; i += 256) {
+  for (int i = t; i < n * kAsK; i += T) {
     const int R = i / kAsK, k = i % kAsK;
     const int d = s_dst[R], cp = d / kAsRS, rs = d % kAsRS;
     reinterpret_cast<uint4*>(g.as_slab)[((int64_t)cp * kAsK + k) * kAsRS + rs] =
@@ -1988,7 +2015,7 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
   }
   if (g.as_one) {   // k_as_iter's subdomain-ordered copy: word k of row R at slab[(c·kAsK + k)·kAsD + R] (rows fastest)
     uint4* sl = as_tab_at(g.as_tab, g.as_tab_cap).slab + (int64_t)c * kAsK * kAsD;
-    for (int i = t; i < n * kAsK; i += 256) {
+    for (int i = t; i < n * kAsK; i += T) {
       const int k = i / n, R = i - k * n;
       sl[(int64_t)k * kAsD + R] = reinterpret_cast<const uint4*>(s_z + R * kAsD)[k];
     }
@@ -2000,10 +2027,14 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
 
 // The subdomain inverses of a solve's first GN step (and precond_every steps); the cold start's records x = 0, r = b and
 // the PCG flags too. (A refresh flagged by the previous step runs inside k_pcg_proj<.., true>.)
-__global__ __launch_bounds__(256) void k_as_invert(GnDev g, const double* __restrict__ A, const double* __restrict__ rhs) {
+// k_as_invert's thread grid: 16 x kAsInvTC (16 x 48 = 12 waves measured 119.5 against 110 us per solve with 16 x 16: each
+// step's LDS row / column reads grow with the threads — 172 against 82 KB per two-step — and bound it)
+constexpr int kAsInvTC = 16;
+__global__ __launch_bounds__(16 * kAsInvTC) void k_as_invert(GnDev g, const double* __restrict__ A,
+                                                             const double* __restrict__ rhs) {
   const int c = blockIdx.x, t = threadIdx.x;
   if (g.flags[F_STOPPED]) return;
-  as_invert_body(g, A, c, t);
+  as_invert_body<16, kAsInvTC>(g, A, c, t);
   if (!g.warm_now && t < 6 * kCS) {   // cold start: x = 0, r = b (u = M⁻¹ b comes from k_as_apply into m1)
     const int64_t o = 6 * (int64_t)c * kCS + t;
     const double v[V_N] = {0.0, rhs[o], 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -2124,7 +2155,6 @@ __global__ __launch_bounds__(kAsRS * kL) void k_as_apply(const int32_t* stopw, c
 
 // Galerkin warm start, pass 1: t_j = A x_j for the n_prev stored solutions (own rows) and per-wave
 // partials of the Gram matrix G_ij = x_i·t_j (i <= j, packed) and f_i = x_i·b.
-constexpr int kProjP = kProj * (kProj + 1) / 2 + kProj;
 __device__ __forceinline__ constexpr int tri(int i, int j) { return j * (j + 1) / 2 + i; }   // i <= j
 
 // t_j += A_blk x_j (block bk, gathered history rows x) for the stored solutions j < np, in the loop's order
@@ -2266,7 +2296,7 @@ __global__ __launch_bounds__(kAS ? 256 : 64) __attribute__((amdgpu_waves_per_eu(
       ref = !stopped && refresh == gn_iter ? 1 : 0;
     }
     if constexpr (kAS) {
-      if (ref) as_invert_body(g, g.Aop, blockIdx.x, threadIdx.x);
+      if (ref) as_invert_body<16, 16>(g, g.Aop, blockIdx.x, threadIdx.x);
     }
     (void)ref;
     return;
@@ -3213,7 +3243,7 @@ __device__ __forceinline__ void as_lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 #ifdef OFX_STAMPS   // tuning build: per (iteration < 64, cluster) 8 clock stamps — 0 entry, 1 trip 1 landed, 2 scalars done,
-                    // 3 after barrier 1, 4 after barrier 2, 5 after barrier 3 (own-row wave), 6 end; 7: the last wave's entry
+                    // 3 after barrier 1, 4 after barrier 2, 5 after barrier 3 (own-row wave), 6 end; 7: the row sums done (after 4)
 #define OFX_AS_ITER_STAMP(k, cn) \
   if (lane == 0 && g.stamps && (cn) < 64) g.stamps[((int64_t)(cn) * nwg + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();
 #else
@@ -3247,13 +3277,6 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   // products, (3) the w image. Loads are unconditional (clamped), the roles' data live only inside their branch.
   if (wave >= 8) {  // ---------------- blocks (waves 8-15; tb = block index)
     const int tb = t - kGB;
-#ifdef OFX_STAMPS
-    if (wave == 15) {   // the last block wave's entry
-      const uint64_t t7 = __builtin_amdgcn_s_memtime();
-      const int cn_ = reinterpret_cast<const int32_t*>(scb + kScFlags)[F_PCG_CNT];
-      if (lane == 0 && g.stamps && cn_ < 64) g.stamps[((int64_t)cn_ * nwg + c) * 8 + 7] = t7;
-    }
-#endif
     int stop_ep = stopw[(int64_t)c * 64 + lane];
     const int nb = rt[26];
     typedef double gd2 __attribute__((ext_vector_type(2)));
@@ -3562,6 +3585,9 @@ __global__ __launch_bounds__(kAsIterT) void k_as_iter(const int32_t* stopw, cons
   double nc = 0.0;
 #pragma unroll
   for (int k = 0; k < kRowMax; ++k) nc += k < rlen ? tv[k] : 0.0;
+#ifdef OFX_STAMPS
+  if (jr == 0) { asm volatile("" :: "v"(nc)); OFX_AS_ITER_STAMP(7, cnt) }
+#endif
   double d[kPcgStreams] = {0.0, 0.0, 0.0, 0.0};
   double w2;
   if (jr == 0) {
@@ -4222,7 +4248,8 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   if (as) {
     // the subdomain inverses: rebuilt like the cluster inverses (invert); a refresh flagged by the previous step runs
     // inside k_pcg_proj<.., true>
-    if (invert) hipLaunchKernelGGL(k_as_invert, dim3(ncl), dim3(256), 0, hs, *g, (const double*)A, (const double*)rhs);
+    if (invert)
+      hipLaunchKernelGGL(k_as_invert, dim3(ncl), dim3(16 * kAsInvTC), 0, hs, *g, (const double*)A, (const double*)rhs);
     if (!g->warm_now) as_apply(false, rhs, g->m1);   // cold start: u0 = M⁻¹ b
   } else if (invert) {
     hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);
@@ -4876,8 +4903,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   const bool optimistic = !g->h_perm.empty() && g->h_nodes.size() == 3 * (size_t)N0 &&
                           g->h_edges.size() == (size_t)N0 * NB && g->gcap_n >= 3 * (int64_t)N0 &&
                           g->gcap_e >= (int64_t)N0 * NB && g->d_gdiff;
-  if (optimistic) {
-    OFX_HIP(hipMemsetAsync(g->d_gdiff, 0, sizeof(int32_t), hs));
+  if (optimistic) {   // (d_gdiff is zero: k_setup_status cleared it after reading)
     const int64_t na = 3 * (int64_t)N0, nc = (int64_t)N0 * NB;
     hipLaunchKernelGGL(k_graph_cmp, dim3(grid_for(na > nc ? na : nc, 256, 1 << 30)), dim3(256), 0, hs, pb->nodes,
                        (const float*)g->d_gnodes, na, pb->edges, (const int32_t*)g->d_gedges, nc, g->d_gdiff);
@@ -4912,6 +4938,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
       OFX_HIP(hipMalloc((void**)&g->d_gedges, g->gcap_e * sizeof(int32_t)));
     }
     if (!g->d_gdiff) OFX_HIP(hipMalloc((void**)&g->d_gdiff, sizeof(int32_t)));
+    OFX_HIP(hipMemsetAsync(g->d_gdiff, 0, sizeof(int32_t), hs));   // (this path reads none: a stale flag must not stay)
     OFX_HIP(hipMemcpyAsync(g->d_gnodes, pb->nodes, 3 * (size_t)N0 * sizeof(float), hipMemcpyDeviceToDevice, hs));
     if ((int64_t)N0 * NB > 0)
       OFX_HIP(hipMemcpyAsync(g->d_gedges, pb->edges, (size_t)N0 * NB * sizeof(int32_t), hipMemcpyDeviceToDevice, hs));
@@ -4968,8 +4995,8 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->pcg_ku = pcg_ku_for(g->nwg_row);
   g->nw_pad = 128 * g->pcg_ku;
   // every partial stream is read unconditionally up to nw_pad: the tails must be zero (the kernels write only the
-  // entries of their own waves; k_pcg_w0 re-zeroes the iteration streams' tails, nothing writes the others')
-  OFX_HIP(hipMemsetAsync(g->part_p, 0, (size_t)kProjP * g->nw_pad * sizeof(double), hs));
+  // entries of their own waves; k_pcg_w0 re-zeroes the iteration streams' tails, nothing writes the others'): k_upload
+  // clears them
   g->nwg_node = (N + kBlk - 1) / kBlk;
   g->nwg_terms = (int32_t)((4 * g->T + kBlk - 1) / kBlk);
   // per-solve buffers sized by T
@@ -5005,7 +5032,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   {
     int64_t n = g->T;
     for (int64_t v : {9 * (int64_t)N, 4 * (int64_t)M, ne, u.old_nnzb, (int64_t)3 * kMaxLog, (int64_t)2 * (kMaxLog + 1),
-                      (int64_t)F_COUNT})
+                      (int64_t)F_COUNT, (int64_t)kProjP * g->nw_pad})
       n = v > n ? v : n;
     u.n = n;
   }
@@ -5019,14 +5046,13 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   // terms -> block pattern
   unsigned gT = grid_for(g->T, 256, 1 << 30);
   hipLaunchKernelGGL(k_mark, dim3(gT), dim3(256), 0, hs, *g);
-  OFX_HIP(hipMemsetAsync(g->row_cnt + N + 1, 0, sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_row_count, dim3(N), dim3(256), 0, hs, N, g->map, g->row_cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->row_cnt, g->row_ptr, g->row_cnt + N, false);
   hipLaunchKernelGGL(k_wave_max, dim3(grid_for(N / kCS, 256)), dim3(256), 0, hs, N / kCS, g->row_ptr, g->row_cnt + N + 1);
   OFX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_setup_status, dim3(1), dim3(64), 0, hs, (const int32_t*)g->row_ptr, N,
                      (const int32_t*)g->row_cnt,
-                     (const int32_t*)(optimistic ? g->d_gdiff : nullptr), g->d_setup_stat);
+                     optimistic ? g->d_gdiff : nullptr, g->d_setup_stat);
   OFX_LAUNCH_CHECK();
   OFX_HIP(hipStreamSynchronize(hs));
   const volatile int32_t* ss = g->setup_stat;
@@ -5062,19 +5088,15 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
   g->pat_N = N;
   g->pat_nnzb = nnz;
   // upper blocks: slot -> u by a scan of the flags (blk_cnt as scratch), u -> slot and transpose
-  OFX_HIP(hipMemsetAsync(g->up_slot, 0xFF, (size_t)(nnz + 32) * sizeof(int32_t), hs));   // -1: no upper block
   hipLaunchKernelGGL(k_up_flags, dim3(grid_for(nnz, 256, 1 << 30)), dim3(256), 0, hs, *g, g->blk_cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->up_of, (int32_t*)nullptr);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->up_of, (int32_t*)nullptr, false);
   hipLaunchKernelGGL(k_up_list, dim3(grid_for(nnz, 256, 1 << 30)), dim3(256), 0, hs, *g);
   // contribution lists (sorted -> deterministic assembly order); blocks indexed by u (the entries past the upper
   // count stay empty)
-  OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
-  OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
   hipLaunchKernelGGL(k_pair_count, dim3(gT), dim3(256), 0, hs, *g);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->blk_off, (int32_t*)nullptr);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->node_cnt, g->node_off, (int32_t*)nullptr);
-  OFX_HIP(hipMemsetAsync(g->blk_cnt, 0, (size_t)(nnz + 1) * sizeof(int32_t), hs));
-  OFX_HIP(hipMemsetAsync(g->node_cnt, 0, (size_t)(N + 1) * sizeof(int32_t), hs));
+  // (the scans clear the counts behind them: k_pair_scatter reuses them as cursors)
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)nnz, g->blk_cnt, g->blk_off, (int32_t*)nullptr, true);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, hs, (int64_t)N, g->node_cnt, g->node_off, (int32_t*)nullptr, true);
   hipLaunchKernelGGL(k_pair_scatter, dim3(gT), dim3(256), 0, hs, *g);
   hipLaunchKernelGGL(k_seg_rank, dim3(grid_for(nnz, 4, 1 << 30)), dim3(256), 0, hs, (const int32_t*)g->blk_off, (int64_t)nnz,
                      (const int32_t*)g->blk_list, g->blk_tmp);
@@ -5122,6 +5144,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
       OFX_HIP(hipMemsetAsync(g->as_tab, 0, (size_t)as_tab_bytes(cap), hs));
       OFX_HIP(hipMalloc((void**)&g->as_mem, (size_t)g->max_pad * 4 * sizeof(int32_t)));
       OFX_HIP(hipMalloc((void**)&g->as_memn, (size_t)g->max_pad * sizeof(int32_t)));
+      OFX_HIP(hipMemsetAsync(g->as_memn, 0, (size_t)g->max_pad * sizeof(int32_t), hs));
       g->as_cap = cap;
       g->as_tab_cap = cap;
     }
@@ -5132,8 +5155,7 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
     // one launch per iteration (k_as_iter) unless OFX_AS_ONE=0 (A/B: k_pcg_iter<.., kAS> + k_as_apply, bitwise the same)
     const char* one = getenv("OFX_AS_ONE");
     g->as_one = ((one && atoi(one) == 0) || g->pcg_ku > 4) ? 0 : 1;   // (kU > 4: its partial registers spill)
-    if (g->as_one) {
-      OFX_HIP(hipMemsetAsync(g->as_memn, 0, (size_t)N * sizeof(int32_t), hs));
+    if (g->as_one) {   // (as_memn: cleared by k_upload, or at allocation)
       hipLaunchKernelGGL(k_as_members, dim3(grid_for((int64_t)ncl * kAsDN, 256)), dim3(256), 0, hs, *g, ncl);
       hipLaunchKernelGGL(k_as_tab, dim3(ncl), dim3(256), 0, hs, *g);
     }

@@ -18,7 +18,8 @@ import sys
 import numpy as np
 
 KERNELS = {"k_pcg_iter": ("ofx::k_pcg_iter<true, false",), "k_as_apply": ("ofx::k_as_apply<true",),
-           "k_as_iter": ("ofx::k_as_iter<false",),
+           "k_as_iter": ("ofx::k_as_iter<false",), "k_as_w0": ("ofx::k_as_w0<true",),
+           "k_as_proj2": ("ofx::k_as_proj2<",), "k_pcg_proj": ("ofx::k_pcg_proj<",),
            "k_as_invert": ("ofx::k_as_invert(",),
            "k_integrate_warp": ("ofx::k_integrate_pal4<true>", "ofx::k_integrate<true, true"),
            "k_assemble": ("ofx::k_assemble(",), "k_terms": ("ofx::k_terms(",),

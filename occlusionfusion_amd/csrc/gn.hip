@@ -2025,16 +2025,253 @@ __device__ __forceinline__ void as_invert_body(const GnDev& g, const double* __r
 #undef OFX_AS_STAMP
 }
 
+// k_as_invert's MFMA form (round 6; OFX_AS_INV_MFMA=1 — as_invert_body stays the default, measured faster below): the same damped
+// A_{D_c D_c}, inverted by a blocked Gauss-Jordan on 16 x 16 tiles with f64 MFMA (v_mfma_f64_16x16x4f64) in place of
+// 72 two-pivot VALU steps. One workgroup of kNT waves per subdomain: wave w holds tile column w of the padded
+// kNP x kNP matrix as MFMA accumulators (tile i, lane l, entry r: row 16·i + (l >> 4) + 4r, column 16·w + (l & 15)).
+// Per 16-row panel p: (a) wave p publishes its column — the pivot columns C, with the pivot block as P - I — and P;
+// (b) every wave inverts P itself (scalar Gauss-Jordan in its LDS copy, SPD: no pivoting); (c) every wave forms its
+// V' = P⁻¹ R_w (R_w: its own tile of the pivot rows) or, in the pivot column, I + P⁻¹; (d) every tile M -= C V' (four
+// MFMAs): off the panel the Schur update, on the pivot rows V, on the pivot columns -C P⁻¹, on the pivot block P⁻¹.
+// A tile in the C/D layout is already the B operand of its k-steps (register r = k-step), so V' never leaves the
+// registers; one barrier per panel (C and P double-buffered). Then the stored form as as_invert_body (scales d, fp16
+// Ẑ with the certified margin σ, the slab rows), up to f64 rounding of the inverse.
+typedef double as_d4 __attribute__((ext_vector_type(4)));
+constexpr int kNT = (kAsD + 15) / 16, kNP = 16 * kNT, kInvT = 64 * kNT;
+__device__ __forceinline__ void as_invert_mfma(const GnDev& g, const double* __restrict__ A, int c, int t) {
+  constexpr int kPanel = 16 * kNP;                             // doubles of one pivot-column panel
+  constexpr int kGJ = (2 * kPanel + 2 * 16 * 17) * 8, kZ = kAsD * kAsD * 2;
+  __shared__ __attribute__((aligned(16))) char s_buf[kGJ > kZ ? kGJ : kZ];   // the panels, then the stored form
+  __shared__ int s_dom[kAsDN];
+  __shared__ int s_sl[kAsDN][kAsDN];
+  __shared__ int s_dst[kAsD];
+  __shared__ double s_d[kNP], s_e[kInvT];
+  __shared__ double s_sig;
+  double* s_C = reinterpret_cast<double*>(s_buf);      // [2][kNP][16] the pivot columns (pivot block: P - I)
+  double* s_P = s_C + 2 * kPanel;                      // [2][16][17] P⁻¹ (wave p's Gauss-Jordan in place; column 16: scratch)
+  uint16_t* s_z = reinterpret_cast<uint16_t*>(s_buf);  // (after the elimination) the stored fp16 form, (R, C)
+  const int l = t & 63, lr = l >> 4, lc = l & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+#ifdef OFX_STAMPS
+#define OFX_AS_STAMP(k) \
+  if (t == 0 && g.stamps) g.stamps[((int64_t)63 * g.nwg_row + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define OFX_AS_STAMP(k)
+#endif
+  OFX_AS_STAMP(0)
+  if (t < kAsDN) s_dom[t] = g.as_dom[c * kAsDN + t];
+  if (t < kAsD) s_dst[t] = g.as_dst[(int64_t)c * kAsD + t];
+  __syncthreads();
+  int nd = 0;
+  for (int i = 0; i < kAsDN; ++i) nd += s_dom[i] >= 0 ? 1 : 0;
+  for (int q = t; q < kAsDN * kAsDN; q += kInvT) {
+    const int i = q / kAsDN, j = q % kAsDN;
+    s_sl[i][j] = (i < nd && j < nd) ? g.map[(int64_t)s_dom[i] * g.N + s_dom[j]] - 1 : -1;
+  }
+  __syncthreads();
+  const int n = 6 * nd;
+  const int C0 = 16 * w + lc;   // the lane's column
+  auto slot = [&](int R, int C) { return (R < n && C < n) ? s_sl[min(R / 6, kAsDN - 1)][min(C / 6, kAsDN - 1)] : -1; };
+  as_d4 acc[kNT];
+  // every load unconditional (clamped addresses), masked after (the slot looked up again: no registers held)
+#pragma unroll
+  for (int i = 0; i < kNT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int R = 16 * i + lr + 4 * r;
+      const int sl = slot(R, C0);
+      acc[i][r] = A[36 * (int64_t)(sl >= 0 ? sl : 0) + 6 * (R % 6) + C0 % 6];
+      if (r == 3) __builtin_amdgcn_sched_barrier(0);   // (per tile: the registers)
+    }
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < kNT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int R = 16 * i + lr + 4 * r;
+      // (beyond n: the identity, which the elimination leaves alone)
+      acc[i][r] = (R < n && C0 < n) ? (slot(R, C0) >= 0 ? acc[i][r] : 0.0) : (R == C0 ? 1.0 : 0.0);
+      if (r == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  OFX_AS_STAMP(1)
+  bool bad = false;
+#ifdef OFX_STAMPS
+  uint64_t st_b = 0, st_d = 0;
+#endif
+  for (int p = 0; p < kNT && 16 * p < n; ++p) {
+    // (the lane's row / column offsets from an opaque copy: otherwise every address of the unrolled body is hoisted out
+    // of the panel loop and held in registers, which spilled)
+    int lo = l;
+    asm volatile("" : "+v"(lo));
+    const int lr = lo >> 4, lc = lo & 15;
+    double* sC = s_C + (p & 1) * kPanel;
+    double* sP = s_P + (p & 1) * 16 * 17;
+#ifdef OFX_STAMPS
+    const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
+    // (a) wave p: its column (the pivot columns; the pivot block as P - I) and P⁻¹ (in-place Gauss-Jordan with scalar
+    // pivots, SPD: no pivoting; row k and column k of the current block published per step, a wave's LDS operations
+    // completing in order); the other waves wait at the barrier
+    double e[4];
+    if (w == p) {
+#pragma unroll
+      for (int i = 0; i < kNT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lr + 4 * r;
+          sC[(16 * i + row) * 16 + lc] = acc[i][r] - (i == p && row == lc ? 1.0 : 0.0);
+          if (i == p) e[r] = acc[i][r];
+        }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (lr == (k & 3)) sP[k * 17 + lc] = e[k >> 2];
+        if (lc == k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sP[(lr + 4 * r) * 17 + 16] = e[r];
+        wave_lds_sync();   // (other lanes' writes: no load may move above them)
+        const double piv = sP[k * 17 + k], rk = sP[k * 17 + lc];
+        double ck[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ck[r] = sP[(lr + 4 * r) * 17 + 16];
+        bad = bad || !(piv > 0.0) || !isfinite(piv);
+        const double ip = 1.0 / piv;
+        const double rki = rk * ip;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lr + 4 * r;
+          e[r] = row == k ? (lc == k ? ip : rki) : (lc == k ? -ck[r] * ip : fma(-ck[r], rki, e[r]));
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sP[(lr + 4 * r) * 17 + lc] = e[r];
+    }
+    __syncthreads();
+#ifdef OFX_STAMPS
+    const uint64_t tb1 = __builtin_amdgcn_s_memtime();
+    st_b += tb1 - tb0;
+#endif
+    // (c) V' = P⁻¹ R_w (R_w = tile p of the wave's column, in the C/D layout = the B operand by k-step), or I + P⁻¹
+    as_d4 v;
+    if (w == p) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = e[r] + (lr + 4 * r == lc ? 1.0 : 0.0);
+    } else {
+      as_d4 rw = acc[0];
+#pragma unroll
+      for (int i = 1; i < kNT; ++i)
+        if (i == p) rw = acc[i];
+      v = as_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        v = __builtin_amdgcn_mfma_f64_16x16x4f64(sP[lc * 17 + 4 * s4 + lr], rw[s4], v, 0, 0, 0);
+    }
+    // (d) every tile of the column: M -= C V'
+#pragma unroll
+    for (int i = 0; i < kNT; ++i) {
+      const double* ca = sC + (16 * i + lc) * 16 + lr;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ca[4 * s4], v[s4], acc[i], 0, 0, 0);
+      if (i & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+#ifdef OFX_STAMPS
+    asm volatile("" :: "v"(acc[0]));
+    st_d += __builtin_amdgcn_s_memtime() - tb1;
+#endif
+  }
+#ifdef OFX_STAMPS
+  if (t == 0 && g.stamps) {
+    g.stamps[((int64_t)63 * g.nwg_row + c) * 8 + 6] = st_b;
+    g.stamps[((int64_t)63 * g.nwg_row + c) * 8 + 7] = st_d;
+  }
+#endif
+  bad = __syncthreads_or(bad ? 1 : 0) != 0;   // (also: every panel read is done before s_z reuses the buffer)
+  OFX_AS_STAMP(2)
+  // the stored form (as_invert_body's): d = √diag Z, Ẑ = Z / (d dᵀ) in fp16 with the diagonal 1 + σ
+#pragma unroll
+  for (int r = 0; r < 4; ++r)   // (the diagonal: tile w of column w)
+    if (lr + 4 * r == lc) {
+      const int R = 16 * w + lc;
+      as_d4 dd = acc[0];
+#pragma unroll
+      for (int i = 1; i < kNT; ++i)
+        if (i == w) dd = acc[i];
+      s_d[R] = (R < n && !bad) ? sqrt(dd[r]) : 1.0;
+    }
+  __syncthreads();
+  auto h16 = [](double z) -> _Float16 { return (_Float16)(float)z; };
+  auto b16 = [](_Float16 h) { return __builtin_bit_cast(uint16_t, h); };
+  // the off-diagonal entries (one division each: rounded, their error summed, both triangles written); the diagonal
+  // after σ below
+  double e2 = 0.0;
+  const double dC = s_d[C0];
+#pragma unroll
+  for (int i = 0; i < kNT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int R = 16 * i + lr + 4 * r;
+      if (R >= n || C0 >= kAsD) continue;
+      if (C0 >= n) {
+        s_z[R * kAsD + C0] = 0;
+      } else if (R < C0) {
+        const double z = bad ? 0.0 : acc[i][r] / (s_d[R] * dC);
+        const _Float16 h = h16(z);
+        const double err = (double)(float)h - z;
+        e2 += 2.0 * err * err;
+        s_z[R * kAsD + C0] = b16(h);
+        s_z[C0 * kAsD + R] = b16(h);
+      }
+      if (r == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  s_e[t] = e2;
+  __syncthreads();
+  if (t < 64) {   // ‖E‖²_F in a fixed order
+    double sum = 0.0;
+    for (int i = t; i < kInvT; i += 64) sum += s_e[i];
+    sum = wave_sum(sum);
+    if (t == 0) s_sig = sqrt(sum) + 0x1p-10;
+  }
+  __syncthreads();
+  OFX_AS_STAMP(3)
+  const double sig = s_sig;
+  if (t < n) s_z[t * kAsD + t] = b16(bad ? (_Float16)(t < 6 * kCS ? 1.0f : 0.0f) : h16(1.0 + sig));
+  if (t < kAsD) {
+    const double dr = s_d[t];
+    g.as_dsc[(int64_t)c * kAsD + t] = t < n ? (float)dr : 0.f;
+    if (g.as_one) as_tab_at(g.as_tab, g.as_tab_cap).dsc[(int64_t)c * kAsD + t] = t < n ? (float)dr : 0.f;
+    if (t < n) g.as_rsc[s_dst[t]] = (float)dr;
+  }
+  __syncthreads();
+  OFX_AS_STAMP(4)
+  for (int i = t; i < n * kAsK; i += kInvT) {
+    const int R = i / kAsK, k = i % kAsK;
+    const int d = s_dst[R], cp = d / kAsRS, rs = d % kAsRS;
+    reinterpret_cast<uint4*>(g.as_slab)[((int64_t)cp * kAsK + k) * kAsRS + rs] =
+        reinterpret_cast<const uint4*>(s_z + R * kAsD)[k];
+  }
+  if (g.as_one) {   // k_as_iter's subdomain-ordered copy (rows fastest)
+    uint4* sl = as_tab_at(g.as_tab, g.as_tab_cap).slab + (int64_t)c * kAsK * kAsD;
+    for (int i = t; i < n * kAsK; i += kInvT) {
+      const int k = i / n, R = i - k * n;
+      sl[(int64_t)k * kAsD + R] = reinterpret_cast<const uint4*>(s_z + R * kAsD)[k];
+    }
+  }
+  if (t < kCS) g.racc[c * kCS + t] = 0.0;
+  OFX_AS_STAMP(5)
+#undef OFX_AS_STAMP
+}
+
 // The subdomain inverses of a solve's first GN step (and precond_every steps); the cold start's records x = 0, r = b and
 // the PCG flags too. (A refresh flagged by the previous step runs inside k_pcg_proj<.., true>.)
 // k_as_invert's thread grid: 16 x kAsInvTC (16 x 48 = 12 waves measured 119.5 against 110 us per solve with 16 x 16: each
 // step's LDS row / column reads grow with the threads — 172 against 82 KB per two-step — and bound it)
 constexpr int kAsInvTC = 16;
-__global__ __launch_bounds__(16 * kAsInvTC) void k_as_invert(GnDev g, const double* __restrict__ A,
-                                                             const double* __restrict__ rhs) {
+template <bool kMfma>   // (as_invert_mfma: kInvT threads, OFX_AS_INV_MFMA=1; or as_invert_body, the default: 256)
+__global__ __launch_bounds__(kMfma ? kInvT : 16 * kAsInvTC) void k_as_invert(GnDev g, const double* __restrict__ A,
+                                                                                   const double* __restrict__ rhs) {
   const int c = blockIdx.x, t = threadIdx.x;
   if (g.flags[F_STOPPED]) return;
-  as_invert_body<16, kAsInvTC>(g, A, c, t);
+  if constexpr (kMfma) as_invert_mfma(g, A, c, t);
+  else as_invert_body<16, kAsInvTC>(g, A, c, t);
   if (!g.warm_now && t < 6 * kCS) {   // cold start: x = 0, r = b (u = M⁻¹ b comes from k_as_apply into m1)
     const int64_t o = 6 * (int64_t)c * kCS + t;
     const double v[V_N] = {0.0, rhs[o], 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -4248,8 +4485,12 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
   if (as) {
     // the subdomain inverses: rebuilt like the cluster inverses (invert); a refresh flagged by the previous step runs
     // inside k_pcg_proj<.., true>
-    if (invert)
-      hipLaunchKernelGGL(k_as_invert, dim3(ncl), dim3(16 * kAsInvTC), 0, hs, *g, (const double*)A, (const double*)rhs);
+    if (invert) {
+      const char* me = getenv("OFX_AS_INV_MFMA");   // (A/B; read per solve): 1 = the MFMA form
+      const bool mf = me && atoi(me) == 1;
+      hipLaunchKernelGGL(mf ? k_as_invert<true> : k_as_invert<false>, dim3(ncl), dim3(mf ? kInvT : 16 * kAsInvTC), 0,
+                         hs, *g, (const double*)A, (const double*)rhs);
+    }
     if (!g->warm_now) as_apply(false, rhs, g->m1);   // cold start: u0 = M⁻¹ b
   } else if (invert) {
     hipLaunchKernelGGL(k_pcg_prep, dim3(g->N / kCS), dim3(64), 0, hs, *g, lm, A, (const double*)rhs, invert);

@@ -170,3 +170,23 @@ def test_one_launch_moose_is_bitwise_the_two_launch_form(cuda, monkeypatch):
     assert torch.equal(two["node_translations"], one["node_translations"])
     assert two["convergence_info"]["pcg_iterations"] == one["convergence_info"]["pcg_iterations"]
     assert max(dr, dt) < TOL
+
+
+def test_mfma_subdomain_inversion_matches_the_valu_form(cuda, monkeypatch):
+    """k_as_invert's blocked Gauss-Jordan on f64 MFMA tiles (OFX_AS_INV_MFMA=1) and the two-pivot VALU form (the
+    default) invert the same subdomain blocks: the chained gn_2k solve takes the same PCG work and lands on
+    the same transforms to 1e-7 (the inverses differ only in f64 rounding before their fp16 storage)."""
+    g = _load("gn_2k.npz")
+    monkeypatch.setenv("OFX_PRECOND", "as")
+    monkeypatch.setenv("OFX_AS_INV_MFMA", "0")
+    valu = _chain(g, cuda)
+    monkeypatch.setenv("OFX_AS_INV_MFMA", "1")
+    mfma = _chain(g, cuda)
+    for q, (a, b) in enumerate(zip(valu, mfma)):
+        assert _err(b, g, q) < TOL
+        d = max((a["node_rotations"] - b["node_rotations"]).abs().max().item(),
+                (a["node_translations"] - b["node_translations"]).abs().max().item())
+        print(f"gn_2k frame {q}: PCG {a['convergence_info']['pcg_iterations']} (VALU) / "
+              f"{b['convergence_info']['pcg_iterations']} (MFMA), transforms {d:.2e} apart")
+        assert d < 1e-7, (q, d)
+    assert abs(_pcg(valu) - _pcg(mfma)) <= 0.03 * _pcg(valu), (_pcg(valu), _pcg(mfma))

@@ -1,7 +1,7 @@
 """Tuning study (not product): phase clock stamps of the Schwarz subdomain inversion (k_as_invert) on the bench workload.
 
-Needs the stamps build: python -c "from occlusionfusion_amd import build; build.build(out='tools/bin/libofx_stamps.so',
-defines=['OFX_STAMPS'])", then OFX_LIB=tools/bin/libofx_stamps.so python tools/as_invert_stamps.py
+Needs the stamps build: python -c "from occlusionfusion_amd import build; build.build(out='tools/stampslib/libofx_stamps.so',
+defines=['OFX_STAMPS'])", then OFX_LIB=tools/stampslib/libofx_stamps.so python tools/as_invert_stamps.py
 Phases (thread 0 of each subdomain's workgroup, s_memtime cycles): 1 tables + A gather | 2 block Gauss-Jordan |
 3 scales + fp16 margin | 4 LDS image | 5 slab rows.
 """
@@ -17,7 +17,7 @@ from occlusionfusion_amd import _lib
 from occlusionfusion_amd import synthetic as S
 from occlusionfusion_amd.pipeline import FusionPipeline
 
-assert "stamps" in _lib.LIB_PATH, "run with OFX_LIB=tools/bin/libofx_stamps.so"
+assert "stamps" in _lib.LIB_PATH, "run with OFX_LIB=tools/stampslib/libofx_stamps.so"
 fn = _lib.lib.ofx_gn_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
 fn.restype = ctypes.c_int32
@@ -45,6 +45,9 @@ print(f"subdomains {nw}, stamped {int(ok.sum())}")
 for k, nme in enumerate(["tables+A", "gauss-jordan", "scale+margin", "lds image", "slab rows"]):
     x = d[:, k]
     print(f"  {nme:14s} median {np.median(x):8.0f} cyc  p90 {np.percentile(x, 90):8.0f}")
+ex = buf.reshape(64, nw, 8)[63, :, 6:].astype(np.int64)[ok]
+if (ex > 0).any():   # the MFMA form: cycles spent in the pivot-block inversions / the tile updates, summed over panels
+    print(f"  (MFMA form) pivot blocks {np.median(ex[:, 0]):8.0f} cyc, V + update {np.median(ex[:, 1]):8.0f} cyc")
 tot = st[ok, 5] - st[ok, 0]
 print(f"  total          median {np.median(tot):8.0f} cyc  p90 {np.percentile(tot, 90):8.0f}; "
       f"first entry -> last exit {st[ok, 5].max() - st[ok, 0].min()} cyc")

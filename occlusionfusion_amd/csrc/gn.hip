@@ -5393,9 +5393,20 @@ static int gn_setup(Gn* g, const ofx_gn_problem* pb, const ofx_gn_params* prm, i
     hipLaunchKernelGGL(k_as_accept, dim3(grid_for(N, 4)), dim3(256), 0, hs, *g);
     hipLaunchKernelGGL(k_as_compact, dim3(ncl), dim3(64), 0, hs, *g);
     hipLaunchKernelGGL(k_as_segments, dim3(ncl), dim3(256), 0, hs, *g);
-    // one launch per iteration (k_as_iter) unless OFX_AS_ONE=0 (A/B: k_pcg_iter<.., kAS> + k_as_apply, bitwise the same)
+    // one launch per iteration (k_as_iter) when every subdomain's workgroup gets a CU at once: a k_as_iter workgroup
+    // holds a whole CU (16 waves at 120 VGPRs), so more subdomains than CUs run in two rounds per launch (config 4's 502
+    // on 256 CUs: 12.4 us per iteration, 142.8 frames/s against 165.6 with two launches). OFX_AS_ONE=0 / 1: off / on
+    // regardless of the CU count (A/B, tests: k_pcg_iter<.., kAS> + k_as_apply is bitwise the same); never past kU = 4
+    // (its partial registers spill)
     const char* one = getenv("OFX_AS_ONE");
-    g->as_one = ((one && atoi(one) == 0) || g->pcg_ku > 4) ? 0 : 1;   // (kU > 4: its partial registers spill)
+    int ncu = 0;
+    {
+      int dev = 0;
+      OFX_HIP(hipGetDevice(&dev));
+      OFX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const bool one_on = one ? atoi(one) != 0 : ncl <= ncu;
+    g->as_one = (one_on && g->pcg_ku <= 4) ? 1 : 0;
     if (g->as_one) {   // (as_memn: cleared by k_upload, or at allocation)
       hipLaunchKernelGGL(k_as_members, dim3(grid_for((int64_t)ncl * kAsDN, 256)), dim3(256), 0, hs, *g, ncl);
       hipLaunchKernelGGL(k_as_tab, dim3(ncl), dim3(256), 0, hs, *g);

@@ -28,6 +28,7 @@ TSDF/weight/colour integrate of the new frame. All inputs are device-resident be
     no device work — what tests/test_bench_launch.py runs on the CPU over gloo.
 """
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -83,6 +84,9 @@ def parse():
     p.add_argument("--gn", action="append", default=[], metavar="KEY=VALUE", help=argparse.SUPPRESS)   # (A/B: GN params)
     p.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                    help="set up each frame's solve inline instead of prefetching it during the previous frame")
+    p.add_argument("--no-overlap", dest="overlap", action="store_false",
+                   help="run each frame's integrate on the solve's stream (default: on a stream of its own, beside the "
+                        "next frame's solve, which needs only this frame's transforms)")
     p.add_argument("--cpu-sample", type=int, default=1 << 24)
     p.add_argument("--json-out", default=None)
     p.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
@@ -190,7 +194,7 @@ def main():
         k, v = kv.split("=", 1)
         gn_over[k] = v if k == "precond" else float(v)
     pipe = FusionPipeline(seq, origin, a.voxel, (D, D, D), n_matches=a.matches, device=dev, shard=shard,
-                          gn_params=gn_over or None)
+                          gn_params=gn_over or None, overlap=a.overlap)
     total = a.warmup + a.steps + 1
     frames = [pipe.prepare(t) for t in range(total + 1)]   # + the frame the last timed step prefetches
     torch.cuda.synchronize()
@@ -215,6 +219,11 @@ def main():
         return pipe.solve(fi, nxt if prefetch else None)
 
     ev = lambda: torch.cuda.Event(enable_timing=True)
+    # overlapped integrates: the frame loop's solves go on a stream of the greatest priority, so the hardware queues
+    # dispatch the latency-bound solve chain's workgroups ahead of the integrate beside it (default priority)
+    loop_stream = torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1]) if a.overlap else None
+    loop_ctx = torch.cuda.stream(loop_stream) if loop_stream is not None else contextlib.nullcontext()
+    loop_ctx.__enter__()
     for t in range(1, 1 + a.warmup):
         solve(frames[t], frames[t + 1])
         pipe.integrate(frames[t], t)
@@ -234,16 +243,22 @@ def main():
         e0.record()
         out = solve(frames[t], frames[t + 1])
         e1.record()
-        pipe.integrate(frames[t], t, count_updates=True)
-        e2.record()
-        upd.append(pipe.vol.n_updated[:cache.n_list].sum(dtype=torch.int32))   # one device reduce, read after timing
-        marks.append((e0, e1, e2, out))
+        ie = pipe.integrate(frames[t], t, count_updates=True)
+        if ie is None:   # (sequential: the integrate on the solve's stream)
+            e2.record()
+            upd.append(pipe.vol.n_updated[:cache.n_list].sum(dtype=torch.int32))   # one device reduce, read after timing
+            marks.append((e0, e1, e1, e2, out))
+        else:            # (overlapped: on its own stream, events around it there)
+            with torch.cuda.stream(pipe.int_stream):
+                upd.append(pipe.vol.n_updated[:cache.n_list].sum(dtype=torch.int32))
+            marks.append((e0, e1, ie[0], ie[1], out))
     pipe.solver.drain()   # the last step's prefetched setup (of a frame not timed) counts inside the region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    loop_ctx.__exit__(None, None, None)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -253,10 +268,10 @@ def main():
     N_, M_, nnzb, _T, rows = pipe.solver.info()
     pci = pipe.solver.precond_info()
     t_solve = np.array([m[0].elapsed_time(m[1]) for m in marks]) * 1e-3
-    t_int = np.array([m[1].elapsed_time(m[2]) for m in marks]) * 1e-3
-    pcg = [int(m[3]["_status"][2].item()) for m in marks]
-    gn_it = [int(m[3]["_status"][1].item()) for m in marks]
-    valid = [int(m[3]["_status"][0].item()) for m in marks]
+    t_int = np.array([m[2].elapsed_time(m[3]) for m in marks]) * 1e-3
+    pcg = [int(m[4]["_status"][2].item()) for m in marks]
+    gn_it = [int(m[4]["_status"][1].item()) for m in marks]
+    valid = [int(m[4]["_status"][0].item()) for m in marks]
     U = float(np.mean([int(u.item()) for u in upd]))
     kint_ms, kint_n = pipe.vol.integrate_timing(False)
     t_kint_loop = kint_ms * 1e-3 / max(1, kint_n)
@@ -358,7 +373,7 @@ def main():
                    "solve": (a.solve if sharded else "local"), "dims": D, "voxel_size_m": a.voxel,
                    "nodes": int(seq.nodes.shape[0]), "matches": a.matches,
                    "parallelism": f"{a.mode}{world}" + (f"-{a.solve}" if sharded else ""),
-                   "setup_prefetch": prefetch, "scene_seed": scene_seed},
+                   "setup_prefetch": prefetch, "integrate_overlap": bool(a.overlap), "scene_seed": scene_seed},
         "breakdown_ms": {"solve": 1e3 * float(np.mean(t_solve)), "integrate": 1e3 * float(np.mean(t_int)),
                          "allreduce": 1e3 * t_ar, "pcg_iters_per_frame": float(np.mean(pcg)),
                          "gn_iters": float(np.mean(gn_it)), "valid_solves": int(np.sum(valid)),

@@ -32,7 +32,7 @@ class FrameInputs:
 
 class FusionPipeline:
     def __init__(self, seq, origin, voxel_size, dims, n_matches=10000, device=None, shard=None, gn_params=None,
-                 with_color=True):
+                 with_color=True, overlap=False):
         self.seq = seq
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         cam = seq.cam
@@ -50,6 +50,11 @@ class FusionPipeline:
         self.prev_rot = None
         self.prev_trans = None
         self.last = None
+        # overlap=True: frame t's integrate runs on a stream of its own, ordered after frame t's solve but not before
+        # frame t+1's — the next solve needs frame t's transforms, not its volume (bit for bit the sequential result;
+        # a caller reading the volume synchronises the device, not only its own stream)
+        self.overlap = overlap
+        self.int_stream = None
 
     def prepare(self, t):
         """Host-side synthetic inputs of frame t -> device (outside any timed region)."""
@@ -83,6 +88,28 @@ class FusionPipeline:
         return out
 
     def integrate(self, fi, t, count_updates=False):
+        if not (self.overlap and self.device.type == "cuda"):
+            self._integrate(fi, t, count_updates)
+            return None
+        if self.int_stream is None:
+            self.int_stream = torch.cuda.Stream(self.device)
+        s = self.int_stream
+        after_solve = torch.cuda.Event()
+        after_solve.record()
+        s.wait_event(after_solve)
+        # tensors made on the solve's stream that the integrate reads: kept from reuse until it has run
+        st = getattr(self.vol, "_staged", None)
+        for x in (self.prev_rot, self.prev_trans) + (tuple(st[1:]) if st is not None else ()):
+            if isinstance(x, torch.Tensor) and x.is_cuda:
+                x.record_stream(s)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            e0.record()
+            self._integrate(fi, t, count_updates)
+            e1.record()
+        return e0, e1
+
+    def _integrate(self, fi, t, count_updates=False):
         self.wf.set_node_transforms(self.prev_rot, self.prev_trans)
         self.wf.frame_id = t
         self.vol.update(fi.im, t)

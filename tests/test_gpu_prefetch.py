@@ -123,3 +123,34 @@ def test_gated_prefetch_without_its_trigger_solve(cuda, destroy_trigger):
         _lib.lib.ofx_gn_destroy(trig)
     assert s.prefetch_stats() == (1, 0)
     assert torch.equal(pipe.prev_rot, ref.prev_rot) and torch.equal(pipe.prev_trans, ref.prev_trans)
+
+
+def test_overlapped_integrate_equals_sequential(cuda):
+    """FusionPipeline(overlap=True) (bench.py's default): frame t's integrate on a stream of its own, beside frame t+1's
+    solve — the same transforms and bit for bit the same fused volume and per-brick update counts as the sequential
+    loop, with the prefetched setup on as well."""
+    from occlusionfusion_amd import synthetic as S
+    from occlusionfusion_amd.pipeline import FusionPipeline
+    res = []
+    for overlap in (False, True):
+        c = S.BASELINE_CONFIGS[1]
+        seq = S.config_sequence(1)
+        D = c["dims"]
+        pipe = FusionPipeline(seq, c["origin"], c["voxel"], (D, D, D), device=cuda, overlap=overlap)
+        frames = [pipe.prepare(t) for t in range(8)]
+        pipe.integrate_source(frames[0])
+        outs = []
+        for t in range(1, 7):
+            pipe.solve(frames[t], frames[t + 1])
+            pipe.integrate(frames[t], t, count_updates=True)
+            outs.append((pipe.prev_rot, pipe.prev_trans))
+        pipe.solver.drain()
+        torch.cuda.synchronize()
+        assert (pipe.int_stream is not None) == overlap
+        res.append((pipe, outs))
+    (p0, o0), (p1, o1) = res
+    for (R0, T0), (R1, T1) in zip(o0, o1):
+        assert torch.equal(R0, R1) and torch.equal(T0, T1)
+    for a, b in ((p0.vol.tsdf_b, p1.vol.tsdf_b), (p0.vol.weight_b, p1.vol.weight_b), (p0.vol.color_b, p1.vol.color_b),
+                 (p0.vol.n_updated, p1.vol.n_updated)):
+        assert torch.equal(a, b)

@@ -524,6 +524,11 @@ int ofx_gn_prepare_wait(void* handle, ofx_stream_t s);
 int ofx_gn_share_history(void* handle, void* other);
 /* Solves on this handle that used a prefetched setup / discarded one (a different problem or a failure). */
 int ofx_gn_prefetch_stats(void* handle, int64_t* used, int64_t* missed);
+/* Host work to run once inside the next solve on this handle, while its host loop waits for the first GN step's PCG
+ * chunk (the host is otherwise idle there): fn(arg) is called on the solving thread, then forgotten; NULL fn clears a
+ * pending one. A frame loop uses it to enqueue the previous frame's integrate (on a stream of its own) without holding
+ * back the next solve's first launches. (Round 6; no ABI struct changes.) */
+int ofx_gn_set_idle_hook(void* handle, void (*fn)(void*), void* arg);
 
 #ifdef __cplusplus
 }

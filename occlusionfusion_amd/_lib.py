@@ -119,6 +119,7 @@ _SIGS = {
     "ofx_gn_prepare_wait": [P, P],
     "ofx_gn_prefetch_stats": [P, P, P],
     "ofx_gn_share_history": [P, P],
+    "ofx_gn_set_idle_hook": [P, P, P],
 }
 
 

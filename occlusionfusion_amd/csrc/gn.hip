@@ -266,6 +266,8 @@ struct Gn : GnDev {
   int64_t pf_used = 0, pf_missed = 0;   // solves that used / discarded a prefetched setup
   int32_t ep_next = 1;
   int as_env = -1;                  // OFX_PRECOND override of params.precond (-1: none)
+  void (*idle_fn)(void*) = nullptr; // ofx_gn_set_idle_hook: host work run once at the next solve's first PCG wait
+  void* idle_arg = nullptr;
   int as_lanes = 2;                 // k_as_apply's lanes per segment (OFX_AS_LANES)
   int as_cap = 0;                   // clusters the Schwarz tables are allocated for
   // the PCG iteration's constant launch arguments (struct PcgIt) in device memory, and the bytes last copied there
@@ -4665,6 +4667,13 @@ static int gn_pcg(Gn* g, int gn_iter, double* A, double* rhs, hipStream_t hs) {
     if (g->timing) OFX_HIP(hipEventRecord(e1, hs));
     OFX_HIP(hipEventRecord(g->poll_ev, hs));
     bool ran = false;
+    if (g->idle_fn) {   // (ofx_gn_set_idle_hook: the host would only spin here)
+      void (*fn)(void*) = g->idle_fn;
+      void* arg = g->idle_arg;
+      g->idle_fn = nullptr;
+      g->idle_arg = nullptr;
+      fn(arg);
+    }
     // converged: the converging launch's lead lane stored H_DONE (the next step's kernels follow it on the stream);
     // stopped (by an earlier solve: this one's launches end at their stop words; by this solve's converging launch):
     // nothing to wait for
@@ -5101,6 +5110,14 @@ int ofx_gn_share_history(void* handle, void* other) {
   Gn* o = (Gn*)other;
   OFX_CHECK_ARG(g && o, "null handle");
   g->last_pcg = o->last_pcg;
+  return OFX_OK;
+}
+
+int ofx_gn_set_idle_hook(void* handle, void (*fn)(void*), void* arg) {
+  Gn* g = (Gn*)handle;
+  OFX_CHECK_ARG(g, "null handle");
+  g->idle_fn = fn;
+  g->idle_arg = fn ? arg : nullptr;
   return OFX_OK;
 }
 

@@ -87,27 +87,52 @@ class FusionPipeline:
         self.prev_rot, self.prev_trans = out["node_rotations"], out["node_translations"]
         return out
 
-    def integrate(self, fi, t, count_updates=False):
+    def integrate(self, fi, t, count_updates=False, after=None):
+        """Frame t's warp + integrate. overlap=True: on the pipeline's integrate stream, ordered after frame t's solve,
+        and enqueued by the host inside the NEXT solve (GaussNewtonSolver.defer_to_next_solve: while that solve's host
+        loop waits for its first PCG chunk), so the host work of the enqueue no longer sits between two solves;
+        flush() runs a pending one now. after(): more work for that stream, right after the integrate. Returns a list
+        that gets the integrate's (start, end) timing events once it is enqueued (overlap) or None."""
         if not (self.overlap and self.device.type == "cuda"):
             self._integrate(fi, t, count_updates)
+            if after is not None:
+                after()
             return None
         if self.int_stream is None:
             self.int_stream = torch.cuda.Stream(self.device)
         s = self.int_stream
-        after_solve = torch.cuda.Event()
-        after_solve.record()
-        s.wait_event(after_solve)
-        # tensors made on the solve's stream that the integrate reads: kept from reuse until it has run
-        st = getattr(self.vol, "_staged", None)
-        for x in (self.prev_rot, self.prev_trans) + (tuple(st[1:]) if st is not None else ()):
-            if isinstance(x, torch.Tensor) and x.is_cuda:
-                x.record_stream(s)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(s):
-            e0.record()
-            self._integrate(fi, t, count_updates)
-            e1.record()
-        return e0, e1
+        solved = torch.cuda.Event()
+        solved.record()   # (the solve's stream: frame t's transforms are final here)
+        staged, self.vol._staged = getattr(self.vol, "_staged", None), None   # (frame t's unpacked depth / colour)
+        R, T = self.prev_rot, self.prev_trans
+        events = []
+
+        def enqueue():
+            s.wait_event(solved)
+            for x in (R, T) + (tuple(staged[1:]) if staged is not None else ()):
+                if isinstance(x, torch.Tensor) and x.is_cuda:
+                    x.record_stream(s)   # (made on the solve's stream: kept from reuse until the integrate has run)
+            cur = getattr(self.vol, "_staged", None)
+            self.vol._staged = staged
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(s):
+                e0.record()
+                self.wf.set_node_transforms(R, T)
+                self.wf.frame_id = t
+                self.vol.update(fi.im, t)
+                self.vol.integrate_device(count_updates=count_updates)
+                e1.record()
+                if after is not None:
+                    after()
+            self.vol._staged = cur
+            events.extend((e0, e1))
+
+        self.solver.defer_to_next_solve(enqueue)
+        return events
+
+    def flush(self):
+        """Enqueue a deferred (overlapped) integrate now: before reading the volume or timing the loop's end."""
+        self.solver.flush_deferred()
 
     def _integrate(self, fi, t, count_updates=False):
         self.wf.set_node_transforms(self.prev_rot, self.prev_trans)

@@ -52,6 +52,9 @@ def _prefetch_lead(num_iter):
     return min(max(v, 0), int(num_iter))
 
 
+_IDLE_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p)   # ofx_gn_set_idle_hook's fn
+
+
 class GaussNewtonSolver:
     def __init__(self, max_nodes, max_matches=MAX_MATCHES_EVAL, device=None, **params):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -64,6 +67,9 @@ class GaussNewtonSolver:
         self._slots = [self._new_slot()]
         self._cur = 0                   # slot of the next optimize()
         self._pending = [None, None]    # a prefetched problem's tensors, alive until its solve
+        self._deferred = None           # defer_to_next_solve: (fn, handle) pending
+        self._deferred_cb = None        # its ctypes callback, kept alive
+        self._deferred_exc = None       # an exception it raised inside a solve, re-raised by the next call
         self._side = None               # torch stream that orders a prefetch before the current solve
         # GN steps of the current solve a prefetch overlaps: its setup starts when the solve begins step
         # num_iter - prefetch_lead (ofx_gn_prepare_after); 0 = when the solve's host loop returns
@@ -104,6 +110,38 @@ class GaussNewtonSolver:
             call("ofx_gn_prefetch_stats", h, byref(u), byref(m))
             used, missed = used + u.value, missed + m.value
         return used, missed
+
+    def defer_to_next_solve(self, fn):
+        """Run fn() once inside the next optimize(), while its host loop waits for the first GN step's PCG chunk
+        (ofx_gn_set_idle_hook: the host only spins there), or at that optimize's return if it never waited. A frame
+        loop enqueues the previous frame's integrate this way without delaying the next solve's first launches.
+        flush_deferred() runs a pending fn now."""
+        self.flush_deferred()
+        h = self._slots[self._cur][0]
+
+        def hook(_arg):
+            self._run_deferred()
+        self._deferred_cb = _IDLE_HOOK(hook)
+        self._deferred = (fn, h)
+        call("ofx_gn_set_idle_hook", h, ctypes.cast(self._deferred_cb, ctypes.c_void_p), None)
+
+    def _run_deferred(self):
+        d, self._deferred = self._deferred, None
+        if d is None:
+            return
+        try:
+            d[0]()
+        except BaseException as e:   # (inside the library's host loop: kept, raised by the next Python-level call)
+            self._deferred_exc = e
+
+    def flush_deferred(self):
+        """Run a pending defer_to_next_solve() fn now (and raise what a deferred fn raised)."""
+        if self._deferred is not None:
+            call("ofx_gn_set_idle_hook", self._deferred[1], None, None)
+            self._run_deferred()
+        if self._deferred_exc is not None:
+            e, self._deferred_exc = self._deferred_exc, None
+            raise e
 
     def drain(self):
         """Order the current stream after any prefetched setup still in flight (ofx_gn_prepare_wait): a
@@ -247,7 +285,10 @@ class GaussNewtonSolver:
             lead = int(self.prefetch_lead)
             if lead > 0:   # queued now, started by this solve at GN step num_iter - lead (or when it returns)
                 self._prefetch(pa, before, h, int(self.params["num_iter"]) - lead, fp, ip)
+        if self._deferred is not None and self._deferred[1].value != h.value:   # (hooked on another slot)
+            self.flush_deferred()
         out = torch.ops.ofx.gn_solve(st, h.value, *args, fp, ip)
+        self.flush_deferred()   # (a deferred fn the solve never reached — no PCG wait — runs now; its exception too)
         self._pending[cur] = None
         self._h, self._state = h, st
         if prefetch is not None:

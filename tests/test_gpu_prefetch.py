@@ -127,8 +127,9 @@ def test_gated_prefetch_without_its_trigger_solve(cuda, destroy_trigger):
 
 def test_overlapped_integrate_equals_sequential(cuda):
     """FusionPipeline(overlap=True) (bench.py's default): frame t's integrate on a stream of its own, beside frame t+1's
-    solve — the same transforms and bit for bit the same fused volume and per-brick update counts as the sequential
-    loop, with the prefetched setup on as well."""
+    solve, enqueued by the host inside that solve (GaussNewtonSolver.defer_to_next_solve) — the same transforms and
+    bit for bit the same fused volume and per-brick update counts as the sequential loop, with the prefetched setup
+    on as well."""
     from occlusionfusion_amd import synthetic as S
     from occlusionfusion_amd.pipeline import FusionPipeline
     res = []
@@ -144,6 +145,7 @@ def test_overlapped_integrate_equals_sequential(cuda):
             pipe.solve(frames[t], frames[t + 1])
             pipe.integrate(frames[t], t, count_updates=True)
             outs.append((pipe.prev_rot, pipe.prev_trans))
+        pipe.flush()
         pipe.solver.drain()
         torch.cuda.synchronize()
         assert (pipe.int_stream is not None) == overlap

@@ -592,34 +592,58 @@ __global__ __launch_bounds__(256) void k_wave_list(GnDev g) {
 // (max_out, nullable: max of cnt)
 __global__ __launch_bounds__(1024) void k_scan(int64_t n, int32_t* cnt, int32_t* __restrict__ off,
                                                int32_t* __restrict__ max_out, bool clear) {   // clear: cnt = 0 after
-  // tiles of 1024 x 8 counts: thread t scans its 8 contiguous entries (two coalesced 16-B loads), the
-  // block scan combines the threads, a carry runs across tiles (fixed order)
+  // tiles of 1024 x 32 counts (the setup's lists, up to ~33k entries, in one tile: one memory trip instead of one per
+  // 8k entries): thread t scans its 32 contiguous entries (16-B loads and stores), the block scan combines the threads,
+  // a carry runs across tiles (fixed order)
   __shared__ int s_w[16];
   __shared__ int s_mx[16];
-  constexpr int kPer = 8;
+  constexpr int kPer = 32;
   int carry = 0, mx = 0;
   for (int64_t base = 0; base < n; base += (int64_t)blockDim.x * kPer) {
     const int64_t s0 = base + (int64_t)threadIdx.x * kPer;
+    const bool vec = s0 + kPer <= n && ((reinterpret_cast<uintptr_t>(cnt + s0) & 15) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(off + s0) & 15) == 0);
     int v[kPer];
-    if (s0 + kPer <= n && ((reinterpret_cast<uintptr_t>(cnt + s0) & 15) == 0)) {
-      const int4 a = *reinterpret_cast<const int4*>(cnt + s0), b = *reinterpret_cast<const int4*>(cnt + s0 + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    if (vec) {
+#pragma unroll
+      for (int q = 0; q < kPer / 4; ++q) {
+        const int4 a = reinterpret_cast<const int4*>(cnt + s0)[q];
+        v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < kPer; ++k) v[k] = s0 + k < n ? cnt[s0 + k] : 0;
     }
-    if (clear)
+    if (clear) {
+      if (vec) {
 #pragma unroll
-      for (int k = 0; k < kPer; ++k)
-        if (s0 + k < n) cnt[s0 + k] = 0;
+        for (int q = 0; q < kPer / 4; ++q) reinterpret_cast<int4*>(cnt + s0)[q] = make_int4(0, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+          if (s0 + k < n) cnt[s0 + k] = 0;
+      }
+    }
     int c = 0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) { c += v[k]; mx = max(mx, v[k]); }
     int total;
     int o = block_exscan(c, s_w, total) + carry;
+    if (vec) {
 #pragma unroll
-    for (int k = 0; k < kPer; ++k)
-      if (s0 + k < n) { off[s0 + k] = o; o += v[k]; }
+      for (int q = 0; q < kPer / 4; ++q) {
+        int4 r;
+        r.x = o; o += v[4 * q];
+        r.y = o; o += v[4 * q + 1];
+        r.z = o; o += v[4 * q + 2];
+        r.w = o; o += v[4 * q + 3];
+        reinterpret_cast<int4*>(off + s0)[q] = r;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k)
+        if (s0 + k < n) { off[s0 + k] = o; o += v[k]; }
+    }
     carry += total;
   }
   if (threadIdx.x == 0) off[n] = carry;

@@ -1785,16 +1785,22 @@ __global__ __launch_bounds__(256) void k_as_members(GnDev g, int ncl) {
 __global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
   __shared__ int s_dom[kAsDN], s_rs[kAsDN + 1];
   __shared__ int s_col[kGB], s_slot[kGB], s_l[kGB], s_first[kGB], s_rank[kGB];
-  __shared__ int s_key[kGB], s_scan[kGB];
+  __shared__ int s_key[kGB], s_scan[kGB], s_len[kAsDN], s_r0[kAsDN];
   const int c = blockIdx.x, t = threadIdx.x;
   const AsTabP tp = as_tab_at(g.as_tab, g.as_tab_cap);
-  if (t < kAsDN) s_dom[t] = g.as_dom[c * kAsDN + t];
+  if (t < kAsDN) {   // every row's length in parallel (one trip; the serial loop below waited for each row's in turn)
+    const int d = g.as_dom[c * kAsDN + t];
+    s_dom[t] = d;
+    const int r0 = g.row_ptr[d >= 0 ? d : 0], r1 = g.row_ptr[d >= 0 ? d + 1 : 0];
+    s_r0[t] = r0;
+    s_len[t] = d >= 0 ? r1 - r0 : 0;
+  }
   __syncthreads();
   if (t == 0) {
     int acc = 0, l = 0;
     for (; l < kAsDN && s_dom[l] >= 0; ++l) {
       s_rs[l] = acc;
-      acc += g.row_ptr[s_dom[l] + 1] - g.row_ptr[s_dom[l]];
+      acc += s_len[l];
     }
     for (; l <= kAsDN; ++l) s_rs[l] = acc;
   }
@@ -1806,7 +1812,7 @@ __global__ __launch_bounds__(256) void k_as_tab(GnDev g) {
     if (i < nb) {
       int l = 0;
       while (l + 1 < nd && s_rs[l + 1] <= i) ++l;
-      const int b = g.row_ptr[s_dom[l]] + (i - s_rs[l]);
+      const int b = s_r0[l] + (i - s_rs[l]);
       s_col[i] = g.col[b]; s_slot[i] = b; s_l[i] = l;
       s_key[i] = (g.col[b] << 9) | i;   // (rows < 2^22)
     } else {
